@@ -1,0 +1,159 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ResNet-18, CIFAR-10-shape synthetic data, PowerSGD r=4 (BASELINE.json).
+
+    python bench.py --gpus N --steps K --warmup W
+    torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
+        bench.py --gpus N --steps K --warmup W
+
+One process per GPU, RCCL over xGMI (backend "nccl" = RCCL on ROCm).  Each timed step is
+the full reference training step (ddp_powersgd_guide_cifar10/ddp_init.py:142-178):
+forward, cross-entropy, backward, EF pack, PowerSGD compress + 2 all-reduces,
+decompress, error memory, momentum, SGD update — fused by PowerSGDOptimizer into
+6 gfx950 kernels + 2 collectives.  fp32 everywhere (the reference's dtype), random-init
+weights, synthetic device-resident data.  Weak scaling: per-GPU batch fixed (default
+512 = the reference's global batch at N=1, ddp_powersgd_guide_cifar10/ddp_init.py:52).
+
+Rank 0 prints ONE JSON line.  `value` = whole-job samples/s (max step time over ranks).
+`bytes_per_step` = bytes all-reduced per rank per step with the reference's accounting.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+METRIC = "samples/sec + bytes/step all-reduced, ResNet18 CIFAR10 PowerSGD r=4, 1/2/4/8 GPU"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--model", default="resnet18")
+    ap.add_argument("--num-classes", type=int, default=1000)
+    ap.add_argument("--batch", type=int, default=512, help="per-GPU batch (weak scaling)")
+    ap.add_argument("--reducer", choices=["powersgd", "dense", "dense-ref", "powersgd-ref"], default="powersgd")
+    ap.add_argument("--rank", type=int, default=4)
+    ap.add_argument("--lr", type=float, default=1e-3)
+    ap.add_argument("--channels-last", action="store_true")
+    ap.add_argument("--link", default="none", help="none|1g|10g|100g link emulation")
+    ap.add_argument("--bucket-mb", type=float, default=25.0)
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    from network_distributed_pytorch_amd.models import build_model
+    from network_distributed_pytorch_amd.parallel.comm import LINK_PRESETS, Communicator
+    from network_distributed_pytorch_amd.parallel.trainer import build_grad_sync
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.manual_seed(714)
+    torch.backends.cudnn.benchmark = True
+
+    model = build_model(args.model, args.num_classes).to(device)
+    if args.channels_last:
+        model = model.to(memory_format=torch.channels_last)
+    link = None if args.link == "none" else LINK_PRESETS[args.link]
+    comm = Communicator(link=link)
+    sync = build_grad_sync(args.reducer, model, comm, lr=args.lr, momentum=0.9, rank=args.rank,
+                           bucket_mb=args.bucket_mb)
+    crit = torch.nn.CrossEntropyLoss()
+
+    # synthetic CIFAR-10-shape data, normalised to [-1, 1] like ToTensor+Normalize(0.5, 0.5)
+    g = torch.Generator(device=device)
+    g.manual_seed(1234 + rank)
+    n_pool = 4
+    xs = (torch.rand(n_pool, args.batch, 3, 32, 32, device=device, generator=g) * 2 - 1)
+    if args.channels_last:
+        xs = torch.stack([x.contiguous(memory_format=torch.channels_last) for x in xs])
+    ys = torch.randint(0, 10, (n_pool, args.batch), device=device, generator=g)
+
+    loss_acc = torch.zeros((), device=device)
+
+    def step(i):
+        sync.zero_grad()
+        out = model(xs[i % n_pool])
+        loss = crit(out, ys[i % n_pool])
+        loss.backward()
+        sync.step()
+        loss_acc.add_(loss.detach())
+
+    for i in range(args.warmup):
+        step(i)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    comm.stats.reset()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    final_loss = float(loss_acc.item()) / max(1, args.warmup + args.steps)
+
+    if rank == 0:
+        global_batch = args.batch * world
+        sps = global_batch * args.steps / elapsed
+        rec = {
+            "metric": METRIC,
+            "value": round(sps, 2),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic CIFAR-10-shape (3x32x32, 10 labels), random-init weights",
+            "bytes_per_step": sync.bytes_per_step,
+            "collectives_per_step": sync.collectives_per_step,
+            "config": {
+                "model": args.model,
+                "num_classes": args.num_classes,
+                "global_batch": global_batch,
+                "per_gpu_batch": args.batch,
+                "seq_len": None,
+                "image": [3, 32, 32],
+                "parallelism": f"dp{world}",
+                "reducer": args.reducer,
+                "powersgd_rank": args.rank if "powersgd" in args.reducer else None,
+                "link_emulation": args.link,
+                "channels_last": args.channels_last,
+            },
+            "mean_loss": round(final_loss, 5),
+        }
+        line = json.dumps(rec)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,209 @@
+// Multi-tensor / flat-arena kernels for gfx950.
+//
+//  * seg_reduce: ONE launch that performs any number of (strided multi-slab) reduce-copies:
+//      - TensorBuffer pack   (reference: tensor_buffer.py:19 torch.cat, :27-32 pack)
+//      - TensorBuffer unpack with the all-reduce mean folded in (reducer.py:167-168)
+//      - deterministic split-K sum of the PowerSGD P / Q partial slabs
+//    The workgroup -> entry map is a block-prefix table searched in scalar registers.
+//  * sgd_momentum: dense-arm torch.optim.SGD(momentum) step with the all-reduce mean
+//    folded in (ddp_guide_cifar10/ddp_init.py:57-62,111,125) over the flat gradient arena.
+//  * add: EF pack  send = g + e  (ddp_powersgd_guide_cifar10/ddp_init.py:156-157).
+//  * delay_ns: wall-clock spin used by the link emulator to pace collectives to a
+//    1/10/100 Gb budget on the stream (reference README.md:2 experiments).
+//  * checksum: deterministic fp64 sum of a flat buffer (cross-rank divergence detector).
+#include <hip/hip_runtime.h>
+#include "ndp_kernels.h"
+
+namespace ndp {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+
+__global__ __launch_bounds__(256) void seg_reduce_kernel(const SegEntry* __restrict__ ents,
+                                                         const int64_t* __restrict__ prefix,
+                                                         int n_ent) {
+  const int64_t blk = blockIdx.x;
+  int lo = 0, hi = n_ent - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (prefix[mid] <= blk) lo = mid; else hi = mid - 1;
+  }
+  const SegEntry E = ents[lo];
+  const int64_t base = (blk - prefix[lo]) * kSegBlockElems;
+  const bool scale = E.div != 1.0f;
+  if (E.vec) {
+#pragma unroll
+    for (int q = 0; q < kSegBlockElems / 1024; ++q) {
+      const int64_t k = base + (int64_t)(q * 256 + threadIdx.x) * 4;
+      if (k + 3 < E.numel) {
+        f32x4 acc = ld4(E.src + k);
+        for (int c = 1; c < E.chunks; ++c) acc += ld4(E.src + (int64_t)c * E.stride + k);
+        if (scale) acc = acc / E.div;
+        st4(E.dst + k, acc);
+      } else {
+        for (int j = 0; j < 4; ++j) {
+          if (k + j >= E.numel) break;
+          float acc = E.src[k + j];
+          for (int c = 1; c < E.chunks; ++c) acc += E.src[(int64_t)c * E.stride + k + j];
+          if (scale) acc = acc / E.div;
+          E.dst[k + j] = acc;
+        }
+      }
+    }
+  } else {
+    for (int q = 0; q < kSegBlockElems / 256; ++q) {
+      const int64_t k = base + q * 256 + threadIdx.x;
+      if (k >= E.numel) break;
+      float acc = E.src[k];
+      for (int c = 1; c < E.chunks; ++c) acc += E.src[(int64_t)c * E.stride + k];
+      if (scale) acc = acc / E.div;
+      E.dst[k] = acc;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void sgd_momentum_vec_kernel(float* __restrict__ x,
+                                                               const float* __restrict__ g,
+                                                               float* __restrict__ buf,
+                                                               int64_t n4, float lr, float mu,
+                                                               float div) {
+  const bool scale = div != 1.0f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    f32x4 gg = ld4(g + 4 * i);
+    if (scale) gg = gg / div;
+    f32x4 b = ld4(buf + 4 * i);
+    f32x4 xx = ld4(x + 4 * i);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      b[j] = __fadd_rn(__fmul_rn(b[j], mu), gg[j]);
+      xx[j] = fmaf(-lr, b[j], xx[j]);
+    }
+    st4(buf + 4 * i, b);
+    st4(x + 4 * i, xx);
+  }
+}
+
+__global__ __launch_bounds__(256) void sgd_momentum_kernel(float* __restrict__ x,
+                                                           const float* __restrict__ g,
+                                                           float* __restrict__ buf,
+                                                           int64_t start, int64_t n, float lr,
+                                                           float mu, float div) {
+  for (int64_t i = start + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float gg = g[i];
+    if (div != 1.0f) gg = gg / div;
+    const float b = __fadd_rn(__fmul_rn(buf[i], mu), gg);
+    buf[i] = b;
+    x[i] = fmaf(-lr, b, x[i]);
+  }
+}
+
+__global__ __launch_bounds__(256) void add_vec_kernel(const float* __restrict__ a,
+                                                      const float* __restrict__ b,
+                                                      float* __restrict__ o, int64_t n4) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x)
+    st4(o + 4 * i, ld4(a + 4 * i) + ld4(b + 4 * i));
+}
+
+__global__ __launch_bounds__(256) void add_kernel(const float* __restrict__ a,
+                                                  const float* __restrict__ b,
+                                                  float* __restrict__ o, int64_t start,
+                                                  int64_t n) {
+  for (int64_t i = start + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    o[i] = a[i] + b[i];
+}
+
+__global__ void delay_kernel(int64_t ticks) {
+  // s_memrealtime is the 100 MHz constant-rate clock: 1 tick = 10 ns.  Bounded spin.
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+constexpr int kCkBlocks = 256;
+
+__global__ __launch_bounds__(256) void checksum_partial_kernel(const float* __restrict__ x,
+                                                               int64_t n,
+                                                               double* __restrict__ part) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)kCkBlocks * 256)
+    s += (double)x[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void checksum_final_kernel(double* out) {
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int i = 0; i < kCkBlocks; ++i) s += out[1 + i];
+    out[0] = s;
+  }
+}
+
+// ---------------------------------- launchers -------------------------------------
+static inline unsigned grid_for(int64_t n, int64_t per_block = 256, int64_t cap = 2048) {
+  int64_t b = (n + per_block - 1) / per_block;
+  if (b < 1) b = 1;
+  if (b > cap) b = cap;
+  return (unsigned)b;
+}
+
+static inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+void launch_seg_reduce(const SegEntry* entries, const int64_t* block_prefix, int n_entries,
+                       int64_t n_blocks, hipStream_t s) {
+  if (n_entries <= 0 || n_blocks <= 0) return;
+  hipLaunchKernelGGL(seg_reduce_kernel, dim3((unsigned)n_blocks), dim3(256), 0, s, entries,
+                     block_prefix, n_entries);
+}
+
+void launch_sgd_momentum(float* x, const float* g, float* buf, int64_t n, float lr, float mu,
+                         float div, hipStream_t s) {
+  if (n <= 0) return;
+  int64_t done = 0;
+  if (aligned16(x) && aligned16(g) && aligned16(buf)) {
+    const int64_t n4 = n / 4;
+    if (n4 > 0)
+      hipLaunchKernelGGL(sgd_momentum_vec_kernel, dim3(grid_for(n4)), dim3(256), 0, s, x, g, buf,
+                         n4, lr, mu, div);
+    done = n4 * 4;
+  }
+  if (done < n)
+    hipLaunchKernelGGL(sgd_momentum_kernel, dim3(grid_for(n - done)), dim3(256), 0, s, x, g, buf,
+                       done, n, lr, mu, div);
+}
+
+void launch_add(const float* a, const float* b, float* out, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  int64_t done = 0;
+  if (aligned16(a) && aligned16(b) && aligned16(out)) {
+    const int64_t n4 = n / 4;
+    if (n4 > 0)
+      hipLaunchKernelGGL(add_vec_kernel, dim3(grid_for(n4)), dim3(256), 0, s, a, b, out, n4);
+    done = n4 * 4;
+  }
+  if (done < n)
+    hipLaunchKernelGGL(add_kernel, dim3(grid_for(n - done)), dim3(256), 0, s, a, b, out, done, n);
+}
+
+void launch_delay_ns(int64_t ns, hipStream_t s) {
+  if (ns <= 0) return;
+  hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, s, (ns + 9) / 10);
+}
+
+void launch_checksum(const float* x, int64_t n, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(checksum_partial_kernel, dim3(kCkBlocks), dim3(256), 0, s, x, n, out + 1);
+  hipLaunchKernelGGL(checksum_final_kernel, dim3(1), dim3(64), 0, s, out);
+}
+
+}  // namespace ndp

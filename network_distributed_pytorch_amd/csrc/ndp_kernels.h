@@ -1,0 +1,96 @@
+// Shared device-table layouts and host launch entry points for the gfx950 kernels.
+//
+// Every hot op of the reference's PowerSGD step is a grouped
+// kernel driven by a device-side table built once per model by the plan builder
+// (plan.cpp).  The tables replace the reference's per-tensor Python loops
+// (reference: ddp_powersgd_guide_cifar10/reducer.py:86-168).
+//
+// All launchers take raw device pointers + a hipStream_t and never allocate or
+// synchronise, so every call is hipGraph-capturable.
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+namespace ndp {
+
+// ---- PowerSGD plan geometry (one per high-rank matrix, 64 B) ----------------------
+struct MatGeom {
+  int32_t n, m, r;      // matrix = param.view(n, m); r = min(n, m, R)
+  int32_t vec;          // 1 -> m % 4 == 0 and every bound pointer 16-B aligned (float4 path)
+  int32_t p_off, q_off; // element offsets into the flat P / Q buffers (reference order)
+  int32_t pp_off, qp_off;     // element offsets into the P / Q split-K partial scratch
+  int32_t p_chunks, q_chunks; // number of split-K slabs for P (over m) and Q (over n)
+  int32_t pad[6];
+};
+
+// ---- per-matrix bound pointers (64 B) -------------------------------------------
+// engine mode : min = grad, e = error memory (M = g + e is written back into e),
+//               mread = e, mom = momentum, x = parameter, g = grad (optional write)
+// api mode    : min = M (caller's send buffer), e = nullptr, mread = M,
+//               out = grad_out, mem = memory_out
+struct MatPtrs {
+  const float* min;
+  float* e;
+  const float* mread;
+  float* out;
+  float* mem;
+  float* mom;
+  float* x;
+  float* g;
+};
+
+// Work items.  One workgroup (4 waves) per item.
+struct PItem { int32_t mat, row0, k0, k1, chunk, pad[3]; };   // 64 rows x [k0,k1)
+struct QItem { int32_t mat, col0, row0, row1, chunk, pad[3]; }; // [row0,row1) x 256 cols
+struct UItem { int32_t mat, row0, col0, pad; };                 // 64 rows x 64 cols
+
+// Segmented reduce-copy entry: dst[k] = (sum_c src[c*stride + k]) / div
+struct SegEntry {
+  const float* src;
+  float* dst;
+  int64_t numel;
+  int64_t stride;
+  int32_t chunks;
+  float div;
+  int32_t vec;
+  int32_t pad;
+};
+
+constexpr int kPRows = 64;    // rows per P item (4 waves x 16)
+constexpr int kPK = 256;      // k-chunk of a P item
+constexpr int kQCols = 256;   // columns per Q item (4 waves x 64)
+constexpr int kQRowsMax = 256;  // max rows per Q item (LDS: 256 x (16*NCG+pad) floats)
+constexpr int kURows = 64;
+constexpr int kUCols = 64;
+constexpr int kMaxRank = 64;
+constexpr int kSegBlockElems = 2048;  // elements per workgroup in seg_reduce
+
+// ---- launchers (powersgd.hip) --------------------------------------------------
+void launch_psgd_p(const MatGeom* geom, const MatPtrs* ptrs, const PItem* items, int n_items,
+                   const float* q_warm, float* p_part, int fuse_ef, int max_rank, hipStream_t s);
+void launch_psgd_q(const MatGeom* geom, const MatPtrs* ptrs, const QItem* items, int n_items,
+                   const float* p_hat, float* q_part, int max_rank, hipStream_t s);
+void launch_psgd_orth(const MatGeom* geom, int n_mats, float* p, float p_div, float eps,
+                      int max_rank, hipStream_t s);
+// mode 0 = api (out/mem), 1 = engine (EF + momentum + SGD), 2 = engine + write grad
+void launch_psgd_update(const MatGeom* geom, const MatPtrs* ptrs, const UItem* items,
+                        int n_items, const float* p_hat, const float* q_sum, float q_div,
+                        float* q_warm, int mode, float lr, float momentum, hipStream_t s);
+// rank-1 (<=1-D) group of the fused engine: out = buf/div; m = lam*m + out; x -= lr*(out+m)
+void launch_rank1_step(const float* buf, float div, float* mom, float* x, float* g,
+                       int64_t n, float lr, float momentum, hipStream_t s);
+
+// ---- launchers (multitensor.hip) -----------------------------------------------
+void launch_seg_reduce(const SegEntry* entries, const int64_t* block_prefix, int n_entries,
+                       int64_t n_blocks, hipStream_t s);
+// dense arm: b = mu*b + g/div ; x -= lr*b   (torch.optim.SGD(momentum) with zero-init buf)
+void launch_sgd_momentum(float* x, const float* g, float* buf, int64_t n, float lr, float mu,
+                         float div, hipStream_t s);
+// out = a + b  (EF pack: send = g + e)
+void launch_add(const float* a, const float* b, float* out, int64_t n, hipStream_t s);
+// spin the stream for `ns` nanoseconds of wall time (link-emulation pacing)
+void launch_delay_ns(int64_t ns, hipStream_t s);
+// deterministic fp64-accumulated checksum of a flat buffer (replica divergence detector)
+void launch_checksum(const float* x, int64_t n, double* out, hipStream_t s);
+
+}  // namespace ndp

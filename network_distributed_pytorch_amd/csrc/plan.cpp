@@ -1,0 +1,120 @@
+// PowerSGD execution-plan builder (host C++).
+//
+// The reference re-derives its P/Q layout every call with Python loops
+// (ddp_powersgd_guide_cifar10/reducer.py:72-98) and allocates p_memory / q_memory once
+// (reducer.py:82-84).  Here the layout and the load-balanced work lists for every
+// grouped kernel are computed ONCE per parameter set:
+//   * P / Q buffer offsets in reference order (so the all-reduced payload and its byte
+//     count are identical to the reference: SURVEY.md §2.7);
+//   * P items  : (matrix, 64-row block, 256-wide k-chunk)   -> split-K over m;
+//   * Q items  : (matrix, 256-col block, row chunk)          -> split-K over n;
+//   * U items  : (matrix, 64x64 tile)                        -> fused decompress/update;
+//   * split-K slab offsets for the deterministic seg_reduce.
+#include "plan.h"
+
+#include <algorithm>
+#include <stdexcept>
+
+namespace ndp {
+
+static int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+Plan build_plan(const std::vector<std::pair<int64_t, int64_t>>& shapes, int rank) {
+  if (rank < 1 || rank > kMaxRank)
+    throw std::invalid_argument("PowerSGD rank must be in [1, 64]");
+  Plan pl;
+  pl.max_rank = 0;
+  int64_t p_off = 0, q_off = 0, pp_off = 0, qp_off = 0;
+  for (size_t i = 0; i < shapes.size(); ++i) {
+    const int64_t n = shapes[i].first, m = shapes[i].second;
+    if (n < 1 || m < 1) throw std::invalid_argument("empty matrix in PowerSGD plan");
+    if (n > (1LL << 30) || m > (1LL << 30)) throw std::invalid_argument("matrix too large");
+    const int64_t r = std::min<int64_t>(std::min(n, m), rank);
+    MatGeom g{};
+    g.n = (int32_t)n;
+    g.m = (int32_t)m;
+    g.r = (int32_t)r;
+    g.vec = 0;
+    g.p_off = (int32_t)p_off;
+    g.q_off = (int32_t)q_off;
+    g.p_chunks = (int32_t)cdiv(m, kPK);
+    // Q split over n: 64-row chunks, but at most 64 chunks (cap the slab scratch), and
+    // never more rows than the LDS tile holds.
+    int64_t rc = 64;
+    if (cdiv(n, rc) > 64) rc = std::min<int64_t>(kQRowsMax, ((cdiv(n, 64) + 3) / 4) * 4);
+    if (rc > n) rc = n;
+    g.q_chunks = (int32_t)cdiv(n, rc);
+    g.pp_off = (int32_t)pp_off;
+    g.qp_off = (int32_t)qp_off;
+    pl.geom.push_back(g);
+    pl.q_rows.push_back((int32_t)rc);
+
+    for (int64_t row0 = 0; row0 < n; row0 += kPRows)
+      for (int64_t c = 0; c < g.p_chunks; ++c) {
+        PItem it{};
+        it.mat = (int32_t)i;
+        it.row0 = (int32_t)row0;
+        it.k0 = (int32_t)(c * kPK);
+        it.k1 = (int32_t)std::min<int64_t>(m, (c + 1) * kPK);
+        it.chunk = (int32_t)c;
+        pl.p_items.push_back(it);
+      }
+    for (int64_t c = 0; c < g.q_chunks; ++c)
+      for (int64_t col0 = 0; col0 < m; col0 += kQCols) {
+        QItem it{};
+        it.mat = (int32_t)i;
+        it.col0 = (int32_t)col0;
+        it.row0 = (int32_t)(c * rc);
+        it.row1 = (int32_t)std::min<int64_t>(n, (c + 1) * rc);
+        it.chunk = (int32_t)c;
+        pl.q_items.push_back(it);
+      }
+    for (int64_t row0 = 0; row0 < n; row0 += kURows)
+      for (int64_t col0 = 0; col0 < m; col0 += kUCols) {
+        UItem it{};
+        it.mat = (int32_t)i;
+        it.row0 = (int32_t)row0;
+        it.col0 = (int32_t)col0;
+        pl.u_items.push_back(it);
+      }
+
+    p_off += n * r;
+    q_off += m * r;
+    pp_off += g.p_chunks * n * r;
+    qp_off += g.q_chunks * m * r;
+    pl.max_rank = std::max<int>(pl.max_rank, (int)r);
+    if (p_off > (1LL << 31) - 1 || q_off > (1LL << 31) - 1 || pp_off > (1LL << 31) - 1 ||
+        qp_off > (1LL << 31) - 1)
+      throw std::invalid_argument("PowerSGD plan exceeds int32 offsets");
+  }
+  pl.p_total = p_off;
+  pl.q_total = q_off;
+  pl.pp_total = pp_off;
+  pl.qp_total = qp_off;
+  if (pl.max_rank == 0) pl.max_rank = 1;
+  return pl;
+}
+
+SegTable build_seg_table(const std::vector<SegSpec>& specs) {
+  SegTable t;
+  int64_t blocks = 0;
+  for (const SegSpec& s : specs) {
+    if (s.numel <= 0) continue;
+    SegEntry e{};
+    e.src = reinterpret_cast<const float*>(s.src);
+    e.dst = reinterpret_cast<float*>(s.dst);
+    e.numel = s.numel;
+    e.stride = s.stride;
+    e.chunks = s.chunks < 1 ? 1 : s.chunks;
+    e.div = s.div;
+    e.vec = ((s.src & 15) == 0 && (s.dst & 15) == 0 && (e.chunks == 1 || (s.stride & 3) == 0))
+                ? 1 : 0;
+    t.entries.push_back(e);
+    t.prefix.push_back(blocks);
+    blocks += cdiv(s.numel, kSegBlockElems);
+  }
+  t.n_blocks = blocks;
+  return t;
+}
+
+}  // namespace ndp

@@ -1,0 +1,38 @@
+#pragma once
+#include <cstdint>
+#include <utility>
+#include <vector>
+
+#include "ndp_kernels.h"
+
+namespace ndp {
+
+struct Plan {
+  std::vector<MatGeom> geom;
+  std::vector<int32_t> q_rows;  // rows per Q split-K chunk, per matrix
+  std::vector<PItem> p_items;
+  std::vector<QItem> q_items;
+  std::vector<UItem> u_items;
+  int64_t p_total = 0, q_total = 0, pp_total = 0, qp_total = 0;
+  int max_rank = 1;
+};
+
+// shapes[i] = (n_i, m_i) of every >1-D tensor, in model.parameters() order
+Plan build_plan(const std::vector<std::pair<int64_t, int64_t>>& shapes, int rank);
+
+struct SegSpec {
+  uintptr_t src, dst;
+  int64_t numel, stride;
+  int32_t chunks;
+  float div;
+};
+
+struct SegTable {
+  std::vector<SegEntry> entries;
+  std::vector<int64_t> prefix;
+  int64_t n_blocks = 0;
+};
+
+SegTable build_seg_table(const std::vector<SegSpec>& specs);
+
+}  // namespace ndp

@@ -1,0 +1,509 @@
+// PowerSGD compression pipeline on gfx950 (CDNA4) — hand-written HIP, f32 MFMA.
+//
+// Replaces the reference's per-tensor eager loop
+//   P = M Q            (ddp_powersgd_guide_cifar10/reducer.py:121-123)   -> psgd_p_kernel
+//   orthogonalize(P)   (reducer.py:136-137, 180-191)                     -> psgd_orth_kernel
+//   Q = M^T P          (reducer.py:140-142)                              -> psgd_q_kernel
+//   out = P Q^T, mem = M - out (reducer.py:158-163) + Algorithm-2 momentum/SGD
+//                      (ddp_powersgd_guide_cifar10/ddp_init.py:156-178)  -> psgd_update_kernel
+// with ONE launch per stage for all matrices (work-item tables from plan.cpp).
+//
+// Design notes (MI355X):
+//  * The GEMMs are tall-skinny (r <= 64) and HBM-bound (~r/2 FLOP/B).  They run on
+//    v_mfma_f32_16x16x4_f32 (exact f32, k-ordered fmaf chain), the small operand (Q or P)
+//    is staged in LDS and shared by the 4 waves of a workgroup, the big operand (M) is
+//    streamed straight to VGPRs with 16-B loads (cdna_hip_programming.md §5 'GEMV' row).
+//  * Split-K partials are written to slabs and summed in a fixed order by seg_reduce,
+//    so P and Q are bitwise reproducible: every rank computes the identical P-hat and the
+//    identical decompressed gradient (SURVEY.md §7.4 hard part 1).  No float atomics.
+//  * M = g + e is formed on the fly in the P pass and written back into e, so the Q and
+//    update passes read one array; the update pass fuses decompression, error feedback,
+//    momentum and the parameter update (one read-modify-write of e, m, x).
+#include <hip/hip_runtime.h>
+#include "ndp_kernels.h"
+
+namespace ndp {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  // D(16x16) += A(16x4) * B(4x16); lane l: A[l&15][l>>4], B[l>>4][l&15];
+  // D: col = l&15, row = 4*(l>>4) + reg.
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+
+__device__ __forceinline__ float wave_sum(float v) {
+  // xor butterfly: every lane ends with the bitwise-identical total (fp add commutes)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ----------------------------------------------------------------------------------
+// P partial:  p_part[chunk][a][c] = sum_{k in chunk} M[a][k] * Q[k][c]
+// workgroup = 64 rows x kPK columns of one matrix; wave w owns rows row0+16w..+15.
+// Q[k0:k1, :] is staged transposed in LDS: qt[c][k] (row stride kPK+4).
+// ----------------------------------------------------------------------------------
+template <int NCG>
+__global__ __launch_bounds__(256) void psgd_p_kernel(const MatGeom* __restrict__ geom,
+                                                     const MatPtrs* __restrict__ ptrs,
+                                                     const PItem* __restrict__ items,
+                                                     const float* __restrict__ q_warm,
+                                                     float* __restrict__ p_part, int fuse_ef) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int LD = kPK + 4;
+  constexpr int CW = 16 * NCG;
+  const PItem it = items[blockIdx.x];
+  const MatGeom g = geom[it.mat];
+  const MatPtrs pt = ptrs[it.mat];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = g.r;
+  const int klen = it.k1 - it.k0;
+  const float* Q = q_warm + g.q_off + (int64_t)it.k0 * r;
+  for (int idx = tid; idx < kPK * CW; idx += 256) {
+    const int b = idx / CW, c = idx - (idx / CW) * CW;
+    float v = 0.f;
+    if (b < klen && c < r) v = Q[b * r + c];
+    smem[c * LD + b] = v;
+  }
+  __syncthreads();
+
+  const int a0 = it.row0 + wave * 16;
+  if (a0 >= g.n) return;  // no barrier below
+  const int arow = a0 + (lane & 15);
+  const bool rowok = arow < g.n;
+  const int kq = 4 * (lane >> 4);
+  const int64_t rowbase = (int64_t)arow * g.m + it.k0;
+
+  f32x4 mv[16];
+  if (g.vec) {
+    f32x4 ev[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int kl = 16 * s + kq;
+      mv[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+      ev[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (rowok && kl < klen) {
+        mv[s] = ld4(pt.min + rowbase + kl);
+        if (fuse_ef) ev[s] = ld4(pt.e + rowbase + kl);
+      }
+    }
+    if (fuse_ef) {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int kl = 16 * s + kq;
+        mv[s] = mv[s] + ev[s];  // send = g + e   (ddp_init.py:156-157)
+        if (rowok && kl < klen) st4(pt.e + rowbase + kl, mv[s]);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int kl = 16 * s + kq;
+      float t[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v = 0.f;
+        if (rowok && kl + j < klen) {
+          v = pt.min[rowbase + kl + j];
+          if (fuse_ef) {
+            v = v + pt.e[rowbase + kl + j];
+            pt.e[rowbase + kl + j] = v;
+          }
+        }
+        t[j] = v;
+      }
+      mv[s] = f32x4{t[0], t[1], t[2], t[3]};
+    }
+  }
+
+  float* dst = p_part + g.pp_off + (int64_t)it.chunk * g.n * r;
+#pragma unroll
+  for (int cg = 0; cg < NCG; ++cg) {
+    if (cg * 16 >= r) break;
+    const float* qrow = smem + (cg * 16 + (lane & 15)) * LD + kq;
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 16; s += 2) {
+      const f32x4 q0 = ld4(qrow + 16 * s);
+      const f32x4 q1 = ld4(qrow + 16 * (s + 1));
+      acc0 = mfma4(mv[s].x, q0.x, acc0);
+      acc1 = mfma4(mv[s + 1].x, q1.x, acc1);
+      acc0 = mfma4(mv[s].y, q0.y, acc0);
+      acc1 = mfma4(mv[s + 1].y, q1.y, acc1);
+      acc0 = mfma4(mv[s].z, q0.z, acc0);
+      acc1 = mfma4(mv[s + 1].z, q1.z, acc1);
+      acc0 = mfma4(mv[s].w, q0.w, acc0);
+      acc1 = mfma4(mv[s + 1].w, q1.w, acc1);
+    }
+    const f32x4 acc = acc0 + acc1;
+    const int c = cg * 16 + (lane & 15);
+    if (c < r) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int a = a0 + 4 * (lane >> 4) + j;
+        if (a < g.n) dst[(int64_t)a * r + c] = acc[j];
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------
+// Q partial:  q_part[chunk][b][c] = sum_{a in [row0,row1)} M[a][b] * Phat[a][c]
+// workgroup = [row0,row1) x 256 columns; wave w owns columns col0+64w..+63.
+// Lane l streams M[a][b0+4(l&15) .. +3] for row a = step + (l>>4): 4 rows x 256 B per
+// wave instruction.  MFMA j consumes component j (column b0 + 4i + j of row block).
+// P-hat rows [row0,row1) are staged in LDS (row stride LDP, bank-conflict padded).
+// ----------------------------------------------------------------------------------
+template <int NCG>
+__global__ __launch_bounds__(256) void psgd_q_kernel(const MatGeom* __restrict__ geom,
+                                                     const MatPtrs* __restrict__ ptrs,
+                                                     const QItem* __restrict__ items,
+                                                     const float* __restrict__ p_hat,
+                                                     float* __restrict__ q_part) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int CW = 16 * NCG;
+  constexpr int LDP = CW + (NCG > 1 ? 16 : 0);
+  const QItem it = items[blockIdx.x];
+  const MatGeom g = geom[it.mat];
+  const MatPtrs pt = ptrs[it.mat];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = g.r;
+  const int nrows = it.row1 - it.row0;
+  const int nrows4 = (nrows + 3) & ~3;
+  const float* P = p_hat + g.p_off + (int64_t)it.row0 * r;
+  for (int idx = tid; idx < nrows4 * CW; idx += 256) {
+    const int a = idx / CW, c = idx - (idx / CW) * CW;
+    float v = 0.f;
+    if (a < nrows && c < r) v = P[(int64_t)a * r + c];
+    smem[a * LDP + c] = v;
+  }
+  __syncthreads();
+
+  const int b0 = it.col0 + wave * 64;
+  if (b0 >= g.m) return;
+  const int bl = b0 + 4 * (lane & 15);
+  const int rsub = lane >> 4;
+  const int cl = lane & 15;
+  const float* Mb = pt.mread + (int64_t)it.row0 * g.m;
+
+  f32x4 acc[NCG][4];
+#pragma unroll
+  for (int cg = 0; cg < NCG; ++cg)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[cg][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto load_m = [&](int s) -> f32x4 {
+    const int al = s + rsub;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (al < nrows) {
+      const float* row = Mb + (int64_t)al * g.m;
+      if (g.vec) {
+        if (bl < g.m) v = ld4(row + bl);
+      } else {
+        float t[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t[j] = (bl + j < g.m) ? row[bl + j] : 0.f;
+        v = f32x4{t[0], t[1], t[2], t[3]};
+      }
+    }
+    return v;
+  };
+  auto consume = [&](int s, f32x4 mv) {
+#pragma unroll
+    for (int cg = 0; cg < NCG; ++cg) {
+      const float pv = smem[(s + rsub) * LDP + cg * 16 + cl];
+      acc[cg][0] = mfma4(mv.x, pv, acc[cg][0]);
+      acc[cg][1] = mfma4(mv.y, pv, acc[cg][1]);
+      acc[cg][2] = mfma4(mv.z, pv, acc[cg][2]);
+      acc[cg][3] = mfma4(mv.w, pv, acc[cg][3]);
+    }
+  };
+
+  int s = 0;
+  for (; s + 16 <= nrows4; s += 16) {
+    const f32x4 m0 = load_m(s), m1 = load_m(s + 4), m2 = load_m(s + 8), m3 = load_m(s + 12);
+    consume(s, m0);
+    consume(s + 4, m1);
+    consume(s + 8, m2);
+    consume(s + 12, m3);
+  }
+  for (; s < nrows4; s += 4) consume(s, load_m(s));
+
+  float* dst = q_part + g.qp_off + (int64_t)it.chunk * g.m * r;
+#pragma unroll
+  for (int cg = 0; cg < NCG; ++cg) {
+    const int c = cg * 16 + cl;
+    if (c >= r) continue;
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int b = b0 + 4 * (4 * rsub + reg) + j;
+        if (b < g.m) dst[(int64_t)b * r + c] = acc[cg][j][reg];
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------
+// Batched modified Gram-Schmidt, one workgroup per matrix, deterministic reductions.
+// Same arithmetic as the reference (reducer.py:180-191):
+//   col_i /= sqrt(sum(col_i^2)) + eps ;  rest_j -= sum(col_i * rest_j) * col_i
+// with the all-reduce mean folded into the prologue (reducer.py:128).
+// ----------------------------------------------------------------------------------
+template <int K>
+__device__ __forceinline__ void block_sum_vec(float (&v)[K], float* red /*[4][K]*/) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = wave_sum(v[k]);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) red[wave * K + k] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = ((red[k] + red[K + k]) + red[2 * K + k]) + red[3 * K + k];
+  __syncthreads();
+}
+
+template <int RMAX>
+__global__ __launch_bounds__(256) void psgd_orth_kernel(const MatGeom* __restrict__ geom,
+                                                        float* __restrict__ p, float p_div,
+                                                        float eps) {
+  __shared__ float red[4 * RMAX];
+  const MatGeom g = geom[blockIdx.x];
+  const int r = g.r, n = g.n;
+  float* P = p + g.p_off;
+  const int tid = threadIdx.x;
+
+  float s1[1] = {0.f};
+  for (int a = tid; a < n; a += 256) {
+    float* row = P + (int64_t)a * r;
+    for (int c = 0; c < r; ++c) row[c] = row[c] / p_div;
+    s1[0] += row[0] * row[0];
+  }
+  block_sum_vec<1>(s1, red);
+
+  for (int i = 0; i < r; ++i) {
+    const float nrm = sqrtf(s1[0]) + eps;
+    float d[RMAX];
+#pragma unroll
+    for (int j = 0; j < RMAX; ++j) d[j] = 0.f;
+    for (int a = tid; a < n; a += 256) {
+      float* row = P + (int64_t)a * r;
+      const float vi = row[i] / nrm;
+      row[i] = vi;
+#pragma unroll
+      for (int j = 0; j < RMAX; ++j)
+        if (j > i && j < r) d[j] += vi * row[j];
+    }
+    if (i + 1 >= r) break;
+    block_sum_vec<RMAX>(d, red);
+    s1[0] = 0.f;
+    for (int a = tid; a < n; a += 256) {
+      float* row = P + (int64_t)a * r;
+      const float vi = row[i];
+#pragma unroll
+      for (int j = 0; j < RMAX; ++j)
+        if (j > i && j < r) row[j] = row[j] - d[j] * vi;
+      const float w = row[i + 1];
+      s1[0] += w * w;
+    }
+    block_sum_vec<1>(s1, red);
+  }
+}
+
+// ----------------------------------------------------------------------------------
+// Decompress + error feedback (+ momentum + SGD):  out[a][b] = sum_c Phat[a][c] * Qs[b][c]
+// computed as D = Qs * Phat^T on MFMA so each lane holds 4 consecutive b of one row a
+// (16-B accesses of e / m / x).  Qs = Q_sum / q_div (reducer.py:147).  One designated
+// wave per column block also writes Qs into the warm-start buffer (reducer.py:101-111).
+// ----------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void psgd_update_kernel(
+    const MatGeom* __restrict__ geom, const MatPtrs* __restrict__ ptrs,
+    const UItem* __restrict__ items, const float* __restrict__ p_hat,
+    const float* __restrict__ q_sum, float q_div, float* __restrict__ q_warm, int mode,
+    float lr, float momentum) {
+  const UItem it = items[blockIdx.x];
+  const MatGeom g = geom[it.mat];
+  const MatPtrs pt = ptrs[it.mat];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = g.r, n = g.n, m = g.m;
+  const float* P = p_hat + g.p_off;
+  const float* Q = q_sum + g.q_off;
+
+  if (q_warm != nullptr && it.row0 == 0 && wave == 0) {
+    float* W = q_warm + g.q_off;
+    const int cnt = min(kUCols, m - it.col0) * r;
+    const int64_t base = (int64_t)it.col0 * r;
+    for (int idx = lane; idx < cnt; idx += 64) W[base + idx] = Q[base + idx] / q_div;
+  }
+
+  const int a0 = it.row0 + wave * 16;
+  if (a0 >= n) return;
+  const int aL = a0 + (lane & 15);
+  const int kq = lane >> 4;
+  const int nk = (r + 3) >> 2;
+  f32x4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int kc = 0; kc < nk; ++kc) {
+    const int c = 4 * kc + kq;
+    const float bv = (aL < n && c < r) ? P[(int64_t)aL * r + c] : 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int b = it.col0 + 16 * t + (lane & 15);
+      const float av = (b < m && c < r) ? Q[(int64_t)b * r + c] / q_div : 0.f;
+      acc[t] = mfma4(av, bv, acc[t]);
+    }
+  }
+  if (aL >= n) return;
+  const int64_t ro = (int64_t)aL * m;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int b = it.col0 + 16 * t + 4 * kq;
+    if (b >= m) continue;
+    const f32x4 o = acc[t];
+    if (g.vec) {
+      const f32x4 M = ld4(pt.mread + ro + b);
+      if (mode == 0) {
+        st4(pt.out + ro + b, o);
+        st4(pt.mem + ro + b, M - o);
+      } else {
+        f32x4 mm = ld4(pt.mom + ro + b);
+        f32x4 xx = ld4(pt.x + ro + b);
+        st4(pt.e + ro + b, M - o);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) mm[j] = __fadd_rn(__fmul_rn(mm[j], momentum), o[j]);
+        const f32x4 up = o + mm;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xx[j] = fmaf(-lr, up[j], xx[j]);
+        st4(pt.mom + ro + b, mm);
+        st4(pt.x + ro + b, xx);
+        if (mode == 2) st4(pt.g + ro + b, up);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (b + j >= m) break;
+        const int64_t k = ro + b + j;
+        const float M = pt.mread[k];
+        if (mode == 0) {
+          pt.out[k] = o[j];
+          pt.mem[k] = M - o[j];
+        } else {
+          pt.e[k] = M - o[j];
+          const float mm = __fadd_rn(__fmul_rn(pt.mom[k], momentum), o[j]);
+          pt.mom[k] = mm;
+          const float up = o[j] + mm;
+          pt.x[k] = fmaf(-lr, up, pt.x[k]);
+          if (mode == 2) pt.g[k] = up;
+        }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void rank1_step_kernel(const float* __restrict__ buf, float div,
+                                                         float* __restrict__ mom,
+                                                         float* __restrict__ x,
+                                                         float* __restrict__ g, int64_t n,
+                                                         float lr, float momentum) {
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const float o = buf[k] / div;
+    const float mm = __fadd_rn(__fmul_rn(mom[k], momentum), o);
+    mom[k] = mm;
+    const float up = o + mm;
+    x[k] = fmaf(-lr, up, x[k]);
+    if (g) g[k] = up;
+  }
+}
+
+// ---------------------------------- launchers -------------------------------------
+static inline void allow_lds(const void* fn, size_t bytes) {
+  // gfx950 has 160 KiB of LDS per CU; dynamic requests above 64 KiB must be opted in.
+  if (bytes > 65536) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+static inline int ncg_for(int max_rank) {
+  const int c = (max_rank + 15) / 16;
+  return c <= 1 ? 1 : (c == 2 ? 2 : 4);
+}
+
+void launch_psgd_p(const MatGeom* geom, const MatPtrs* ptrs, const PItem* items, int n_items,
+                   const float* q_warm, float* p_part, int fuse_ef, int max_rank,
+                   hipStream_t s) {
+  if (n_items <= 0) return;
+  const int ncg = ncg_for(max_rank);
+  const size_t lds = sizeof(float) * 16 * ncg * (kPK + 4);
+  if (ncg == 4) allow_lds(reinterpret_cast<const void*>(psgd_p_kernel<4>), lds);
+  if (ncg == 1)
+    hipLaunchKernelGGL(psgd_p_kernel<1>, dim3(n_items), dim3(256), lds, s, geom, ptrs, items,
+                       q_warm, p_part, fuse_ef);
+  else if (ncg == 2)
+    hipLaunchKernelGGL(psgd_p_kernel<2>, dim3(n_items), dim3(256), lds, s, geom, ptrs, items,
+                       q_warm, p_part, fuse_ef);
+  else
+    hipLaunchKernelGGL(psgd_p_kernel<4>, dim3(n_items), dim3(256), lds, s, geom, ptrs, items,
+                       q_warm, p_part, fuse_ef);
+}
+
+void launch_psgd_q(const MatGeom* geom, const MatPtrs* ptrs, const QItem* items, int n_items,
+                   const float* p_hat, float* q_part, int max_rank, hipStream_t s) {
+  if (n_items <= 0) return;
+  const int ncg = ncg_for(max_rank);
+  const int ldp = 16 * ncg + (ncg > 1 ? 16 : 0);
+  const size_t lds = sizeof(float) * kQRowsMax * ldp;
+  if (ncg == 4) allow_lds(reinterpret_cast<const void*>(psgd_q_kernel<4>), lds);
+  if (ncg == 1)
+    hipLaunchKernelGGL(psgd_q_kernel<1>, dim3(n_items), dim3(256), lds, s, geom, ptrs, items,
+                       p_hat, q_part);
+  else if (ncg == 2)
+    hipLaunchKernelGGL(psgd_q_kernel<2>, dim3(n_items), dim3(256), lds, s, geom, ptrs, items,
+                       p_hat, q_part);
+  else
+    hipLaunchKernelGGL(psgd_q_kernel<4>, dim3(n_items), dim3(256), lds, s, geom, ptrs, items,
+                       p_hat, q_part);
+}
+
+void launch_psgd_orth(const MatGeom* geom, int n_mats, float* p, float p_div, float eps,
+                      int max_rank, hipStream_t s) {
+  if (n_mats <= 0) return;
+  if (max_rank <= 4)
+    hipLaunchKernelGGL(psgd_orth_kernel<4>, dim3(n_mats), dim3(256), 0, s, geom, p, p_div, eps);
+  else if (max_rank <= 8)
+    hipLaunchKernelGGL(psgd_orth_kernel<8>, dim3(n_mats), dim3(256), 0, s, geom, p, p_div, eps);
+  else if (max_rank <= 16)
+    hipLaunchKernelGGL(psgd_orth_kernel<16>, dim3(n_mats), dim3(256), 0, s, geom, p, p_div,
+                       eps);
+  else if (max_rank <= 32)
+    hipLaunchKernelGGL(psgd_orth_kernel<32>, dim3(n_mats), dim3(256), 0, s, geom, p, p_div,
+                       eps);
+  else
+    hipLaunchKernelGGL(psgd_orth_kernel<64>, dim3(n_mats), dim3(256), 0, s, geom, p, p_div,
+                       eps);
+}
+
+void launch_psgd_update(const MatGeom* geom, const MatPtrs* ptrs, const UItem* items,
+                        int n_items, const float* p_hat, const float* q_sum, float q_div,
+                        float* q_warm, int mode, float lr, float momentum, hipStream_t s) {
+  if (n_items <= 0) return;
+  hipLaunchKernelGGL(psgd_update_kernel, dim3(n_items), dim3(256), 0, s, geom, ptrs, items,
+                     p_hat, q_sum, q_div, q_warm, mode, lr, momentum);
+}
+
+void launch_rank1_step(const float* buf, float div, float* mom, float* x, float* g, int64_t n,
+                       float lr, float momentum, hipStream_t s) {
+  if (n <= 0) return;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(rank1_step_kernel, dim3((unsigned)blocks), dim3(256), 0, s, buf, div, mom,
+                     x, g, n, lr, momentum);
+}
+
+}  // namespace ndp

@@ -1,0 +1,22 @@
+"""Model families: ResNet (torchvision keys), DistilBERT (HF keys), toy MLP."""
+from .distilbert import DistilBertConfig, DistilBertForSequenceClassification, distilbert_base
+from .mlp import ToyMLP
+from .resnet import (BasicBlock, Bottleneck, ResNet, build_resnet, resnet18, resnet34, resnet50,
+                     resnet101, resnet152)
+
+__all__ = [
+    "ResNet", "BasicBlock", "Bottleneck", "build_resnet", "resnet18", "resnet34", "resnet50",
+    "resnet101", "resnet152", "DistilBertConfig", "DistilBertForSequenceClassification",
+    "distilbert_base", "ToyMLP", "build_model",
+]
+
+
+def build_model(name: str, num_classes: int = 1000):
+    name = name.lower()
+    if name.startswith("resnet"):
+        return build_resnet(int(name[len("resnet"):]), num_classes)
+    if name in ("distilbert", "distilbert-base", "distilbert-base-uncased"):
+        return distilbert_base(num_labels=num_classes)
+    if name in ("mlp", "toy_mlp"):
+        return ToyMLP()
+    raise ValueError(f"unknown model {name!r}")

@@ -1,0 +1,183 @@
+"""DistilBERT-base for sequence classification, HF-``state_dict``-compatible.
+
+The reference fine-tunes ``DistilBertForSequenceClassification.from_pretrained(
+'distilbert-base-uncased')`` on IMDb (ddp_powersgd_distillBERT_IMDb/ddp_init.py:150-152).
+There is no network, so weights are random-init (HF init: N(0, 0.02) linear/embedding,
+zero bias, LayerNorm (1, 0)).  Parameter names and registration order equal HF's
+(``distilbert.embeddings.word_embeddings.weight`` ... ``classifier.bias``: 104 tensors,
+66,955,010 parameters for the default config), so the PowerSGD P/Q layout, the byte
+count per step and checkpoints interchange with ``transformers``.
+
+Attention is computed explicitly (QK^T -> mask -> softmax -> PV) on PyTorch-ROCm GEMMs;
+no Triton/AOTriton path is used.
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+__all__ = ["DistilBertConfig", "DistilBertForSequenceClassification", "distilbert_base"]
+
+
+@dataclasses.dataclass
+class DistilBertConfig:
+    vocab_size: int = 30522
+    max_position_embeddings: int = 512
+    dim: int = 768
+    n_layers: int = 6
+    n_heads: int = 12
+    hidden_dim: int = 3072
+    dropout: float = 0.1
+    attention_dropout: float = 0.1
+    seq_classif_dropout: float = 0.2
+    num_labels: int = 2
+    pad_token_id: int = 0
+    initializer_range: float = 0.02
+    layer_norm_eps: float = 1e-12
+
+
+class Embeddings(nn.Module):
+    def __init__(self, c: DistilBertConfig):
+        super().__init__()
+        self.word_embeddings = nn.Embedding(c.vocab_size, c.dim, padding_idx=c.pad_token_id)
+        self.position_embeddings = nn.Embedding(c.max_position_embeddings, c.dim)
+        self.LayerNorm = nn.LayerNorm(c.dim, eps=c.layer_norm_eps)
+        self.dropout = nn.Dropout(c.dropout)
+
+    def forward(self, input_ids):
+        s = input_ids.size(1)
+        pos = torch.arange(s, device=input_ids.device)
+        x = self.word_embeddings(input_ids) + self.position_embeddings(pos)[None]
+        return self.dropout(self.LayerNorm(x))
+
+
+class MultiHeadSelfAttention(nn.Module):
+    def __init__(self, c: DistilBertConfig):
+        super().__init__()
+        self.n_heads = c.n_heads
+        self.dim = c.dim
+        self.q_lin = nn.Linear(c.dim, c.dim)
+        self.k_lin = nn.Linear(c.dim, c.dim)
+        self.v_lin = nn.Linear(c.dim, c.dim)
+        self.out_lin = nn.Linear(c.dim, c.dim)
+        self.dropout = nn.Dropout(c.attention_dropout)
+
+    def forward(self, x, mask: Optional[torch.Tensor]):
+        bs, s, d = x.shape
+        h = self.n_heads
+        dh = d // h
+
+        def split(t):
+            return t.view(bs, s, h, dh).transpose(1, 2)
+
+        q = split(self.q_lin(x)) / math.sqrt(dh)
+        k = split(self.k_lin(x))
+        v = split(self.v_lin(x))
+        scores = torch.matmul(q, k.transpose(-1, -2))
+        if mask is not None:
+            scores = scores.masked_fill((mask == 0).view(bs, 1, 1, s), torch.finfo(scores.dtype).min)
+        w = self.dropout(F.softmax(scores, dim=-1))
+        ctx = torch.matmul(w, v).transpose(1, 2).reshape(bs, s, d)
+        return self.out_lin(ctx)
+
+
+class FFN(nn.Module):
+    def __init__(self, c: DistilBertConfig):
+        super().__init__()
+        self.lin1 = nn.Linear(c.dim, c.hidden_dim)
+        self.lin2 = nn.Linear(c.hidden_dim, c.dim)
+        self.dropout = nn.Dropout(c.dropout)
+
+    def forward(self, x):
+        return self.dropout(self.lin2(F.gelu(self.lin1(x))))
+
+
+class TransformerBlock(nn.Module):
+    def __init__(self, c: DistilBertConfig):
+        super().__init__()
+        self.attention = MultiHeadSelfAttention(c)
+        self.sa_layer_norm = nn.LayerNorm(c.dim, eps=c.layer_norm_eps)
+        self.ffn = FFN(c)
+        self.output_layer_norm = nn.LayerNorm(c.dim, eps=c.layer_norm_eps)
+
+    def forward(self, x, mask):
+        x = self.sa_layer_norm(self.attention(x, mask) + x)
+        return self.output_layer_norm(self.ffn(x) + x)
+
+
+class Transformer(nn.Module):
+    def __init__(self, c: DistilBertConfig):
+        super().__init__()
+        self.layer = nn.ModuleList([TransformerBlock(c) for _ in range(c.n_layers)])
+
+    def forward(self, x, mask):
+        for blk in self.layer:
+            x = blk(x, mask)
+        return x
+
+
+class DistilBertModel(nn.Module):
+    def __init__(self, c: DistilBertConfig):
+        super().__init__()
+        self.embeddings = Embeddings(c)
+        self.transformer = Transformer(c)
+
+    def forward(self, input_ids, attention_mask=None):
+        return self.transformer(self.embeddings(input_ids), attention_mask)
+
+
+class SequenceClassifierOutput(tuple):
+    """``outputs[0]`` is the loss when labels are given (ddp_init.py:189-191 indexing)."""
+
+    @property
+    def loss(self):
+        return self[0] if len(self) == 2 else None
+
+    @property
+    def logits(self):
+        return self[-1]
+
+
+class DistilBertForSequenceClassification(nn.Module):
+    def __init__(self, config: Optional[DistilBertConfig] = None):
+        super().__init__()
+        c = config or DistilBertConfig()
+        self.config = c
+        self.distilbert = DistilBertModel(c)
+        self.pre_classifier = nn.Linear(c.dim, c.dim)
+        self.classifier = nn.Linear(c.dim, c.num_labels)
+        self.dropout = nn.Dropout(c.seq_classif_dropout)
+        self.apply(self._init)
+
+    def _init(self, m):
+        std = self.config.initializer_range
+        if isinstance(m, nn.Linear):
+            nn.init.normal_(m.weight, 0.0, std)
+            if m.bias is not None:
+                nn.init.zeros_(m.bias)
+        elif isinstance(m, nn.Embedding):
+            nn.init.normal_(m.weight, 0.0, std)
+            if m.padding_idx is not None:
+                with torch.no_grad():
+                    m.weight[m.padding_idx].zero_()
+        elif isinstance(m, nn.LayerNorm):
+            nn.init.ones_(m.weight)
+            nn.init.zeros_(m.bias)
+
+    def forward(self, input_ids, attention_mask=None, labels=None):
+        hidden = self.distilbert(input_ids, attention_mask)
+        pooled = self.dropout(F.relu(self.pre_classifier(hidden[:, 0])))
+        logits = self.classifier(pooled)
+        if labels is not None:
+            loss = F.cross_entropy(logits.view(-1, self.config.num_labels), labels.view(-1))
+            return SequenceClassifierOutput((loss, logits))
+        return SequenceClassifierOutput((logits,))
+
+
+def distilbert_base(num_labels: int = 2, **overrides) -> DistilBertForSequenceClassification:
+    return DistilBertForSequenceClassification(DistilBertConfig(num_labels=num_labels, **overrides))

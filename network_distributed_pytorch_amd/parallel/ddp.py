@@ -1,0 +1,137 @@
+"""Dense data parallelism: the reference's blocking per-parameter arm and a bucketed,
+backward-overlapped MI355X arm.
+
+* :func:`average_gradients` — reference semantics (ddp_guide_cifar10/ddp_init.py:57-62):
+  one blocking SUM all-reduce per parameter followed by ``grad /= world_size``.
+* :class:`BucketedDataParallel` — gradients live in ONE flat arena laid out in reverse
+  parameter order (≈ backward production order) and cut into contiguous buckets
+  (default 25 MB: few, large RCCL all-reduces that saturate a ring over the 7 xGMI
+  links).  A post-accumulate-grad hook launches each bucket's async all-reduce as soon
+  as its last gradient lands, so communication overlaps the rest of backward; ``step()``
+  waits and runs ONE fused gfx950 SGD-momentum kernel over the arena with the ``/N``
+  mean folded in (the reference's ``grad /= N`` + ``optim.SGD.step``).
+  Parameters are broadcast from rank 0 at construction (quirk Q4 fixed).
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+
+from ..ops import sgd_momentum_
+from .comm import Communicator, all_reduce, world_size
+
+__all__ = ["average_gradients", "BucketedDataParallel"]
+
+
+def average_gradients(model: torch.nn.Module, comm: Optional[Communicator] = None) -> int:
+    """Blocking per-parameter SUM all-reduce then ``/= N`` (ddp_init.py:57-62). Returns bits."""
+    bits = 0
+    size = float(comm.world_size if comm is not None else world_size())
+    for p in model.parameters():
+        if p.grad is None:
+            continue
+        if comm is not None:
+            comm.all_reduce(p.grad.data)
+        else:
+            all_reduce(p.grad.data)
+        p.grad.data /= size
+        bits += 8 * p.grad.numel() * p.grad.element_size()
+    return bits
+
+
+class BucketedDataParallel:
+    def __init__(self, model: torch.nn.Module, comm: Optional[Communicator] = None, lr: float = 1e-3,
+                 momentum: float = 0.9, bucket_mb: float = 25.0, broadcast_params: bool = True,
+                 overlap: bool = True):
+        self.model = model
+        self.comm = comm if comm is not None else Communicator()
+        self.lr = float(lr)
+        self.momentum = float(momentum)
+        self.params: List[torch.nn.Parameter] = [p for p in model.parameters() if p.requires_grad]
+        self.device = self.params[0].device
+        order = list(reversed(self.params))
+        offs, o = {}, 0
+        for p in order:
+            offs[id(p)] = o
+            o += (p.numel() + 15) // 16 * 16
+        self.numel = o
+        f32 = dict(dtype=torch.float32, device=self.device)
+        self.x = torch.zeros(o, **f32)
+        self.g = torch.zeros(o, **f32)
+        self.buf = torch.zeros(o, **f32)
+        with torch.no_grad():
+            for p in self.params:
+                s = offs[id(p)]
+                v = self.x[s: s + p.numel()].view_as(p)
+                v.copy_(p.data)
+                p.data = v
+                p.grad = self.g[s: s + p.numel()].view_as(p)
+        if broadcast_params:
+            self.comm.broadcast(self.x, src=0)
+        # buckets: contiguous arena ranges in backward order
+        cap = max(1, int(bucket_mb * 1024 * 1024 / 4))
+        self.buckets = []  # (start, end, n_params)
+        self.bucket_of = {}
+        start, cnt, cur_end = 0, 0, 0
+        for p in order:
+            s = offs[id(p)]
+            e = s + (p.numel() + 15) // 16 * 16
+            if cnt and e - start > cap:
+                self.buckets.append([start, cur_end, cnt])
+                start, cnt = s, 0
+            self.bucket_of[id(p)] = len(self.buckets)
+            cnt += 1
+            cur_end = e
+        if cnt:
+            self.buckets.append([start, cur_end, cnt])
+        self._ready = [0] * len(self.buckets)
+        self._works = [None] * len(self.buckets)
+        self.overlap = overlap and self.comm.world_size > 1
+        self._hooks = []
+        if self.overlap:
+            for p in self.params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+
+    @property
+    def bytes_per_step(self) -> int:
+        return 4 * sum(p.numel() for p in self.params)
+
+    @property
+    def collectives_per_step(self) -> int:
+        return len(self.buckets) if self.comm.world_size > 1 else 0
+
+    def _launch(self, b: int):
+        s, e, _ = self.buckets[b]
+        self._works[b] = self.comm.all_reduce(self.g[s:e], async_op=True)
+
+    def _on_grad(self, p):
+        b = self.bucket_of[id(p)]
+        self._ready[b] += 1
+        if self._ready[b] == self.buckets[b][2] and self._works[b] is None:
+            self._launch(b)
+
+    def zero_grad(self, set_to_none: bool = False):
+        self.g.zero_()
+        self._ready = [0] * len(self.buckets)
+        self._works = [None] * len(self.buckets)
+
+    @torch.no_grad()
+    def step(self) -> int:
+        n = self.comm.world_size
+        if n > 1:
+            for b in range(len(self.buckets)):
+                if self._works[b] is None:  # unused params / overlap disabled
+                    self._launch(b)
+            for w in self._works:
+                w.wait()
+        sgd_momentum_(self.x, self.g, self.buf, self.lr, self.momentum, float(n))
+        return 8 * self.bytes_per_step
+
+    def state_dict(self):
+        return {"momentum_buffer": self.buf.detach().cpu().clone(), "lr": self.lr, "momentum": self.momentum}
+
+    def load_state_dict(self, sd):
+        self.buf.copy_(sd["momentum_buffer"])
+        self.lr = float(sd["lr"])
+        self.momentum = float(sd["momentum"])

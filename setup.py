@@ -1,0 +1,34 @@
+"""Build the in-tree gfx950 extension:  python setup.py build_ext --inplace
+
+Kernels (*.hip) are compiled by hipcc for gfx950 only; the host plan builder and the
+pybind11 bindings by the host compiler.  The resulting
+network_distributed_pytorch_amd/_C*.so stays in the source tree (it travels to the GPU
+box with the snapshot; nothing is installed into site-packages).
+"""
+import os
+
+from setuptools import find_packages, setup
+from torch.utils.cpp_extension import BuildExtension, CUDAExtension
+
+os.environ.setdefault("PYTORCH_ROCM_ARCH", "gfx950")
+
+CSRC = os.path.join("network_distributed_pytorch_amd", "csrc")
+SOURCES = [os.path.join(CSRC, f) for f in ("bindings.cpp", "plan.cpp", "powersgd.hip", "multitensor.hip")]
+
+ext = CUDAExtension(
+    name="network_distributed_pytorch_amd._C",
+    sources=SOURCES,
+    include_dirs=[os.path.abspath(CSRC)],
+    extra_compile_args={
+        "cxx": ["-O3", "-std=c++17"],
+        "nvcc": ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=fast"],
+    },
+)
+
+setup(
+    name="network_distributed_pytorch_amd",
+    version="0.1.0",
+    packages=find_packages(include=["network_distributed_pytorch_amd", "network_distributed_pytorch_amd.*"]),
+    ext_modules=[ext],
+    cmdclass={"build_ext": BuildExtension.with_options(use_ninja=True)},
+)
