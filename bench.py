@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--link", default="none", help="none|1g|10g|100g link emulation")
     ap.add_argument("--bucket-mb", type=float, default=25.0)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--graph-mode", default="auto", choices=["auto", "full", "piecewise", "none"],
+                    help="hipGraph capture of the step: full (N=1 default), piecewise (collectives "
+                         "eager between captured compute; N>1 default), none")
     return ap.parse_args()
 
 
@@ -59,10 +62,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; NDP_BACKEND=gloo lets several ranks share one GPU (testing only)
+    backend = os.environ.get("NDP_BACKEND", "nccl")
+    dev_index = local % max(1, torch.cuda.device_count())
+    device = torch.device("cuda", dev_index)
+    torch.cuda.set_device(device)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
     torch.manual_seed(714)
     torch.backends.cudnn.benchmark = True
 
@@ -86,13 +95,40 @@ def main():
 
     loss_acc = torch.zeros((), device=device)
 
-    def step(i):
-        sync.zero_grad()
-        out = model(xs[i % n_pool])
-        loss = crit(out, ys[i % n_pool])
-        loss.backward()
-        sync.step()
-        loss_acc.add_(loss.detach())
+    graph_mode = args.graph_mode
+    if graph_mode == "auto" and "ref" in args.reducer:
+        graph_mode = "none"  # reference-semantics arms are eager by definition
+    if graph_mode != "none":
+        from network_distributed_pytorch_amd.utils.graph import StepRunner
+
+        x_static = xs[0].clone()
+        y_static = ys[0].clone()
+        loss_static = torch.zeros((), device=device)
+
+        def pre():
+            sync.zero_grad()
+            loss = crit(model(x_static), y_static)
+            loss.backward()
+            loss_static.copy_(loss.detach())
+
+        def post():
+            loss_acc.add_(loss_static)
+
+        runner = StepRunner(pre, sync, mode=graph_mode, warmup=3, post=post)
+        graph_mode = runner.mode
+
+        def step(i):
+            x_static.copy_(xs[i % n_pool], non_blocking=True)
+            y_static.copy_(ys[i % n_pool], non_blocking=True)
+            runner()
+    else:
+        def step(i):
+            sync.zero_grad()
+            out = model(xs[i % n_pool])
+            loss = crit(out, ys[i % n_pool])
+            loss.backward()
+            sync.step()
+            loss_acc.add_(loss.detach())
 
     for i in range(args.warmup):
         step(i)
@@ -143,6 +179,7 @@ def main():
                 "powersgd_rank": args.rank if "powersgd" in args.reducer else None,
                 "link_emulation": args.link,
                 "channels_last": args.channels_last,
+                "hip_graph": graph_mode,
             },
             "mean_loss": round(final_loss, 5),
         }

@@ -207,7 +207,8 @@ void rank1_step(torch::Tensor buf, double div, torch::Tensor mom, torch::Tensor 
 
 void seg_reduce(torch::Tensor entries, torch::Tensor prefix, int64_t n_entries, int64_t n_blocks) {
   check_dev(entries, "entries"); check_dev(prefix, "prefix");
-  TORCH_CHECK(entries.numel() == n_entries * (int64_t)sizeof(SegEntry), "seg table size mismatch");
+  TORCH_CHECK(entries.numel() >= n_entries * (int64_t)sizeof(SegEntry) && prefix.numel() >= n_entries,
+              "seg table size mismatch");
   ndp::launch_seg_reduce(reinterpret_cast<const SegEntry*>(entries.data_ptr()),
                          prefix.data_ptr<int64_t>(), (int)n_entries, n_blocks, cur_stream());
   check_launch("launch_seg_reduce");

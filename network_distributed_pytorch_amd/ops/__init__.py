@@ -21,6 +21,9 @@ __all__ = [
     "seg_copy",
     "delay_ns",
     "checksum",
+    "capturing",
+    "upload",
+    "SegPlan",
 ]
 
 
@@ -53,31 +56,112 @@ def seg_copy(specs: Sequence[tuple], device: torch.device) -> "SegPlan":
     return SegPlan(specs, device)
 
 
+class _PinnedPool:
+    """Bump allocator over one pinned host buffer, reserved before any graph capture.
+
+    Pinned allocation is not permitted while a stream is capturing, so capture-time table
+    uploads take never-reused slices of this pool (the graph's memcpy nodes read them on
+    every replay).
+    """
+
+    def __init__(self):
+        self.buf = None
+        self.off = 0
+
+    def reserve(self, nbytes: int = 16 << 20):
+        if self.buf is None and torch.cuda.is_available():
+            self.buf = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+
+    def take(self, nbytes: int) -> torch.Tensor:
+        assert self.buf is not None, "pinned pool not reserved before capture"
+        start = (self.off + 255) // 256 * 256
+        assert start + nbytes <= self.buf.numel(), "pinned upload pool exhausted"
+        self.off = start + nbytes
+        return self.buf[start: start + nbytes]
+
+
+_PINNED = _PinnedPool()
+
+
+def capturing() -> bool:
+    """True while the current HIP stream is being captured into a graph."""
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
+def upload(dev: torch.Tensor, host: torch.Tensor) -> None:
+    """Copy a small host table into a preallocated device buffer, hipGraph-capture safe.
+
+    Outside capture: an ordinary (synchronous) copy.  Inside capture: the bytes go to a
+    never-reused slice of a pre-reserved pinned pool and the copy becomes an async memcpy
+    node, so every replay re-uploads exactly the capture-time table.
+    """
+    n = host.numel()
+    assert dev.numel() >= n and dev.dtype == host.dtype
+    if n == 0:
+        return
+    if dev.is_cuda and capturing():
+        nbytes = n * host.element_size()
+        pinned = _PINNED.take(nbytes).view(host.dtype)
+        pinned.copy_(host.reshape(-1))
+        dev[:n].copy_(pinned, non_blocking=True)
+    else:
+        if dev.is_cuda:
+            _PINNED.reserve()
+        dev[:n].copy_(host)
+
+
 class SegPlan:
     """One-launch multi-tensor reduce-copy: ``dst_i = (sum_c src_i[c*stride_i:]) / div_i``.
 
     ``specs`` = list of (src_tensor, dst_tensor, chunks, stride, div); src/dst are flat
-    float32 tensors (views are fine).  On device the table is uploaded once and the whole
-    list is ONE kernel launch; the tensors must stay alive and keep their storage.
+    float32 tensors (views are fine).  On device the table lives in a device buffer and the
+    whole list is ONE kernel launch.  :meth:`set` re-targets the plan at new tensors (the
+    table is only re-uploaded when an address changed; capture-safe via :func:`upload`).
     """
 
-    def __init__(self, specs: Sequence[tuple], device: torch.device):
-        self.specs = list(specs)
+    def __init__(self, specs: Sequence[tuple] = (), device: torch.device = "cpu", capacity: int = 0):
         self.device = torch.device(device)
-        self._dev = None
-        if self.device.type == "cuda" and self.specs:
-            rows = []
-            for src, dst, chunks, stride, div in self.specs:
-                rows.append((src.data_ptr(), dst.data_ptr(), dst.numel(), int(stride), int(chunks), float(div)))
-            ent, prefix, n_ent, n_blocks = ext().make_seg_table(rows)
-            self._dev = (ent.to(self.device), prefix.to(self.device), int(n_ent), int(n_blocks))
+        self.specs: list = []
+        self._key = None
+        self._ent = None
+        self._prefix = None
+        self._n_ent = 0
+        self._n_blocks = 0
+        self._cap = 0
+        if self.device.type == "cuda":
+            self._reserve(max(capacity, len(specs), 1))
+        self.set(specs)
+
+    def _reserve(self, n_entries: int):
+        X = ext()
+        self._cap = n_entries
+        self._ent = torch.empty(n_entries * X.SIZEOF_SEGENTRY, dtype=torch.uint8, device=self.device)
+        self._prefix = torch.empty(n_entries, dtype=torch.int64, device=self.device)
+
+    def set(self, specs: Sequence[tuple]) -> None:
+        specs = list(specs)
+        key = tuple((s.data_ptr(), d.data_ptr(), d.numel(), int(c), int(st), float(dv)) for s, d, c, st, dv in specs)
+        self.specs = specs
+        if key == self._key:
+            return
+        self._key = key
+        if self.device.type != "cuda" or not specs:
+            return
+        rows = [(a, b, n, st, c, dv) for a, b, n, c, st, dv in key]
+        ent, prefix, n_ent, n_blocks = ext().make_seg_table(rows)
+        if n_ent > self._cap:
+            assert not capturing(), "SegPlan must be sized before graph capture"
+            self._reserve(max(n_ent, 2 * self._cap))
+        upload(self._ent, ent.to(self._ent.dtype) if ent.dtype != torch.uint8 else ent)
+        upload(self._prefix, prefix)
+        self._n_ent, self._n_blocks = int(n_ent), int(n_blocks)
 
     def run(self) -> None:
         if not self.specs:
             return
-        if self._dev is not None:
-            ent, prefix, n_ent, n_blocks = self._dev
-            ext().seg_reduce(ent, prefix, n_ent, n_blocks)
+        if self.device.type == "cuda":
+            if self._n_ent:
+                ext().seg_reduce(self._ent, self._prefix, self._n_ent, self._n_blocks)
             return
         for src, dst, chunks, stride, div in self.specs:
             n = dst.numel()

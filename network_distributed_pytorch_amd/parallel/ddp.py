@@ -18,7 +18,7 @@ from typing import List, Optional
 
 import torch
 
-from ..ops import sgd_momentum_
+from ..ops import SegPlan, capturing, sgd_momentum_
 from .comm import Communicator, all_reduce, world_size
 
 __all__ = ["average_gradients", "BucketedDataParallel"]
@@ -56,6 +56,7 @@ class BucketedDataParallel:
             offs[id(p)] = o
             o += (p.numel() + 15) // 16 * 16
         self.numel = o
+        self.offsets = offs
         f32 = dict(dtype=torch.float32, device=self.device)
         self.x = torch.zeros(o, **f32)
         self.g = torch.zeros(o, **f32)
@@ -66,32 +67,35 @@ class BucketedDataParallel:
                 v = self.x[s: s + p.numel()].view_as(p)
                 v.copy_(p.data)
                 p.data = v
-                p.grad = self.g[s: s + p.numel()].view_as(p)
+                p.grad = None
         if broadcast_params:
             self.comm.broadcast(self.x, src=0)
         # buckets: contiguous arena ranges in backward order
         cap = max(1, int(bucket_mb * 1024 * 1024 / 4))
-        self.buckets = []  # (start, end, n_params)
+        self.buckets = []  # [start, end, [params]]
         self.bucket_of = {}
-        start, cnt, cur_end = 0, 0, 0
+        cur, start, cur_end = [], 0, 0
         for p in order:
             s = offs[id(p)]
             e = s + (p.numel() + 15) // 16 * 16
-            if cnt and e - start > cap:
-                self.buckets.append([start, cur_end, cnt])
-                start, cnt = s, 0
+            if cur and e - start > cap:
+                self.buckets.append([start, cur_end, cur])
+                start, cur = s, []
             self.bucket_of[id(p)] = len(self.buckets)
-            cnt += 1
+            cur.append(p)
             cur_end = e
-        if cnt:
-            self.buckets.append([start, cur_end, cnt])
+        if cur:
+            self.buckets.append([start, cur_end, cur])
+        self._segs = [SegPlan([], self.device, capacity=len(b[2])) for b in self.buckets]
         self._ready = [0] * len(self.buckets)
         self._works = [None] * len(self.buckets)
+        self._launched = [False] * len(self.buckets)
         self.overlap = overlap and self.comm.world_size > 1
         self._hooks = []
         if self.overlap:
             for p in self.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+        self.step_count = 0
 
     @property
     def bytes_per_step(self) -> int:
@@ -101,32 +105,83 @@ class BucketedDataParallel:
     def collectives_per_step(self) -> int:
         return len(self.buckets) if self.comm.world_size > 1 else 0
 
-    def _launch(self, b: int):
+    def _flatten(self, b: int):
+        _, _, ps = self.buckets[b]
+        specs = []
+        for p in ps:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            o = self.offsets[id(p)]
+            specs.append((p.grad.reshape(-1), self.g[o: o + p.numel()], 1, 0, 1.0))
+        seg = self._segs[b]
+        seg.set(specs)
+        seg.run()                      # one flatten launch per bucket
+
+    def _allreduce(self, b: int):
         s, e, _ = self.buckets[b]
-        self._works[b] = self.comm.all_reduce(self.g[s:e], async_op=True)
+        if self.comm.world_size > 1:
+            self._works[b] = self.comm.all_reduce(self.g[s:e], async_op=True)
+
+    def _launch(self, b: int):
+        self._flatten(b)
+        self._allreduce(b)
+        self._launched[b] = True
 
     def _on_grad(self, p):
+        if not self.overlap:
+            return
         b = self.bucket_of[id(p)]
         self._ready[b] += 1
-        if self._ready[b] == self.buckets[b][2] and self._works[b] is None:
+        if self._ready[b] == len(self.buckets[b][2]) and not self._launched[b]:
             self._launch(b)
 
-    def zero_grad(self, set_to_none: bool = False):
-        self.g.zero_()
+    # -- piecewise-graph phases (collectives run eagerly between captured phases) -----------
+    @torch.no_grad()
+    def phase_flatten(self):
+        for b in range(len(self.buckets)):
+            self._flatten(b)
+
+    @torch.no_grad()
+    def comm_buckets(self):
+        for b in range(len(self.buckets)):
+            self._allreduce(b)
+        for b, w in enumerate(self._works):
+            if w is not None:
+                w.wait()
+            self._works[b] = None
+
+    @torch.no_grad()
+    def phase_sgd(self):
+        sgd_momentum_(self.x, self.g, self.buf, self.lr, self.momentum, float(self.comm.world_size))
+        self.count_step()
+
+    def phases(self):
+        self.overlap = False  # hooks must not launch collectives inside a captured backward
+        return [(self.phase_flatten, False), (self.comm_buckets, True), (self.phase_sgd, False)]
+
+    def zero_grad(self, set_to_none: bool = True):
+        for p in self.params:
+            p.grad = None
         self._ready = [0] * len(self.buckets)
         self._works = [None] * len(self.buckets)
+        self._launched = [False] * len(self.buckets)
 
     @torch.no_grad()
     def step(self) -> int:
         n = self.comm.world_size
-        if n > 1:
-            for b in range(len(self.buckets)):
-                if self._works[b] is None:  # unused params / overlap disabled
-                    self._launch(b)
-            for w in self._works:
+        for b in range(len(self.buckets)):
+            if not self._launched[b]:  # overlap disabled / unused params
+                self._launch(b)
+        for w in self._works:
+            if w is not None:
                 w.wait()
         sgd_momentum_(self.x, self.g, self.buf, self.lr, self.momentum, float(n))
+        self.count_step()
         return 8 * self.bytes_per_step
+
+    def count_step(self):
+        if not capturing():
+            self.step_count += 1
 
     def state_dict(self):
         return {"momentum_buffer": self.buf.detach().cpu().clone(), "lr": self.lr, "momentum": self.momentum}

@@ -36,7 +36,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from ..ops import SegPlan, ext
+from ..ops import SegPlan, capturing, ext, upload
 from .comm import Communicator, n_bits
 
 __all__ = [
@@ -154,8 +154,10 @@ class _PlanBuffers:
             self.pp_offs, self.qp_offs = d["pp_offs"], d["qp_offs"]
             self.p_chunks, self.q_chunks = d["p_chunks"], d["q_chunks"]
             self.counts = {k: d[k] for k in ("n_p_items", "n_q_items", "n_u_items", "pp_total", "qp_total")}
-            self.geom = None
-            self.ptrs = None
+            nb = max(1, len(shapes)) * X.SIZEOF_MATGEOM
+            self.geom = torch.zeros(nb, dtype=torch.uint8, device=device)
+            self.ptrs = torch.zeros(nb, dtype=torch.uint8, device=device)
+            self._bind_key = None
             self.q_seg = SegPlan(
                 [(self.q_part[o:], self.q_memory[qo: qo + m * r], c, m * r, 1.0)
                  for (n, m), r, o, qo, c in zip(shapes, self.ranks, self.qp_offs, self.q_offs, self.q_chunks)],
@@ -165,10 +167,16 @@ class _PlanBuffers:
         return [(self.p_part[o:], self.p_memory[po: po + n * r], c, n * r, 1.0)
                 for (n, m), r, o, po, c in zip(self.shapes, self.ranks, self.pp_offs, self.p_offs, self.p_chunks)]
 
-    def bind(self, rows: List[List[int]], vec: List[int]):
+    def bind(self, rows: List[List[int]], vec: List[int]) -> bool:
+        """Point the grouped kernels at new tensors; returns True if the tables changed."""
+        key = (tuple(map(tuple, rows)), tuple(vec))
+        if key == self._bind_key:
+            return False
         X = ext()
-        self.geom = X.patch_geom_vec(self._geom_host, vec).to(self.device)
-        self.ptrs = X.make_mat_ptrs(rows).to(self.device)
+        upload(self.geom, X.patch_geom_vec(self._geom_host, vec))
+        upload(self.ptrs, X.make_mat_ptrs(rows))
+        self._bind_key = key
+        return True
 
     def p_view(self, i):
         n, _ = self.shapes[i]
@@ -198,6 +206,8 @@ class PowerSGDReducer(Reducer):
         self.p_memory = None
         self.q_memory = None
         self._bind_key = None
+        self._p_seg = None
+        self._r1_unpack = None
 
     def _set_random(self, q: torch.Tensor):
         # reducer.py:36-38 with a private generator (quirk Q1): same seed stream, same values
@@ -255,13 +265,17 @@ class PowerSGDReducer(Reducer):
         for t, _, _ in rank1:
             specs.append((t.reshape(-1), B.rank1_buf[off: off + t.numel()], 1, 0, 1.0))
             off += t.numel()
-        self._p_seg = SegPlan(specs, B.device)
         off = 0
         unpack = []
         for _, o, _ in rank1:
             unpack.append((B.rank1_buf[off: off + o.numel()], o.view(-1), 1, 0, float(self.n_workers)))
             off += o.numel()
-        self._r1_unpack = SegPlan(unpack, B.device)
+        if self._p_seg is None:
+            self._p_seg = SegPlan(specs, B.device)
+            self._r1_unpack = SegPlan(unpack, B.device)
+        else:
+            self._p_seg.set(specs)
+            self._r1_unpack.set(unpack)
         self._bind_key = key
 
     def _reduce_native(self, high, rank1, N):
@@ -310,12 +324,15 @@ class PowerSGDReducer(Reducer):
 
 
 class PowerSGDOptimizer:
-    """Fused EF-SGD-with-momentum PowerSGD step over flat arenas (ddp_init.py:121-178).
+    """Fused EF-SGD-with-momentum PowerSGD step (ddp_init.py:121-178) over flat arenas.
 
-    Parameters are re-pointed into a flat parameter arena and their ``.grad`` into a flat
-    gradient arena (every high-rank slot 64-B aligned, the <=1-D group contiguous at the
-    end), so autograd accumulates straight into the arena and one ``zero_grad()`` memset
-    clears everything.  ``step()`` returns the bits communicated (reducer.py:170).
+    Parameters are re-pointed into a flat parameter arena ``x`` (every high-rank slot 64-B
+    aligned, the <=1-D group contiguous at the end) with matching error-memory ``e`` and
+    momentum ``m`` arenas.  Gradients stay wherever autograd produced them (no in-place
+    accumulation into a preset ``.grad`` — that costs one extra add kernel per parameter);
+    the grouped kernels reach them through a device pointer table that is re-uploaded only
+    when an address changes (hipGraph-capture safe).  ``step()`` returns the bits
+    communicated (reducer.py:170).
 
     ``write_grad=True`` also leaves ``p.grad = out + m`` exactly like the reference loop
     (ddp_init.py:172); it costs one extra write pass and is off by default.
@@ -360,7 +377,6 @@ class PowerSGDOptimizer:
         self.arena_numel = o
         f32 = dict(dtype=torch.float32, device=self.device)
         self.x = torch.zeros(o, **f32)
-        self.g = torch.zeros(o, **f32)
         self.e = torch.zeros(o, **f32)
         self.m = torch.zeros(o, **f32)
         self.offsets = offs
@@ -370,36 +386,66 @@ class PowerSGDOptimizer:
                 view = self.x[s: s + p.numel()].view_as(p)
                 view.copy_(p.data)
                 p.data = view
-                p.grad = self.g[s: s + p.numel()].view_as(p)
+                p.grad = None
         if broadcast_params:  # quirks Q3/Q4: replicas start identical (one flat broadcast)
             self.comm.broadcast(self.x, src=0)
 
         shapes = [(p.shape[0], p.numel() // p.shape[0]) for p in hi]
         self.r1_numel = o - self.r1_start
+        self.r1_upd = torch.zeros(self.r1_numel if write_grad else 0, **f32)
         self.buf = _PlanBuffers(shapes, self.rank, self.r1_numel, self.device, native=native is not False)
-        B = self.buf
-        self.native = B.native
-        if self.native:
-            rows, vec = [], []
-            for p, (n, m) in zip(hi, shapes):
-                s = offs[id(p)]
-                g, e, mo, x = (t[s:].data_ptr() for t in (self.g, self.e, self.m, self.x))
-                row = [g, e, e, 0, 0, mo, x, g]
-                rows.append(row)
-                vec.append(_vec_ok(m, row))
-            B.bind(rows, vec)
-            specs = B.p_seg_specs()
-            if self.r1_numel:
-                specs.append((self.g[self.r1_start:], B.rank1_buf, 1, 0, 1.0))
-            self._p_seg = SegPlan(specs, self.device)
+        self.native = self.buf.native
+        self._p_seg = SegPlan([], self.device, capacity=len(shapes) + len(r1) + 1) if self.native else None
+        self._r1_out = SegPlan([], self.device, capacity=len(r1) + 1) if self.native else None
+        self._grad_key = None
 
     # -- helpers -------------------------------------------------------------------------
-    def zero_grad(self, set_to_none: bool = False):
-        self.g.zero_()
+    def zero_grad(self, set_to_none: bool = True):
+        for p in self.params:
+            if set_to_none:
+                p.grad = None
+            elif p.grad is not None:
+                p.grad.zero_()
 
     def _view(self, t, p):
         s = self.offsets[id(p)]
         return t[s: s + p.numel()]
+
+    def _grads(self):
+        gs = []
+        for p in self.params:
+            if p.grad is None:  # parameter unused this step: zero gradient
+                p.grad = torch.zeros_like(p)
+            g = p.grad
+            assert g.is_contiguous() and g.dtype == torch.float32, "PowerSGD needs dense fp32 grads"
+            gs.append(g)
+        return gs
+
+    def _bind(self):
+        gmap = {id(p): p.grad for p in self.params}
+        key = tuple(g.data_ptr() for g in gmap.values())
+        if key == self._grad_key:
+            return
+        B = self.buf
+        rows, vec = [], []
+        for p, (n, m) in zip(self.high, B.shapes):
+            s = self.offsets[id(p)]
+            g = gmap[id(p)].data_ptr()
+            e, mo, x = (t[s:].data_ptr() for t in (self.e, self.m, self.x))
+            row = [g, e, e, 0, 0, mo, x, g]
+            rows.append(row)
+            vec.append(_vec_ok(m, row))
+        B.bind(rows, vec)
+        specs = B.p_seg_specs()
+        outs = []
+        for p in self.rank1:
+            s = self.offsets[id(p)] - self.r1_start
+            specs.append((gmap[id(p)].view(-1), B.rank1_buf[s: s + p.numel()], 1, 0, 1.0))
+            if self.write_grad:
+                outs.append((self.r1_upd[s: s + p.numel()], gmap[id(p)].view(-1), 1, 0, 1.0))
+        self._p_seg.set(specs)
+        self._r1_out.set(outs)
+        self._grad_key = key
 
     def _init_queries(self):
         B = self.buf
@@ -415,49 +461,97 @@ class PowerSGDOptimizer:
         return 32 * (B.p_total + B.r1_numel + B.q_total)
 
     # -- the step --------------------------------------------------------------------------
+    # step() = phase_p -> comm_p -> phase_q -> comm_q -> phase_update.  The phases are
+    # exposed separately so a piecewise hipGraph can capture the compute phases and run
+    # the two collectives eagerly in between (utils/graph.py).
     @torch.no_grad()
-    def step(self) -> int:
+    def phase_p(self):
         B = self.buf
         if self.step_count == 0 or not self.reuse_query:
+            assert not capturing(), \
+                "run one eager step before capturing; reuse_query=False is not graph-capturable"
             self._init_queries()
+        self._grads()
+        if not self.native:
+            return
+        self._bind()
+        if B.shapes:
+            ext().psgd_p(B.geom, B.ptrs, B.p_items, B.q_warm, B.p_part, True, B.max_rank)
+        self._p_seg.run()                                      # P split-K sum + rank-1 pack
+
+    @torch.no_grad()
+    def comm_p(self):
+        if self.native:
+            self.comm.all_reduce(self.buf.comm_buf)            # [P | rank-1]: one collective
+
+    @torch.no_grad()
+    def phase_q(self):
+        B = self.buf
+        if self.native and B.shapes:
+            X = ext()
+            X.psgd_orth(B.geom, B.comm_buf, float(self.comm.world_size), self.eps, B.max_rank)
+            X.psgd_q(B.geom, B.ptrs, B.q_items, B.comm_buf, B.q_part, B.max_rank)
+            B.q_seg.run()
+
+    @torch.no_grad()
+    def comm_q(self):
+        if self.native and self.buf.shapes:
+            self.comm.all_reduce(self.buf.q_memory)
+
+    @torch.no_grad()
+    def phase_update(self):
+        B = self.buf
         N = self.comm.world_size
         if self.native:
             X = ext()
             if B.shapes:
-                X.psgd_p(B.geom, B.ptrs, B.p_items, B.q_warm, B.p_part, True, B.max_rank)
-            self._p_seg.run()
-            self.comm.all_reduce(B.comm_buf)
-            if B.shapes:
-                X.psgd_orth(B.geom, B.comm_buf, float(N), self.eps, B.max_rank)
-                X.psgd_q(B.geom, B.ptrs, B.q_items, B.comm_buf, B.q_part, B.max_rank)
-                B.q_seg.run()
-                self.comm.all_reduce(B.q_memory)
                 X.psgd_update(B.geom, B.ptrs, B.u_items, B.comm_buf, B.q_memory, float(N), B.q_warm,
                               2 if self.write_grad else 1, self.lr, self.momentum)
             if self.r1_numel:
                 r1 = slice(self.r1_start, self.arena_numel)
                 X.rank1_step(B.rank1_buf, float(N), self.m[r1], self.x[r1],
-                             self.g[r1] if self.write_grad else None, self.lr, self.momentum)
+                             self.r1_upd if self.write_grad else None, self.lr, self.momentum)
+                if self.write_grad:
+                    self._r1_out.run()
         else:
-            self._step_torch(N)
-        self.step_count += 1
-        bits = self.bits_per_step
-        self.bits_communicated += bits
-        return bits
+            self._step_torch(N, [p.grad for p in self.params])
+        self.count_step()
 
-    def _step_torch(self, N):
+    def count_step(self):
+        """Host-side bookkeeping of one step (graph replays call this explicitly)."""
+        if capturing():  # the capture pass is not a real step
+            return
+        self.step_count += 1
+        self.bits_communicated += self.bits_per_step
+
+    def step(self) -> int:
+        self.phase_p()
+        self.comm_p()
+        self.phase_q()
+        self.comm_q()
+        self.phase_update()
+        return self.bits_per_step
+
+    def phases(self):
+        """[(fn, is_collective)] in execution order (for piecewise graph capture)."""
+        return [(self.phase_p, False), (self.comm_p, True), (self.phase_q, False), (self.comm_q, True),
+                (self.phase_update, False)]
+
+    def _step_torch(self, N, grads):
         B = self.buf
         lam, lr = self.momentum, self.lr
+        gmap = {id(p): g for p, g in zip(self.params, grads)}
         Ms = []
         for i, p in enumerate(self.high):
             n, m = B.shapes[i]
             e = self._view(self.e, p)
-            e.add_(self._view(self.g, p))               # M = g + e (stored in e)
+            e.add_(gmap[id(p)].reshape(-1))              # M = g + e (stored in e)
             M = e.view(n, m)
             Ms.append(M)
             torch.matmul(M, B.q_view(i), out=B.p_view(i))
-        if self.r1_numel:
-            B.rank1_buf.copy_(self.g[self.r1_start:])
+        for p in self.rank1:
+            s = self.offsets[id(p)] - self.r1_start
+            B.rank1_buf[s: s + p.numel()].copy_(gmap[id(p)].reshape(-1))
         self.comm.all_reduce(B.comm_buf)
         B.p_memory.div_(N)
         for i in range(len(self.high)):
@@ -475,7 +569,7 @@ class PowerSGDOptimizer:
             upd = out + mom
             self._view(self.x, p).add_(upd, alpha=-lr)
             if self.write_grad:
-                self._view(self.g, p).copy_(upd)
+                gmap[id(p)].copy_(upd.view_as(p))
         if self.r1_numel:
             r1 = slice(self.r1_start, self.arena_numel)
             out = B.rank1_buf / N
@@ -483,7 +577,9 @@ class PowerSGDOptimizer:
             upd = out + self.m[r1]
             self.x[r1].add_(upd, alpha=-lr)
             if self.write_grad:
-                self.g[r1].copy_(upd)
+                for p in self.rank1:
+                    s = self.offsets[id(p)] - self.r1_start
+                    gmap[id(p)].copy_(upd[s: s + p.numel()].view_as(p))
 
     # -- checkpoint / resume ---------------------------------------------------------------
     def state_dict(self):

@@ -39,6 +39,12 @@ class PowerSGDSync:
     def step(self):
         return self.opt.step()
 
+    def phases(self):
+        return self.opt.phases()
+
+    def count_step(self):
+        self.opt.count_step()
+
     def state_dict(self):
         return self.opt.state_dict()
 
@@ -116,6 +122,12 @@ class _DenseSync:
 
     def step(self):
         return self.ddp.step()
+
+    def phases(self):
+        return self.ddp.phases()
+
+    def count_step(self):
+        self.ddp.count_step()
 
     def state_dict(self):
         return self.ddp.state_dict()
