@@ -11,12 +11,13 @@ __all__ = [
 ]
 
 
-def build_model(name: str, num_classes: int = 1000):
+def build_model(name: str, num_classes=None):
+    """``num_classes`` defaults to the reference's heads: 1000 (ImageNet ResNet), 2 (IMDb)."""
     name = name.lower()
     if name.startswith("resnet"):
-        return build_resnet(int(name[len("resnet"):]), num_classes)
+        return build_resnet(int(name[len("resnet"):]), 1000 if num_classes is None else num_classes)
     if name in ("distilbert", "distilbert-base", "distilbert-base-uncased"):
-        return distilbert_base(num_labels=num_classes)
+        return distilbert_base(num_labels=2 if num_classes is None else num_classes)
     if name in ("mlp", "toy_mlp"):
         return ToyMLP()
     raise ValueError(f"unknown model {name!r}")

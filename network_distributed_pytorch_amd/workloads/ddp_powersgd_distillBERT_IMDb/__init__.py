@@ -1,0 +1,1 @@
+"""See ddp_init.py / run_script.py."""
