@@ -37,12 +37,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--model", default="resnet18")
-    ap.add_argument("--num-classes", type=int, default=1000)
-    ap.add_argument("--batch", type=int, default=512, help="per-GPU batch (weak scaling)")
-    ap.add_argument("--reducer", choices=["powersgd", "dense", "dense-ref", "powersgd-ref"], default="powersgd")
+    ap.add_argument("--model", default="resnet18", help="resnet18/34/50/101/152 | distilbert")
+    ap.add_argument("--num-classes", type=int, default=None, help="default: 1000 (ResNet, reference head) / 2")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="per-GPU batch (weak scaling); default 512 ResNet, 16 DistilBERT (reference)")
+    ap.add_argument("--seq-len", type=int, default=512)
+    ap.add_argument("--reducer", choices=["powersgd", "dense", "dense-ref", "powersgd-ref", "powersgd-api"],
+                    default="powersgd")
     ap.add_argument("--rank", type=int, default=4)
-    ap.add_argument("--lr", type=float, default=1e-3)
+    ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--channels-last", action="store_true")
     ap.add_argument("--link", default="none", help="none|1g|10g|100g link emulation")
     ap.add_argument("--bucket-mb", type=float, default=25.0)
@@ -50,7 +53,21 @@ def parse():
     ap.add_argument("--graph-mode", default="auto", choices=["auto", "full", "piecewise", "none"],
                     help="hipGraph capture of the step: full (N=1 default), piecewise (collectives "
                          "eager between captured compute; N>1 default), none")
-    return ap.parse_args()
+    a = ap.parse_args()
+    bert = a.model.startswith("distilbert")
+    if a.batch is None:
+        a.batch = 16 if bert else 512
+    if a.lr is None:
+        a.lr = 5e-5 if bert else 1e-3
+    return a
+
+
+def metric_name(args) -> str:
+    if args.model == "resnet18" and args.reducer.startswith("powersgd") and args.rank == 4:
+        return METRIC
+    what = "DistilBERT IMDb" if args.model.startswith("distilbert") else f"{args.model} CIFAR10"
+    red = f"PowerSGD r={args.rank}" if args.reducer.startswith("powersgd") else "dense all-reduce"
+    return f"samples/sec + bytes/step all-reduced, {what} {red}"
 
 
 def main():
@@ -83,15 +100,31 @@ def main():
     sync = build_grad_sync(args.reducer, model, comm, lr=args.lr, momentum=0.9, rank=args.rank,
                            bucket_mb=args.bucket_mb)
     crit = torch.nn.CrossEntropyLoss()
+    is_bert = args.model.startswith("distilbert")
 
-    # synthetic CIFAR-10-shape data, normalised to [-1, 1] like ToTensor+Normalize(0.5, 0.5)
+    # synthetic data pools (device-resident): CIFAR-10-shape images in [-1, 1] (what
+    # ToTensor+Normalize(0.5, 0.5) yields) or IMDb-shape token batches (512 tokens, masks)
     g = torch.Generator(device=device)
     g.manual_seed(1234 + rank)
     n_pool = 4
-    xs = (torch.rand(n_pool, args.batch, 3, 32, 32, device=device, generator=g) * 2 - 1)
-    if args.channels_last:
-        xs = torch.stack([x.contiguous(memory_format=torch.channels_last) for x in xs])
-    ys = torch.randint(0, 10, (n_pool, args.batch), device=device, generator=g)
+    if is_bert:
+        from network_distributed_pytorch_amd.utils.data import SyntheticIMDb
+
+        ds = SyntheticIMDb(n=n_pool * args.batch, seq_len=args.seq_len, seed=1234 + rank, device=device)
+        pool = [{k: v[i * args.batch:(i + 1) * args.batch].contiguous() for k, v in ds.columns.items()}
+                for i in range(n_pool)]
+
+        def loss_of(b):
+            return model(b["input_ids"], attention_mask=b["attention_mask"], labels=b["labels"])[0]
+    else:
+        xs = (torch.rand(n_pool, args.batch, 3, 32, 32, device=device, generator=g) * 2 - 1)
+        if args.channels_last:
+            xs = torch.stack([x.contiguous(memory_format=torch.channels_last) for x in xs])
+        ys = torch.randint(0, 10, (n_pool, args.batch), device=device, generator=g)
+        pool = [{"x": xs[i], "y": ys[i]} for i in range(n_pool)]
+
+        def loss_of(b):
+            return crit(model(b["x"]), b["y"])
 
     loss_acc = torch.zeros((), device=device)
 
@@ -101,13 +134,12 @@ def main():
     if graph_mode != "none":
         from network_distributed_pytorch_amd.utils.graph import StepRunner
 
-        x_static = xs[0].clone()
-        y_static = ys[0].clone()
+        static = {k: v.clone() for k, v in pool[0].items()}
         loss_static = torch.zeros((), device=device)
 
         def pre():
             sync.zero_grad()
-            loss = crit(model(x_static), y_static)
+            loss = loss_of(static)
             loss.backward()
             loss_static.copy_(loss.detach())
 
@@ -118,14 +150,13 @@ def main():
         graph_mode = runner.mode
 
         def step(i):
-            x_static.copy_(xs[i % n_pool], non_blocking=True)
-            y_static.copy_(ys[i % n_pool], non_blocking=True)
+            for k, v in pool[i % n_pool].items():
+                static[k].copy_(v, non_blocking=True)
             runner()
     else:
         def step(i):
             sync.zero_grad()
-            out = model(xs[i % n_pool])
-            loss = crit(out, ys[i % n_pool])
+            loss = loss_of(pool[i % n_pool])
             loss.backward()
             sync.step()
             loss_acc.add_(loss.detach())
@@ -153,7 +184,7 @@ def main():
         global_batch = args.batch * world
         sps = global_batch * args.steps / elapsed
         rec = {
-            "metric": METRIC,
+            "metric": metric_name(args),
             "value": round(sps, 2),
             "unit": "samples/s",
             "n_gpus": world,
@@ -164,16 +195,18 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32",
-            "data": "synthetic CIFAR-10-shape (3x32x32, 10 labels), random-init weights",
+            "data": ("synthetic IMDb-shape (512-token ids + masks, 2 labels)" if is_bert else
+                     "synthetic CIFAR-10-shape (3x32x32, 10 labels)") + ", random-init weights",
             "bytes_per_step": sync.bytes_per_step,
+            "dense_bytes_per_step": 4 * sum(p.numel() for p in model.parameters()),
             "collectives_per_step": sync.collectives_per_step,
             "config": {
                 "model": args.model,
-                "num_classes": args.num_classes,
+                "num_classes": args.num_classes if args.num_classes is not None else (2 if is_bert else 1000),
                 "global_batch": global_batch,
                 "per_gpu_batch": args.batch,
-                "seq_len": None,
-                "image": [3, 32, 32],
+                "seq_len": args.seq_len if is_bert else None,
+                "image": None if is_bert else [3, 32, 32],
                 "parallelism": f"dp{world}",
                 "reducer": args.reducer,
                 "powersgd_rank": args.rank if "powersgd" in args.reducer else None,

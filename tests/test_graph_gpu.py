@@ -1,0 +1,91 @@
+"""hipGraph step capture and multi-rank native paths on one MI355X.
+
+* full / piecewise graph capture of forward + backward + fused PowerSGD (or dense SGD)
+  reproduces eager execution step for step;
+* two ranks sharing the GPU through gloo with device tensors (RCCL refuses two ranks per
+  GPU): the native reducer keeps Q / outputs identical across ranks and the native fused
+  optimizer keeps replicas bitwise identical and matches the eager reference loop.
+"""
+import os
+
+import pytest
+import torch
+
+from network_distributed_pytorch_amd.parallel.trainer import build_grad_sync
+from network_distributed_pytorch_amd.utils.graph import StepRunner
+from network_distributed_pytorch_amd.utils.launcher import spawn
+
+from . import dist_helpers as H
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(dev):
+    torch.manual_seed(11)
+    return torch.nn.Sequential(
+        torch.nn.Conv2d(3, 16, 3, padding=1), torch.nn.BatchNorm2d(16), torch.nn.ReLU(),
+        torch.nn.Conv2d(16, 16, 3, stride=2), torch.nn.ReLU(), torch.nn.Flatten(), torch.nn.Linear(16 * 7 * 7, 10)
+    ).to(dev)
+
+
+@pytest.mark.parametrize("kind", ["powersgd", "dense"])
+@pytest.mark.parametrize("mode", ["full", "piecewise"])
+def test_graph_matches_eager(device, kind, mode):
+    g = torch.Generator(device="cpu").manual_seed(0)
+    batches = [(torch.randn(32, 3, 16, 16, generator=g).to(device), torch.randint(0, 10, (32,), generator=g).to(device))
+               for _ in range(8)]
+    results = []
+    for graphed in (False, True):
+        model = _model(device)
+        sync = build_grad_sync(kind, model, lr=0.05, momentum=0.9, rank=4)
+        static = [batches[0][0].clone(), batches[0][1].clone()]
+
+        def pre():
+            sync.zero_grad()
+            torch.nn.functional.cross_entropy(model(static[0]), static[1]).backward()
+
+        runner = StepRunner(pre, sync, mode=mode if graphed else "none", warmup=2)
+        # the warmup of the graphed runner consumes 2 extra steps on batch 0: mirror it eagerly
+        if not graphed:
+            for _ in range(2):
+                static[0].copy_(batches[0][0]); static[1].copy_(batches[0][1])
+                runner()
+        for x, y in batches:
+            static[0].copy_(x)
+            static[1].copy_(y)
+            runner()
+        torch.cuda.synchronize()
+        results.append([p.detach().clone() for p in model.parameters()])
+        if graphed:
+            assert runner.graphs is not None and runner.replays == len(batches)
+    for a, b in zip(*results):
+        assert torch.allclose(a, b, atol=1e-5, rtol=1e-4), (a - b).abs().max()
+
+
+def test_gloo_two_ranks_on_device_reducer(tmp_path):
+    os.environ["NDP_TEST_DEVICE"] = "cuda"
+    try:
+        spawn(H.reducer_rank_body, 2, args=(str(tmp_path), 4))
+    finally:
+        os.environ.pop("NDP_TEST_DEVICE", None)
+    d = [torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=True) for r in range(2)]
+    for call in range(2):
+        a, b = d[0]["rec"][call], d[1]["rec"][call]
+        assert torch.equal(a["q"], b["q"])
+        for x, y in zip(a["outs"], b["outs"]):
+            assert torch.equal(x, y)
+
+
+def test_gloo_two_ranks_on_device_training(tmp_path):
+    os.environ["NDP_TEST_DEVICE"] = "cuda"
+    try:
+        spawn(H.train_rank_body, 2, args=(str(tmp_path), "powersgd", 4, True))
+        spawn(H.train_rank_body, 2, args=(str(tmp_path), "powersgd-ref", 4, True))
+    finally:
+        os.environ.pop("NDP_TEST_DEVICE", None)
+    nat = [torch.load(os.path.join(tmp_path, f"powersgd_rank{r}.pt"), weights_only=True) for r in range(2)]
+    ref = [torch.load(os.path.join(tmp_path, f"powersgd-ref_rank{r}.pt"), weights_only=True) for r in range(2)]
+    for a, b in zip(nat[0]["params"], nat[1]["params"]):
+        assert torch.equal(a, b), "native replicas diverged"
+    for a, b in zip(nat[0]["params"], ref[0]["params"]):
+        assert torch.allclose(a, b, atol=1e-5, rtol=1e-4)
