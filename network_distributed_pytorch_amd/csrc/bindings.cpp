@@ -51,6 +51,8 @@ py::dict build_plan(const std::vector<std::pair<int64_t, int64_t>>& shapes, int 
   d["p_items"] = to_bytes(pl.p_items);
   d["q_items"] = to_bytes(pl.q_items);
   d["u_items"] = to_bytes(pl.u_items);
+  d["orth_items"] = to_bytes(pl.orth_items);
+  d["n_orth_items"] = (int64_t)pl.orth_items.size();
   d["n_mats"] = (int64_t)pl.geom.size();
   d["n_p_items"] = (int64_t)pl.p_items.size();
   d["n_q_items"] = (int64_t)pl.q_items.size();
@@ -125,9 +127,10 @@ py::tuple make_seg_table(const std::vector<std::tuple<int64_t, int64_t, int64_t,
   return py::make_tuple(to_bytes(tab.entries), prefix, (int64_t)tab.entries.size(), tab.n_blocks);
 }
 
-// geometry for a standalone batched orthogonalisation: rows of (n, r, p_off)
-torch::Tensor make_orth_geom(const std::vector<std::tuple<int64_t, int64_t, int64_t>>& mats) {
+// geometry + work list for a standalone batched orthogonalisation: rows of (n, r, p_off)
+py::tuple make_orth_geom(const std::vector<std::tuple<int64_t, int64_t, int64_t>>& mats) {
   std::vector<MatGeom> v(mats.size());
+  int max_rank = 1;
   for (size_t i = 0; i < mats.size(); ++i) {
     v[i] = MatGeom{};
     v[i].n = (int32_t)std::get<0>(mats[i]);
@@ -135,8 +138,10 @@ torch::Tensor make_orth_geom(const std::vector<std::tuple<int64_t, int64_t, int6
     TORCH_CHECK(v[i].r >= 1 && v[i].r <= ndp::kMaxRank, "orthogonalize supports 1..64 columns");
     v[i].m = v[i].r;
     v[i].p_off = (int32_t)std::get<2>(mats[i]);
+    max_rank = std::max<int>(max_rank, v[i].r);
   }
-  return to_bytes(v);
+  auto items = ndp::build_orth_items(v, max_rank);
+  return py::make_tuple(to_bytes(v), to_bytes(items), (int64_t)items.size(), max_rank);
 }
 
 int64_t n_of(const torch::Tensor& bytes, size_t sz) { return bytes.numel() / (int64_t)sz; }
@@ -165,11 +170,21 @@ void psgd_q(torch::Tensor geom, torch::Tensor ptrs, torch::Tensor items, torch::
   check_launch("launch_psgd_q");
 }
 
-void psgd_orth(torch::Tensor geom, torch::Tensor p, double p_div, double eps, int max_rank) {
-  check_dev(geom, "geom"); check_f32(p, "p");
+// scratch: float32 tensor of >= 2*n_items*kMaxRank partials; ctr: int32 tensor of
+// >= n_mats + 1 words (counters, then the error word at index n_mats)
+void psgd_orth(torch::Tensor geom, torch::Tensor items, torch::Tensor p, double p_div, double eps,
+               int max_rank, torch::Tensor scratch, torch::Tensor ctr) {
+  check_dev(geom, "geom"); check_dev(items, "items"); check_f32(p, "p"); check_f32(scratch, "scratch");
+  check_dev(ctr, "ctr");
+  const int n_items = (int)n_of(items, sizeof(ndp::OrthItem));
+  const int n_mats = (int)n_of(geom, sizeof(MatGeom));
+  TORCH_CHECK(scratch.numel() >= 2LL * n_items * ndp::kMaxRank, "orth scratch too small");
+  TORCH_CHECK(ctr.numel() * ctr.element_size() >= 4LL * (n_mats + 1), "orth counters too small");
+  auto* c = reinterpret_cast<unsigned*>(ctr.data_ptr());
   ndp::launch_psgd_orth(reinterpret_cast<const MatGeom*>(geom.data_ptr()),
-                        (int)n_of(geom, sizeof(MatGeom)), p.data_ptr<float>(), (float)p_div,
-                        (float)eps, max_rank, cur_stream());
+                        reinterpret_cast<const ndp::OrthItem*>(items.data_ptr()), n_items, n_mats,
+                        p.data_ptr<float>(), (float)p_div, (float)eps, max_rank,
+                        scratch.data_ptr<float>(), c, c + n_mats, cur_stream());
   check_launch("launch_psgd_orth");
 }
 

@@ -43,6 +43,8 @@ struct MatPtrs {
 struct PItem { int32_t mat, row0, k0, k1, chunk, pad[3]; };   // 64 rows x [k0,k1)
 struct QItem { int32_t mat, col0, row0, row1, chunk, pad[3]; }; // [row0,row1) x 256 cols
 struct UItem { int32_t mat, row0, col0, pad; };                 // 64 rows x 64 cols
+// orth: rows [row0,row1) of matrix `mat`; workgroup `wg` of `nwg`; slab0 = first item of mat
+struct OrthItem { int32_t mat, row0, row1, wg, nwg, slab0, pad[2]; };
 
 // Segmented reduce-copy entry: dst[k] = (sum_c src[c*stride + k]) / div
 struct SegEntry {
@@ -70,8 +72,11 @@ void launch_psgd_p(const MatGeom* geom, const MatPtrs* ptrs, const PItem* items,
                    const float* q_warm, float* p_part, int fuse_ef, int max_rank, hipStream_t s);
 void launch_psgd_q(const MatGeom* geom, const MatPtrs* ptrs, const QItem* items, int n_items,
                    const float* p_hat, float* q_part, int max_rank, hipStream_t s);
-void launch_psgd_orth(const MatGeom* geom, int n_mats, float* p, float p_div, float eps,
-                      int max_rank, hipStream_t s);
+// partial: 2 * n_items * kMaxRank floats; counters: n_mats uint32 (zeroed by the launcher)
+void launch_psgd_orth(const MatGeom* geom, const OrthItem* items, int n_items, int n_mats, float* p,
+                      float p_div, float eps, int max_rank, float* partial, unsigned* counters,
+                      unsigned* err, hipStream_t s);
+int orth_rows_per_thread(int max_rank);
 // mode 0 = api (out/mem), 1 = engine (EF + momentum + SGD), 2 = engine + write grad
 void launch_psgd_update(const MatGeom* geom, const MatPtrs* ptrs, const UItem* items,
                         int n_items, const float* p_hat, const float* q_sum, float q_div,

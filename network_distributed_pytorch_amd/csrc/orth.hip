@@ -1,0 +1,192 @@
+// Batched, multi-workgroup, deterministic modified Gram-Schmidt for PowerSGD's P-hat.
+//
+// Reference: orthogonalize() (ddp_powersgd_guide_cifar10/reducer.py:180-191), a TorchScript
+// per-column loop run once per matrix (reducer.py:136-137):
+//     col_i /= sqrt(sum(col_i^2)) + eps ;   rest_j -= sum(col_i * rest_j) * col_i
+// with the all-reduce mean folded in (reducer.py:128, p_memory /= N).
+//
+// MI355X design:
+//  * ONE launch for every matrix.  Matrix i is split into nwg_i workgroups of 256*RPT rows;
+//    each thread keeps its RPT rows x RMAX columns in VGPRs for the whole factorisation
+//    (P is read once and written once; every column step is register work + reductions).
+//  * Column reductions: wave butterfly (bitwise-identical in every lane) -> fixed-order LDS
+//    combine -> for nwg_i > 1 a fixed-order sum of per-workgroup partial slabs exchanged
+//    through the agent-scope release / acquire protocol of cdna_hip_programming.md §6
+//    Guideline 16 (plain stores + vmcnt drain + release fence + relaxed agent counter;
+//    poller: relaxed loads, ONE acquire fence).  Every workgroup of a matrix, and every
+//    rank (same plan), computes the bitwise-identical result: replicas stay consistent.
+//  * Partial slabs are double-buffered by barrier parity (a fast workgroup can be at most
+//    one barrier ahead); counters are zeroed by a memset node before each launch; spins are
+//    bounded and report through an error word instead of hanging the GPU.
+//  * Residency: the plan keeps the grid small (<= a few hundred 256-thread workgroups, a
+//    fraction of 256 CUs x 8), and the kernel runs alone on its stream after the P
+//    all-reduce, so all workgroups of a matrix are co-resident.
+#include <hip/hip_runtime.h>
+#include "ndp_kernels.h"
+
+namespace ndp {
+
+__device__ __forceinline__ float wave_sum_o(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int K>
+__device__ __forceinline__ void block_sum_o(float (&v)[K], float* red /*[4][K]*/) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = wave_sum_o(v[k]);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) red[wave * K + k] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = ((red[k] + red[K + k]) + red[2 * K + k]) + red[3 * K + k];
+  __syncthreads();
+}
+
+struct OrthCtx {
+  float* partial;     // [2][n_items][kMaxRank]
+  unsigned* ctr;      // [n_mats]
+  unsigned* err;      // [1]
+  int n_items;
+};
+
+// Sum v[] over all workgroups of the matrix (deterministic, identical everywhere).
+template <int K>
+__device__ __forceinline__ void group_sum(float (&v)[K], float* red, const OrthItem& it, const OrthCtx& cx,
+                                          int& bar) {
+  block_sum_o<K>(v, red);
+  if (it.nwg == 1) return;
+  float* slab = cx.partial + ((size_t)(bar & 1) * cx.n_items + it.slab0) * kMaxRank;
+  if (threadIdx.x < K) {
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if ((int)threadIdx.x == k) slab[it.wg * kMaxRank + k] = v[k];
+  }
+  if (threadIdx.x < 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(cx.ctr + it.mat, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned target = (unsigned)(bar + 1) * (unsigned)it.nwg;
+    unsigned spins = 0;
+    while (__hip_atomic_load(cx.ctr + it.mat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1u << 25)) {  // ~seconds: report instead of hanging
+        __hip_atomic_fetch_or(cx.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    float acc = 0.f;
+    for (int w = 0; w < it.nwg; ++w) acc += slab[w * kMaxRank + k];
+    v[k] = acc;
+  }
+  ++bar;
+}
+
+template <int RMAX, int RPT>
+__global__ __launch_bounds__(256) void psgd_orth_mw_kernel(const MatGeom* __restrict__ geom,
+                                                           const OrthItem* __restrict__ items,
+                                                           float* __restrict__ p, float p_div,
+                                                           float eps, OrthCtx cx) {
+  __shared__ float red[4 * RMAX];
+  const OrthItem it = items[blockIdx.x];
+  const MatGeom g = geom[it.mat];
+  const int r = g.r;
+  float* P = p + g.p_off;
+  const int tid = threadIdx.x;
+
+  float v[RPT][RMAX];
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) {
+    const int a = it.row0 + tid + 256 * k;
+    const bool ok = a < it.row1;
+#pragma unroll
+    for (int c = 0; c < RMAX; ++c) v[k][c] = (ok && c < r) ? P[(int64_t)a * r + c] / p_div : 0.f;
+  }
+
+  int bar = 0;
+  for (int i = 0; i < r; ++i) {
+    float s[1] = {0.f};
+#pragma unroll
+    for (int k = 0; k < RPT; ++k)
+#pragma unroll
+      for (int c = 0; c < RMAX; ++c)
+        if (c == i) s[0] += v[k][c] * v[k][c];
+    group_sum<1>(s, red, it, cx, bar);
+    const float nrm = sqrtf(s[0]) + eps;
+    float vi[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      vi[k] = 0.f;
+#pragma unroll
+      for (int c = 0; c < RMAX; ++c)
+        if (c == i) {
+          v[k][c] = v[k][c] / nrm;
+          vi[k] = v[k][c];
+        }
+    }
+    if (i + 1 >= r) break;
+    float d[RMAX];
+#pragma unroll
+    for (int j = 0; j < RMAX; ++j) {
+      d[j] = 0.f;
+#pragma unroll
+      for (int k = 0; k < RPT; ++k)
+        if (j > i) d[j] += vi[k] * v[k][j];
+    }
+    group_sum<RMAX>(d, red, it, cx, bar);
+#pragma unroll
+    for (int k = 0; k < RPT; ++k)
+#pragma unroll
+      for (int j = 0; j < RMAX; ++j)
+        if (j > i && j < r) v[k][j] = v[k][j] - d[j] * vi[k];
+  }
+
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) {
+    const int a = it.row0 + tid + 256 * k;
+    if (a < it.row1) {
+#pragma unroll
+      for (int c = 0; c < RMAX; ++c)
+        if (c < r) P[(int64_t)a * r + c] = v[k][c];
+    }
+  }
+}
+
+int orth_rows_per_thread(int max_rank) {
+  if (max_rank <= 8) return 8;
+  if (max_rank <= 16) return 4;
+  if (max_rank <= 32) return 2;
+  return 1;
+}
+
+void launch_psgd_orth(const MatGeom* geom, const OrthItem* items, int n_items, int n_mats, float* p,
+                      float p_div, float eps, int max_rank, float* partial, unsigned* counters,
+                      unsigned* err, hipStream_t s) {
+  if (n_items <= 0) return;
+  (void)hipMemsetAsync(counters, 0, sizeof(unsigned) * (size_t)n_mats, s);
+  OrthCtx cx{partial, counters, err, n_items};
+  if (max_rank <= 4)
+    hipLaunchKernelGGL((psgd_orth_mw_kernel<4, 8>), dim3(n_items), dim3(256), 0, s, geom, items, p, p_div, eps, cx);
+  else if (max_rank <= 8)
+    hipLaunchKernelGGL((psgd_orth_mw_kernel<8, 8>), dim3(n_items), dim3(256), 0, s, geom, items, p, p_div, eps, cx);
+  else if (max_rank <= 16)
+    hipLaunchKernelGGL((psgd_orth_mw_kernel<16, 4>), dim3(n_items), dim3(256), 0, s, geom, items, p, p_div, eps, cx);
+  else if (max_rank <= 32)
+    hipLaunchKernelGGL((psgd_orth_mw_kernel<32, 2>), dim3(n_items), dim3(256), 0, s, geom, items, p, p_div, eps, cx);
+  else
+    hipLaunchKernelGGL((psgd_orth_mw_kernel<64, 1>), dim3(n_items), dim3(256), 0, s, geom, items, p, p_div, eps, cx);
+}
+
+}  // namespace ndp

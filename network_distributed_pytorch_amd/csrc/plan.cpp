@@ -92,7 +92,34 @@ Plan build_plan(const std::vector<std::pair<int64_t, int64_t>>& shapes, int rank
   pl.pp_total = pp_off;
   pl.qp_total = qp_off;
   if (pl.max_rank == 0) pl.max_rank = 1;
+  pl.orth_items = build_orth_items(pl.geom, pl.max_rank);
   return pl;
+}
+
+std::vector<OrthItem> build_orth_items(const std::vector<MatGeom>& geom, int max_rank) {
+  const int64_t rows_per_wg = 256LL * orth_rows_per_thread(max_rank);
+  std::vector<OrthItem> items;
+  for (size_t i = 0; i < geom.size(); ++i) {
+    const int64_t n = geom[i].n;
+    const int64_t nwg = std::max<int64_t>(1, cdiv(n, rows_per_wg));
+    const int32_t slab0 = (int32_t)items.size();
+    for (int64_t w = 0; w < nwg; ++w) {
+      OrthItem it{};
+      it.mat = (int32_t)i;
+      it.row0 = (int32_t)(w * rows_per_wg);
+      it.row1 = (int32_t)std::min<int64_t>(n, (w + 1) * rows_per_wg);
+      it.wg = (int32_t)w;
+      it.nwg = (int32_t)nwg;
+      it.slab0 = slab0;
+      items.push_back(it);
+    }
+  }
+  // every workgroup of a matrix must be co-resident (spin barriers): the kernel fits
+  // >= 3 workgroups per CU for RMAX <= 32 and 1 for RMAX = 64 (kernel-resource-usage),
+  // so stay well below 256 CUs x that
+  const size_t cap = max_rank <= 32 ? 512 : 192;
+  if (items.size() > cap) throw std::invalid_argument("orthogonalisation grid too large for co-residency");
+  return items;
 }
 
 SegTable build_seg_table(const std::vector<SegSpec>& specs) {

@@ -13,12 +13,16 @@ struct Plan {
   std::vector<PItem> p_items;
   std::vector<QItem> q_items;
   std::vector<UItem> u_items;
+  std::vector<OrthItem> orth_items;
   int64_t p_total = 0, q_total = 0, pp_total = 0, qp_total = 0;
   int max_rank = 1;
 };
 
 // shapes[i] = (n_i, m_i) of every >1-D tensor, in model.parameters() order
 Plan build_plan(const std::vector<std::pair<int64_t, int64_t>>& shapes, int rank);
+
+// multi-workgroup MGS work list for the given matrices (rows split in 256*RPT blocks)
+std::vector<OrthItem> build_orth_items(const std::vector<MatGeom>& geom, int max_rank);
 
 struct SegSpec {
   uintptr_t src, dst;

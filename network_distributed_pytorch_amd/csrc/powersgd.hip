@@ -2,7 +2,7 @@
 //
 // Replaces the reference's per-tensor eager loop
 //   P = M Q            (ddp_powersgd_guide_cifar10/reducer.py:121-123)   -> psgd_p_kernel
-//   orthogonalize(P)   (reducer.py:136-137, 180-191)                     -> psgd_orth_kernel
+//   orthogonalize(P)   (reducer.py:136-137, 180-191)                     -> orth.hip
 //   Q = M^T P          (reducer.py:140-142)                              -> psgd_q_kernel
 //   out = P Q^T, mem = M - out (reducer.py:158-163) + Algorithm-2 momentum/SGD
 //                      (ddp_powersgd_guide_cifar10/ddp_init.py:156-178)  -> psgd_update_kernel
@@ -250,74 +250,6 @@ __global__ __launch_bounds__(256) void psgd_q_kernel(const MatGeom* __restrict__
 }
 
 // ----------------------------------------------------------------------------------
-// Batched modified Gram-Schmidt, one workgroup per matrix, deterministic reductions.
-// Same arithmetic as the reference (reducer.py:180-191):
-//   col_i /= sqrt(sum(col_i^2)) + eps ;  rest_j -= sum(col_i * rest_j) * col_i
-// with the all-reduce mean folded into the prologue (reducer.py:128).
-// ----------------------------------------------------------------------------------
-template <int K>
-__device__ __forceinline__ void block_sum_vec(float (&v)[K], float* red /*[4][K]*/) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int k = 0; k < K; ++k) v[k] = wave_sum(v[k]);
-  if (lane == 0) {
-#pragma unroll
-    for (int k = 0; k < K; ++k) red[wave * K + k] = v[k];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < K; ++k) v[k] = ((red[k] + red[K + k]) + red[2 * K + k]) + red[3 * K + k];
-  __syncthreads();
-}
-
-template <int RMAX>
-__global__ __launch_bounds__(256) void psgd_orth_kernel(const MatGeom* __restrict__ geom,
-                                                        float* __restrict__ p, float p_div,
-                                                        float eps) {
-  __shared__ float red[4 * RMAX];
-  const MatGeom g = geom[blockIdx.x];
-  const int r = g.r, n = g.n;
-  float* P = p + g.p_off;
-  const int tid = threadIdx.x;
-
-  float s1[1] = {0.f};
-  for (int a = tid; a < n; a += 256) {
-    float* row = P + (int64_t)a * r;
-    for (int c = 0; c < r; ++c) row[c] = row[c] / p_div;
-    s1[0] += row[0] * row[0];
-  }
-  block_sum_vec<1>(s1, red);
-
-  for (int i = 0; i < r; ++i) {
-    const float nrm = sqrtf(s1[0]) + eps;
-    float d[RMAX];
-#pragma unroll
-    for (int j = 0; j < RMAX; ++j) d[j] = 0.f;
-    for (int a = tid; a < n; a += 256) {
-      float* row = P + (int64_t)a * r;
-      const float vi = row[i] / nrm;
-      row[i] = vi;
-#pragma unroll
-      for (int j = 0; j < RMAX; ++j)
-        if (j > i && j < r) d[j] += vi * row[j];
-    }
-    if (i + 1 >= r) break;
-    block_sum_vec<RMAX>(d, red);
-    s1[0] = 0.f;
-    for (int a = tid; a < n; a += 256) {
-      float* row = P + (int64_t)a * r;
-      const float vi = row[i];
-#pragma unroll
-      for (int j = 0; j < RMAX; ++j)
-        if (j > i && j < r) row[j] = row[j] - d[j] * vi;
-      const float w = row[i + 1];
-      s1[0] += w * w;
-    }
-    block_sum_vec<1>(s1, red);
-  }
-}
-
-// ----------------------------------------------------------------------------------
 // Decompress + error feedback (+ momentum + SGD):  out[a][b] = sum_c Phat[a][c] * Qs[b][c]
 // computed as D = Qs * Phat^T on MFMA so each lane holds 4 consecutive b of one row a
 // (16-B accesses of e / m / x).  Qs = Q_sum / q_div (reducer.py:147).  One designated
@@ -469,24 +401,6 @@ void launch_psgd_q(const MatGeom* geom, const MatPtrs* ptrs, const QItem* items,
   else
     hipLaunchKernelGGL(psgd_q_kernel<4>, dim3(n_items), dim3(256), lds, s, geom, ptrs, items,
                        p_hat, q_part);
-}
-
-void launch_psgd_orth(const MatGeom* geom, int n_mats, float* p, float p_div, float eps,
-                      int max_rank, hipStream_t s) {
-  if (n_mats <= 0) return;
-  if (max_rank <= 4)
-    hipLaunchKernelGGL(psgd_orth_kernel<4>, dim3(n_mats), dim3(256), 0, s, geom, p, p_div, eps);
-  else if (max_rank <= 8)
-    hipLaunchKernelGGL(psgd_orth_kernel<8>, dim3(n_mats), dim3(256), 0, s, geom, p, p_div, eps);
-  else if (max_rank <= 16)
-    hipLaunchKernelGGL(psgd_orth_kernel<16>, dim3(n_mats), dim3(256), 0, s, geom, p, p_div,
-                       eps);
-  else if (max_rank <= 32)
-    hipLaunchKernelGGL(psgd_orth_kernel<32>, dim3(n_mats), dim3(256), 0, s, geom, p, p_div,
-                       eps);
-  else
-    hipLaunchKernelGGL(psgd_orth_kernel<64>, dim3(n_mats), dim3(256), 0, s, geom, p, p_div,
-                       eps);
 }
 
 void launch_psgd_update(const MatGeom* geom, const MatPtrs* ptrs, const UItem* items,

@@ -83,8 +83,11 @@ def orthogonalize(matrix: torch.Tensor, eps: float = 1e-8) -> torch.Tensor:
     if matrix.is_cuda:
         assert matrix.dtype == torch.float32 and matrix.is_contiguous()
         X = ext()
-        geom = X.make_orth_geom([(int(n), int(m), 0)]).to(matrix.device)
-        X.psgd_orth(geom, matrix.view(-1), 1.0, float(eps), int(m))
+        geom, items, n_items, max_rank = X.make_orth_geom([(int(n), int(m), 0)])
+        scratch = torch.empty(2 * n_items * X.MAX_RANK, dtype=torch.float32, device=matrix.device)
+        ctr = torch.zeros(2, dtype=torch.int32, device=matrix.device)
+        X.psgd_orth(geom.to(matrix.device), items.to(matrix.device), matrix.view(-1), 1.0, float(eps),
+                    int(max_rank), scratch, ctr)
         return matrix
     for i in range(m):
         col = matrix[:, i: i + 1]
@@ -153,7 +156,11 @@ class _PlanBuffers:
             self.q_part = torch.zeros(max(1, d["qp_total"]), **f32)
             self.pp_offs, self.qp_offs = d["pp_offs"], d["qp_offs"]
             self.p_chunks, self.q_chunks = d["p_chunks"], d["q_chunks"]
-            self.counts = {k: d[k] for k in ("n_p_items", "n_q_items", "n_u_items", "pp_total", "qp_total")}
+            self.counts = {k: d[k] for k in ("n_p_items", "n_q_items", "n_u_items", "n_orth_items", "pp_total",
+                                             "qp_total")}
+            self.orth_items = d["orth_items"].to(device)
+            self.orth_scratch = torch.zeros(max(1, 2 * d["n_orth_items"] * X.MAX_RANK), **f32)
+            self.orth_ctr = torch.zeros(len(shapes) + 1, dtype=torch.int32, device=device)
             nb = max(1, len(shapes)) * X.SIZEOF_MATGEOM
             self.geom = torch.zeros(nb, dtype=torch.uint8, device=device)
             self.ptrs = torch.zeros(nb, dtype=torch.uint8, device=device)
@@ -166,6 +173,15 @@ class _PlanBuffers:
     def p_seg_specs(self):
         return [(self.p_part[o:], self.p_memory[po: po + n * r], c, n * r, 1.0)
                 for (n, m), r, o, po, c in zip(self.shapes, self.ranks, self.pp_offs, self.p_offs, self.p_chunks)]
+
+    def orth(self, p_div: float, eps: float):
+        """P-hat = MGS(P / p_div) for every matrix, one multi-workgroup launch."""
+        ext().psgd_orth(self.geom, self.orth_items, self.comm_buf, p_div, eps, self.max_rank,
+                        self.orth_scratch, self.orth_ctr)
+
+    def orth_error(self) -> int:
+        """Non-zero if a cross-workgroup barrier of the MGS kernel ever timed out."""
+        return int(self.orth_ctr[-1].item())
 
     def bind(self, rows: List[List[int]], vec: List[int]) -> bool:
         """Point the grouped kernels at new tensors; returns True if the tables changed."""
@@ -287,7 +303,7 @@ class PowerSGDReducer(Reducer):
         self._p_seg.run()                                   # P split-K sum + rank-1 pack
         self.comm.all_reduce(B.comm_buf)                    # reducer.py:126 + :132 fused
         if B.shapes:
-            X.psgd_orth(B.geom, B.comm_buf, float(N), self.eps, B.max_rank)
+            B.orth(float(N), self.eps)
             X.psgd_q(B.geom, B.ptrs, B.q_items, B.comm_buf, B.q_part, B.max_rank)
             B.q_seg.run()
             self.comm.all_reduce(B.q_memory)                # reducer.py:145
@@ -489,7 +505,7 @@ class PowerSGDOptimizer:
         B = self.buf
         if self.native and B.shapes:
             X = ext()
-            X.psgd_orth(B.geom, B.comm_buf, float(self.comm.world_size), self.eps, B.max_rank)
+            B.orth(float(self.comm.world_size), self.eps)
             X.psgd_q(B.geom, B.ptrs, B.q_items, B.comm_buf, B.q_part, B.max_rank)
             B.q_seg.run()
 

@@ -149,4 +149,34 @@ def build_grad_sync(kind: str, model: torch.nn.Module, comm: Optional[Communicat
         return _DenseSync(model, comm, lr, momentum, bucket_mb)
     if kind == "dense-ref":
         return ReferenceDenseLoop(model, comm, lr, momentum)
+    if kind in ("local-sgd-nesterov", "local-adamw"):
+        return LocalOptimizer(model, kind, lr, momentum)
     raise ValueError(f"unknown grad sync {kind!r}")
+
+
+class LocalOptimizer:
+    """Single-GPU baselines, no communication (reference C17):
+    ``local-sgd-nesterov`` = SGD(lr, momentum=0.9, nesterov=True)
+    (ddp_powersgd_distillBERT_IMDb/IMDb_distillBERT_example.py:57);
+    ``local-adamw`` = AdamW(lr) (IMDb_dataset_distributer.py:55)."""
+
+    def __init__(self, model, kind, lr, momentum):
+        if kind == "local-adamw":
+            self.opt = torch.optim.AdamW(model.parameters(), lr=lr)
+        else:
+            self.opt = torch.optim.SGD(model.parameters(), lr=lr, momentum=momentum, nesterov=True)
+        self.bytes_per_step = 0
+        self.collectives_per_step = 0
+
+    def zero_grad(self):
+        self.opt.zero_grad()
+
+    def step(self):
+        self.opt.step()
+        return 0
+
+    def state_dict(self):
+        return self.opt.state_dict()
+
+    def load_state_dict(self, sd):
+        self.opt.load_state_dict(sd)
