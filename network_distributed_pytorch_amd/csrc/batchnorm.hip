@@ -1,0 +1,325 @@
+// Fused training BatchNorm2d (+ residual add) (+ ReLU) for NCHW fp32 on gfx950.
+//
+// ResNet's conv -> BN -> (+identity) -> ReLU tail costs, in PyTorch-ROCm, a MIOpen BN
+// kernel, an ATen ReLU, an ATen add and an ATen `num_batches_tracked += 1` per layer in
+// forward and the mirror image in backward: ~100 latency-bound launches per ResNet-18
+// step (profiles/resnet18_powersgd_r4_graph_kernels.md).  Here each direction is two
+// kernels over a (slice, channel) grid:
+//   fwd:  stats  -> per-(channel, slice) fp64 sum / sum of squares
+//         apply  -> every workgroup folds its channel's slices in a fixed order (same
+//                   value everywhere), y = relu(x*scale + shift [+ res]); slice 0 also
+//                   writes save_mean/invstd, the running stats and num_batches_tracked
+//   bwd:  stats  -> per-slice sums of dz = dy*(y>0) and dz*xhat
+//         apply  -> dx = gamma*invstd/M * (M dz - sum dz - xhat * sum dz*xhat),
+//                   dres = dz (residual branch), slice 0 writes dgamma / dbeta
+// Statistics are accumulated in fp64 and combined in a fixed order: bitwise
+// reproducible, and at least as accurate as the reference's cuDNN/MIOpen BN.
+// Semantics follow torch.nn.BatchNorm2d (training): biased variance for normalisation,
+// unbiased variance in running_var, running = (1-momentum)*running + momentum*batch.
+#include <hip/hip_runtime.h>
+#include "ndp_kernels.h"
+
+namespace ndp {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// block-wide sum of two doubles (fixed order); result valid in every thread
+__device__ __forceinline__ void block_sum2(double& a, double& b, double* red /*[2][8]*/) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  a = wave_sum_d(a);
+  b = wave_sum_d(b);
+  if (lane == 0) {
+    red[wave] = a;
+    red[8 + wave] = b;
+  }
+  __syncthreads();
+  a = 0.0;
+  b = 0.0;
+  for (int w = 0; w < nw; ++w) {
+    a += red[w];
+    b += red[8 + w];
+  }
+  __syncthreads();
+}
+
+struct BnSlice {
+  int64_t n0, n1;
+};
+
+__device__ __forceinline__ BnSlice slice_of(int N, int S, int s) {
+  const int64_t base = N / S, rem = N % S;
+  const int64_t n0 = s * base + (s < rem ? s : rem);
+  return {n0, n0 + base + (s < rem ? 1 : 0)};
+}
+
+// ---- forward statistics -------------------------------------------------------------
+template <bool VEC>
+__global__ __launch_bounds__(256) void bn_fwd_stats_kernel(const float* __restrict__ x, double* __restrict__ part,
+                                                           int N, int C, int HW, int S) {
+  __shared__ double red[16];
+  const int s = blockIdx.x, c = blockIdx.y;
+  const BnSlice sl = slice_of(N, S, s);
+  double sum = 0.0, sq = 0.0;
+  if (VEC) {
+    const int hw4 = HW >> 2;
+    const int64_t cnt = (sl.n1 - sl.n0) * hw4;
+    for (int64_t e = threadIdx.x; e < cnt; e += blockDim.x) {
+      const int64_t n = sl.n0 + e / hw4;
+      const int q = (int)(e - (e / hw4) * hw4);
+      const f32x4 v = *reinterpret_cast<const f32x4*>(x + (n * C + c) * HW + 4 * q);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        sum += (double)v[j];
+        sq += (double)v[j] * (double)v[j];
+      }
+    }
+  } else {
+    const int64_t cnt = (sl.n1 - sl.n0) * HW;
+    for (int64_t e = threadIdx.x; e < cnt; e += blockDim.x) {
+      const int64_t n = sl.n0 + e / HW;
+      const int hw = (int)(e - (e / HW) * HW);
+      const double v = (double)x[(n * C + c) * HW + hw];
+      sum += v;
+      sq += v * v;
+    }
+  }
+  block_sum2(sum, sq, red);
+  if (threadIdx.x == 0) {
+    part[((int64_t)c * S + s) * 2] = sum;
+    part[((int64_t)c * S + s) * 2 + 1] = sq;
+  }
+}
+
+// ---- forward apply --------------------------------------------------------------------
+template <bool VEC>
+__global__ __launch_bounds__(256) void bn_fwd_apply_kernel(
+    const float* __restrict__ x, const float* __restrict__ res, float* __restrict__ y,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ rmean,
+    float* __restrict__ rvar, int64_t* __restrict__ nbt, float* __restrict__ save_mean,
+    float* __restrict__ save_invstd, const double* __restrict__ part, int N, int C, int HW, int S,
+    float eps, float momentum, int relu, int training) {
+  const int s = blockIdx.x, c = blockIdx.y;
+  float mean, invstd;
+  if (training) {
+    double sum = 0.0, sq = 0.0;
+    for (int k = 0; k < S; ++k) {
+      sum += part[((int64_t)c * S + k) * 2];
+      sq += part[((int64_t)c * S + k) * 2 + 1];
+    }
+    const double M = (double)N * HW;
+    const double mu = sum / M;
+    double var = sq / M - mu * mu;
+    if (var < 0.0) var = 0.0;
+    mean = (float)mu;
+    invstd = (float)(1.0 / sqrt(var + (double)eps));
+    if (s == 0 && threadIdx.x == 0) {
+      save_mean[c] = mean;
+      save_invstd[c] = invstd;
+      if (rmean != nullptr) {
+        const double unb = M > 1.0 ? var * M / (M - 1.0) : var;
+        rmean[c] = (float)((1.0 - momentum) * (double)rmean[c] + momentum * mu);
+        rvar[c] = (float)((1.0 - momentum) * (double)rvar[c] + momentum * unb);
+      }
+      if (nbt != nullptr && c == 0) nbt[0] += 1;
+    }
+  } else {
+    mean = rmean[c];
+    invstd = 1.0f / sqrtf(rvar[c] + eps);
+  }
+  const float scale = (gamma ? gamma[c] : 1.f) * invstd;
+  const float shift = (beta ? beta[c] : 0.f) - mean * scale;
+  const BnSlice sl = slice_of(N, S, s);
+  if (VEC) {
+    const int hw4 = HW >> 2;
+    const int64_t cnt = (sl.n1 - sl.n0) * hw4;
+    for (int64_t e = threadIdx.x; e < cnt; e += blockDim.x) {
+      const int64_t n = sl.n0 + e / hw4;
+      const int q = (int)(e - (e / hw4) * hw4);
+      const int64_t o = (n * C + c) * HW + 4 * q;
+      f32x4 v = *reinterpret_cast<const f32x4*>(x + o);
+      f32x4 r = {0.f, 0.f, 0.f, 0.f};
+      if (res) r = *reinterpret_cast<const f32x4*>(res + o);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float z = fmaf(v[j], scale, shift) + r[j];
+        v[j] = relu ? fmaxf(z, 0.f) : z;
+      }
+      *reinterpret_cast<f32x4*>(y + o) = v;
+    }
+  } else {
+    const int64_t cnt = (sl.n1 - sl.n0) * HW;
+    for (int64_t e = threadIdx.x; e < cnt; e += blockDim.x) {
+      const int64_t n = sl.n0 + e / HW;
+      const int hw = (int)(e - (e / HW) * HW);
+      const int64_t o = (n * C + c) * HW + hw;
+      float z = fmaf(x[o], scale, shift) + (res ? res[o] : 0.f);
+      y[o] = relu ? fmaxf(z, 0.f) : z;
+    }
+  }
+}
+
+// ---- backward statistics ----------------------------------------------------------------
+template <bool VEC>
+__global__ __launch_bounds__(256) void bn_bwd_stats_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                                                           const float* __restrict__ x,
+                                                           const float* __restrict__ save_mean,
+                                                           const float* __restrict__ save_invstd,
+                                                           double* __restrict__ part, int N, int C, int HW,
+                                                           int S, int relu) {
+  __shared__ double red[16];
+  const int s = blockIdx.x, c = blockIdx.y;
+  const BnSlice sl = slice_of(N, S, s);
+  const float mean = save_mean[c], invstd = save_invstd[c];
+  double sdz = 0.0, sdzx = 0.0;
+  if (VEC) {
+    const int hw4 = HW >> 2;
+    const int64_t cnt = (sl.n1 - sl.n0) * hw4;
+    for (int64_t e = threadIdx.x; e < cnt; e += blockDim.x) {
+      const int64_t n = sl.n0 + e / hw4;
+      const int q = (int)(e - (e / hw4) * hw4);
+      const int64_t o = (n * C + c) * HW + 4 * q;
+      const f32x4 g = *reinterpret_cast<const f32x4*>(dy + o);
+      const f32x4 xv = *reinterpret_cast<const f32x4*>(x + o);
+      f32x4 yv = {1.f, 1.f, 1.f, 1.f};
+      if (relu) yv = *reinterpret_cast<const f32x4*>(y + o);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float dz = (yv[j] > 0.f) ? g[j] : 0.f;
+        sdz += (double)dz;
+        sdzx += (double)dz * (double)((xv[j] - mean) * invstd);
+      }
+    }
+  } else {
+    const int64_t cnt = (sl.n1 - sl.n0) * HW;
+    for (int64_t e = threadIdx.x; e < cnt; e += blockDim.x) {
+      const int64_t n = sl.n0 + e / HW;
+      const int hw = (int)(e - (e / HW) * HW);
+      const int64_t o = (n * C + c) * HW + hw;
+      const float dz = (!relu || y[o] > 0.f) ? dy[o] : 0.f;
+      sdz += (double)dz;
+      sdzx += (double)dz * (double)((x[o] - mean) * invstd);
+    }
+  }
+  block_sum2(sdz, sdzx, red);
+  if (threadIdx.x == 0) {
+    part[((int64_t)c * S + s) * 2] = sdz;
+    part[((int64_t)c * S + s) * 2 + 1] = sdzx;
+  }
+}
+
+// ---- backward apply ----------------------------------------------------------------------
+template <bool VEC>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
+    const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ x,
+    const float* __restrict__ gamma, const float* __restrict__ save_mean, const float* __restrict__ save_invstd,
+    float* __restrict__ dx, float* __restrict__ dres, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    const double* __restrict__ part, int N, int C, int HW, int S, int relu) {
+  const int s = blockIdx.x, c = blockIdx.y;
+  double sdz = 0.0, sdzx = 0.0;
+  for (int k = 0; k < S; ++k) {
+    sdz += part[((int64_t)c * S + k) * 2];
+    sdzx += part[((int64_t)c * S + k) * 2 + 1];
+  }
+  if (s == 0 && threadIdx.x == 0) {
+    if (dgamma) dgamma[c] = (float)sdzx;
+    if (dbeta) dbeta[c] = (float)sdz;
+  }
+  const double M = (double)N * HW;
+  const float mean = save_mean[c], invstd = save_invstd[c];
+  const float g = gamma ? gamma[c] : 1.f;
+  const float k1 = g * invstd;                    // dx = k1 * (dz - mdz - xhat * mdzx)
+  const float mdz = (float)(sdz / M);
+  const float mdzx = (float)(sdzx / M);
+  const BnSlice sl = slice_of(N, S, s);
+  if (VEC) {
+    const int hw4 = HW >> 2;
+    const int64_t cnt = (sl.n1 - sl.n0) * hw4;
+    for (int64_t e = threadIdx.x; e < cnt; e += blockDim.x) {
+      const int64_t n = sl.n0 + e / hw4;
+      const int q = (int)(e - (e / hw4) * hw4);
+      const int64_t o = (n * C + c) * HW + 4 * q;
+      const f32x4 gy = *reinterpret_cast<const f32x4*>(dy + o);
+      const f32x4 xv = *reinterpret_cast<const f32x4*>(x + o);
+      f32x4 yv = {1.f, 1.f, 1.f, 1.f};
+      if (relu) yv = *reinterpret_cast<const f32x4*>(y + o);
+      f32x4 dz, out;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        dz[j] = (yv[j] > 0.f) ? gy[j] : 0.f;
+        const float xh = (xv[j] - mean) * invstd;
+        out[j] = k1 * (dz[j] - mdz - xh * mdzx);
+      }
+      *reinterpret_cast<f32x4*>(dx + o) = out;
+      if (dres) *reinterpret_cast<f32x4*>(dres + o) = dz;
+    }
+  } else {
+    const int64_t cnt = (sl.n1 - sl.n0) * HW;
+    for (int64_t e = threadIdx.x; e < cnt; e += blockDim.x) {
+      const int64_t n = sl.n0 + e / HW;
+      const int hw = (int)(e - (e / HW) * HW);
+      const int64_t o = (n * C + c) * HW + hw;
+      const float dz = (!relu || y[o] > 0.f) ? dy[o] : 0.f;
+      const float xh = (x[o] - mean) * invstd;
+      dx[o] = k1 * (dz - mdz - xh * mdzx);
+      if (dres) dres[o] = dz;
+    }
+  }
+}
+
+// ----------------------------------- launchers -------------------------------------------
+int bn_slices(int N, int C, int HW) {
+  // ~4 workgroups per CU over the whole launch, >= ~2K elements per workgroup
+  int64_t s = (1024 + C - 1) / C;
+  const int64_t by_work = ((int64_t)N * HW) / 2048;
+  if (s > by_work) s = by_work;
+  if (s > N) s = N;
+  if (s < 1) s = 1;
+  return (int)s;
+}
+
+void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamma, const float* beta,
+                   float* rmean, float* rvar, int64_t* nbt, float* save_mean, float* save_invstd,
+                   double* part, int N, int C, int HW, int S, float eps, float momentum, int relu,
+                   int training, hipStream_t s) {
+  const bool vec = (HW % 4) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 &&
+                   (res == nullptr || ((uintptr_t)res & 15) == 0);
+  const dim3 grid(S, C);
+  if (training) {
+    if (vec) hipLaunchKernelGGL(bn_fwd_stats_kernel<true>, grid, dim3(256), 0, s, x, part, N, C, HW, S);
+    else hipLaunchKernelGGL(bn_fwd_stats_kernel<false>, grid, dim3(256), 0, s, x, part, N, C, HW, S);
+  }
+  if (vec)
+    hipLaunchKernelGGL(bn_fwd_apply_kernel<true>, grid, dim3(256), 0, s, x, res, y, gamma, beta, rmean, rvar, nbt,
+                       save_mean, save_invstd, part, N, C, HW, S, eps, momentum, relu, training);
+  else
+    hipLaunchKernelGGL(bn_fwd_apply_kernel<false>, grid, dim3(256), 0, s, x, res, y, gamma, beta, rmean, rvar, nbt,
+                       save_mean, save_invstd, part, N, C, HW, S, eps, momentum, relu, training);
+}
+
+void launch_bn_bwd(const float* dy, const float* y, const float* x, const float* gamma, const float* save_mean,
+                   const float* save_invstd, float* dx, float* dres, float* dgamma, float* dbeta, double* part,
+                   int N, int C, int HW, int S, int relu, hipStream_t s) {
+  const bool vec = (HW % 4) == 0 && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)x & 15) == 0 &&
+                   ((uintptr_t)dx & 15) == 0 && (!relu || ((uintptr_t)y & 15) == 0) &&
+                   (dres == nullptr || ((uintptr_t)dres & 15) == 0);
+  const dim3 grid(S, C);
+  if (vec) {
+    hipLaunchKernelGGL(bn_bwd_stats_kernel<true>, grid, dim3(256), 0, s, dy, y, x, save_mean, save_invstd, part, N, C,
+                       HW, S, relu);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, grid, dim3(256), 0, s, dy, y, x, gamma, save_mean, save_invstd, dx,
+                       dres, dgamma, dbeta, part, N, C, HW, S, relu);
+  } else {
+    hipLaunchKernelGGL(bn_bwd_stats_kernel<false>, grid, dim3(256), 0, s, dy, y, x, save_mean, save_invstd, part, N,
+                       C, HW, S, relu);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, grid, dim3(256), 0, s, dy, y, x, gamma, save_mean, save_invstd, dx,
+                       dres, dgamma, dbeta, part, N, C, HW, S, relu);
+  }
+}
+
+}  // namespace ndp

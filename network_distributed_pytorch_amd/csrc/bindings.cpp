@@ -246,6 +246,62 @@ void add(torch::Tensor a, torch::Tensor b, torch::Tensor out) {
   check_launch("launch_add");
 }
 
+const float* opt_f32(const c10::optional<torch::Tensor>& t, const char* name) {
+  if (!t.has_value()) return nullptr;
+  check_f32(*t, name);
+  return t->data_ptr<float>();
+}
+
+// fused BN(+res)(+relu) forward; returns nothing, writes y / save_mean / save_invstd
+void bn_fwd(torch::Tensor x, c10::optional<torch::Tensor> res, torch::Tensor y,
+            c10::optional<torch::Tensor> gamma, c10::optional<torch::Tensor> beta,
+            c10::optional<torch::Tensor> rmean, c10::optional<torch::Tensor> rvar,
+            c10::optional<torch::Tensor> nbt, torch::Tensor save_mean, torch::Tensor save_invstd,
+            torch::Tensor part, double eps, double momentum, bool relu, bool training) {
+  check_f32(x, "x"); check_f32(y, "y"); check_f32(save_mean, "save_mean"); check_f32(save_invstd, "save_invstd");
+  check_dev(part, "part");
+  TORCH_CHECK(x.dim() >= 2 && x.sizes() == y.sizes(), "bn_fwd: bad shapes");
+  const int N = (int)x.size(0), C = (int)x.size(1);
+  const int HW = (int)(x.numel() / ((int64_t)N * C));
+  const int S = ndp::bn_slices(N, C, HW);
+  TORCH_CHECK(part.scalar_type() == torch::kFloat64 && part.numel() >= (int64_t)C * S * 2, "bn part too small");
+  TORCH_CHECK(save_mean.numel() >= C && save_invstd.numel() >= C, "bn save buffers too small");
+  if (res.has_value()) TORCH_CHECK(res->sizes() == x.sizes(), "bn residual shape");
+  int64_t* nb = nullptr;
+  if (nbt.has_value()) {
+    check_dev(*nbt, "nbt");
+    TORCH_CHECK(nbt->scalar_type() == torch::kInt64, "num_batches_tracked must be int64");
+    nb = nbt->data_ptr<int64_t>();
+  }
+  ndp::launch_bn_fwd(x.data_ptr<float>(), opt_f32(res, "res"), y.data_ptr<float>(), opt_f32(gamma, "gamma"),
+                     opt_f32(beta, "beta"), const_cast<float*>(opt_f32(rmean, "running_mean")),
+                     const_cast<float*>(opt_f32(rvar, "running_var")), nb, save_mean.data_ptr<float>(),
+                     save_invstd.data_ptr<float>(), part.data_ptr<double>(), N, C, HW, S, (float)eps,
+                     (float)momentum, relu ? 1 : 0, training ? 1 : 0, cur_stream());
+  check_launch("launch_bn_fwd");
+}
+
+void bn_bwd(torch::Tensor dy, c10::optional<torch::Tensor> y, torch::Tensor x, c10::optional<torch::Tensor> gamma,
+            torch::Tensor save_mean, torch::Tensor save_invstd, torch::Tensor dx, c10::optional<torch::Tensor> dres,
+            c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta, torch::Tensor part,
+            bool relu) {
+  check_f32(dy, "dy"); check_f32(x, "x"); check_f32(dx, "dx"); check_dev(part, "part");
+  TORCH_CHECK(dy.sizes() == x.sizes() && dx.sizes() == x.sizes(), "bn_bwd: bad shapes");
+  TORCH_CHECK(!relu || y.has_value(), "bn_bwd: relu needs y");
+  const int N = (int)x.size(0), C = (int)x.size(1);
+  const int HW = (int)(x.numel() / ((int64_t)N * C));
+  const int S = ndp::bn_slices(N, C, HW);
+  TORCH_CHECK(part.scalar_type() == torch::kFloat64 && part.numel() >= (int64_t)C * S * 2, "bn part too small");
+  ndp::launch_bn_bwd(dy.data_ptr<float>(), opt_f32(y, "y"), x.data_ptr<float>(), opt_f32(gamma, "gamma"),
+                     save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(), dx.data_ptr<float>(),
+                     const_cast<float*>(opt_f32(dres, "dres")), const_cast<float*>(opt_f32(dgamma, "dgamma")),
+                     const_cast<float*>(opt_f32(dbeta, "dbeta")), part.data_ptr<double>(), N, C, HW, S,
+                     relu ? 1 : 0, cur_stream());
+  check_launch("launch_bn_bwd");
+}
+
+int bn_slices(int N, int C, int HW) { return ndp::bn_slices(N, C, HW); }
+
 void delay_ns(int64_t ns) { ndp::launch_delay_ns(ns, cur_stream()); }
 
 void checksum(torch::Tensor x, torch::Tensor out) {
@@ -280,5 +336,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sgd_momentum", &sgd_momentum);
   m.def("add", &add);
   m.def("delay_ns", &delay_ns);
+  m.def("bn_fwd", &bn_fwd);
+  m.def("bn_bwd", &bn_bwd);
+  m.def("bn_slices", &bn_slices);
   m.def("checksum", &checksum);
 }

@@ -99,3 +99,16 @@ void launch_delay_ns(int64_t ns, hipStream_t s);
 void launch_checksum(const float* x, int64_t n, double* out, hipStream_t s);
 
 }  // namespace ndp
+
+// ---- fused BatchNorm2d (+residual) (+ReLU), NCHW fp32 (batchnorm.hip) -------------------
+namespace ndp {
+int bn_slices(int N, int C, int HW);
+// part: C * S * 2 doubles of scratch; rmean/rvar/nbt may be null; training=0 uses running stats
+void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamma, const float* beta,
+                   float* rmean, float* rvar, int64_t* nbt, float* save_mean, float* save_invstd,
+                   double* part, int N, int C, int HW, int S, float eps, float momentum, int relu,
+                   int training, hipStream_t s);
+void launch_bn_bwd(const float* dy, const float* y, const float* x, const float* gamma, const float* save_mean,
+                   const float* save_invstd, float* dx, float* dres, float* dgamma, float* dbeta, double* part,
+                   int N, int C, int HW, int S, int relu, hipStream_t s);
+}  // namespace ndp

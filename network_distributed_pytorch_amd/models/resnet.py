@@ -10,8 +10,10 @@ Q-init RNG order match the reference exactly), same init (Kaiming-normal fan_out
 BN = (1, 0)).  Weights are random (the GPU box has no network for pretrained downloads);
 checkpoints written by torchvision load with ``load_state_dict`` unchanged.
 
-MI355X notes: convolutions/BN run on PyTorch-ROCm (MIOpen); ``channels_last`` is supported
-by the training loops (``--channels-last``) and measured in ``profiles/``.
+MI355X notes: convolutions run on PyTorch-ROCm (MIOpen).  Every BatchNorm is a
+:class:`~network_distributed_pytorch_amd.ops.batchnorm.BatchNormAct2d` (``fused_bn=True``):
+BN, the residual add and the ReLU of each block run as two fused gfx950 kernels per
+direction (same parameters/buffers/state_dict keys as ``nn.BatchNorm2d``).
 """
 from __future__ import annotations
 
@@ -19,6 +21,8 @@ from typing import List, Optional, Type, Union
 
 import torch
 import torch.nn as nn
+
+from ..ops.batchnorm import BatchNormAct2d
 
 __all__ = ["ResNet", "BasicBlock", "Bottleneck", "resnet18", "resnet34", "resnet50", "resnet101",
            "resnet152", "build_resnet"]
@@ -35,18 +39,23 @@ def conv1x1(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
 class BasicBlock(nn.Module):
     expansion = 1
 
-    def __init__(self, inplanes: int, planes: int, stride: int = 1, downsample: Optional[nn.Module] = None):
+    def __init__(self, inplanes: int, planes: int, stride: int = 1, downsample: Optional[nn.Module] = None,
+                 norm=nn.BatchNorm2d):
         super().__init__()
         self.conv1 = conv3x3(inplanes, planes, stride)
-        self.bn1 = nn.BatchNorm2d(planes)
+        self.bn1 = norm(planes)
         self.relu = nn.ReLU(inplace=True)
         self.conv2 = conv3x3(planes, planes)
-        self.bn2 = nn.BatchNorm2d(planes)
+        self.bn2 = norm(planes)
         self.downsample = downsample
         self.stride = stride
+        self.fused = norm is BatchNormAct2d
 
     def forward(self, x):
         identity = x if self.downsample is None else self.downsample(x)
+        if self.fused:  # conv -> BN+ReLU ; conv -> BN + identity + ReLU (fused kernels)
+            out = self.bn1(self.conv1(x), relu=True)
+            return self.bn2(self.conv2(out), residual=identity, relu=True)
         out = self.relu(self.bn1(self.conv1(x)))
         out = self.bn2(self.conv2(out))
         return self.relu(out + identity)
@@ -55,20 +64,26 @@ class BasicBlock(nn.Module):
 class Bottleneck(nn.Module):
     expansion = 4
 
-    def __init__(self, inplanes: int, planes: int, stride: int = 1, downsample: Optional[nn.Module] = None):
+    def __init__(self, inplanes: int, planes: int, stride: int = 1, downsample: Optional[nn.Module] = None,
+                 norm=nn.BatchNorm2d):
         super().__init__()
         self.conv1 = conv1x1(inplanes, planes)
-        self.bn1 = nn.BatchNorm2d(planes)
+        self.bn1 = norm(planes)
         self.conv2 = conv3x3(planes, planes, stride)
-        self.bn2 = nn.BatchNorm2d(planes)
+        self.bn2 = norm(planes)
         self.conv3 = conv1x1(planes, planes * self.expansion)
-        self.bn3 = nn.BatchNorm2d(planes * self.expansion)
+        self.bn3 = norm(planes * self.expansion)
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
         self.stride = stride
+        self.fused = norm is BatchNormAct2d
 
     def forward(self, x):
         identity = x if self.downsample is None else self.downsample(x)
+        if self.fused:
+            out = self.bn1(self.conv1(x), relu=True)
+            out = self.bn2(self.conv2(out), relu=True)
+            return self.bn3(self.conv3(out), residual=identity, relu=True)
         out = self.relu(self.bn1(self.conv1(x)))
         out = self.relu(self.bn2(self.conv2(out)))
         out = self.bn3(self.conv3(out))
@@ -76,11 +91,14 @@ class Bottleneck(nn.Module):
 
 
 class ResNet(nn.Module):
-    def __init__(self, block: Type[Union[BasicBlock, Bottleneck]], layers: List[int], num_classes: int = 1000):
+    def __init__(self, block: Type[Union[BasicBlock, Bottleneck]], layers: List[int], num_classes: int = 1000,
+                 fused_bn: bool = True):
         super().__init__()
+        self.norm = BatchNormAct2d if fused_bn else nn.BatchNorm2d
+        self.fused = fused_bn
         self.inplanes = 64
         self.conv1 = nn.Conv2d(3, 64, kernel_size=7, stride=2, padding=3, bias=False)
-        self.bn1 = nn.BatchNorm2d(64)
+        self.bn1 = self.norm(64)
         self.relu = nn.ReLU(inplace=True)
         self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
         self.layer1 = self._make_layer(block, 64, layers[0])
@@ -92,7 +110,7 @@ class ResNet(nn.Module):
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
-            elif isinstance(m, nn.BatchNorm2d):
+            elif isinstance(m, nn.BatchNorm2d):  # includes BatchNormAct2d
                 nn.init.constant_(m.weight, 1)
                 nn.init.constant_(m.bias, 0)
 
@@ -100,15 +118,18 @@ class ResNet(nn.Module):
         downsample = None
         if stride != 1 or self.inplanes != planes * block.expansion:
             downsample = nn.Sequential(conv1x1(self.inplanes, planes * block.expansion, stride),
-                                       nn.BatchNorm2d(planes * block.expansion))
-        layers = [block(self.inplanes, planes, stride, downsample)]
+                                       self.norm(planes * block.expansion))
+        layers = [block(self.inplanes, planes, stride, downsample, norm=self.norm)]
         self.inplanes = planes * block.expansion
         for _ in range(1, blocks):
-            layers.append(block(self.inplanes, planes))
+            layers.append(block(self.inplanes, planes, norm=self.norm))
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        if self.fused:
+            x = self.maxpool(self.bn1(self.conv1(x), relu=True))
+        else:
+            x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)
@@ -123,11 +144,11 @@ _CFG = {
 }
 
 
-def build_resnet(depth: int, num_classes: int = 1000) -> ResNet:
+def build_resnet(depth: int, num_classes: int = 1000, fused_bn: bool = True) -> ResNet:
     if depth not in _CFG:
         raise ValueError(f"unsupported ResNet depth {depth}; choose from {sorted(_CFG)}")
     block, layers = _CFG[depth]
-    return ResNet(block, layers, num_classes=num_classes)
+    return ResNet(block, layers, num_classes=num_classes, fused_bn=fused_bn)
 
 
 def resnet18(num_classes: int = 1000, **_) -> ResNet:

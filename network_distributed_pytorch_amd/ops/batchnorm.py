@@ -1,0 +1,97 @@
+"""Fused BatchNorm2d (+ residual add) (+ ReLU) — gfx950 kernels with a torch fallback.
+
+:class:`BatchNormAct2d` is a drop-in ``nn.BatchNorm2d`` (same parameters, buffers and
+``state_dict`` keys, so torchvision checkpoints load unchanged) whose forward optionally
+fuses the residual add and the ReLU that follow BN in every ResNet block:
+``y = relu(bn(x) + residual)``.  On device it runs two kernels per direction
+(csrc/batchnorm.hip) instead of MIOpen BN + ATen ReLU + ATen add + the
+``num_batches_tracked`` increment; on CPU it computes the same math with torch ops.
+Training statistics follow ``torch.nn.BatchNorm2d`` exactly (biased variance for the
+normalisation, unbiased in ``running_var``, momentum 0.1).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ._ext import ext
+
+__all__ = ["BatchNormAct2d", "bn_act"]
+
+
+class _BNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, res, weight, bias, running_mean, running_var, nbt, part, eps, momentum, relu):
+        X = ext()
+        x = x.contiguous()
+        if res is not None:
+            res = res.contiguous()
+        C = x.shape[1]
+        y = torch.empty_like(x)
+        save_mean = torch.empty(C, device=x.device, dtype=torch.float32)
+        save_invstd = torch.empty(C, device=x.device, dtype=torch.float32)
+        X.bn_fwd(x, res, y, weight, bias, running_mean, running_var, nbt, save_mean, save_invstd, part,
+                 float(eps), float(momentum), bool(relu), True)
+        ctx.relu = bool(relu)
+        ctx.has_res = res is not None
+        ctx.has_w = weight is not None
+        ctx.save_for_backward(x, y if relu else None, weight, save_mean, save_invstd, part)
+        ctx.mark_non_differentiable(save_mean, save_invstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, weight, save_mean, save_invstd, part = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(x) if ctx.has_res else None
+        dgamma = torch.empty_like(weight) if ctx.has_w else None
+        dbeta = torch.empty_like(weight) if ctx.has_w else None
+        ext().bn_bwd(dy, y, x, weight, save_mean, save_invstd, dx, dres, dgamma, dbeta, part, ctx.relu)
+        return dx, dres, dgamma, dbeta, None, None, None, None, None, None, None
+
+
+def bn_act(x, weight, bias, running_mean, running_var, nbt, part, training, momentum, eps,
+           residual=None, relu=False):
+    if x.is_cuda:
+        assert x.dtype == torch.float32, "fused BN is fp32 (the reference dtype)"
+        if training:
+            return _BNActFn.apply(x, residual, weight, bias, running_mean, running_var, nbt, part, eps,
+                                  momentum, relu)
+        y = torch.empty_like(x := x.contiguous())
+        C = x.shape[1]
+        sm = torch.empty(C, device=x.device)
+        si = torch.empty(C, device=x.device)
+        ext().bn_fwd(x, residual.contiguous() if residual is not None else None, y, weight, bias, running_mean,
+                     running_var, None, sm, si, part, float(eps), 0.0, bool(relu), False)
+        return y
+    y = F.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps)
+    if training and nbt is not None:
+        nbt.add_(1)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y) if relu else y
+
+
+class BatchNormAct2d(nn.BatchNorm2d):
+    """``nn.BatchNorm2d`` with optional fused residual add and ReLU (same state_dict)."""
+
+    def __init__(self, num_features: int, eps: float = 1e-5, momentum: float = 0.1, **kw):
+        super().__init__(num_features, eps=eps, momentum=momentum, **kw)
+        # per-(channel, slice) fp64 partials: C * S * 2 with S <= ceil(1024 / C) (bn_slices)
+        self.register_buffer("_part", torch.zeros((num_features + 1024) * 2, dtype=torch.float64),
+                             persistent=False)
+
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, relu: bool = False):
+        if self.momentum is None or not self.track_running_stats:
+            y = super().forward(x)
+            if residual is not None:
+                y = y + residual
+            return F.relu(y) if relu else y
+        training = self.training
+        return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var,
+                      self.num_batches_tracked if training else None, self._part, training, self.momentum,
+                      self.eps, residual, relu)

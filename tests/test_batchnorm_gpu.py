@@ -1,0 +1,81 @@
+"""Fused BN(+residual)(+ReLU) gfx950 kernels vs torch.nn.BatchNorm2d (fp32 reference)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from network_distributed_pytorch_amd import ops
+from network_distributed_pytorch_amd.models import build_resnet
+from network_distributed_pytorch_amd.ops.batchnorm import BatchNormAct2d
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("shape", [(512, 64, 8, 8), (64, 128, 4, 4), (32, 512, 1, 1), (16, 24, 7, 7),
+                                   (8, 64, 16, 16), (3, 5, 2, 3)])
+@pytest.mark.parametrize("res,relu", [(False, False), (False, True), (True, True)])
+def test_bn_act_train_fwd_bwd(device, shape, res, relu):
+    assert ops.native_available()
+    torch.manual_seed(0)
+    C = shape[1]
+    ref = torch.nn.BatchNorm2d(C).to(device)
+    ours = BatchNormAct2d(C).to(device)
+    with torch.no_grad():
+        ref.weight.uniform_(0.5, 1.5)
+        ref.bias.uniform_(-0.5, 0.5)
+    ours.load_state_dict(ref.state_dict())
+    x = (torch.randn(shape, device=device) * 2 + 0.3).requires_grad_(True)
+    x2 = x.detach().clone().requires_grad_(True)
+    r = torch.randn(shape, device=device, requires_grad=True) if res else None
+    r2 = r.detach().clone().requires_grad_(True) if res else None
+    y_ref = ref(x)
+    if res:
+        y_ref = y_ref + r
+    if relu:
+        y_ref = F.relu(y_ref)
+    y = ours(x2, residual=r2, relu=relu)
+    assert torch.allclose(y, y_ref, atol=2e-5, rtol=1e-4), (y - y_ref).abs().max()
+    g = torch.randn(shape, device=device)
+    y_ref.backward(g)
+    y.backward(g)
+    assert torch.allclose(x2.grad, x.grad, atol=5e-5, rtol=1e-3), (x2.grad - x.grad).abs().max()
+    assert torch.allclose(ours.weight.grad, ref.weight.grad, atol=1e-3, rtol=1e-4)
+    assert torch.allclose(ours.bias.grad, ref.bias.grad, atol=1e-3, rtol=1e-4)
+    if res:
+        assert torch.allclose(r2.grad, r.grad, atol=1e-6)
+    assert torch.allclose(ours.running_mean, ref.running_mean, atol=1e-6)
+    assert torch.allclose(ours.running_var, ref.running_var, atol=1e-5, rtol=1e-5)
+    assert int(ours.num_batches_tracked) == int(ref.num_batches_tracked) == 1
+    # eval mode uses running statistics
+    ref.eval()
+    ours.eval()
+    with torch.no_grad():
+        ye = ours(x, relu=relu)
+        yr = F.relu(ref(x)) if relu else ref(x)
+    assert torch.allclose(ye, yr, atol=2e-5, rtol=1e-4)
+
+
+def test_bn_deterministic(device):
+    torch.manual_seed(1)
+    m = BatchNormAct2d(64).to(device)
+    x = torch.randn(512, 64, 8, 8, device=device)
+    a = m(x, relu=True)
+    b = m(x, relu=True)
+    assert torch.equal(a, b)
+
+
+def test_resnet18_fused_matches_unfused(device):
+    torch.manual_seed(0)
+    fused = build_resnet(18, 10, fused_bn=True).to(device)
+    plain = build_resnet(18, 10, fused_bn=False).to(device)
+    plain.load_state_dict(fused.state_dict())
+    assert list(fused.state_dict()) == list(plain.state_dict())
+    x = torch.randn(64, 3, 32, 32, device=device)
+    y = torch.randint(0, 10, (64,), device=device)
+    lf = F.cross_entropy(fused(x), y)
+    lp = F.cross_entropy(plain(x), y)
+    assert torch.allclose(lf, lp, atol=1e-4, rtol=1e-4)
+    lf.backward()
+    lp.backward()
+    for (n, a), b in zip(fused.named_parameters(), plain.parameters()):
+        scale = b.grad.abs().max().item() + 1e-8
+        assert torch.allclose(a.grad, b.grad, atol=2e-3 * scale, rtol=1e-2), n
