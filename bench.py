@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--rank", type=int, default=4)
     ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--channels-last", action="store_true")
+    ap.add_argument("--no-fused-bn", action="store_true", help="use nn.BatchNorm2d + ReLU (MIOpen) instead")
     ap.add_argument("--link", default="none", help="none|1g|10g|100g link emulation")
     ap.add_argument("--bucket-mb", type=float, default=25.0)
     ap.add_argument("--json-out", default=None)
@@ -92,7 +93,7 @@ def main():
     torch.manual_seed(714)
     torch.backends.cudnn.benchmark = True
 
-    model = build_model(args.model, args.num_classes).to(device)
+    model = build_model(args.model, args.num_classes, fused_bn=not args.no_fused_bn).to(device)
     if args.channels_last:
         model = model.to(memory_format=torch.channels_last)
     link = None if args.link == "none" else LINK_PRESETS[args.link]

@@ -63,24 +63,16 @@ __global__ __launch_bounds__(256) void psgd_p_kernel(const MatGeom* __restrict__
   const int r = g.r;
   const int klen = it.k1 - it.k0;
   const float* Q = q_warm + g.q_off + (int64_t)it.k0 * r;
-  for (int idx = tid; idx < kPK * CW; idx += 256) {
-    const int b = idx / CW, c = idx - (idx / CW) * CW;
-    float v = 0.f;
-    if (b < klen && c < r) v = Q[b * r + c];
-    smem[c * LD + b] = v;
-  }
-  __syncthreads();
-
   const int a0 = it.row0 + wave * 16;
-  if (a0 >= g.n) return;  // no barrier below
   const int arow = a0 + (lane & 15);
   const bool rowok = arow < g.n;
   const int kq = 4 * (lane >> 4);
   const int64_t rowbase = (int64_t)arow * g.m + it.k0;
 
+  // issue the HBM stream (M = g [+ e]) first, so it is in flight while Q is staged
   f32x4 mv[16];
+  f32x4 ev[16];
   if (g.vec) {
-    f32x4 ev[16];
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       const int kl = 16 * s + kq;
@@ -91,6 +83,17 @@ __global__ __launch_bounds__(256) void psgd_p_kernel(const MatGeom* __restrict__
         if (fuse_ef) ev[s] = ld4(pt.e + rowbase + kl);
       }
     }
+  }
+  for (int idx = tid; idx < kPK * CW; idx += 256) {
+    const int b = idx / CW, c = idx - (idx / CW) * CW;
+    float v = 0.f;
+    if (b < klen && c < r) v = Q[b * r + c];
+    smem[c * LD + b] = v;
+  }
+  __syncthreads();
+  if (a0 >= g.n) return;  // no barrier below
+
+  if (g.vec) {
     if (fuse_ef) {
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
@@ -280,12 +283,28 @@ __global__ __launch_bounds__(256) void psgd_update_kernel(
   const int aL = a0 + (lane & 15);
   const int kq = lane >> 4;
   const int nk = (r + 3) >> 2;
+  const bool rowok = aL < n;
+  const int64_t ro = (int64_t)aL * m;
+  // prefetch the HBM stream (M, momentum, parameters) before the MFMA chain
+  f32x4 Mv[4], Mm[4], Xv[4];
+  if (g.vec) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int b = it.col0 + 16 * t + 4 * kq;
+      const bool ok = rowok && b < m;
+      Mv[t] = ok ? ld4(pt.mread + ro + b) : f32x4{0.f, 0.f, 0.f, 0.f};
+      if (mode != 0) {
+        Mm[t] = ok ? ld4(pt.mom + ro + b) : f32x4{0.f, 0.f, 0.f, 0.f};
+        Xv[t] = ok ? ld4(pt.x + ro + b) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  }
   f32x4 acc[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int kc = 0; kc < nk; ++kc) {
     const int c = 4 * kc + kq;
-    const float bv = (aL < n && c < r) ? P[(int64_t)aL * r + c] : 0.f;
+    const float bv = (rowok && c < r) ? P[(int64_t)aL * r + c] : 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int b = it.col0 + 16 * t + (lane & 15);
@@ -293,21 +312,20 @@ __global__ __launch_bounds__(256) void psgd_update_kernel(
       acc[t] = mfma4(av, bv, acc[t]);
     }
   }
-  if (aL >= n) return;
-  const int64_t ro = (int64_t)aL * m;
+  if (!rowok) return;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int b = it.col0 + 16 * t + 4 * kq;
     if (b >= m) continue;
     const f32x4 o = acc[t];
     if (g.vec) {
-      const f32x4 M = ld4(pt.mread + ro + b);
+      const f32x4 M = Mv[t];
       if (mode == 0) {
         st4(pt.out + ro + b, o);
         st4(pt.mem + ro + b, M - o);
       } else {
-        f32x4 mm = ld4(pt.mom + ro + b);
-        f32x4 xx = ld4(pt.x + ro + b);
+        f32x4 mm = Mm[t];
+        f32x4 xx = Xv[t];
         st4(pt.e + ro + b, M - o);
 #pragma unroll
         for (int j = 0; j < 4; ++j) mm[j] = __fadd_rn(__fmul_rn(mm[j], momentum), o[j]);

@@ -146,3 +146,18 @@ def test_engine_tasks(tmp_path, task, grad_sync, extra):
     assert len(out["epoch_losses"]) == 2 and all(np.isfinite(out["epoch_losses"]))
     assert os.path.exists(tmp_path / "ck" / "last.pt")
     assert (tmp_path / "log.jsonl").read_text().count("\n") == 3
+
+
+def test_batchnorm_act_cpu_matches_torch():
+    from network_distributed_pytorch_amd.ops.batchnorm import BatchNormAct2d
+    torch.manual_seed(0)
+    ref = torch.nn.BatchNorm2d(6)
+    ours = BatchNormAct2d(6)
+    ours.load_state_dict(ref.state_dict())
+    assert list(ours.state_dict()) == list(ref.state_dict())
+    x = torch.randn(4, 6, 5, 5)
+    r = torch.randn(4, 6, 5, 5)
+    y = ours(x, residual=r, relu=True)
+    y_ref = torch.relu(ref(x) + r)
+    assert torch.allclose(y, y_ref, atol=1e-6)
+    assert torch.equal(ours.running_mean, ref.running_mean) and int(ours.num_batches_tracked) == 1
