@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--channels-last", action="store_true")
     ap.add_argument("--no-fused-bn", action="store_true", help="use nn.BatchNorm2d + ReLU (MIOpen) instead")
+    ap.add_argument("--amp", choices=["none", "bf16"], default="none",
+                    help="opt-in bf16 autocast for model math (NOT the headline: the reference is fp32)")
     ap.add_argument("--link", default="none", help="none|1g|10g|100g link emulation")
     ap.add_argument("--bucket-mb", type=float, default=25.0)
     ap.add_argument("--json-out", default=None)
@@ -64,6 +66,8 @@ def parse():
 
 
 def metric_name(args) -> str:
+    if args.amp != "none":
+        return f"[non-headline, {args.amp} autocast] " + metric_name(argparse.Namespace(**{**vars(args), "amp": "none"}))
     if args.model == "resnet18" and args.reducer.startswith("powersgd") and args.rank == 4:
         return METRIC
     what = "DistilBERT IMDb" if args.model.startswith("distilbert") else f"{args.model} CIFAR10"
@@ -126,6 +130,13 @@ def main():
 
         def loss_of(b):
             return crit(model(b["x"]), b["y"])
+
+    if args.amp == "bf16":  # opt-in mixed precision: bf16 model math, fp32 params/grads/reducer
+        fp32_loss_of = loss_of
+
+        def loss_of(b):
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                return fp32_loss_of(b).float()
 
     loss_acc = torch.zeros((), device=device)
 
@@ -195,7 +206,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": "fp32" if args.amp == "none" else "bf16-autocast (fp32 params/grads/reducer)",
             "data": ("synthetic IMDb-shape (512-token ids + masks, 2 labels)" if is_bert else
                      "synthetic CIFAR-10-shape (3x32x32, 10 labels)") + ", random-init weights",
             "bytes_per_step": sync.bytes_per_step,

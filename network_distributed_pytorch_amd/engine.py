@@ -34,7 +34,7 @@ from .parallel.trainer import build_grad_sync
 from .utils.checkpoint import load_checkpoint, save_checkpoint
 from .utils.data import DeviceLoader, SyntheticCIFAR10, SyntheticIMDb, train_val_split
 from .utils.divergence import ReplicaChecker
-from .utils.metrics import JsonlLogger, print_epoch
+from .utils.metrics import JsonlLogger, PhaseTimer, print_epoch
 from .utils.partition_helper import DataPartitioner
 
 __all__ = ["setup", "run_task", "cleanup", "device_for", "default_config"]
@@ -49,7 +49,7 @@ def default_config(**over) -> Dict[str, Any]:
         task="cifar", model="resnet18", num_classes=1000, global_batch=512, grad_sync="powersgd",
         dataset_size=None, data_seed=0, max_steps_per_epoch=None, graph_mode="none", link="none",
         bucket_mb=25.0, checkpoint_dir=None, resume=None, log_file=None, check_replicas_every=0,
-        write_grad=False, verbose=True,
+        write_grad=False, verbose=True, trace_phases=False,
     )
     cfg.update(over)
     return cfg
@@ -215,6 +215,7 @@ def run_task(config) -> Dict[str, Any]:
             loss_static.copy_(loss.detach())
         runner = StepRunner(pre, sync, mode=graph_mode)
 
+    timer = PhaseTimer() if (config.get("trace_phases") and runner is None) else None
     losses = []
     step = 0
     t_start = time.perf_counter()
@@ -233,6 +234,20 @@ def run_task(config) -> Dict[str, Any]:
                     _copy_batch(static["batch"], batch)
                 runner()
                 epoch_loss += loss_static
+            elif timer is not None:  # eager + per-phase HIP-event tracing
+                sync.zero_grad()
+                with timer.phase("forward"):
+                    loss = loss_fn(batch)
+                epoch_loss += loss.detach()
+                with timer.phase("backward"):
+                    loss.backward()
+                if hasattr(sync, "phases"):
+                    for fn, is_comm in sync.phases():
+                        with timer.phase(("comm:" if is_comm else "compute:") + fn.__name__):
+                            fn()
+                else:
+                    with timer.phase("grad_sync+update"):
+                        sync.step()
             else:
                 sync.zero_grad()
                 loss = loss_fn(batch)
@@ -250,7 +265,8 @@ def run_task(config) -> Dict[str, Any]:
             print_epoch(rank, epoch, mean)
             print(">>>>> Rank ", rank, ", epoch ", epoch, " Finished...\n", flush=True)
         logger.log(kind="epoch", epoch=epoch, mean_loss=mean, steps=i, num_batches=num_batches,
-                   bytes_per_step=getattr(sync, "bytes_per_step", None), comm=comm.stats.as_dict())
+                   bytes_per_step=getattr(sync, "bytes_per_step", None), comm=comm.stats.as_dict(),
+                   phase_ms=timer.summary() if timer is not None else None)
         if config.get("checkpoint_dir"):
             save_checkpoint(os.path.join(config["checkpoint_dir"], "last.pt"), model, sync, epoch=epoch, step=step)
     if device.type == "cuda":

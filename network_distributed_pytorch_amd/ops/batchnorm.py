@@ -57,7 +57,9 @@ class _BNActFn(torch.autograd.Function):
 def bn_act(x, weight, bias, running_mean, running_var, nbt, part, training, momentum, eps,
            residual=None, relu=False):
     if x.is_cuda:
-        assert x.dtype == torch.float32, "fused BN is fp32 (the reference dtype)"
+        if x.dtype != torch.float32:  # bf16 autocast: normalise in fp32 (stats are fp64 anyway)
+            x = x.float()
+            residual = residual.float() if residual is not None else None
         if training:
             return _BNActFn.apply(x, residual, weight, bias, running_mean, running_var, nbt, part, eps,
                                   momentum, relu)

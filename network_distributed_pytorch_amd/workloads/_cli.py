@@ -42,6 +42,7 @@ def build_parser(default_world: int, world_required: bool = False) -> argparse.A
     p.add_argument("-dataset_size", type=int, default=None)
     p.add_argument("-check_replicas", type=int, default=None, help="replica checksum every N steps")
     p.add_argument("-toy_steps", type=int, default=None, help="ddp_guide: toy-MLP dense-DP steps")
+    p.add_argument("-trace", action="store_true", help="per-phase HIP-event timings into the JSONL log")
     p.add_argument("-quiet", action="store_true")
     return p
 
@@ -68,6 +69,8 @@ def apply_args(ddp_init: ModuleType, args, rank: int, world: int, cuda: Optional
             c[k] = v
     if args.quiet:
         c["verbose"] = False
+    if args.trace:
+        c["trace_phases"] = True
 
 
 def _spawned(rank, world, module_name, argv):
