@@ -52,6 +52,21 @@ struct BnSlice {
   int64_t n0, n1;
 };
 
+// Visit every access of one (channel, slice): W = floats per access (4 or 1).  When a row's
+// HW/W accesses divide the 256 threads, each thread owns a fixed column q and strides
+// over rows with 32-bit math (no per-element 64-bit division).
+template <int W, typename F>
+__device__ __forceinline__ void for_slice(int64_t n0, int64_t n1, int C, int c, int HW, F f) {
+  const int per = HW / W;
+  if (per <= 256 && (256 % per) == 0) {
+    const int q = (int)threadIdx.x % per, r = (int)threadIdx.x / per, step = 256 / per;
+    for (int64_t n = n0 + r; n < n1; n += step) f((n * C + c) * HW + W * q);
+  } else {
+    for (int64_t n = n0; n < n1; ++n)
+      for (int q = threadIdx.x; q < per; q += 256) f((n * C + c) * HW + W * q);
+  }
+}
+
 __device__ __forceinline__ BnSlice slice_of(int N, int S, int s) {
   const int64_t base = N / S, rem = N % S;
   const int64_t n0 = s * base + (s < rem ? s : rem);
@@ -67,27 +82,20 @@ __global__ __launch_bounds__(256) void bn_fwd_stats_kernel(const float* __restri
   const BnSlice sl = slice_of(N, S, s);
   double sum = 0.0, sq = 0.0;
   if (VEC) {
-    const int hw4 = HW >> 2;
-    const int64_t cnt = (sl.n1 - sl.n0) * hw4;
-    for (int64_t e = threadIdx.x; e < cnt; e += blockDim.x) {
-      const int64_t n = sl.n0 + e / hw4;
-      const int q = (int)(e - (e / hw4) * hw4);
-      const f32x4 v = *reinterpret_cast<const f32x4*>(x + (n * C + c) * HW + 4 * q);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        sum += (double)v[j];
-        sq += (double)v[j] * (double)v[j];
-      }
-    }
+    for_slice<4>(sl.n0, sl.n1, C, c, HW, [&](int64_t o) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(x + o);
+      // fp32 pair sums first (exact enough), fp64 across the slice
+      const float s4 = (v[0] + v[1]) + (v[2] + v[3]);
+      const float q4 = (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]);
+      sum += (double)s4;
+      sq += (double)q4;
+    });
   } else {
-    const int64_t cnt = (sl.n1 - sl.n0) * HW;
-    for (int64_t e = threadIdx.x; e < cnt; e += blockDim.x) {
-      const int64_t n = sl.n0 + e / HW;
-      const int hw = (int)(e - (e / HW) * HW);
-      const double v = (double)x[(n * C + c) * HW + hw];
+    for_slice<1>(sl.n0, sl.n1, C, c, HW, [&](int64_t o) {
+      const double v = (double)x[o];
       sum += v;
       sq += v * v;
-    }
+    });
   }
   block_sum2(sum, sq, red);
   if (threadIdx.x == 0) {
@@ -136,31 +144,22 @@ __global__ __launch_bounds__(256) void bn_fwd_apply_kernel(
   const float shift = (beta ? beta[c] : 0.f) - mean * scale;
   const BnSlice sl = slice_of(N, S, s);
   if (VEC) {
-    const int hw4 = HW >> 2;
-    const int64_t cnt = (sl.n1 - sl.n0) * hw4;
-    for (int64_t e = threadIdx.x; e < cnt; e += blockDim.x) {
-      const int64_t n = sl.n0 + e / hw4;
-      const int q = (int)(e - (e / hw4) * hw4);
-      const int64_t o = (n * C + c) * HW + 4 * q;
+    for_slice<4>(sl.n0, sl.n1, C, c, HW, [&](int64_t o) {
       f32x4 v = *reinterpret_cast<const f32x4*>(x + o);
       f32x4 r = {0.f, 0.f, 0.f, 0.f};
       if (res) r = *reinterpret_cast<const f32x4*>(res + o);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        float z = fmaf(v[j], scale, shift) + r[j];
+        const float z = fmaf(v[j], scale, shift) + r[j];
         v[j] = relu ? fmaxf(z, 0.f) : z;
       }
       *reinterpret_cast<f32x4*>(y + o) = v;
-    }
+    });
   } else {
-    const int64_t cnt = (sl.n1 - sl.n0) * HW;
-    for (int64_t e = threadIdx.x; e < cnt; e += blockDim.x) {
-      const int64_t n = sl.n0 + e / HW;
-      const int hw = (int)(e - (e / HW) * HW);
-      const int64_t o = (n * C + c) * HW + hw;
-      float z = fmaf(x[o], scale, shift) + (res ? res[o] : 0.f);
+    for_slice<1>(sl.n0, sl.n1, C, c, HW, [&](int64_t o) {
+      const float z = fmaf(x[o], scale, shift) + (res ? res[o] : 0.f);
       y[o] = relu ? fmaxf(z, 0.f) : z;
-    }
+    });
   }
 }
 
@@ -178,33 +177,27 @@ __global__ __launch_bounds__(256) void bn_bwd_stats_kernel(const float* __restri
   const float mean = save_mean[c], invstd = save_invstd[c];
   double sdz = 0.0, sdzx = 0.0;
   if (VEC) {
-    const int hw4 = HW >> 2;
-    const int64_t cnt = (sl.n1 - sl.n0) * hw4;
-    for (int64_t e = threadIdx.x; e < cnt; e += blockDim.x) {
-      const int64_t n = sl.n0 + e / hw4;
-      const int q = (int)(e - (e / hw4) * hw4);
-      const int64_t o = (n * C + c) * HW + 4 * q;
+    for_slice<4>(sl.n0, sl.n1, C, c, HW, [&](int64_t o) {
       const f32x4 g = *reinterpret_cast<const f32x4*>(dy + o);
       const f32x4 xv = *reinterpret_cast<const f32x4*>(x + o);
       f32x4 yv = {1.f, 1.f, 1.f, 1.f};
       if (relu) yv = *reinterpret_cast<const f32x4*>(y + o);
+      float a = 0.f, b = 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float dz = (yv[j] > 0.f) ? g[j] : 0.f;
-        sdz += (double)dz;
-        sdzx += (double)dz * (double)((xv[j] - mean) * invstd);
+        a += dz;
+        b += dz * ((xv[j] - mean) * invstd);
       }
-    }
+      sdz += (double)a;
+      sdzx += (double)b;
+    });
   } else {
-    const int64_t cnt = (sl.n1 - sl.n0) * HW;
-    for (int64_t e = threadIdx.x; e < cnt; e += blockDim.x) {
-      const int64_t n = sl.n0 + e / HW;
-      const int hw = (int)(e - (e / HW) * HW);
-      const int64_t o = (n * C + c) * HW + hw;
+    for_slice<1>(sl.n0, sl.n1, C, c, HW, [&](int64_t o) {
       const float dz = (!relu || y[o] > 0.f) ? dy[o] : 0.f;
       sdz += (double)dz;
       sdzx += (double)dz * (double)((x[o] - mean) * invstd);
-    }
+    });
   }
   block_sum2(sdz, sdzx, red);
   if (threadIdx.x == 0) {
@@ -238,12 +231,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   const float mdzx = (float)(sdzx / M);
   const BnSlice sl = slice_of(N, S, s);
   if (VEC) {
-    const int hw4 = HW >> 2;
-    const int64_t cnt = (sl.n1 - sl.n0) * hw4;
-    for (int64_t e = threadIdx.x; e < cnt; e += blockDim.x) {
-      const int64_t n = sl.n0 + e / hw4;
-      const int q = (int)(e - (e / hw4) * hw4);
-      const int64_t o = (n * C + c) * HW + 4 * q;
+    for_slice<4>(sl.n0, sl.n1, C, c, HW, [&](int64_t o) {
       const f32x4 gy = *reinterpret_cast<const f32x4*>(dy + o);
       const f32x4 xv = *reinterpret_cast<const f32x4*>(x + o);
       f32x4 yv = {1.f, 1.f, 1.f, 1.f};
@@ -257,18 +245,14 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
       }
       *reinterpret_cast<f32x4*>(dx + o) = out;
       if (dres) *reinterpret_cast<f32x4*>(dres + o) = dz;
-    }
+    });
   } else {
-    const int64_t cnt = (sl.n1 - sl.n0) * HW;
-    for (int64_t e = threadIdx.x; e < cnt; e += blockDim.x) {
-      const int64_t n = sl.n0 + e / HW;
-      const int hw = (int)(e - (e / HW) * HW);
-      const int64_t o = (n * C + c) * HW + hw;
+    for_slice<1>(sl.n0, sl.n1, C, c, HW, [&](int64_t o) {
       const float dz = (!relu || y[o] > 0.f) ? dy[o] : 0.f;
       const float xh = (x[o] - mean) * invstd;
       dx[o] = k1 * (dz - mdz - xh * mdzx);
       if (dres) dres[o] = dz;
-    }
+    });
   }
 }
 
