@@ -1,0 +1,122 @@
+"""Small-spatial convolutions as exact dense GEMMs ("Toeplitz" convolution).
+
+ResNet on 32x32 inputs runs layer3 / layer4 at 4x4 -> 2x2 -> 1x1 feature maps.  There,
+MIOpen's fp32 Winograd / implicit-GEMM kernels work on mostly-padding tiles: a 3x3 conv on
+a 1x1 map is really a 512x512 matrix product (8 of its 9 taps only ever see padding), yet
+it costs ~125 µs fwd+bwd per layer on MI355X (tools/conv_bench.py, profiles/).
+
+For an input of C x H x W with H*W small, the convolution is a linear map
+    out.view(B, Co*OH*OW) = x.view(B, C*H*W) @ W_big,
+where W_big[(ci,ih,iw), (co,oh,ow)] = W[co, ci, ih - oh*s + p, iw - ow*s + p] (0 outside
+the kernel).  Both views are plain NCHW, so forward, grad-input and grad-weight are three
+hipBLASLt GEMMs; W_big is gathered from W and grad-W is gathered back from grad-W_big with
+a fixed-order sum (deterministic, no atomics).  Only the taps that can ever touch real
+pixels cost FLOPs.  1x1 strided convs subsample the input first.
+
+``GemmConv2d`` is a drop-in ``nn.Conv2d`` (same parameters / state_dict); it switches to
+the GEMM form only where it pays: input H*W <= 16 and output OH*OW <= 4.
+"""
+from __future__ import annotations
+
+from typing import Dict, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+__all__ = ["GemmConv2d", "toeplitz_maps", "eligible"]
+
+
+def eligible(h: int, w: int, oh: int, ow: int) -> bool:
+    return h * w <= 16 and oh * ow <= 4
+
+
+def toeplitz_maps(C: int, H: int, W: int, Co: int, KH: int, KW: int, s: int, p: int):
+    """Index maps for W_big (K x N) and for gathering grad-W back (numel(W) x R)."""
+    OH = (H + 2 * p - KH) // s + 1
+    OW = (W + 2 * p - KW) // s + 1
+    K, N = C * H * W, Co * OH * OW
+    nw = Co * C * KH * KW
+    co, ci, kh, kw, oh, ow = torch.meshgrid(torch.arange(Co), torch.arange(C), torch.arange(KH), torch.arange(KW),
+                                            torch.arange(OH), torch.arange(OW), indexing="ij")
+    ih = oh * s - p + kh
+    iw = ow * s - p + kw
+    ok = (ih >= 0) & (ih < H) & (iw >= 0) & (iw < W)
+    widx = ((co * C + ci) * KH + kh) * KW + kw
+    row = (ci * H + ih.clamp(0, H - 1)) * W + iw.clamp(0, W - 1)
+    col = (co * OH + oh) * OW + ow
+    flat = row * N + col
+    src = torch.full((K * N,), nw, dtype=torch.long)            # nw -> the appended zero
+    src[flat[ok]] = widx[ok]
+    # grad-W: every tap lists the W_big positions it was copied to (<= OH*OW of them)
+    R = OH * OW
+    dst = torch.where(ok, flat, torch.full_like(flat, K * N))   # K*N -> appended zero
+    dst = dst.reshape(nw, R)
+    return src.view(K, N), dst, (OH, OW)
+
+
+class _ToeplitzConv(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, src, dst, oh, ow):
+        B = x.shape[0]
+        co = weight.shape[0]
+        w_ext = torch.cat([weight.reshape(-1), weight.new_zeros(1)])
+        w_big = w_ext[src]                                        # [K, N]
+        X = x.reshape(B, -1)
+        out = X @ w_big
+        ctx.save_for_backward(X, w_big, dst)
+        ctx.x_shape = x.shape
+        ctx.w_shape = weight.shape
+        return out.view(B, co, oh, ow)
+
+    @staticmethod
+    def backward(ctx, g):
+        X, w_big, dst = ctx.saved_tensors
+        G = g.reshape(g.shape[0], -1)
+        dx = (G @ w_big.t()).view(ctx.x_shape) if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw_big = X.t() @ G                                    # [K, N]
+            ext = torch.cat([dw_big.reshape(-1), dw_big.new_zeros(1)])
+            dw = ext[dst].sum(-1).view(ctx.w_shape)               # fixed-order, deterministic
+        return dx, dw, None, None, None, None
+
+
+class GemmConv2d(nn.Conv2d):
+    """``nn.Conv2d`` that runs small-spatial cases as exact hipBLASLt GEMMs."""
+
+    def __init__(self, *a, gemm: bool = True, **kw):
+        super().__init__(*a, **kw)
+        self.gemm = gemm
+        self._maps: Dict[Tuple, tuple] = {}
+
+    def _plan(self, x):
+        C, H, W = x.shape[1:]
+        kh, kw = self.kernel_size
+        s, p = self.stride[0], self.padding[0]
+        sub = 1
+        if kh == 1 and kw == 1 and p == 0 and s > 1:  # 1x1 strided: subsample, then stride 1
+            sub, s = s, 1
+            H, W = (H + sub - 1) // sub, (W + sub - 1) // sub
+        key = (C, H, W, x.device, sub)
+        if key not in self._maps:
+            src, dst, (oh, ow) = toeplitz_maps(C, H, W, self.out_channels, kh, kw, s, p)
+            self._maps[key] = (src.to(x.device), dst.to(x.device), oh, ow, sub)
+        return self._maps[key]
+
+    def forward(self, x):
+        if not (self.gemm and x.is_cuda and self.groups == 1 and self.dilation == (1, 1) and self.bias is None
+                and self.stride[0] == self.stride[1] and self.padding[0] == self.padding[1]
+                and self.padding_mode == "zeros" and x.dtype == torch.float32):
+            return super().forward(x)
+        H, W = x.shape[2:]
+        kh, kw = self.kernel_size
+        s, p = self.stride[0], self.padding[0]
+        oh = (H + 2 * p - kh) // s + 1
+        ow = (W + 2 * p - kw) // s + 1
+        if not eligible(H, W, oh, ow):
+            return super().forward(x)
+        src, dst, oh2, ow2, sub = self._plan(x)
+        if sub > 1:
+            x = x[:, :, ::sub, ::sub]
+        return _ToeplitzConv.apply(x.contiguous(), self.weight, src, dst, oh2, ow2)

@@ -13,7 +13,10 @@ checkpoints written by torchvision load with ``load_state_dict`` unchanged.
 MI355X notes: convolutions run on PyTorch-ROCm (MIOpen).  Every BatchNorm is a
 :class:`~network_distributed_pytorch_amd.ops.batchnorm.BatchNormAct2d` (``fused_bn=True``):
 BN, the residual add and the ReLU of each block run as two fused gfx950 kernels per
-direction (same parameters/buffers/state_dict keys as ``nn.BatchNorm2d``).
+direction (same parameters/buffers/state_dict keys as ``nn.BatchNorm2d``).  Every conv is
+a :class:`~network_distributed_pytorch_amd.models.conv_gemm.GemmConv2d`: on the 4x4 / 2x2 /
+1x1 maps of layer3-4 it runs as exact hipBLASLt GEMMs instead of padding-dominated MIOpen
+tiles (``gemm_convs=False`` restores plain MIOpen everywhere).
 """
 from __future__ import annotations
 
@@ -23,17 +26,19 @@ import torch
 import torch.nn as nn
 
 from ..ops.batchnorm import BatchNormAct2d
+from .conv_gemm import GemmConv2d
 
 __all__ = ["ResNet", "BasicBlock", "Bottleneck", "resnet18", "resnet34", "resnet50", "resnet101",
            "resnet152", "build_resnet"]
 
 
 def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
-    return nn.Conv2d(cin, cout, kernel_size=3, stride=stride, padding=1, bias=False)
+    # GemmConv2d == nn.Conv2d (same params / state_dict); small feature maps run as GEMMs
+    return GemmConv2d(cin, cout, kernel_size=3, stride=stride, padding=1, bias=False)
 
 
 def conv1x1(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
-    return nn.Conv2d(cin, cout, kernel_size=1, stride=stride, bias=False)
+    return GemmConv2d(cin, cout, kernel_size=1, stride=stride, bias=False)
 
 
 class BasicBlock(nn.Module):
@@ -92,7 +97,7 @@ class Bottleneck(nn.Module):
 
 class ResNet(nn.Module):
     def __init__(self, block: Type[Union[BasicBlock, Bottleneck]], layers: List[int], num_classes: int = 1000,
-                 fused_bn: bool = True):
+                 fused_bn: bool = True, gemm_convs: bool = True):
         super().__init__()
         self.norm = BatchNormAct2d if fused_bn else nn.BatchNorm2d
         self.fused = fused_bn
@@ -108,6 +113,8 @@ class ResNet(nn.Module):
         self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
         self.fc = nn.Linear(512 * block.expansion, num_classes)
         for m in self.modules():
+            if isinstance(m, GemmConv2d):
+                m.gemm = gemm_convs
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
             elif isinstance(m, nn.BatchNorm2d):  # includes BatchNormAct2d
@@ -144,11 +151,11 @@ _CFG = {
 }
 
 
-def build_resnet(depth: int, num_classes: int = 1000, fused_bn: bool = True) -> ResNet:
+def build_resnet(depth: int, num_classes: int = 1000, fused_bn: bool = True, gemm_convs: bool = True) -> ResNet:
     if depth not in _CFG:
         raise ValueError(f"unsupported ResNet depth {depth}; choose from {sorted(_CFG)}")
     block, layers = _CFG[depth]
-    return ResNet(block, layers, num_classes=num_classes, fused_bn=fused_bn)
+    return ResNet(block, layers, num_classes=num_classes, fused_bn=fused_bn, gemm_convs=gemm_convs)
 
 
 def resnet18(num_classes: int = 1000, **_) -> ResNet:

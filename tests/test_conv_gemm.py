@@ -1,0 +1,66 @@
+"""Toeplitz-GEMM convolutions == F.conv2d (fp64 on CPU; fp32 on the GPU via GemmConv2d)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from network_distributed_pytorch_amd.models import build_resnet
+from network_distributed_pytorch_amd.models.conv_gemm import GemmConv2d, _ToeplitzConv, eligible, toeplitz_maps
+
+CASES = [(8, 2, 6, 3, 1, 1), (8, 1, 6, 3, 1, 1), (4, 2, 6, 3, 2, 1), (5, 4, 6, 3, 2, 1), (5, 2, 3, 1, 1, 0),
+         (3, 3, 4, 3, 1, 1)]
+
+
+@pytest.mark.parametrize("C,H,Co,k,s,p", CASES)
+def test_toeplitz_exact_fp64(C, H, Co, k, s, p):
+    torch.manual_seed(0)
+    x = torch.randn(3, C, H, H, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(Co, C, k, k, dtype=torch.float64, requires_grad=True)
+    src, dst, (oh, ow) = toeplitz_maps(C, H, H, Co, k, k, s, p)
+    y = _ToeplitzConv.apply(x, w, src, dst, oh, ow)
+    yr = F.conv2d(x, w, stride=s, padding=p)
+    g = torch.randn_like(yr)
+    a = torch.autograd.grad(y, (x, w), g)
+    b = torch.autograd.grad(yr, (x, w), g)
+    assert torch.allclose(y, yr, atol=1e-12)
+    assert torch.allclose(a[0], b[0], atol=1e-12) and torch.allclose(a[1], b[1], atol=1e-12)
+
+
+def test_eligibility_matches_resnet_cifar_maps():
+    assert eligible(2, 2, 2, 2) and eligible(1, 1, 1, 1) and eligible(4, 4, 2, 2)
+    assert not eligible(4, 4, 4, 4) and not eligible(8, 8, 4, 4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,k,s,p,hw", [(256, 256, 3, 1, 1, 2), (512, 512, 3, 1, 1, 1), (256, 512, 3, 2, 1, 2),
+                                               (256, 512, 1, 2, 0, 2), (128, 256, 3, 2, 1, 4), (128, 256, 1, 2, 0, 4)])
+def test_gemm_conv_gpu(device, cin, cout, k, s, p, hw):
+    torch.manual_seed(0)
+    m = GemmConv2d(cin, cout, k, stride=s, padding=p, bias=False).to(device)
+    x = torch.randn(64, cin, hw, hw, device=device, requires_grad=True)
+    y = m(x)
+    yr = F.conv2d(x, m.weight, stride=s, padding=p)
+    assert torch.allclose(y, yr, atol=1e-3, rtol=1e-3), (y - yr).abs().max()
+    g = torch.randn_like(yr)
+    a = torch.autograd.grad(y, (x, m.weight), g)
+    b = torch.autograd.grad(yr, (x, m.weight), g)
+    for u, v in zip(a, b):
+        scale = v.abs().max().item()
+        assert torch.allclose(u, v, atol=1e-4 * scale + 1e-5, rtol=1e-3), (u - v).abs().max()
+
+
+@pytest.mark.gpu
+def test_resnet18_gemm_convs_match_miopen(device):
+    torch.manual_seed(0)
+    a = build_resnet(18, 10, gemm_convs=True).to(device)
+    b = build_resnet(18, 10, gemm_convs=False).to(device)
+    b.load_state_dict(a.state_dict())
+    x = torch.randn(32, 3, 32, 32, device=device)
+    y = torch.randint(0, 10, (32,), device=device)
+    la = F.cross_entropy(a(x), y)
+    lb = F.cross_entropy(b(x), y)
+    assert torch.allclose(la, lb, atol=1e-4, rtol=1e-4)
+    la.backward()
+    lb.backward()
+    for (n, p1), p2 in zip(a.named_parameters(), b.parameters()):
+        scale = p2.grad.abs().max().item() + 1e-8
+        assert torch.allclose(p1.grad, p2.grad, atol=2e-3 * scale, rtol=1e-2), n
