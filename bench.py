@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--channels-last", action="store_true")
     ap.add_argument("--no-fused-bn", action="store_true", help="use nn.BatchNorm2d + ReLU (MIOpen) instead")
     ap.add_argument("--no-gemm-convs", action="store_true", help="run every conv on MIOpen")
+    ap.add_argument("--no-fused-attn", action="store_true", help="DistilBERT: explicit attention math")
     ap.add_argument("--amp", choices=["none", "bf16"], default="none",
                     help="opt-in bf16 autocast for model math (NOT the headline: the reference is fp32)")
     ap.add_argument("--link", default="none", help="none|1g|10g|100g link emulation")
@@ -99,7 +100,8 @@ def main():
     torch.backends.cudnn.benchmark = True
 
     model = build_model(args.model, args.num_classes, fused_bn=not args.no_fused_bn,
-                        gemm_convs=not args.no_gemm_convs).to(device)
+                        gemm_convs=not args.no_gemm_convs,
+                        fused_attention=not args.no_fused_attn).to(device)
     if args.channels_last:
         model = model.to(memory_format=torch.channels_last)
     link = None if args.link == "none" else LINK_PRESETS[args.link]
@@ -227,6 +229,7 @@ def main():
                 "link_emulation": args.link,
                 "channels_last": args.channels_last,
                 "hip_graph": graph_mode,
+                "fused_attention": (not args.no_fused_attn) if is_bert else None,
             },
             "mean_loss": round(final_loss, 5),
         }

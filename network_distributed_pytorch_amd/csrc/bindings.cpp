@@ -302,16 +302,78 @@ void bn_bwd(torch::Tensor dy, c10::optional<torch::Tensor> y, torch::Tensor x, c
 
 int bn_slices(int N, int C, int HW) { return ndp::bn_slices(N, C, HW); }
 
-void delay_ns(int64_t ns) { ndp::launch_delay_ns(ns, cur_stream()); }
+void delay_ns(int64_t ns) {
+  ndp::launch_delay_ns(ns, cur_stream());
+  check_launch("launch_delay_ns");
+}
 
 void checksum(torch::Tensor x, torch::Tensor out) {
   check_f32(x, "x");
-  check_launch("launch_delay_ns");
   check_dev(out, "out");
   TORCH_CHECK(out.scalar_type() == torch::kFloat64 && out.numel() >= 257,
               "checksum out must be float64[>=257]");
   ndp::launch_checksum(x.data_ptr<float>(), x.numel(), out.data_ptr<double>(), cur_stream());
   check_launch("launch_checksum");
+}
+
+// q/k/v/o: [B, S, H, 64] fp32 contiguous (== the [B, S, H*64] projections); mask [B, S] int32 or None
+void attn_check(const torch::Tensor& t, const char* n, const torch::Tensor& q) {
+  check_f32(t, n);
+  TORCH_CHECK(t.sizes() == q.sizes(), n, ": shape mismatch");
+}
+
+const int32_t* attn_seed(const c10::optional<torch::Tensor>& seed, double p_drop) {
+  TORCH_CHECK(p_drop >= 0.0 && p_drop < 1.0, "attn: p_drop in [0, 1)");
+  if (p_drop == 0.0) return nullptr;
+  TORCH_CHECK(seed.has_value(), "attn: dropout needs a device seed tensor");
+  check_dev(*seed, "seed");
+  TORCH_CHECK(seed->scalar_type() == torch::kInt32 && seed->numel() >= 1, "attn: seed must be int32[1]");
+  return seed->data_ptr<int32_t>();
+}
+
+void attn_fwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, c10::optional<torch::Tensor> mask, torch::Tensor o,
+              torch::Tensor lse, double scale, c10::optional<torch::Tensor> seed, double p_drop) {
+  check_f32(q, "q");
+  TORCH_CHECK(q.dim() == 4 && q.size(3) == 64, "attn: q must be [B, S, H, 64]");
+  attn_check(k, "k", q); attn_check(v, "v", q); attn_check(o, "o", q); check_f32(lse, "lse");
+  const int B = (int)q.size(0), S = (int)q.size(1), H = (int)q.size(2);
+  TORCH_CHECK(lse.numel() >= (int64_t)B * H * S, "attn: lse too small");
+  const int32_t* mp = nullptr;
+  if (mask.has_value()) {
+    check_dev(*mask, "mask");
+    TORCH_CHECK(mask->scalar_type() == torch::kInt32 && mask->is_contiguous() && mask->numel() == (int64_t)B * S,
+                "attn: mask must be int32 [B, S]");
+    mp = mask->data_ptr<int32_t>();
+  }
+  const int32_t* sp = attn_seed(seed, p_drop);
+  ndp::launch_attn_fwd(q.data_ptr<float>(), k.data_ptr<float>(), v.data_ptr<float>(), mp, o.data_ptr<float>(),
+                       lse.data_ptr<float>(), B, S, H, (float)scale, sp, (float)p_drop, cur_stream());
+  check_launch("launch_attn_fwd");
+}
+
+void attn_bwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, c10::optional<torch::Tensor> mask, torch::Tensor o,
+              torch::Tensor dout, torch::Tensor lse, torch::Tensor delta, torch::Tensor dq, torch::Tensor dk,
+              torch::Tensor dv, double scale, c10::optional<torch::Tensor> seed, double p_drop) {
+  check_f32(q, "q");
+  TORCH_CHECK(q.dim() == 4 && q.size(3) == 64, "attn: q must be [B, S, H, 64]");
+  attn_check(k, "k", q); attn_check(v, "v", q); attn_check(o, "o", q); attn_check(dout, "dout", q);
+  attn_check(dq, "dq", q); attn_check(dk, "dk", q); attn_check(dv, "dv", q);
+  check_f32(lse, "lse"); check_f32(delta, "delta");
+  const int B = (int)q.size(0), S = (int)q.size(1), H = (int)q.size(2);
+  TORCH_CHECK(lse.numel() >= (int64_t)B * H * S && delta.numel() >= (int64_t)B * H * S, "attn: lse/delta too small");
+  const int32_t* mp = nullptr;
+  if (mask.has_value()) {
+    check_dev(*mask, "mask");
+    TORCH_CHECK(mask->scalar_type() == torch::kInt32 && mask->is_contiguous() && mask->numel() == (int64_t)B * S,
+                "attn: mask must be int32 [B, S]");
+    mp = mask->data_ptr<int32_t>();
+  }
+  const int32_t* sp = attn_seed(seed, p_drop);
+  ndp::launch_attn_bwd(q.data_ptr<float>(), k.data_ptr<float>(), v.data_ptr<float>(), mp, o.data_ptr<float>(),
+                       dout.data_ptr<float>(), lse.data_ptr<float>(), delta.data_ptr<float>(), dq.data_ptr<float>(),
+                       dk.data_ptr<float>(), dv.data_ptr<float>(), B, S, H, (float)scale, sp,
+                       (float)p_drop, cur_stream());
+  check_launch("launch_attn_bwd");
 }
 
 }  // namespace
@@ -340,4 +402,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd", &bn_bwd);
   m.def("bn_slices", &bn_slices);
   m.def("checksum", &checksum);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
 }

@@ -112,3 +112,15 @@ void launch_bn_bwd(const float* dy, const float* y, const float* x, const float*
                    const float* save_invstd, float* dx, float* dres, float* dgamma, float* dbeta, double* part,
                    int N, int C, int HW, int S, int relu, hipStream_t s);
 }  // namespace ndp
+
+// ---- fused fp32 attention, q/k/v/o [B, S, H, 64] (attention.hip) ------------------------
+namespace ndp {
+// mask: [B, S] int32 (nonzero = attend) or null; lse: [B, H, S]; p_drop in [0, 1);
+// seed: device int32[1] read by the kernels (so a replayed hipGraph sees fresh seeds)
+void launch_attn_fwd(const float* q, const float* k, const float* v, const int32_t* mask, float* o, float* lse,
+                     int B, int S, int H, float scale, const int32_t* seed, float p_drop, hipStream_t s);
+// delta: [B, H, S] scratch
+void launch_attn_bwd(const float* q, const float* k, const float* v, const int32_t* mask, const float* o,
+                     const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv, int B,
+                     int S, int H, float scale, const int32_t* seed, float p_drop, hipStream_t s);
+}  // namespace ndp

@@ -11,14 +11,16 @@ __all__ = [
 ]
 
 
-def build_model(name: str, num_classes=None, fused_bn: bool = True, gemm_convs: bool = True):
+def build_model(name: str, num_classes=None, fused_bn: bool = True, gemm_convs: bool = True,
+                fused_attention: bool = True):
     """``num_classes`` defaults to the reference's heads: 1000 (ImageNet ResNet), 2 (IMDb)."""
     name = name.lower()
     if name.startswith("resnet"):
         return build_resnet(int(name[len("resnet"):]), 1000 if num_classes is None else num_classes,
                             fused_bn=fused_bn, gemm_convs=gemm_convs)
     if name in ("distilbert", "distilbert-base", "distilbert-base-uncased"):
-        return distilbert_base(num_labels=2 if num_classes is None else num_classes)
+        return distilbert_base(num_labels=2 if num_classes is None else num_classes,
+                               fused_attention=fused_attention)
     if name in ("mlp", "toy_mlp"):
         return ToyMLP()
     raise ValueError(f"unknown model {name!r}")

@@ -8,8 +8,10 @@ zero bias, LayerNorm (1, 0)).  Parameter names and registration order equal HF's
 66,955,010 parameters for the default config), so the PowerSGD P/Q layout, the byte
 count per step and checkpoints interchange with ``transformers``.
 
-Attention is computed explicitly (QK^T -> mask -> softmax -> PV) on PyTorch-ROCm GEMMs;
-no Triton/AOTriton path is used.
+On the GPU (fp32, head dim 64) attention runs the fused flash-style HIP kernels of
+``ops/attention.py`` (csrc/attention.hip): the [B, H, S, S] score / probability tensors
+never reach HBM.  ``fused_attention=False`` (or CPU / autocast) runs the explicit
+QK^T -> mask -> softmax -> dropout -> PV math.  No Triton/AOTriton path is used.
 """
 from __future__ import annotations
 
@@ -20,6 +22,8 @@ from typing import Optional
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from ..ops.attention import attention, fused_ok
 
 __all__ = ["DistilBertConfig", "DistilBertForSequenceClassification", "distilbert_base"]
 
@@ -39,6 +43,7 @@ class DistilBertConfig:
     pad_token_id: int = 0
     initializer_range: float = 0.02
     layer_norm_eps: float = 1e-12
+    fused_attention: bool = True   # not an HF field: selects csrc/attention.hip on the GPU
 
 
 class Embeddings(nn.Module):
@@ -66,16 +71,22 @@ class MultiHeadSelfAttention(nn.Module):
         self.v_lin = nn.Linear(c.dim, c.dim)
         self.out_lin = nn.Linear(c.dim, c.dim)
         self.dropout = nn.Dropout(c.attention_dropout)
+        self.fused = c.fused_attention
 
     def forward(self, x, mask: Optional[torch.Tensor]):
         bs, s, d = x.shape
         h = self.n_heads
         dh = d // h
+        q4 = self.q_lin(x).view(bs, s, h, dh)
+        if self.fused and fused_ok(q4):
+            ctx = attention(q4, self.k_lin(x).view(bs, s, h, dh), self.v_lin(x).view(bs, s, h, dh), mask,
+                            self.dropout.p if self.training else 0.0)
+            return self.out_lin(ctx.reshape(bs, s, d))
 
         def split(t):
             return t.view(bs, s, h, dh).transpose(1, 2)
 
-        q = split(self.q_lin(x)) / math.sqrt(dh)
+        q = q4.transpose(1, 2) / math.sqrt(dh)
         k = split(self.k_lin(x))
         v = split(self.v_lin(x))
         scores = torch.matmul(q, k.transpose(-1, -2))
@@ -116,6 +127,8 @@ class Transformer(nn.Module):
         self.layer = nn.ModuleList([TransformerBlock(c) for _ in range(c.n_layers)])
 
     def forward(self, x, mask):
+        if mask is not None and x.is_cuda:
+            mask = mask.to(torch.int32).contiguous()   # once per pass, not per layer
         for blk in self.layer:
             x = blk(x, mask)
         return x

@@ -1,0 +1,96 @@
+"""Fused fp32 attention (csrc/attention.hip) vs explicit fp64 math; dropout mask exactness."""
+import pytest
+import torch
+
+from network_distributed_pytorch_amd.models import distilbert_base
+from network_distributed_pytorch_amd.ops.attention import attention, attention_reference, dropout_keep_mask
+
+
+def _inputs(B, S, H, device, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    q, k, v = (torch.randn(B, S, H, 64, generator=g).to(device).requires_grad_() for _ in range(3))
+    return q, k, v
+
+
+def test_keep_mask_rate_and_determinism():
+    a = dropout_keep_mask(7, 2, 3, 96, 0.1)
+    b = dropout_keep_mask(7, 2, 3, 96, 0.1)
+    c = dropout_keep_mask(8, 2, 3, 96, 0.1)
+    assert torch.equal(a, b) and not torch.equal(a, c)
+    assert abs(1 - a.float().mean().item() - 0.1) < 0.01
+
+
+def test_reference_matches_model_math_cpu():
+    torch.manual_seed(0)
+    q, k, v = _inputs(2, 40, 3, "cpu")
+    mask = torch.ones(2, 40, dtype=torch.long)
+    mask[1, 25:] = 0
+    o = attention(q, k, v, mask)                                     # CPU -> reference
+    r = attention_reference(q.double(), k.double(), v.double(), mask)
+    assert torch.allclose(o.double(), r, atol=1e-5)
+
+
+def _check(o, r, tol=2e-5):
+    err = (o.double() - r).abs().max().item()
+    scale = r.abs().max().item() + 1e-12
+    assert err <= tol * scale + 1e-6, (err, scale)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,S,H,masked", [(2, 128, 3, False), (2, 100, 2, True), (1, 512, 2, True), (3, 17, 1, True)])
+def test_fused_attention_fwd_bwd(device, B, S, H, masked):
+    q, k, v = _inputs(B, S, H, device)
+    mask = None
+    if masked:
+        mask = torch.ones(B, S, dtype=torch.long, device=device)
+        mask[0, S // 2:] = 0
+        if B > 2:
+            mask[2, :] = 0          # fully padded sequence: HF yields a uniform average
+    o = attention(q, k, v, mask)
+    qd, kd, vd = (t.detach().double().requires_grad_() for t in (q, k, v))
+    r = attention_reference(qd, kd, vd, mask)
+    _check(o, r)
+    go = torch.randn_like(o)
+    g = torch.autograd.grad(o, (q, k, v), go)
+    gr = torch.autograd.grad(r, (qd, kd, vd), go.double())
+    for a, b in zip(g, gr):
+        _check(a, b, 5e-5)
+
+
+@pytest.mark.gpu
+def test_fused_attention_dropout_exact_mask(device):
+    B, S, H, p = 2, 96, 2, 0.3
+    q, k, v = _inputs(B, S, H, device, seed=1)
+    mask = torch.ones(B, S, dtype=torch.long, device=device)
+    mask[1, 70:] = 0
+    seed = torch.tensor([12345], dtype=torch.int32, device=device)
+    o = attention(q, k, v, mask, p_drop=p, seed=seed)
+    keep = dropout_keep_mask(12345, B, H, S, p, device=device)
+    qd, kd, vd = (t.detach().double().requires_grad_() for t in (q, k, v))
+    r = attention_reference(qd, kd, vd, mask, p_drop=p, keep=keep)
+    _check(o, r)
+    go = torch.randn_like(o)
+    g = torch.autograd.grad(o, (q, k, v), go)
+    gr = torch.autograd.grad(r, (qd, kd, vd), go.double())
+    for a, b in zip(g, gr):
+        _check(a, b, 5e-5)
+
+
+@pytest.mark.gpu
+def test_distilbert_fused_matches_explicit(device):
+    torch.manual_seed(0)
+    a = distilbert_base(n_layers=2, fused_attention=True).to(device).eval()
+    b = distilbert_base(n_layers=2, fused_attention=False).to(device).eval()
+    b.load_state_dict(a.state_dict())
+    ids = torch.randint(1, 30522, (2, 130), device=device)
+    mask = torch.ones_like(ids)
+    mask[1, 90:] = 0
+    labels = torch.tensor([0, 1], device=device)
+    la = a(ids, attention_mask=mask, labels=labels)[0]
+    lb = b(ids, attention_mask=mask, labels=labels)[0]
+    assert torch.allclose(la, lb, atol=1e-5, rtol=1e-5)
+    la.backward()
+    lb.backward()
+    for (n, p1), p2 in zip(a.named_parameters(), b.parameters()):
+        scale = p2.grad.abs().max().item() + 1e-10
+        assert torch.allclose(p1.grad, p2.grad, atol=1e-4 * scale, rtol=1e-3), n
