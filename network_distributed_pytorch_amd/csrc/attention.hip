@@ -11,7 +11,8 @@
 //             row, the query on the lane), online softmax per lane, O^T += V^T P~^T with the
 //             S^T accumulator registers used directly as the B operand (no LDS round trip,
 //             cdna_hip_programming.md §3 'accumulator tile as the next MFMA's operand').
-//             Saves LSE = m + log(l) per query.
+//             Saves m and log(l) per query (kept apart: for a fully padded row m is
+//             finfo.min and m + log(l) would round back to m).
 //   backward: delta = rowsum(dO*O); kernel dKdV (one wave = 16 keys, loop over queries);
 //             kernel dQ (one wave = 16 queries, loop over keys).  Two kernels, no atomics:
 //             deterministic.
@@ -52,7 +53,7 @@ __device__ __forceinline__ bool keep_elem(uint32_t seed, uint32_t bh, uint32_t q
 
 struct AttnArgs {
   const float* q; const float* k; const float* v; const int32_t* mask;  // mask [B, S] (1 keep), may be null
-  float* o; float* lse;          // lse [B, H, S]
+  float* o; float* lse;          // lse [2][B, H, S]: row max m, then log(l)
   int B, S, H;
   float scale;                   // 1/sqrt(D)
   const int32_t* seedp;          // device-resident seed (graph-replay safe), may be null
@@ -179,7 +180,11 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt)
     *reinterpret_cast<f32x4*>(a.o + base + (int64_t)q * rs + 16 * dt + 4 * g) = O[dt] * inv;
-  if (g == 0) a.lse[(int64_t)bh * a.S + q] = m + __logf(l);
+  if (g == 0) {
+    const int64_t i = (int64_t)bh * a.S + q;
+    a.lse[i] = m;
+    a.lse[(int64_t)a.B * a.H * a.S + i] = __logf(l);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -218,7 +223,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
   const uint32_t seed = (a.drop_thr && a.seedp) ? (uint32_t)*a.seedp : 0u;
   __shared__ __attribute__((aligned(16))) float Qs[64 * kLD];    // Q[q][d] (scaled)
   __shared__ __attribute__((aligned(16))) float dOs[64 * kLD];   // dO[q][d]
-  __shared__ float Ls[64], Ds[64];
+  __shared__ float Ls[64], LLs[64], Ds[64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
   const int bh = blockIdx.y, b = bh / a.H, h = bh - (bh / a.H) * a.H;
   const int64_t rs = (int64_t)a.H * kD;
@@ -265,6 +270,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
     if (threadIdx.x < 64) {
       const int qq = q0 + threadIdx.x;
       Ls[threadIdx.x] = qq < a.S ? a.lse[(int64_t)bh * a.S + qq] : INFINITY;
+      LLs[threadIdx.x] = qq < a.S ? a.lse[(int64_t)a.B * a.H * a.S + (int64_t)bh * a.S + qq] : 0.f;
       Ds[threadIdx.x] = qq < a.S ? a.delta[(int64_t)bh * a.S + qq] : 0.f;
     }
     __syncthreads();
@@ -287,14 +293,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
       for (int r = 0; r < 4; ++r) {
         const int ql = 16 * qt + 4 * g + r, qq = q0 + ql;
         float sv = kmasked ? kNegBig : s[r];
-        float p = (kok && qq < a.S) ? __expf(sv - Ls[ql]) : 0.f;
+        float p = (kok && qq < a.S) ? __expf((sv - Ls[ql]) - LLs[ql]) : 0.f;
         bool keep = true;
         if (a.drop_thr) keep = keep_elem(seed, (uint32_t)bh, (uint32_t)qq, (uint32_t)key, a.drop_thr);
         const float pd = keep ? p * (a.drop_thr ? a.drop_scale : 1.f) : 0.f;
         const float dpp = keep ? dp[r] * (a.drop_thr ? a.drop_scale : 1.f) : 0.f;   // dP = keep*dPd/(1-p)
         P[r] = p;
         Pd[r] = pd;
-        dS[r] = p * (dpp - Ds[ql]);
+        dS[r] = kmasked ? 0.f : p * (dpp - Ds[ql]);   // masked_fill: no grad to the score
       }
       // dV^T[d][key] += sum_q dO[q][d] * Pd[q][key]: A = dO^T rows d (lane-group k = query),
       // B = Pd (k = query 4g + r, col = key lane).  dK^T likewise with Q and dS.
@@ -349,6 +355,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
     }
   }
   const float L = qok ? a.lse[(int64_t)bh * a.S + q] : 0.f;
+  const float LL = qok ? a.lse[(int64_t)a.B * a.H * a.S + (int64_t)bh * a.S + q] : 0.f;
   const float Dl = qok ? a.delta[(int64_t)bh * a.S + q] : 0.f;
   f32x4 dQ[4];
 #pragma unroll
@@ -393,11 +400,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
         const int kl = 16 * kt + 4 * g + r, key = k0 + kl;
         const float mk = Mk[kl];
         const float sv = (mk == 0.f) ? kNegBig : st[r];
-        const float p = (mk >= 0.f && qok) ? __expf(sv - L) : 0.f;
+        const float p = (mk >= 0.f && qok) ? __expf((sv - L) - LL) : 0.f;
         bool keep = true;
         if (a.drop_thr) keep = keep_elem(seed, (uint32_t)bh, (uint32_t)q, (uint32_t)key, a.drop_thr);
         const float dpp = keep ? dpt[r] * (a.drop_thr ? a.drop_scale : 1.f) : 0.f;
-        dS[r] = p * (dpp - Dl);
+        dS[r] = (mk == 0.f) ? 0.f : p * (dpp - Dl);    // masked_fill: no grad to the score
       }
       // dQ^T[d][q] += K^T[d][key] dS^T[key][q]: A = K^T rows d, B = dS (k = key 4g + r)
 #pragma unroll

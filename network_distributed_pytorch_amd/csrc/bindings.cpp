@@ -337,7 +337,7 @@ void attn_fwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, c10::optional<t
   TORCH_CHECK(q.dim() == 4 && q.size(3) == 64, "attn: q must be [B, S, H, 64]");
   attn_check(k, "k", q); attn_check(v, "v", q); attn_check(o, "o", q); check_f32(lse, "lse");
   const int B = (int)q.size(0), S = (int)q.size(1), H = (int)q.size(2);
-  TORCH_CHECK(lse.numel() >= (int64_t)B * H * S, "attn: lse too small");
+  TORCH_CHECK(lse.numel() >= 2 * (int64_t)B * H * S, "attn: lse must hold 2*B*H*S floats");
   const int32_t* mp = nullptr;
   if (mask.has_value()) {
     check_dev(*mask, "mask");
@@ -360,7 +360,8 @@ void attn_bwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, c10::optional<t
   attn_check(dq, "dq", q); attn_check(dk, "dk", q); attn_check(dv, "dv", q);
   check_f32(lse, "lse"); check_f32(delta, "delta");
   const int B = (int)q.size(0), S = (int)q.size(1), H = (int)q.size(2);
-  TORCH_CHECK(lse.numel() >= (int64_t)B * H * S && delta.numel() >= (int64_t)B * H * S, "attn: lse/delta too small");
+  TORCH_CHECK(lse.numel() >= 2 * (int64_t)B * H * S && delta.numel() >= (int64_t)B * H * S,
+              "attn: lse/delta too small");
   const int32_t* mp = nullptr;
   if (mask.has_value()) {
     check_dev(*mask, "mask");

@@ -75,7 +75,7 @@ class _FusedAttention(torch.autograd.Function):
     def forward(ctx, q, k, v, mask, seed, p_drop):
         B, S, H, _ = q.shape
         o = torch.empty_like(q)
-        lse = torch.empty(B, H, S, device=q.device, dtype=torch.float32)
+        lse = torch.empty(2, B, H, S, device=q.device, dtype=torch.float32)   # row max, log(sum)
         scale = 1.0 / math.sqrt(q.shape[-1])
         ext().attn_fwd(q, k, v, mask, o, lse, scale, seed, p_drop)
         ctx.save_for_backward(q, k, v, mask, o, lse, seed)

@@ -92,5 +92,31 @@ def test_distilbert_fused_matches_explicit(device):
     la.backward()
     lb.backward()
     for (n, p1), p2 in zip(a.named_parameters(), b.parameters()):
+        if n.endswith("k_lin.bias"):
+            # softmax is shift-invariant per query row: d loss / d k_bias == 0 exactly, so
+            # both sides are rounding noise; compare against the k_lin.weight grad scale
+            continue
         scale = p2.grad.abs().max().item() + 1e-10
         assert torch.allclose(p1.grad, p2.grad, atol=1e-4 * scale, rtol=1e-3), n
+
+
+@pytest.mark.gpu
+def test_fused_attention_distilbert_shape(device):
+    """The bench shape (B=16, S=512, H=12) with padding + dropout, vs fp64 explicit math."""
+    B, S, H, p = 16, 512, 12, 0.1
+    q, k, v = _inputs(B, S, H, device, seed=2)
+    mask = torch.ones(B, S, dtype=torch.long, device=device)
+    for b in range(B):
+        mask[b, 64 + 29 * b:] = 0
+    seed = torch.tensor([777], dtype=torch.int32, device=device)
+    o = attention(q, k, v, mask, p_drop=p, seed=seed)
+    go = torch.randn_like(o)
+    g = torch.autograd.grad(o, (q, k, v), go)
+    torch.cuda.synchronize()
+    keep = dropout_keep_mask(777, B, H, S, p, device=device)
+    qd, kd, vd = (t.detach().double().requires_grad_() for t in (q, k, v))
+    r = attention_reference(qd, kd, vd, mask, p_drop=p, keep=keep)
+    _check(o, r)
+    gr = torch.autograd.grad(r, (qd, kd, vd), go.double())
+    for x, y in zip(g, gr):
+        _check(x, y, 5e-5)

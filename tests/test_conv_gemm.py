@@ -50,17 +50,25 @@ def test_gemm_conv_gpu(device, cin, cout, k, s, p, hw):
 
 @pytest.mark.gpu
 def test_resnet18_gemm_convs_match_miopen(device):
+    """Both fp32 GPU paths vs an fp64 CPU oracle: the GEMM convs must be no less accurate
+    than MIOpen's (grads of early layers are conditioned badly through 17 BN layers, so
+    a direct fp32-vs-fp32 comparison is dominated by rounding noise of either side)."""
     torch.manual_seed(0)
     a = build_resnet(18, 10, gemm_convs=True).to(device)
     b = build_resnet(18, 10, gemm_convs=False).to(device)
     b.load_state_dict(a.state_dict())
-    x = torch.randn(32, 3, 32, 32, device=device)
-    y = torch.randint(0, 10, (32,), device=device)
-    la = F.cross_entropy(a(x), y)
-    lb = F.cross_entropy(b(x), y)
-    assert torch.allclose(la, lb, atol=1e-4, rtol=1e-4)
-    la.backward()
-    lb.backward()
-    for (n, p1), p2 in zip(a.named_parameters(), b.parameters()):
-        scale = p2.grad.abs().max().item() + 1e-8
-        assert torch.allclose(p1.grad, p2.grad, atol=2e-3 * scale, rtol=1e-2), n
+    ref = build_resnet(18, 10, gemm_convs=False).double()
+    ref.load_state_dict(a.state_dict())
+    x = torch.randn(32, 3, 32, 32)
+    y = torch.randint(0, 10, (32,))
+    losses = []
+    for m, dev, dt in ((a, device, torch.float32), (b, device, torch.float32), (ref, "cpu", torch.float64)):
+        loss = F.cross_entropy(m(x.to(dev, dt)), y.to(dev))
+        loss.backward()
+        losses.append(loss.item())
+    assert abs(losses[0] - losses[2]) < 1e-4 and abs(losses[1] - losses[2]) < 1e-4
+    for (n, pa), pb, pr in zip(a.named_parameters(), b.parameters(), ref.parameters()):
+        g = pr.grad
+        ea = (pa.grad.cpu().double() - g).abs().max().item()
+        eb = (pb.grad.cpu().double() - g).abs().max().item()
+        assert ea <= 3 * eb + 1e-5 * g.abs().max().item() + 1e-7, (n, ea, eb)
