@@ -51,6 +51,28 @@ __device__ __forceinline__ bool keep_elem(uint32_t seed, uint32_t bh, uint32_t q
   return hash4(seed, bh, q, k) >= thr;  // thr = p * 2^32
 }
 
+// Padding-block map: blkv[j] = 1 if key block j (64 keys) holds an attended key; returns
+// whether row b attends to any key at all.  A block with no attended key contributes
+// exactly nothing (p = exp(finfo.min - m) == 0) unless the whole row is padding (then HF's
+// masked softmax is uniform), so such blocks are skipped — exact, not an approximation.
+constexpr int kMaxBlk = 64;   // S <= 4096 gets the map; longer sequences never skip
+__device__ __forceinline__ bool scan_mask(const int32_t* __restrict__ mask, int b, int S, int* blkv) {
+  if (mask == nullptr) return true;
+  if (threadIdx.x < kMaxBlk) blkv[threadIdx.x] = 0;
+  __syncthreads();
+  int any = 0;
+  for (int i = threadIdx.x; i < S; i += blockDim.x)
+    if (mask[(int64_t)b * S + i] != 0) {
+      any = 1;
+      if ((i >> 6) < kMaxBlk) blkv[i >> 6] = 1;   // benign same-value race
+    }
+  return __syncthreads_or(any) != 0;
+}
+
+__device__ __forceinline__ bool skip_block(const int32_t* mask, bool row_any, const int* blkv, int k0) {
+  return mask != nullptr && row_any && (k0 >> 6) < kMaxBlk && blkv[k0 >> 6] == 0;
+}
+
 struct AttnArgs {
   const float* q; const float* k; const float* v; const int32_t* mask;  // mask [B, S] (1 keep), may be null
   float* o; float* lse;          // lse [2][B, H, S]: row max m, then log(l)
@@ -69,8 +91,10 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) float Ks[kBK * kLD];   // K[key][d]
   __shared__ __attribute__((aligned(16))) float Vt[kD * kLD];    // V^T[d][key]
   __shared__ float Mk[kBK];                                      // key mask (1 / 0)
+  __shared__ int blkv[kMaxBlk];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
   const int bh = blockIdx.y, b = bh / a.H, h = bh - (bh / a.H) * a.H;
+  const bool row_any = scan_mask(a.mask, b, a.S, blkv);
   const int64_t rs = (int64_t)a.H * kD;                       // row stride of [B,S,H,D]
   const int64_t base = (int64_t)b * a.S * rs + (int64_t)h * kD;
   const int q = blockIdx.x * 64 + wave * 16 + c16;            // this lane's query
@@ -91,6 +115,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   float m = kNegBig, l = 0.f;
 
   for (int k0 = 0; k0 < a.S; k0 += kBK) {
+    if (skip_block(a.mask, row_any, blkv, k0)) continue;
     __syncthreads();
     // stage K[k0:k0+64][0:64] and V^T
     for (int idx = threadIdx.x; idx < kBK * (kD / 4); idx += 256) {
@@ -223,13 +248,26 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
   const uint32_t seed = (a.drop_thr && a.seedp) ? (uint32_t)*a.seedp : 0u;
   __shared__ __attribute__((aligned(16))) float Qs[64 * kLD];    // Q[q][d] (scaled)
   __shared__ __attribute__((aligned(16))) float dOs[64 * kLD];   // dO[q][d]
+  __shared__ __attribute__((aligned(16))) float Qt[kD * kLD];    // Q^T[d][q] (scaled)
+  __shared__ __attribute__((aligned(16))) float dOt[kD * kLD];   // dO^T[d][q]
   __shared__ float Ls[64], LLs[64], Ds[64];
+  __shared__ int blkv[kMaxBlk];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
   const int bh = blockIdx.y, b = bh / a.H, h = bh - (bh / a.H) * a.H;
   const int64_t rs = (int64_t)a.H * kD;
   const int64_t base = (int64_t)b * a.S * rs + (int64_t)h * kD;
   const int key = blockIdx.x * 64 + wave * 16 + c16;             // this lane's key
   const bool kok = key < a.S;
+  const bool row_any = scan_mask(a.mask, b, a.S, blkv);
+  if (skip_block(a.mask, row_any, blkv, blockIdx.x * 64)) {      // all-padding keys: zero grads
+    if (kok)
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        *reinterpret_cast<f32x4*>(a.dk + base + (int64_t)key * rs + 16 * dt + 4 * g) = f32x4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f32x4*>(a.dv + base + (int64_t)key * rs + 16 * dt + 4 * g) = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    return;
+  }
   const bool kmasked = kok && a.mask != nullptr && a.mask[(int64_t)b * a.S + key] == 0;
 
   // K and V rows of this lane's key as B operands: lane (g, c16): [key][16c + 4g + t]
@@ -266,6 +304,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
       }
       *reinterpret_cast<f32x4*>(&Qs[qr * kLD + dq]) = qv;
       *reinterpret_cast<f32x4*>(&dOs[qr * kLD + dq]) = gv;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        Qt[(dq + t) * kLD + qr] = qv[t];
+        dOt[(dq + t) * kLD + qr] = gv[t];
+      }
     }
     if (threadIdx.x < 64) {
       const int qq = q0 + threadIdx.x;
@@ -306,10 +349,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
       // B = Pd (k = query 4g + r, col = key lane).  dK^T likewise with Q and dS.
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        const f32x4 gq = {dOs[(16 * qt + 4 * g + 0) * kLD + 16 * dt + c16], dOs[(16 * qt + 4 * g + 1) * kLD + 16 * dt + c16],
-                          dOs[(16 * qt + 4 * g + 2) * kLD + 16 * dt + c16], dOs[(16 * qt + 4 * g + 3) * kLD + 16 * dt + c16]};
-        const f32x4 qq4 = {Qs[(16 * qt + 4 * g + 0) * kLD + 16 * dt + c16], Qs[(16 * qt + 4 * g + 1) * kLD + 16 * dt + c16],
-                           Qs[(16 * qt + 4 * g + 2) * kLD + 16 * dt + c16], Qs[(16 * qt + 4 * g + 3) * kLD + 16 * dt + c16]};
+        const f32x4 gq = *reinterpret_cast<const f32x4*>(&dOt[(16 * dt + c16) * kLD + 16 * qt + 4 * g]);
+        const f32x4 qq4 = *reinterpret_cast<const f32x4*>(&Qt[(16 * dt + c16) * kLD + 16 * qt + 4 * g]);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           dV[dt] = mfma16(gq[r], Pd[r], dV[dt]);
@@ -333,9 +374,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   const uint32_t seed = (a.drop_thr && a.seedp) ? (uint32_t)*a.seedp : 0u;
   __shared__ __attribute__((aligned(16))) float Ks[kBK * kLD];   // K[key][d]
   __shared__ __attribute__((aligned(16))) float Vs[kBK * kLD];   // V[key][d]
+  __shared__ __attribute__((aligned(16))) float Kt[kD * kLD];    // K^T[d][key]
   __shared__ float Mk[kBK];
+  __shared__ int blkv[kMaxBlk];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
   const int bh = blockIdx.y, b = bh / a.H, h = bh - (bh / a.H) * a.H;
+  const bool row_any = scan_mask(a.mask, b, a.S, blkv);
   const int64_t rs = (int64_t)a.H * kD;
   const int64_t base = (int64_t)b * a.S * rs + (int64_t)h * kD;
   const int q = blockIdx.x * 64 + wave * 16 + c16;
@@ -362,6 +406,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   for (int dt = 0; dt < 4; ++dt) dQ[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   for (int k0 = 0; k0 < a.S; k0 += kBK) {
+    if (skip_block(a.mask, row_any, blkv, k0)) continue;
     __syncthreads();
     for (int idx = threadIdx.x; idx < kBK * 16; idx += 256) {
       const int kr = idx >> 4, dq = (idx & 15) * 4;
@@ -373,6 +418,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
       }
       *reinterpret_cast<f32x4*>(&Ks[kr * kLD + dq]) = kv;
       *reinterpret_cast<f32x4*>(&Vs[kr * kLD + dq]) = vv;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) Kt[(dq + t) * kLD + kr] = kv[t];
     }
     if (threadIdx.x < kBK) {
       const int key = k0 + threadIdx.x;
@@ -409,8 +456,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
       // dQ^T[d][q] += K^T[d][key] dS^T[key][q]: A = K^T rows d, B = dS (k = key 4g + r)
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        const f32x4 kd = {Ks[(16 * kt + 4 * g + 0) * kLD + 16 * dt + c16], Ks[(16 * kt + 4 * g + 1) * kLD + 16 * dt + c16],
-                          Ks[(16 * kt + 4 * g + 2) * kLD + 16 * dt + c16], Ks[(16 * kt + 4 * g + 3) * kLD + 16 * dt + c16]};
+        const f32x4 kd = *reinterpret_cast<const f32x4*>(&Kt[(16 * dt + c16) * kLD + 16 * kt + 4 * g]);
 #pragma unroll
         for (int r = 0; r < 4; ++r) dQ[dt] = mfma16(kd[r], dS[r], dQ[dt]);
       }

@@ -37,7 +37,8 @@ def _check(o, r, tol=2e-5):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("B,S,H,masked", [(2, 128, 3, False), (2, 100, 2, True), (1, 512, 2, True), (3, 17, 1, True)])
+@pytest.mark.parametrize("B,S,H,masked", [(2, 128, 3, False), (2, 100, 2, True), (1, 512, 2, True), (3, 17, 1, True),
+                                           (3, 300, 2, True)])
 def test_fused_attention_fwd_bwd(device, B, S, H, masked):
     q, k, v = _inputs(B, S, H, device)
     mask = None
@@ -46,6 +47,8 @@ def test_fused_attention_fwd_bwd(device, B, S, H, masked):
         mask[0, S // 2:] = 0
         if B > 2:
             mask[2, :] = 0          # fully padded sequence: HF yields a uniform average
+        if S >= 256:
+            mask[-1, 64:192] = 0    # fully padded key blocks in the middle (skipped blocks)
     o = attention(q, k, v, mask)
     qd, kd, vd = (t.detach().double().requires_grad_() for t in (q, k, v))
     r = attention_reference(qd, kd, vd, mask)
