@@ -316,6 +316,39 @@ void checksum(torch::Tensor x, torch::Tensor out) {
   check_launch("launch_checksum");
 }
 
+// conv geometry from (C, H, W, Co, KH, KW, stride, pad); OH/OW derived
+ndp::ConvGeom conv_geom(const std::vector<int64_t>& v) {
+  TORCH_CHECK(v.size() == 8, "conv geometry needs (C, H, W, Co, KH, KW, stride, pad)");
+  ndp::ConvGeom g{};
+  g.C = (int32_t)v[0]; g.H = (int32_t)v[1]; g.W = (int32_t)v[2];
+  g.Co = (int32_t)v[3]; g.KH = (int32_t)v[4]; g.KW = (int32_t)v[5];
+  g.stride = (int32_t)v[6]; g.pad = (int32_t)v[7];
+  TORCH_CHECK(g.C > 0 && g.H > 0 && g.W > 0 && g.Co > 0 && g.KH > 0 && g.KW > 0 && g.stride > 0 && g.pad >= 0,
+              "bad conv geometry");
+  g.OH = (g.H + 2 * g.pad - g.KH) / g.stride + 1;
+  g.OW = (g.W + 2 * g.pad - g.KW) / g.stride + 1;
+  TORCH_CHECK(g.OH > 0 && g.OW > 0, "conv output is empty");
+  return g;
+}
+
+void toeplitz_expand(torch::Tensor w, torch::Tensor wb, const std::vector<int64_t>& geom) {
+  check_f32(w, "w"); check_f32(wb, "w_big");
+  const ndp::ConvGeom g = conv_geom(geom);
+  TORCH_CHECK(w.numel() == (int64_t)g.Co * g.C * g.KH * g.KW, "toeplitz_expand: weight size");
+  TORCH_CHECK(wb.numel() == (int64_t)g.C * g.H * g.W * g.Co * g.OH * g.OW, "toeplitz_expand: w_big size");
+  ndp::launch_toeplitz_expand(w.data_ptr<float>(), wb.data_ptr<float>(), g, cur_stream());
+  check_launch("launch_toeplitz_expand");
+}
+
+void toeplitz_fold(torch::Tensor dwb, torch::Tensor dw, const std::vector<int64_t>& geom) {
+  check_f32(dwb, "dw_big"); check_f32(dw, "dw");
+  const ndp::ConvGeom g = conv_geom(geom);
+  TORCH_CHECK(dw.numel() == (int64_t)g.Co * g.C * g.KH * g.KW, "toeplitz_fold: weight size");
+  TORCH_CHECK(dwb.numel() == (int64_t)g.C * g.H * g.W * g.Co * g.OH * g.OW, "toeplitz_fold: dw_big size");
+  ndp::launch_toeplitz_fold(dwb.data_ptr<float>(), dw.data_ptr<float>(), g, cur_stream());
+  check_launch("launch_toeplitz_fold");
+}
+
 // q/k/v/o: [B, S, H, 64] fp32 contiguous (== the [B, S, H*64] projections); mask [B, S] int32 or None
 void attn_check(const torch::Tensor& t, const char* n, const torch::Tensor& q) {
   check_f32(t, n);
@@ -403,6 +436,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd", &bn_bwd);
   m.def("bn_slices", &bn_slices);
   m.def("checksum", &checksum);
+  m.def("toeplitz_expand", &toeplitz_expand);
+  m.def("toeplitz_fold", &toeplitz_fold);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
 }

@@ -113,6 +113,20 @@ void launch_bn_bwd(const float* dy, const float* y, const float* x, const float*
                    int N, int C, int HW, int S, int relu, hipStream_t s);
 }  // namespace ndp
 
+// ---- convolutions, NCHW fp32 (conv.hip) -------------------------------------------------
+namespace ndp {
+struct ConvGeom {
+  int32_t C, H, W;        // input channels / spatial
+  int32_t Co, KH, KW;     // output channels / kernel
+  int32_t stride, pad;
+  int32_t OH, OW;         // output spatial
+};
+// Wt_big [Co*OH*OW, C*H*W] <- W [Co, C, KH, KW]  (transposed Toeplitz form of a small-spatial conv)
+void launch_toeplitz_expand(const float* w, float* wb, const ConvGeom& g, hipStream_t s);
+// dW [Co, C, KH, KW] <- fold of dWt_big [Co*OH*OW, C*H*W]  (fixed-order sum, deterministic)
+void launch_toeplitz_fold(const float* dwb, float* dw, const ConvGeom& g, hipStream_t s);
+}  // namespace ndp
+
 // ---- fused fp32 attention, q/k/v/o [B, S, H, 64] (attention.hip) ------------------------
 namespace ndp {
 // mask: [B, S] int32 (nonzero = attend) or null; lse: [B, H, S]; p_drop in [0, 1);

@@ -9,8 +9,8 @@ For an input of C x H x W with H*W small, the convolution is a linear map
     out.view(B, Co*OH*OW) = x.view(B, C*H*W) @ W_big,
 where W_big[(ci,ih,iw), (co,oh,ow)] = W[co, ci, ih - oh*s + p, iw - ow*s + p] (0 outside
 the kernel).  Both views are plain NCHW, so forward, grad-input and grad-weight are three
-hipBLASLt GEMMs; W_big is gathered from W and grad-W is gathered back from grad-W_big with
-a fixed-order sum (deterministic, no atomics).  Only the taps that can ever touch real
+hipBLASLt GEMMs; W_big is built from W and grad-W is folded back from grad-W_big by two
+gfx950 kernels (csrc/conv.hip) with a fixed-order sum (deterministic, no atomics).  Only the taps that can ever touch real
 pixels cost FLOPs.  1x1 strided convs subsample the input first.
 
 ``GemmConv2d`` is a drop-in ``nn.Conv2d`` (same parameters / state_dict); it switches to
@@ -23,6 +23,8 @@ from typing import Dict, Tuple
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from ..ops._ext import ext
 
 __all__ = ["GemmConv2d", "toeplitz_maps", "eligible"]
 
@@ -56,15 +58,25 @@ def toeplitz_maps(C: int, H: int, W: int, Co: int, KH: int, KW: int, s: int, p: 
 
 
 class _ToeplitzConv(torch.autograd.Function):
+    """Device tensors: W_big built / grad-W folded by csrc/conv.hip (index arithmetic, one
+    launch each); CPU tensors (fp64 tests): the same maps as index tensors."""
+
     @staticmethod
-    def forward(ctx, x, weight, src, dst, oh, ow):
+    def forward(ctx, x, weight, src, dst, oh, ow, geom=None):
         B = x.shape[0]
         co = weight.shape[0]
-        w_ext = torch.cat([weight.reshape(-1), weight.new_zeros(1)])
-        w_big = w_ext[src]                                        # [K, N]
         X = x.reshape(B, -1)
-        out = X @ w_big
+        if x.is_cuda and geom is not None:  # device: W_big^T [N, K], built by one kernel
+            C, H, W = x.shape[1:]
+            w_big = torch.empty(co * oh * ow, C * H * W, device=x.device, dtype=x.dtype)
+            ext().toeplitz_expand(weight.contiguous(), w_big, list(geom))
+            out = X @ w_big.t()
+        else:
+            w_ext = torch.cat([weight.reshape(-1), weight.new_zeros(1)])
+            w_big = w_ext[src]                                    # [K, N]
+            out = X @ w_big
         ctx.save_for_backward(X, w_big, dst)
+        ctx.geom = geom
         ctx.x_shape = x.shape
         ctx.w_shape = weight.shape
         return out.view(B, co, oh, ow)
@@ -73,13 +85,21 @@ class _ToeplitzConv(torch.autograd.Function):
     def backward(ctx, g):
         X, w_big, dst = ctx.saved_tensors
         G = g.reshape(g.shape[0], -1)
-        dx = (G @ w_big.t()).view(ctx.x_shape) if ctx.needs_input_grad[0] else None
+        dev = G.is_cuda and ctx.geom is not None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = (G @ w_big if dev else G @ w_big.t()).view(ctx.x_shape)
         dw = None
         if ctx.needs_input_grad[1]:
-            dw_big = X.t() @ G                                    # [K, N]
-            ext = torch.cat([dw_big.reshape(-1), dw_big.new_zeros(1)])
-            dw = ext[dst].sum(-1).view(ctx.w_shape)               # fixed-order, deterministic
-        return dx, dw, None, None, None, None
+            if dev:
+                dwt = G.t() @ X                                   # [N, K]
+                dw = torch.empty(ctx.w_shape, device=dwt.device, dtype=dwt.dtype)
+                ext().toeplitz_fold(dwt, dw, list(ctx.geom))
+            else:
+                dw_big = X.t() @ G                                # [K, N]
+                ext_ = torch.cat([dw_big.reshape(-1), dw_big.new_zeros(1)])
+                dw = ext_[dst].sum(-1).view(ctx.w_shape)          # fixed-order, deterministic
+        return dx, dw, None, None, None, None, None
 
 
 class GemmConv2d(nn.Conv2d):
@@ -100,8 +120,14 @@ class GemmConv2d(nn.Conv2d):
             H, W = (H + sub - 1) // sub, (W + sub - 1) // sub
         key = (C, H, W, x.device, sub)
         if key not in self._maps:
-            src, dst, (oh, ow) = toeplitz_maps(C, H, W, self.out_channels, kh, kw, s, p)
-            self._maps[key] = (src.to(x.device), dst.to(x.device), oh, ow, sub)
+            geom = (C, H, W, self.out_channels, kh, kw, s, p)
+            oh = (H + 2 * p - kh) // s + 1
+            ow = (W + 2 * p - kw) // s + 1
+            if x.is_cuda:  # native expand / fold: no index maps needed
+                self._maps[key] = (None, None, oh, ow, sub, geom)
+            else:
+                src, dst, _ = toeplitz_maps(C, H, W, self.out_channels, kh, kw, s, p)
+                self._maps[key] = (src, dst, oh, ow, sub, None)
         return self._maps[key]
 
     def forward(self, x):
@@ -116,7 +142,7 @@ class GemmConv2d(nn.Conv2d):
         ow = (W + 2 * p - kw) // s + 1
         if not eligible(H, W, oh, ow):
             return super().forward(x)
-        src, dst, oh2, ow2, sub = self._plan(x)
+        src, dst, oh2, ow2, sub, geom = self._plan(x)
         if sub > 1:
             x = x[:, :, ::sub, ::sub]
-        return _ToeplitzConv.apply(x.contiguous(), self.weight, src, dst, oh2, ow2)
+        return _ToeplitzConv.apply(x.contiguous(), self.weight, src, dst, oh2, ow2, geom)

@@ -13,7 +13,8 @@ from torch.utils.cpp_extension import BuildExtension, CUDAExtension
 os.environ.setdefault("PYTORCH_ROCM_ARCH", "gfx950")
 
 CSRC = os.path.join("network_distributed_pytorch_amd", "csrc")
-SOURCES = [os.path.join(CSRC, f) for f in ("bindings.cpp", "plan.cpp", "powersgd.hip", "orth.hip", "multitensor.hip", "batchnorm.hip", "attention.hip")]
+SOURCES = [os.path.join(CSRC, f) for f in ("bindings.cpp", "plan.cpp", "powersgd.hip", "orth.hip", "multitensor.hip", "batchnorm.hip", "attention.hip",
+                                                "conv.hip")]
 
 ext = CUDAExtension(
     name="network_distributed_pytorch_amd._C",

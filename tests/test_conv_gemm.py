@@ -16,7 +16,7 @@ def test_toeplitz_exact_fp64(C, H, Co, k, s, p):
     x = torch.randn(3, C, H, H, dtype=torch.float64, requires_grad=True)
     w = torch.randn(Co, C, k, k, dtype=torch.float64, requires_grad=True)
     src, dst, (oh, ow) = toeplitz_maps(C, H, H, Co, k, k, s, p)
-    y = _ToeplitzConv.apply(x, w, src, dst, oh, ow)
+    y = _ToeplitzConv.apply(x, w, src, dst, oh, ow, None)
     yr = F.conv2d(x, w, stride=s, padding=p)
     g = torch.randn_like(yr)
     a = torch.autograd.grad(y, (x, w), g)
