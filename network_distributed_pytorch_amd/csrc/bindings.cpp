@@ -349,6 +349,64 @@ void toeplitz_fold(torch::Tensor dwb, torch::Tensor dw, const std::vector<int64_
   check_launch("launch_toeplitz_fold");
 }
 
+// (class, fwd images per workgroup, grad-W images per slice, grad-x direct) or class -1
+py::tuple conv_plan(const std::vector<int64_t>& geom) {
+  const ndp::ConvGeom g = conv_geom(geom);
+  const int cls = ndp::conv_direct_class(g);
+  if (cls < 0) return py::make_tuple(-1, 0, 0, false);
+  return py::make_tuple(cls, ndp::conv_fwd_imgs(cls), ndp::conv_wgrad_imgs(cls), ndp::conv_dgrad_direct(cls));
+}
+
+void conv_check(const torch::Tensor& t, const char* n, int64_t b, int64_t c, int64_t h, int64_t w) {
+  check_f32(t, n);
+  TORCH_CHECK(t.dim() == 4 && t.size(0) == b && t.size(1) == c && t.size(2) == h && t.size(3) == w, n,
+              ": shape mismatch with the conv geometry");
+}
+
+int conv_batch(const torch::Tensor& t, const ndp::ConvGeom& g, int imgs) {
+  const int B = (int)t.size(0);
+  TORCH_CHECK(ndp::conv_direct_class(g) >= 0, "conv: no direct kernel for this geometry");
+  TORCH_CHECK(imgs > 0 && B % imgs == 0, "conv: batch must be a multiple of ", imgs);
+  return B;
+}
+
+void conv_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, const std::vector<int64_t>& geom) {
+  const ndp::ConvGeom g = conv_geom(geom);
+  const int B = conv_batch(x, g, ndp::conv_fwd_imgs(ndp::conv_direct_class(g)));
+  conv_check(x, "x", B, g.C, g.H, g.W);
+  conv_check(w, "w", g.Co, g.C, g.KH, g.KW);
+  conv_check(y, "y", B, g.Co, g.OH, g.OW);
+  ndp::launch_conv_fwd(x.data_ptr<float>(), w.data_ptr<float>(), y.data_ptr<float>(), B, g, cur_stream());
+  check_launch("launch_conv_fwd");
+}
+
+void conv_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, const std::vector<int64_t>& geom) {
+  const ndp::ConvGeom g = conv_geom(geom);
+  const int cls = ndp::conv_direct_class(g);
+  TORCH_CHECK(cls >= 0 && ndp::conv_dgrad_direct(cls), "conv_dgrad: no direct grad-x kernel for this geometry");
+  const int B = conv_batch(dy, g, ndp::conv_fwd_imgs(cls));
+  conv_check(dy, "dy", B, g.Co, g.OH, g.OW);
+  conv_check(w, "w", g.Co, g.C, g.KH, g.KW);
+  conv_check(dx, "dx", B, g.C, g.H, g.W);
+  ndp::launch_conv_dgrad(dy.data_ptr<float>(), w.data_ptr<float>(), dx.data_ptr<float>(), B, g, cur_stream());
+  check_launch("launch_conv_dgrad");
+}
+
+void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor part, torch::Tensor dw,
+                const std::vector<int64_t>& geom) {
+  const ndp::ConvGeom g = conv_geom(geom);
+  const int imgs = ndp::conv_wgrad_imgs(ndp::conv_direct_class(g));
+  const int B = conv_batch(x, g, imgs);
+  conv_check(x, "x", B, g.C, g.H, g.W);
+  conv_check(dy, "dy", B, g.Co, g.OH, g.OW);
+  conv_check(dw, "dw", g.Co, g.C, g.KH, g.KW);
+  check_f32(part, "part");
+  TORCH_CHECK(part.numel() >= (int64_t)(B / imgs) * dw.numel(), "conv_wgrad: partial scratch too small");
+  ndp::launch_conv_wgrad(x.data_ptr<float>(), dy.data_ptr<float>(), part.data_ptr<float>(), dw.data_ptr<float>(), B,
+                         g, cur_stream());
+  check_launch("launch_conv_wgrad");
+}
+
 // q/k/v/o: [B, S, H, 64] fp32 contiguous (== the [B, S, H*64] projections); mask [B, S] int32 or None
 void attn_check(const torch::Tensor& t, const char* n, const torch::Tensor& q) {
   check_f32(t, n);
@@ -438,6 +496,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("checksum", &checksum);
   m.def("toeplitz_expand", &toeplitz_expand);
   m.def("toeplitz_fold", &toeplitz_fold);
+  m.def("conv_plan", &conv_plan);
+  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_wgrad", &conv_wgrad);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
 }

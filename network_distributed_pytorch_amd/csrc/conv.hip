@@ -9,6 +9,8 @@
 // scatter chains: profiles/ showed ~0.6 ms per ResNet-18 step in those ATen launches).
 // The fold sums the <= OH*OW taps of each weight in a fixed order: deterministic.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
+
 #include "ndp_kernels.h"
 
 namespace ndp {
@@ -67,6 +69,527 @@ void launch_toeplitz_expand(const float* w, float* wb, const ConvGeom& g, hipStr
 void launch_toeplitz_fold(const float* dwb, float* dw, const ConvGeom& g, hipStream_t s) {
   const int nw = g.Co * g.C * g.KH * g.KW;
   hipLaunchKernelGGL(toeplitz_fold_kernel, dim3((nw + 255) / 256), dim3(256), 0, s, dwb, dw, g);
+}
+
+
+// =====================================================================================
+// Direct (implicit-GEMM) convolutions on v_mfma_f32_32x32x2_f32 — exact f32, NCHW.
+//
+// ResNet-18 on 32x32 images runs its stem at 16x16 and layer1/layer2 at 8x8 / 4x4 maps
+// with 64-128 channels.  MIOpen's fp32 paths for these shapes are Winograd (fwd / grad-x)
+// and NHWC implicit-GEMM (grad-W) kernels that need NCHW<->NHWC transposes and zero-fill
+// passes around every call (profiles/: ~1.1 ms of a 2.7 ms step).  Here each direction is
+// one launch on the matrix cores, reading and writing NCHW directly:
+//
+// forward  Y[k, (b,p,q)] = sum_{c,r,s} W[k,c,r,s] * Xpad[b, c, p*st + r, q*st + s]
+//   GEMM  M = out channels (tile BM), N = output pixels of IMGS whole images, K = C*R*S
+//   chunked by CK input channels.  Per chunk the workgroup stages
+//     A: W[m0:m0+BM, c0:c0+CK, :, :] transposed to [kk][m] (row stride BM+1: conflict-free
+//        transposing writes and conflict-free MFMA reads),
+//     B: the raw input planes x[b, c0:c0+CK] into a zero-bordered [img][c][Hp][Wp] image,
+//        so the im2col operand is ONE ds_read_b32 at (per-lane pixel base + compile-time
+//        tap offset): no bounds checks, no im2col buffer.
+//   The two k-values of each MFMA (lane halves) are channels c and c + CK/2 at the same
+//   tap, so both halves' addresses differ by a constant and every tap offset is an
+//   immediate.  Global loads of chunk i+1 are issued before the MFMAs of chunk i and
+//   written to the other LDS buffer after them (one barrier per chunk).
+// grad-x (stride 1) is the same kernel on dY with the weight transposed and flipped
+//   (TRANSW):  dX[c, (b,h,w)] = sum_{k,r,s} W[k, c, R-1-r, S-1-s] * dYpad[b, k, h + r, w + s]
+//   with pad' = R-1-pad.
+// grad-W   dW[k, (c,r,s)] = sum_{b,p,q} dY[b,k,p,q] * Xpad[b, c, p*st + r, q*st + s]
+//   M = out channels (BM), N = (c,r,s) flattened (CB channels x R*S taps, 32-wide blocks;
+//   each lane carries its (c,r,s) as an LDS base offset), K = pixels, two pixels per MFMA:
+//   rows p and p + P/2.  The batch is split into slices; every slice writes its partial
+//   dW tile to a slab and conv_slab_sum adds the slabs in slice order (deterministic).
+// =====================================================================================
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4c __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+  // D(32x32) += A(32x2) * B(2x32); lane l supplies A[l&31][l>>5] and B[l>>5][l&31];
+  // D: col = l&31, row = (reg&3) + 8*(reg>>2) + 4*(l>>5)
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+template <int R, int S, int ST, int PD, int H, int W, int CK, int BM, int IMGS, int WM, int NBUF, int KB, bool TRANSW>
+struct ConvFwdCfg {
+  static constexpr int P = (H + 2 * PD - R) / ST + 1, Q = (W + 2 * PD - S) / ST + 1, PQ = P * Q;
+  static constexpr int Hp = H + 2 * PD, Wp = W + 2 * PD, HWp = Hp * Wp, HW = H * W;
+  static constexpr int RS = R * S, KK = CK * RS;
+  static constexpr int NSTEP = (CK / 2) * RS, NBLK = NSTEP / KB;
+  static constexpr int BN = IMGS * PQ;
+  static constexpr int WN = 4 / WM;
+  static constexpr int TM = BM / 32 / WM, TN = BN / 32 / WN;
+  static constexpr int LDA = BM + 1;    // [kk][m], odd stride: conflict-free transposing writes
+  static constexpr int A_SZ = KK * LDA;
+  static constexpr int B_SZ = IMGS * CK * HWp;
+  // A staging: float4 rows when every chunk is whole channels and rows are 16-B aligned
+  static constexpr int B4 = IMGS * CK * HW / 4, B_PER_T = (B4 + 255) / 256;
+  static constexpr size_t LDS_BYTES = (size_t)NBUF * (A_SZ + B_SZ) * sizeof(float);
+  static_assert(CK % 2 == 0 && BM % (32 * WM) == 0 && BN % (32 * WN) == 0 && TM >= 1 && TN >= 1, "tile");
+  static_assert(NSTEP % KB == 0, "operand prefetch blocks");
+  static_assert(W % 4 == 0 && BM % 4 == 0, "float4 staging");
+};
+
+// A (weights) is read straight from W: forward rows W[m][c0:c0+CK][:] (CK*RS contiguous
+// floats), grad-x rows W[c][m0:m0+BM][:] (BM*RS contiguous) with the taps flipped; both are
+// written transposed into the [kk][m] LDS image.  VEC=1 needs Cin % CK == 0 (float4 over
+// whole channels); the stem (Cin = 3 < CK) stages scalars.
+template <int R, int S, int ST, int PD, int H, int W, int CK, int BM, int IMGS, int WM, int NBUF, int KB, bool TRANSW,
+          bool VEC>
+__global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                       float* __restrict__ y, int Cin, int Kout) {
+  using G = ConvFwdCfg<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW>;
+  constexpr int AE = (BM * G::KK + 3) / 4;  // float4 slots (scalar path: 4 scalars per slot)
+  constexpr int A_PER_T = (AE + 255) / 256;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* As = smem;
+  float* Bs = smem + NBUF * G::A_SZ;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int m0 = blockIdx.y * BM;
+  const int b0 = blockIdx.x * IMGS;
+  const int nchunks = (Cin + CK - 1) / CK;
+
+  for (int i = tid; i < NBUF * G::B_SZ; i += 256) Bs[i] = 0.f;  // zero borders (never rewritten)
+
+  int a_base[G::TM], b_base[G::TN];
+#pragma unroll
+  for (int tm = 0; tm < G::TM; ++tm) a_base[tm] = h * G::NSTEP * G::LDA + (wm * G::TM + tm) * 32 + l32;
+#pragma unroll
+  for (int tn = 0; tn < G::TN; ++tn) {
+    const int n = (wn * G::TN + tn) * 32 + l32;
+    const int img = n / G::PQ, pq = n - img * G::PQ;
+    const int p = pq / G::Q, q = pq - p * G::Q;
+    b_base[tn] = img * CK * G::HWp + h * (CK / 2) * G::HWp + p * ST * G::Wp + q * ST;
+  }
+
+  f32x4c ra[A_PER_T];
+  f32x4c rb[G::B_PER_T];
+  auto load = [&](int ch) {
+    const int c0 = ch * CK;
+#pragma unroll
+    for (int i = 0; i < A_PER_T; ++i) {
+      const int e = tid + 256 * i;
+      f32x4c v = {0.f, 0.f, 0.f, 0.f};
+      if (e < AE) {
+        if (VEC) {
+          if (!TRANSW) {
+            const int m = e / (G::KK / 4), k4 = e - m * (G::KK / 4);
+            v = *reinterpret_cast<const f32x4c*>(w + ((int64_t)(m0 + m) * Cin + c0) * G::RS + 4 * k4);
+          } else {
+            const int c = e / (BM * G::RS / 4), r4 = e - c * (BM * G::RS / 4);
+            v = *reinterpret_cast<const f32x4c*>(w + ((int64_t)(c0 + c) * Kout + m0) * G::RS + 4 * r4);
+          }
+        } else {  // forward only (stem): 4 scalars, zero past Cin
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int f = 4 * e + j, m = f / G::KK, kk = f - m * G::KK;
+            if (f < BM * G::KK && c0 + kk / G::RS < Cin) v[j] = w[((int64_t)(m0 + m) * Cin + c0) * G::RS + kk];
+          }
+        }
+      }
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < G::B_PER_T; ++i) {
+      const int e = tid + 256 * i;  // float4 index within the IMGS x CK x H x W block
+      f32x4c v = {0.f, 0.f, 0.f, 0.f};
+      if (e < G::B4) {
+        const int img = e / (CK * G::HW / 4), rem4 = e - img * (CK * G::HW / 4);
+        const int c = (4 * rem4) / G::HW;
+        if (c0 + c < Cin)
+          v = *reinterpret_cast<const f32x4c*>(x + ((int64_t)(b0 + img) * Cin + c0) * G::HW + 4 * rem4);
+      }
+      rb[i] = v;
+    }
+  };
+  auto store = [&](int buf) {
+    float* A = As + buf * G::A_SZ;
+    float* B = Bs + buf * G::B_SZ;
+#pragma unroll
+    for (int i = 0; i < A_PER_T; ++i) {
+      const int e = tid + 256 * i;
+      if (e < AE) {
+        if (VEC) {
+          if (!TRANSW) {
+            const int m = e / (G::KK / 4), kk = 4 * (e - m * (G::KK / 4));
+            float* d = A + kk * G::LDA + m;
+            d[0] = ra[i].x; d[G::LDA] = ra[i].y; d[2 * G::LDA] = ra[i].z; d[3 * G::LDA] = ra[i].w;
+          } else {
+            const int c = e / (BM * G::RS / 4), f = 4 * (e - c * (BM * G::RS / 4));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int m = (f + j) / G::RS, rs = (f + j) - m * G::RS;
+              A[(c * G::RS + (G::RS - 1 - rs)) * G::LDA + m] = ra[i][j];  // flip the taps
+            }
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int f = 4 * e + j, m = f / G::KK, kk = f - m * G::KK;
+            if (f < BM * G::KK) A[kk * G::LDA + m] = ra[i][j];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < G::B_PER_T; ++i) {
+      const int e = tid + 256 * i;
+      if (e < G::B4) {
+        const int img = e / (CK * G::HW / 4), rem = 4 * (e - img * (CK * G::HW / 4));
+        const int c = rem / G::HW, hw = rem - c * G::HW;
+        const int hh = hw / W, ww = hw - hh * W;
+        float* d = B + img * CK * G::HWp + c * G::HWp + (hh + PD) * G::Wp + ww + PD;
+        d[0] = rb[i].x; d[1] = rb[i].y; d[2] = rb[i].z; d[3] = rb[i].w;
+      }
+    }
+  };
+
+  f32x16 acc[G::TM][G::TN];
+#pragma unroll
+  for (int tm = 0; tm < G::TM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < G::TN; ++tn)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[tm][tn][r] = 0.f;
+
+  load(0);
+  __syncthreads();  // zero fill before interior writes
+  store(0);
+  __syncthreads();
+  for (int ch = 0; ch < nchunks; ++ch) {
+    const int cur = (NBUF == 2) ? (ch & 1) : 0;
+    if (NBUF == 2 && ch + 1 < nchunks) load(ch + 1);
+    const float* A = As + cur * G::A_SZ;
+    const float* B = Bs + cur * G::B_SZ;
+    // operands of block k+1 are read from LDS while the MFMAs of block k issue
+    float av[2][KB][G::TM], bv[2][KB][G::TN];
+    auto fetch = [&](int blk, int slot) {
+#pragma unroll
+      for (int i = 0; i < KB; ++i) {
+        const int t = blk * KB + i;
+        const int c = t / G::RS, rs = t - c * G::RS, r = rs / S, s = rs - r * S;
+        const int offb = c * G::HWp + r * G::Wp + s;
+#pragma unroll
+        for (int tm = 0; tm < G::TM; ++tm) av[slot][i][tm] = A[a_base[tm] + t * G::LDA];
+#pragma unroll
+        for (int tn = 0; tn < G::TN; ++tn) bv[slot][i][tn] = B[b_base[tn] + offb];
+      }
+    };
+    fetch(0, 0);
+#pragma unroll
+    for (int blk = 0; blk < G::NBLK; ++blk) {
+      if (blk + 1 < G::NBLK) fetch(blk + 1, (blk + 1) & 1);
+#pragma unroll
+      for (int i = 0; i < KB; ++i)
+#pragma unroll
+        for (int tm = 0; tm < G::TM; ++tm)
+#pragma unroll
+          for (int tn = 0; tn < G::TN; ++tn)
+            acc[tm][tn] = mfma32(av[blk & 1][i][tm], bv[blk & 1][i][tn], acc[tm][tn]);
+    }
+    if (ch + 1 < nchunks) {
+      if (NBUF == 2) {
+        store(cur ^ 1);
+      } else {
+        __syncthreads();  // everyone done reading the single buffer
+        load(ch + 1);
+        store(0);
+      }
+    }
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int tm = 0; tm < G::TM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < G::TN; ++tn) {
+      const int n = (wn * G::TN + tn) * 32 + l32;
+      const int img = n / G::PQ, pq = n - img * G::PQ;
+      float* yb = y + (int64_t)(b0 + img) * Kout * G::PQ + pq;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + (wm * G::TM + tm) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        yb[(int64_t)m * G::PQ] = acc[tm][tn][r];
+      }
+    }
+}
+
+// ---- grad-W -----------------------------------------------------------------------------
+template <int R, int S, int ST, int PD, int H, int W, int CB, int BM, int NW, int NBPW, int KB>
+struct ConvWgCfg {
+  static constexpr int P = (H + 2 * PD - R) / ST + 1, Q = (W + 2 * PD - S) / ST + 1, PQ = P * Q;
+  static constexpr int Hp = H + 2 * PD, Wp = W + 2 * PD, HWp = Hp * Wp, HW = H * W;
+  static constexpr int RS = R * S, J = CB * RS, JB = (J + 31) / 32, MB = BM / 32;
+  static constexpr int NSTEP = PQ / 2, NBLK = NSTEP / KB;
+  static constexpr int LDY = PQ + 1;
+  static constexpr int A_SZ = BM * LDY;  // dY tile of one image: [m][pixel]
+  static constexpr int B_SZ = CB * HWp;  // zero-bordered x planes of one image
+  static constexpr int NT = 64 * NW;
+  static constexpr int A4 = BM * PQ / 4, B4 = CB * HW / 4;
+  static constexpr int A_PER_T = (A4 + NT - 1) / NT, B_PER_T = (B4 + NT - 1) / NT;
+  static constexpr size_t LDS_BYTES = 2 * (size_t)(A_SZ + B_SZ) * sizeof(float);
+  static_assert(MB * JB == NW * NBPW, "every wave owns NBPW 32x32 blocks");
+  static_assert(P % 2 == 0 && PQ % 4 == 0 && HW % 4 == 0 && NSTEP % KB == 0, "pixel pairing / float4 loads");
+};
+
+template <int R, int S, int ST, int PD, int H, int W, int CB, int BM, int NW, int NBPW, int KB>
+__global__ __launch_bounds__(64 * NW) void conv_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                                             float* __restrict__ part, int Cin, int Kout,
+                                                             int imgs_per_slice) {
+  using G = ConvWgCfg<R, S, ST, PD, H, W, CB, BM, NW, NBPW, KB>;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* As = smem;                 // [2][A_SZ]
+  float* Bs = smem + 2 * G::A_SZ;   // [2][B_SZ]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int slice = blockIdx.x, m0 = blockIdx.y * BM, c0 = blockIdx.z * CB;
+  const int bb = slice * imgs_per_slice;
+
+  for (int i = tid; i < 2 * G::B_SZ; i += G::NT) Bs[i] = 0.f;
+
+  int a_base[NBPW], b_base[NBPW];
+#pragma unroll
+  for (int t = 0; t < NBPW; ++t) {
+    const int blk = wave * NBPW + t;
+    const int mb = blk / G::JB, jb = blk - mb * G::JB;
+    const int j = jb * 32 + l32;
+    a_base[t] = (mb * 32 + l32) * G::LDY + h * (G::PQ / 2);
+    const int c = j / G::RS, rs = j - c * G::RS;
+    const int r = rs / S, s = rs - r * S;
+    b_base[t] = (j < G::J) ? c * G::HWp + r * G::Wp + s + h * (G::P / 2) * ST * G::Wp : 0;
+  }
+
+  f32x4c ra[G::A_PER_T], rb[G::B_PER_T];
+  auto load = [&](int b) {
+#pragma unroll
+    for (int i = 0; i < G::A_PER_T; ++i) {
+      const int e = tid + G::NT * i;
+      f32x4c v = {0.f, 0.f, 0.f, 0.f};
+      if (e < G::A4) v = *reinterpret_cast<const f32x4c*>(dy + ((int64_t)b * Kout + m0) * G::PQ + 4 * e);
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < G::B_PER_T; ++i) {
+      const int e = tid + G::NT * i;
+      f32x4c v = {0.f, 0.f, 0.f, 0.f};
+      if (e < G::B4 && c0 + (4 * e) / G::HW < Cin)
+        v = *reinterpret_cast<const f32x4c*>(x + ((int64_t)b * Cin + c0) * G::HW + 4 * e);
+      rb[i] = v;
+    }
+  };
+  auto store = [&](int buf) {
+    float* A = As + buf * G::A_SZ;
+    float* B = Bs + buf * G::B_SZ;
+#pragma unroll
+    for (int i = 0; i < G::A_PER_T; ++i) {
+      const int e = tid + G::NT * i;
+      if (e < G::A4) {
+        const int m = (4 * e) / G::PQ, pq = 4 * e - m * G::PQ;
+        float* d = A + m * G::LDY + pq;
+        d[0] = ra[i].x; d[1] = ra[i].y; d[2] = ra[i].z; d[3] = ra[i].w;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < G::B_PER_T; ++i) {
+      const int e = tid + G::NT * i;
+      if (e < G::B4) {
+        const int c = (4 * e) / G::HW, hw = 4 * e - c * G::HW;
+        const int hh = hw / W, ww = hw - hh * W;
+        float* d = B + c * G::HWp + (hh + PD) * G::Wp + ww + PD;
+        d[0] = rb[i].x; d[1] = rb[i].y; d[2] = rb[i].z; d[3] = rb[i].w;
+      }
+    }
+  };
+
+  f32x16 acc[NBPW];
+#pragma unroll
+  for (int t = 0; t < NBPW; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  load(bb);
+  __syncthreads();
+  store(0);
+  __syncthreads();
+  for (int i = 0; i < imgs_per_slice; ++i) {
+    const int cur = i & 1;
+    if (i + 1 < imgs_per_slice) load(bb + i + 1);
+    const float* A = As + cur * G::A_SZ;
+    const float* B = Bs + cur * G::B_SZ;
+    float av[2][KB][NBPW], bv[2][KB][NBPW];
+    auto fetch = [&](int blk, int slot) {
+#pragma unroll
+      for (int k = 0; k < KB; ++k) {
+        const int t = blk * KB + k;
+        const int p = t / G::Q, q = t - p * G::Q;
+#pragma unroll
+        for (int u = 0; u < NBPW; ++u) {
+          av[slot][k][u] = A[a_base[u] + t];
+          bv[slot][k][u] = B[b_base[u] + p * ST * G::Wp + q * ST];
+        }
+      }
+    };
+    fetch(0, 0);
+#pragma unroll
+    for (int blk = 0; blk < G::NBLK; ++blk) {
+      if (blk + 1 < G::NBLK) fetch(blk + 1, (blk + 1) & 1);
+#pragma unroll
+      for (int k = 0; k < KB; ++k)
+#pragma unroll
+        for (int u = 0; u < NBPW; ++u) acc[u] = mfma32(av[blk & 1][k][u], bv[blk & 1][k][u], acc[u]);
+    }
+    if (i + 1 < imgs_per_slice) store(cur ^ 1);
+    __syncthreads();
+  }
+
+  float* out = part + (int64_t)slice * Kout * Cin * G::RS;
+#pragma unroll
+  for (int t = 0; t < NBPW; ++t) {
+    const int blk = wave * NBPW + t;
+    const int mb = blk / G::JB, jb = blk - mb * G::JB;
+    const int j = jb * 32 + l32;
+    if (j < G::J && c0 + j / G::RS < Cin) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + mb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        out[((int64_t)m * Cin + c0) * G::RS + j] = acc[t][r];
+      }
+    }
+  }
+}
+
+// dw[i] = sum_{s < n_slices} part[s * n + i], n % 4 == 0.  A workgroup owns 16 float4
+// columns x 16 slice groups: thread (g, col) sums slices g, g+16, ... of its column, then
+// group 0 adds the 16 group sums in order — a fixed summation tree (deterministic) with
+// 16x the memory-level parallelism of a one-thread-per-column sum.
+__global__ __launch_bounds__(256) void conv_slab_sum_kernel(const float* __restrict__ part, float* __restrict__ dw,
+                                                            int64_t n, int n_slices) {
+  __shared__ f32x4c red[16][16];
+  const int col = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int64_t i4 = ((int64_t)blockIdx.x * 16 + col) * 4;
+  f32x4c acc = {0.f, 0.f, 0.f, 0.f};
+  if (i4 < n) {
+#pragma unroll 4
+    for (int s = g; s < n_slices; s += 16) acc += *reinterpret_cast<const f32x4c*>(part + (int64_t)s * n + i4);
+  }
+  red[g][col] = acc;
+  __syncthreads();
+  if (g == 0 && i4 < n) {
+    f32x4c t = red[0][col];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) t += red[k][col];
+    *reinterpret_cast<f32x4c*>(dw + i4) = t;
+  }
+}
+
+// ---- dispatch -----------------------------------------------------------------------------
+template <typename KernelT>
+static void set_lds(KernelT k, size_t bytes) {
+  hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+template <int R, int S, int ST, int PD, int H, int W, int CK, int BM, int IMGS, int WM, int NBUF, int KB, bool TRANSW,
+          bool VEC>
+static void run_fwd(const float* x, const float* w, float* y, int B, int Cin, int Kout, hipStream_t s) {
+  using G = ConvFwdCfg<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW>;
+  auto k = conv_fwd_kernel<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW, VEC>;
+  static bool attr = false;  // once per instantiation (> 64 KiB of LDS needs the opt-in)
+  if (!attr) { set_lds(k, G::LDS_BYTES); attr = true; }
+  hipLaunchKernelGGL(k, dim3(B / IMGS, Kout / BM), dim3(256), G::LDS_BYTES, s, x, w, y, Cin, Kout);
+}
+
+template <int R, int S, int ST, int PD, int H, int W, int CB, int BM, int NW, int NBPW, int KB>
+static void run_wgrad(const float* x, const float* dy, float* part, float* dw, int B, int Cin, int Kout,
+                      int imgs, hipStream_t s) {
+  using G = ConvWgCfg<R, S, ST, PD, H, W, CB, BM, NW, NBPW, KB>;
+  auto k = conv_wgrad_kernel<R, S, ST, PD, H, W, CB, BM, NW, NBPW, KB>;
+  static bool attr = false;
+  if (!attr) { set_lds(k, G::LDS_BYTES); attr = true; }
+  const int slices = B / imgs;
+  hipLaunchKernelGGL(k, dim3(slices, Kout / BM, (Cin + CB - 1) / CB), dim3(G::NT), G::LDS_BYTES, s, x, dy, part, Cin,
+                     Kout, imgs);
+  const int64_t n = (int64_t)Kout * Cin * G::RS;  // multiple of 4 for every class
+  hipLaunchKernelGGL(conv_slab_sum_kernel, dim3((unsigned)((n / 4 + 15) / 16)), dim3(256), 0, s, part, dw, n, slices);
+}
+
+// Shape classes with a direct kernel (everything else stays on MIOpen / the Toeplitz path)
+//   id 0: 3x3 s1 p1 on 8x8   (ResNet layer1)           C, K % 64 == 0
+//   id 1: 3x3 s1 p1 on 4x4   (ResNet layer2)           C, K % 64 == 0
+//   id 2: 3x3 s2 p1 8x8->4x4 (layer2 first conv)       C % 32 == 0, K % 64 == 0
+//   id 3: 7x7 s2 p3 32x32->16x16, C = 3 (stem)         K % 64 == 0
+int conv_direct_class(const ConvGeom& g) {
+  if (g.KH == 3 && g.KW == 3 && g.pad == 1 && g.stride == 1 && g.H == 8 && g.W == 8 && g.C % 64 == 0 && g.Co % 64 == 0)
+    return 0;
+  if (g.KH == 3 && g.KW == 3 && g.pad == 1 && g.stride == 1 && g.H == 4 && g.W == 4 && g.C % 64 == 0 && g.Co % 64 == 0)
+    return 1;
+  if (g.KH == 3 && g.KW == 3 && g.pad == 1 && g.stride == 2 && g.H == 8 && g.W == 8 && g.C % 32 == 0 && g.Co % 64 == 0)
+    return 2;
+  if (g.KH == 7 && g.KW == 7 && g.pad == 3 && g.stride == 2 && g.H == 32 && g.W == 32 && g.C == 3 && g.Co % 64 == 0)
+    return 3;
+  return -1;
+}
+
+// tuning variant (NDP_CONV_VARIANT, benchmarking only): 0 = default
+static int conv_variant() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("NDP_CONV_VARIANT");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
+}
+
+// images per workgroup of the forward / grad-x kernels, images per grad-W slice
+int conv_fwd_imgs(int cls) {
+  if (cls == 0) return conv_variant() == 1 ? 2 : 1;
+  return cls == 3 ? 1 : 4;
+}
+int conv_wgrad_imgs(int cls) {
+  if (cls == 0) return conv_variant() == 1 ? 2 : 4;
+  return cls == 1 ? 16 : cls == 2 ? 8 : 2;
+}
+bool conv_dgrad_direct(int cls) { return cls == 0 || cls == 1; }
+void launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, hipStream_t s) {
+  switch (conv_direct_class(g)) {
+    case 0:
+      if (conv_variant() == 1) run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 2, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, s);
+      else run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, s);
+      break;
+    case 1: run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, s); break;
+    case 2: run_fwd<3, 3, 2, 1, 8, 8, 8, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, s); break;
+    case 3: run_fwd<7, 7, 2, 3, 32, 32, 4, 64, 1, 2, 1, 7, false, false>(x, w, y, B, g.C, g.Co, s); break;
+    default: break;
+  }
+}
+
+// dx[B, C, H, W] from dy[B, Co, OH, OW] (stride-1 classes only)
+void launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, hipStream_t s) {
+  switch (conv_direct_class(g)) {
+    case 0:
+      if (conv_variant() == 1) run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 2, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, s);
+      else run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, s);
+      break;
+    case 1: run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, s); break;
+    default: break;
+  }
+}
+
+// part: (B / conv_wgrad_imgs) * Co * C * KH * KW floats of scratch
+void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, int B, const ConvGeom& g,
+                       hipStream_t s) {
+  const int cls = conv_direct_class(g);
+  const int imgs = conv_wgrad_imgs(cls);
+  switch (cls) {
+    case 0: run_wgrad<3, 3, 1, 1, 8, 8, 32, 32, 3, 3, 4>(x, dy, part, dw, B, g.C, g.Co, imgs, s); break;
+    case 1: run_wgrad<3, 3, 1, 1, 4, 4, 32, 32, 3, 3, 4>(x, dy, part, dw, B, g.C, g.Co, imgs, s); break;
+    case 2: run_wgrad<3, 3, 2, 1, 8, 8, 32, 32, 3, 3, 4>(x, dy, part, dw, B, g.C, g.Co, imgs, s); break;
+    case 3: run_wgrad<7, 7, 2, 3, 32, 32, 3, 32, 5, 1, 4>(x, dy, part, dw, B, g.C, g.Co, imgs, s); break;
+    default: break;
+  }
 }
 
 }  // namespace ndp

@@ -125,6 +125,16 @@ struct ConvGeom {
 void launch_toeplitz_expand(const float* w, float* wb, const ConvGeom& g, hipStream_t s);
 // dW [Co, C, KH, KW] <- fold of dWt_big [Co*OH*OW, C*H*W]  (fixed-order sum, deterministic)
 void launch_toeplitz_fold(const float* dwb, float* dw, const ConvGeom& g, hipStream_t s);
+// direct fp32-MFMA convolutions: shape class (-1 = none), images per workgroup / slice
+int conv_direct_class(const ConvGeom& g);
+int conv_fwd_imgs(int cls);
+int conv_wgrad_imgs(int cls);
+bool conv_dgrad_direct(int cls);
+void launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, hipStream_t s);
+void launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, hipStream_t s);
+// part: (B / conv_wgrad_imgs(cls)) * Co*C*KH*KW floats of scratch
+void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, int B, const ConvGeom& g,
+                       hipStream_t s);
 }  // namespace ndp
 
 // ---- fused fp32 attention, q/k/v/o [B, S, H, 64] (attention.hip) ------------------------

@@ -13,8 +13,12 @@ hipBLASLt GEMMs; W_big is built from W and grad-W is folded back from grad-W_big
 gfx950 kernels (csrc/conv.hip) with a fixed-order sum (deterministic, no atomics).  Only the taps that can ever touch real
 pixels cost FLOPs.  1x1 strided convs subsample the input first.
 
-``GemmConv2d`` is a drop-in ``nn.Conv2d`` (same parameters / state_dict); it switches to
-the GEMM form only where it pays: input H*W <= 16 and output OH*OW <= 4.
+``GemmConv2d`` is a drop-in ``nn.Conv2d`` (same parameters / state_dict) that picks, per
+input geometry, the fastest native path:
+  1. a direct fp32-MFMA kernel (csrc/conv.hip via ops/conv.py) for the ResNet CIFAR shapes
+     it covers (stem 7x7/2 on 32x32, 3x3 on 8x8 and 4x4, 3x3/2 8x8->4x4);
+  2. the Toeplitz GEMM form where it pays: input H*W <= 16 and output OH*OW <= 4;
+  3. MIOpen otherwise.
 """
 from __future__ import annotations
 
@@ -25,6 +29,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops._ext import ext
+from ..ops.conv import DirectConvFn, direct_plan
 
 __all__ = ["GemmConv2d", "toeplitz_maps", "eligible"]
 
@@ -105,9 +110,10 @@ class _ToeplitzConv(torch.autograd.Function):
 class GemmConv2d(nn.Conv2d):
     """``nn.Conv2d`` that runs small-spatial cases as exact hipBLASLt GEMMs."""
 
-    def __init__(self, *a, gemm: bool = True, **kw):
+    def __init__(self, *a, gemm: bool = True, direct: bool = True, **kw):
         super().__init__(*a, **kw)
         self.gemm = gemm
+        self.direct = direct
         self._maps: Dict[Tuple, tuple] = {}
 
     def _plan(self, x):
@@ -138,6 +144,10 @@ class GemmConv2d(nn.Conv2d):
         H, W = x.shape[2:]
         kh, kw = self.kernel_size
         s, p = self.stride[0], self.padding[0]
+        if self.direct:
+            plan = direct_plan(x, self.weight, s, p)
+            if plan is not None:
+                return DirectConvFn.apply(x, self.weight, plan)
         oh = (H + 2 * p - kh) // s + 1
         ow = (W + 2 * p - kw) // s + 1
         if not eligible(H, W, oh, ow):

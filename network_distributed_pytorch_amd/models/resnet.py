@@ -10,13 +10,13 @@ Q-init RNG order match the reference exactly), same init (Kaiming-normal fan_out
 BN = (1, 0)).  Weights are random (the GPU box has no network for pretrained downloads);
 checkpoints written by torchvision load with ``load_state_dict`` unchanged.
 
-MI355X notes: convolutions run on PyTorch-ROCm (MIOpen).  Every BatchNorm is a
+MI355X notes: every conv is a :class:`~network_distributed_pytorch_amd.models.conv_gemm.GemmConv2d`
+(native direct fp32-MFMA kernels for the stem / layer1 / layer2 CIFAR shapes, Toeplitz
+GEMMs for layer3 / layer4, MIOpen elsewhere).  Every BatchNorm is a
 :class:`~network_distributed_pytorch_amd.ops.batchnorm.BatchNormAct2d` (``fused_bn=True``):
 BN, the residual add and the ReLU of each block run as two fused gfx950 kernels per
-direction (same parameters/buffers/state_dict keys as ``nn.BatchNorm2d``).  Every conv is
-a :class:`~network_distributed_pytorch_amd.models.conv_gemm.GemmConv2d`: on the 4x4 / 2x2 /
-1x1 maps of layer3-4 it runs as exact hipBLASLt GEMMs instead of padding-dominated MIOpen
-tiles (``gemm_convs=False`` restores plain MIOpen everywhere).
+direction (same parameters/buffers/state_dict keys as ``nn.BatchNorm2d``).
+``gemm_convs=False`` restores plain MIOpen everywhere.
 """
 from __future__ import annotations
 
@@ -102,7 +102,7 @@ class ResNet(nn.Module):
         self.norm = BatchNormAct2d if fused_bn else nn.BatchNorm2d
         self.fused = fused_bn
         self.inplanes = 64
-        self.conv1 = nn.Conv2d(3, 64, kernel_size=7, stride=2, padding=3, bias=False)
+        self.conv1 = GemmConv2d(3, 64, kernel_size=7, stride=2, padding=3, bias=False)
         self.bn1 = self.norm(64)
         self.relu = nn.ReLU(inplace=True)
         self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
@@ -115,6 +115,7 @@ class ResNet(nn.Module):
         for m in self.modules():
             if isinstance(m, GemmConv2d):
                 m.gemm = gemm_convs
+                m.direct = gemm_convs
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
             elif isinstance(m, nn.BatchNorm2d):  # includes BatchNormAct2d

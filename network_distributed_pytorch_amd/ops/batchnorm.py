@@ -56,7 +56,9 @@ class _BNActFn(torch.autograd.Function):
 
 def bn_act(x, weight, bias, running_mean, running_var, nbt, part, training, momentum, eps,
            residual=None, relu=False):
-    if x.is_cuda:
+    needs_grad = torch.is_grad_enabled() and (x.requires_grad or (weight is not None and weight.requires_grad)
+                                              or (residual is not None and residual.requires_grad))
+    if x.is_cuda and (training or not needs_grad):  # eval + autograd: differentiable torch path below
         if x.dtype != torch.float32:  # bf16 autocast: normalise in fp32 (stats are fp64 anyway)
             x = x.float()
             residual = residual.float() if residual is not None else None

@@ -1,0 +1,83 @@
+"""Direct fp32-MFMA convolutions (csrc/conv.hip) for ResNet's CIFAR-shape layers.
+
+``conv2d_direct(x, weight, stride, padding)`` runs forward, grad-input and grad-weight on
+hand-written gfx950 kernels for the shape classes the extension reports through
+``conv_plan`` (ResNet stem 7x7/2 on 32x32, layer1 3x3 on 8x8, layer2 3x3 on 4x4 and its
+strided 8x8->4x4 entry conv).  Grad-input of the strided classes goes to MIOpen
+(``aten.convolution_backward``); the stem's input never needs a gradient.
+:func:`direct_plan` returns None for every other geometry, so callers keep their MIOpen /
+Toeplitz paths there.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from ._ext import ext
+
+__all__ = ["direct_plan", "conv2d_direct", "DirectConvFn"]
+
+_PLANS: dict = {}
+
+
+def direct_plan(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int) -> Optional[Tuple]:
+    """(geom, fwd_imgs, wgrad_imgs, dgrad_direct) if a direct kernel covers this conv."""
+    if not (x.is_cuda and x.dtype == torch.float32 and weight.dtype == torch.float32 and x.dim() == 4):
+        return None
+    B, C, H, W = x.shape
+    Co, Ci, KH, KW = weight.shape
+    if Ci != C:
+        return None
+    geom = (C, H, W, Co, KH, KW, int(stride), int(padding))
+    if geom not in _PLANS:
+        cls, fi, wi, dd = ext().conv_plan(list(geom))
+        _PLANS[geom] = None if cls < 0 else (geom, int(fi), int(wi), bool(dd))
+    plan = _PLANS[geom]
+    if plan is None or B % plan[1] or B % plan[2]:
+        return None
+    return plan
+
+
+class DirectConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, plan):
+        geom, _, wgrad_imgs, dgrad_direct = plan
+        C, H, W, Co, KH, KW, s, p = geom
+        x = x.contiguous()
+        weight = weight.contiguous()
+        B = x.shape[0]
+        OH = (H + 2 * p - KH) // s + 1
+        OW = (W + 2 * p - KW) // s + 1
+        y = torch.empty(B, Co, OH, OW, device=x.device, dtype=x.dtype)
+        ext().conv_fwd(x, weight, y, list(geom))
+        ctx.save_for_backward(x, weight)
+        ctx.plan = plan
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        geom, _, wgrad_imgs, dgrad_direct = ctx.plan
+        s, p = geom[6], geom[7]
+        dy = dy.contiguous()
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            if dgrad_direct:
+                dx = torch.empty_like(x)
+                ext().conv_dgrad(dy, weight, dx, list(geom))
+            else:
+                dx = torch.ops.aten.convolution_backward(dy, x, weight, None, [s, s], [p, p], [1, 1], False, [0, 0],
+                                                         1, [True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            B = x.shape[0]
+            dw = torch.empty_like(weight)
+            part = torch.empty((B // wgrad_imgs) * weight.numel(), device=x.device, dtype=x.dtype)
+            ext().conv_wgrad(x, dy, part, dw, list(geom))
+        return dx, dw, None
+
+
+def conv2d_direct(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int, plan=None) -> torch.Tensor:
+    plan = plan if plan is not None else direct_plan(x, weight, stride, padding)
+    assert plan is not None, "no direct kernel for this convolution"
+    return DirectConvFn.apply(x, weight, plan)
