@@ -29,7 +29,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops._ext import ext
-from ..ops.conv import DirectConvFn, direct_plan
+from ..ops import conv as _conv
+from ..ops.conv import DirectConvFn, direct_plan, side_stream
 
 __all__ = ["GemmConv2d", "toeplitz_maps", "eligible"]
 
@@ -91,19 +92,29 @@ class _ToeplitzConv(torch.autograd.Function):
         X, w_big, dst = ctx.saved_tensors
         G = g.reshape(g.shape[0], -1)
         dev = G.is_cuda and ctx.geom is not None
-        dx = None
+        dx = dw = None
+        if dev:  # grad-W (GEMM + fold) on the side stream, grad-x on the current one
+            main = torch.cuda.current_stream()
+            fork = _conv.FORK_WGRAD and ctx.needs_input_grad[0] and ctx.needs_input_grad[1]
+            if ctx.needs_input_grad[1]:
+                dw = torch.empty(ctx.w_shape, device=G.device, dtype=G.dtype)
+                dwt = torch.empty(w_big.shape, device=G.device, dtype=G.dtype)
+                side = side_stream(G.device) if fork else main
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    torch.mm(G.t(), X, out=dwt)                   # [N, K]
+                    ext().toeplitz_fold(dwt, dw, list(ctx.geom))
+            if ctx.needs_input_grad[0]:
+                dx = (G @ w_big).view(ctx.x_shape)
+            if fork:
+                main.wait_stream(side)
+            return dx, dw, None, None, None, None, None
         if ctx.needs_input_grad[0]:
-            dx = (G @ w_big if dev else G @ w_big.t()).view(ctx.x_shape)
-        dw = None
+            dx = (G @ w_big.t()).view(ctx.x_shape)
         if ctx.needs_input_grad[1]:
-            if dev:
-                dwt = G.t() @ X                                   # [N, K]
-                dw = torch.empty(ctx.w_shape, device=dwt.device, dtype=dwt.dtype)
-                ext().toeplitz_fold(dwt, dw, list(ctx.geom))
-            else:
-                dw_big = X.t() @ G                                # [K, N]
-                ext_ = torch.cat([dw_big.reshape(-1), dw_big.new_zeros(1)])
-                dw = ext_[dst].sum(-1).view(ctx.w_shape)          # fixed-order, deterministic
+            dw_big = X.t() @ G                                    # [K, N]
+            ext_ = torch.cat([dw_big.reshape(-1), dw_big.new_zeros(1)])
+            dw = ext_[dst].sum(-1).view(ctx.w_shape)              # fixed-order, deterministic
         return dx, dw, None, None, None, None, None
 
 

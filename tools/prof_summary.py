@@ -15,6 +15,7 @@ import sys
 
 
 def short(name: str) -> str:
+    name = name.replace("(anonymous namespace)", "anon")
     name = re.sub(r"\(.*", "", name)
     name = name.replace("void ", "")
     return name[:110]
