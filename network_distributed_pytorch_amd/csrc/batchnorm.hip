@@ -17,6 +17,8 @@
 // Semantics follow torch.nn.BatchNorm2d (training): biased variance for normalisation,
 // unbiased variance in running_var, running = (1-momentum)*running + momentum*batch.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
+
 #include "ndp_kernels.h"
 
 namespace ndp {
@@ -256,6 +258,203 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   }
 }
 
+// ---- small feature maps (HW <= 16: ResNet layer3/layer4 on 32x32 inputs) -----------------
+// In NCHW a channel's pixels are HW contiguous floats, so the per-(channel, slice) kernels
+// above read 4-64 B per cache line there.  These kernels treat x as [N][C*HW] instead: a
+// thread owns one column j = c*HW + hw and walks its slice of n (every load instruction is
+// 256 consecutive floats), the HW lanes of a channel are combined with shuffles, and a tiny
+// per-channel finalize kernel folds the slice partials in a fixed order (deterministic).
+// part layout: [c][s][2] partial sums, then 3*C doubles of per-channel coefficients.
+constexpr int kSmallNPer = 4;  // images per stats slice: 4 independent loads in flight per thread
+int bn_small_slices(int N, int C, int HW) { return (N + kSmallNPer - 1) / kSmallNPer; }
+
+template <int HW>
+__global__ __launch_bounds__(256) void bn_small_stats_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                                             const float* __restrict__ y,
+                                                             const float* __restrict__ save_mean,
+                                                             const float* __restrict__ save_invstd,
+                                                             double* __restrict__ part, int N, int C, int S, int bwd,
+                                                             int relu) {
+  const int CHW = C * HW;
+  const int j = blockIdx.y * 256 + threadIdx.x;
+  const int s = blockIdx.x;
+  const int n0 = s * kSmallNPer;
+  double a = 0.0, b = 0.0;
+  if (j < CHW) {
+    float v[kSmallNPer], d[kSmallNPer], m[kSmallNPer];
+#pragma unroll
+    for (int k = 0; k < kSmallNPer; ++k) {  // issue every load first
+      const bool ok = n0 + k < N;
+      const int64_t o = (int64_t)(n0 + k) * CHW + j;
+      v[k] = ok ? x[o] : 0.f;
+      d[k] = (bwd && ok) ? dy[o] : 0.f;
+      m[k] = (bwd && relu && ok) ? y[o] : 1.f;
+    }
+    if (!bwd) {
+#pragma unroll
+      for (int k = 0; k < kSmallNPer; ++k) {
+        a += (double)v[k];
+        b += (double)v[k] * (double)v[k];
+      }
+    } else {
+      const int c = j / HW;
+      const float mean = save_mean[c], invstd = save_invstd[c];
+#pragma unroll
+      for (int k = 0; k < kSmallNPer; ++k) {
+        if (n0 + k < N) {
+          const float dz = (m[k] > 0.f) ? d[k] : 0.f;
+          a += (double)dz;
+          b += (double)dz * (double)((v[k] - mean) * invstd);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int o = HW / 2; o > 0; o >>= 1) {  // the HW lanes of one channel are adjacent
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+  }
+  if (j < CHW && (j % HW) == 0) {
+    const int c = j / HW;
+    part[((int64_t)c * S + s) * 2] = a;
+    part[((int64_t)c * S + s) * 2 + 1] = b;
+  }
+}
+
+// one wave per channel: lane l adds slices l, l+64, ... then a fixed xor butterfly
+// forward: coef[c] = scale, coef[C + c] = shift (+ save_mean / invstd / running stats / nbt)
+// backward: coef = (k1, mdz, mdzx) and dgamma / dbeta
+__global__ __launch_bounds__(256) void bn_small_finalize_kernel(
+    const double* __restrict__ part, double* __restrict__ coef, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt,
+    float* __restrict__ save_mean, float* __restrict__ save_invstd, float* __restrict__ dgamma,
+    float* __restrict__ dbeta, int N, int C, int HW, int S, float eps, float momentum, int bwd) {
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (c >= C) return;  // whole waves exit together
+  double a = 0.0, b = 0.0;
+  for (int k = lane; k < S; k += 64) {
+    a += part[((int64_t)c * S + k) * 2];
+    b += part[((int64_t)c * S + k) * 2 + 1];
+  }
+  a = wave_sum_d(a);
+  b = wave_sum_d(b);
+  if (lane != 0) return;
+  const double M = (double)N * HW;
+  if (!bwd) {
+    const double mu = a / M;
+    double var = b / M - mu * mu;
+    if (var < 0.0) var = 0.0;
+    const float mean = (float)mu, invstd = (float)(1.0 / sqrt(var + (double)eps));
+    save_mean[c] = mean;
+    save_invstd[c] = invstd;
+    if (rmean != nullptr) {
+      const double unb = M > 1.0 ? var * M / (M - 1.0) : var;
+      rmean[c] = (float)((1.0 - momentum) * (double)rmean[c] + momentum * mu);
+      rvar[c] = (float)((1.0 - momentum) * (double)rvar[c] + momentum * unb);
+    }
+    if (nbt != nullptr && c == 0) nbt[0] += 1;
+    const float scale = (gamma ? gamma[c] : 1.f) * invstd;
+    coef[c] = scale;
+    coef[C + c] = (beta ? beta[c] : 0.f) - mean * scale;
+  } else {
+    if (dgamma) dgamma[c] = (float)b;
+    if (dbeta) dbeta[c] = (float)a;
+    coef[c] = (gamma ? gamma[c] : 1.f) * save_invstd[c];  // k1
+    coef[C + c] = (float)(a / M);                         // mean dz
+    coef[2 * C + c] = (float)(b / M);                     // mean dz * xhat
+  }
+}
+
+// elementwise over the whole tensor, 4 consecutive elements (one float4) per thread
+__global__ __launch_bounds__(256) void bn_small_apply_kernel(
+    const float* __restrict__ x, const float* __restrict__ res, const float* __restrict__ dy,
+    const float* __restrict__ yin, const float* __restrict__ save_mean, const float* __restrict__ save_invstd,
+    const double* __restrict__ coef, float* __restrict__ out, float* __restrict__ dres, int total, int C, int HW,
+    int relu, int bwd) {
+  const int i0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i0 >= total) return;
+  const bool full = i0 + 3 < total;  // total % 4 == 0 in practice: one float4 per thread
+  f32x4 xv, r = {0.f, 0.f, 0.f, 0.f}, g = {0.f, 0.f, 0.f, 0.f}, yv = {1.f, 1.f, 1.f, 1.f}, o, dz;
+  if (full) {
+    xv = *reinterpret_cast<const f32x4*>(x + i0);
+    if (!bwd && res) r = *reinterpret_cast<const f32x4*>(res + i0);
+    if (bwd) g = *reinterpret_cast<const f32x4*>(dy + i0);
+    if (bwd && relu) yv = *reinterpret_cast<const f32x4*>(yin + i0);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool ok = i0 + k < total;
+      xv[k] = ok ? x[i0 + k] : 0.f;
+      if (!bwd && res) r[k] = ok ? res[i0 + k] : 0.f;
+      if (bwd) g[k] = ok ? dy[i0 + k] : 0.f;
+      if (bwd && relu) yv[k] = ok ? yin[i0 + k] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = ((i0 + k) / HW) % C;
+    if (!bwd) {
+      const float z = fmaf(xv[k], (float)coef[c], (float)coef[C + c]) + r[k];
+      o[k] = relu ? fmaxf(z, 0.f) : z;
+    } else {
+      dz[k] = (yv[k] > 0.f) ? g[k] : 0.f;
+      const float xh = (xv[k] - save_mean[c]) * save_invstd[c];
+      o[k] = (float)coef[c] * (dz[k] - (float)coef[C + c] - xh * (float)coef[2 * C + c]);
+    }
+  }
+  if (full) {
+    *reinterpret_cast<f32x4*>(out + i0) = o;
+    if (bwd && dres) *reinterpret_cast<f32x4*>(dres + i0) = dz;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (i0 + k < total) {
+        out[i0 + k] = o[k];
+        if (bwd && dres) dres[i0 + k] = dz[k];
+      }
+    }
+  }
+}
+
+template <int HW>
+static void small_stats(const float* x, const float* dy, const float* y, const float* sm, const float* si,
+                        double* part, int N, int C, int S, int bwd, int relu, hipStream_t s) {
+  const dim3 grid(S, (C * HW + 255) / 256);
+  hipLaunchKernelGGL(bn_small_stats_kernel<HW>, grid, dim3(256), 0, s, x, dy, y, sm, si, part, N, C, S, bwd, relu);
+}
+
+static void small_stats_any(int HW, const float* x, const float* dy, const float* y, const float* sm, const float* si,
+                            double* part, int N, int C, int S, int bwd, int relu, hipStream_t s) {
+  switch (HW) {
+    case 1: small_stats<1>(x, dy, y, sm, si, part, N, C, S, bwd, relu, s); break;
+    case 2: small_stats<2>(x, dy, y, sm, si, part, N, C, S, bwd, relu, s); break;
+    case 4: small_stats<4>(x, dy, y, sm, si, part, N, C, S, bwd, relu, s); break;
+    case 8: small_stats<8>(x, dy, y, sm, si, part, N, C, S, bwd, relu, s); break;
+    default: small_stats<16>(x, dy, y, sm, si, part, N, C, S, bwd, relu, s); break;
+  }
+}
+
+// largest HW routed to the small-map kernels (NDP_BN_SMALL_MAX, tuning only; default 4)
+static int bn_small_max() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("NDP_BN_SMALL_MAX");
+    v = e ? atoi(e) : 4;  // HW = 16 measured faster on the per-channel kernels
+  }
+  return v;
+}
+
+bool bn_small_path(int N, int C, int HW) {
+  return (HW == 1 || HW == 2 || HW == 4 || HW == 8 || HW == 16) && HW <= bn_small_max() &&
+         (int64_t)N * C * HW < (1LL << 30);
+}
+
+int64_t bn_part_numel(int N, int C, int HW) {
+  const int64_t big = (int64_t)C * bn_slices(N, C, HW) * 2;
+  const int64_t small = (int64_t)C * bn_small_slices(N, C, HW) * 2 + 3 * (int64_t)C;
+  return big > small ? big : small;
+}
+
 // ----------------------------------- launchers -------------------------------------------
 int bn_slices(int N, int C, int HW) {
   // ~4 workgroups per CU over the whole launch, >= ~2K elements per workgroup
@@ -271,6 +470,17 @@ void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamm
                    float* rmean, float* rvar, int64_t* nbt, float* save_mean, float* save_invstd,
                    double* part, int N, int C, int HW, int S, float eps, float momentum, int relu,
                    int training, hipStream_t s) {
+  if (training && bn_small_path(N, C, HW)) {
+    const int Ss = bn_small_slices(N, C, HW);
+    double* coef = part + (int64_t)C * Ss * 2;
+    small_stats_any(HW, x, nullptr, nullptr, nullptr, nullptr, part, N, C, Ss, 0, 0, s);
+    hipLaunchKernelGGL(bn_small_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, s, part, coef, gamma, beta, rmean,
+                       rvar, nbt, save_mean, save_invstd, nullptr, nullptr, N, C, HW, Ss, eps, momentum, 0);
+    const int total = N * C * HW;
+    hipLaunchKernelGGL(bn_small_apply_kernel, dim3((unsigned)((total / 4 + 255) / 256 + 1)), dim3(256), 0, s, x, res,
+                       nullptr, nullptr, nullptr, nullptr, coef, y, nullptr, total, C, HW, relu, 0);
+    return;
+  }
   const bool vec = (HW % 4) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 &&
                    (res == nullptr || ((uintptr_t)res & 15) == 0);
   const dim3 grid(S, C);
@@ -289,6 +499,18 @@ void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamm
 void launch_bn_bwd(const float* dy, const float* y, const float* x, const float* gamma, const float* save_mean,
                    const float* save_invstd, float* dx, float* dres, float* dgamma, float* dbeta, double* part,
                    int N, int C, int HW, int S, int relu, hipStream_t s) {
+  if (bn_small_path(N, C, HW)) {
+    const int Ss = bn_small_slices(N, C, HW);
+    double* coef = part + (int64_t)C * Ss * 2;
+    small_stats_any(HW, x, dy, y, save_mean, save_invstd, part, N, C, Ss, 1, relu, s);
+    hipLaunchKernelGGL(bn_small_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, s, part, coef, gamma, nullptr,
+                       nullptr, nullptr, nullptr, nullptr, const_cast<float*>(save_invstd), dgamma, dbeta, N, C, HW, Ss,
+                       0.f, 0.f, 1);
+    const int total = N * C * HW;
+    hipLaunchKernelGGL(bn_small_apply_kernel, dim3((unsigned)((total / 4 + 255) / 256 + 1)), dim3(256), 0, s, x,
+                       nullptr, dy, y, save_mean, save_invstd, coef, dx, dres, total, C, HW, relu, 1);
+    return;
+  }
   const bool vec = (HW % 4) == 0 && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)x & 15) == 0 &&
                    ((uintptr_t)dx & 15) == 0 && (!relu || ((uintptr_t)y & 15) == 0) &&
                    (dres == nullptr || ((uintptr_t)dres & 15) == 0);

@@ -264,7 +264,8 @@ void bn_fwd(torch::Tensor x, c10::optional<torch::Tensor> res, torch::Tensor y,
   const int N = (int)x.size(0), C = (int)x.size(1);
   const int HW = (int)(x.numel() / ((int64_t)N * C));
   const int S = ndp::bn_slices(N, C, HW);
-  TORCH_CHECK(part.scalar_type() == torch::kFloat64 && part.numel() >= (int64_t)C * S * 2, "bn part too small");
+  TORCH_CHECK(part.scalar_type() == torch::kFloat64 && part.numel() >= ndp::bn_part_numel(N, C, HW),
+              "bn part too small");
   TORCH_CHECK(save_mean.numel() >= C && save_invstd.numel() >= C, "bn save buffers too small");
   if (res.has_value()) TORCH_CHECK(res->sizes() == x.sizes(), "bn residual shape");
   int64_t* nb = nullptr;
@@ -291,7 +292,8 @@ void bn_bwd(torch::Tensor dy, c10::optional<torch::Tensor> y, torch::Tensor x, c
   const int N = (int)x.size(0), C = (int)x.size(1);
   const int HW = (int)(x.numel() / ((int64_t)N * C));
   const int S = ndp::bn_slices(N, C, HW);
-  TORCH_CHECK(part.scalar_type() == torch::kFloat64 && part.numel() >= (int64_t)C * S * 2, "bn part too small");
+  TORCH_CHECK(part.scalar_type() == torch::kFloat64 && part.numel() >= ndp::bn_part_numel(N, C, HW),
+              "bn part too small");
   ndp::launch_bn_bwd(dy.data_ptr<float>(), opt_f32(y, "y"), x.data_ptr<float>(), opt_f32(gamma, "gamma"),
                      save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(), dx.data_ptr<float>(),
                      const_cast<float*>(opt_f32(dres, "dres")), const_cast<float*>(opt_f32(dgamma, "dgamma")),
@@ -301,6 +303,7 @@ void bn_bwd(torch::Tensor dy, c10::optional<torch::Tensor> y, torch::Tensor x, c
 }
 
 int bn_slices(int N, int C, int HW) { return ndp::bn_slices(N, C, HW); }
+int64_t bn_part_numel(int N, int C, int HW) { return ndp::bn_part_numel(N, C, HW); }
 
 void delay_ns(int64_t ns) {
   ndp::launch_delay_ns(ns, cur_stream());
@@ -493,6 +496,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_fwd", &bn_fwd);
   m.def("bn_bwd", &bn_bwd);
   m.def("bn_slices", &bn_slices);
+  m.def("bn_part_numel", &bn_part_numel);
   m.def("checksum", &checksum);
   m.def("toeplitz_expand", &toeplitz_expand);
   m.def("toeplitz_fold", &toeplitz_fold);

@@ -103,6 +103,8 @@ void launch_checksum(const float* x, int64_t n, double* out, hipStream_t s);
 // ---- fused BatchNorm2d (+residual) (+ReLU), NCHW fp32 (batchnorm.hip) -------------------
 namespace ndp {
 int bn_slices(int N, int C, int HW);
+// doubles of `part` scratch a (N, C, HW) BN needs (large-map slices or the small-map path)
+int64_t bn_part_numel(int N, int C, int HW);
 // part: C * S * 2 doubles of scratch; rmean/rvar/nbt may be null; training=0 uses running stats
 void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamma, const float* beta,
                    float* rmean, float* rvar, int64_t* nbt, float* save_mean, float* save_invstd,

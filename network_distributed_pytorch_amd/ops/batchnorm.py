@@ -89,6 +89,16 @@ class BatchNormAct2d(nn.BatchNorm2d):
         self.register_buffer("_part", torch.zeros((num_features + 1024) * 2, dtype=torch.float64),
                              persistent=False)
 
+    def _ensure_part(self, x: torch.Tensor) -> None:
+        """Grow the fp64 partial-sum scratch to what this input shape needs (first call for
+        a shape happens eagerly — warm-up — never inside a graph capture)."""
+        key = (x.shape[0], x.shape[1], x.numel() // max(1, x.shape[0] * x.shape[1]))
+        if key != getattr(self, "_part_key", None):
+            need = int(ext().bn_part_numel(*key))
+            if self._part.numel() < need or self._part.device != x.device:
+                self._part = torch.zeros(need, dtype=torch.float64, device=x.device)
+            self._part_key = key
+
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, relu: bool = False):
         if self.momentum is None or not self.track_running_stats:
             y = super().forward(x)
@@ -96,6 +106,8 @@ class BatchNormAct2d(nn.BatchNorm2d):
                 y = y + residual
             return F.relu(y) if relu else y
         training = self.training
+        if x.is_cuda:
+            self._ensure_part(x)
         return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var,
                       self.num_batches_tracked if training else None, self._part, training, self.momentum,
                       self.eps, residual, relu)

@@ -11,7 +11,8 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("shape", [(512, 64, 8, 8), (64, 128, 4, 4), (32, 512, 1, 1), (16, 24, 7, 7),
-                                   (8, 64, 16, 16), (3, 5, 2, 3)])
+                                   (8, 64, 16, 16), (3, 5, 2, 3), (512, 256, 2, 2), (40, 96, 2, 1),
+                                   (7, 40, 2, 4)])
 @pytest.mark.parametrize("res,relu", [(False, False), (False, True), (True, True)])
 def test_bn_act_train_fwd_bwd(device, shape, res, relu):
     assert ops.native_available()
