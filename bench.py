@@ -147,6 +147,11 @@ def main():
     graph_mode = args.graph_mode
     if graph_mode == "auto" and "ref" in args.reducer:
         graph_mode = "none"  # reference-semantics arms are eager by definition
+    if graph_mode == "auto" and world > 1 and backend != "nccl":
+        # gloo-on-device (test rehearsal of N ranks on one GPU): gloo's host thread waits on
+        # events behind unsynchronised graph replays and stalls for seconds per step
+        # (tools/piecewise_diag.py shows the segments themselves are fine)
+        graph_mode = "none"
     if graph_mode != "none":
         from network_distributed_pytorch_amd.utils.graph import StepRunner
 

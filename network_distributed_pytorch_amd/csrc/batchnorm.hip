@@ -416,6 +416,153 @@ __global__ __launch_bounds__(256) void bn_small_apply_kernel(
   }
 }
 
+// ---- single-launch small-map BN (column block x every image, register resident) ---------
+// The three small-map kernels above are each only a few µs of work on 1-2 MB tensors, so
+// a ResNet-18 step spends most of their ~300 µs in launch gaps.  This kernel does a whole
+// BN direction in ONE launch with no cross-workgroup traffic: a workgroup owns kColW
+// consecutive columns of the [N][C*HW] view (whole channels, since HW | kColW) for EVERY
+// image.  Its 512 threads are kColW columns x kRowG row groups; thread (g, col) keeps rows
+// g, g + kRowG, ... (<= kFusedRows of them) in registers, so the tensor is read once and
+// written once.  Per-channel sums: fp64 per thread -> xor shuffle over the HW lanes of a
+// channel -> fixed-order fold of the kRowG row-group partials through LDS (every thread
+// gets the bitwise-identical value; deterministic).  Each wave-wide load covers 4 rows x
+// kColW consecutive floats.  Used when N <= kRowG * kFusedRows (ResNet's per-GPU 512).
+constexpr int kColW = 16;
+constexpr int kRowG = 32;
+constexpr int kFusedRows = 16;
+constexpr int kFusedThreads = kColW * kRowG;
+
+template <int HW, int BWD>
+__global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
+    const float* __restrict__ x, const float* __restrict__ res, const float* __restrict__ dy,
+    const float* __restrict__ yin, const float* __restrict__ gamma, const float* __restrict__ beta,
+    float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt, float* __restrict__ save_mean,
+    float* __restrict__ save_invstd, float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ out,
+    float* __restrict__ dres, int N, int C, float eps, float momentum, int relu) {
+  constexpr int NP = kFusedRows;
+  __shared__ double red[2][kRowG][kColW];
+  const int CHW = C * HW;
+  const int col = threadIdx.x % kColW, g = threadIdx.x / kColW;
+  const int j = blockIdx.x * kColW + col;
+  const bool ok_col = j < CHW;
+  const int c = ok_col ? j / HW : 0;
+  float v[NP], d[NP], m[NP];
+  float mean_s = 0.f, invstd_s = 0.f;
+  if (BWD && ok_col) {
+    mean_s = save_mean[c];
+    invstd_s = save_invstd[c];
+  }
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {  // every load in flight before any use
+    const int n = g + k * kRowG;
+    const bool ok = ok_col && n < N;
+    const int64_t o = (int64_t)n * CHW + j;
+    v[k] = ok ? x[o] : 0.f;
+    if (BWD) {
+      d[k] = ok ? dy[o] : 0.f;
+      m[k] = (ok && relu) ? yin[o] : 1.f;
+    } else {
+      d[k] = (ok && res) ? res[o] : 0.f;
+    }
+  }
+  double a = 0.0, b = 0.0;
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    if (g + k * kRowG < N) {
+      if (!BWD) {
+        a += (double)v[k];
+        b += (double)v[k] * (double)v[k];
+      } else {
+        const float dz = (m[k] > 0.f) ? d[k] : 0.f;
+        a += (double)dz;
+        b += (double)dz * (double)((v[k] - mean_s) * invstd_s);
+      }
+    }
+  }
+#pragma unroll
+  for (int o = HW / 2; o > 0; o >>= 1) {  // the HW columns of a channel are adjacent lanes
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+  }
+  red[0][g][col] = a;
+  red[1][g][col] = b;
+  __syncthreads();
+  double A = 0.0, B = 0.0;
+#pragma unroll
+  for (int k = 0; k < kRowG; ++k) {
+    A += red[0][k][col];
+    B += red[1][k][col];
+  }
+  if (!ok_col) return;
+  const double M = (double)N * HW;
+  const bool writer = g == 0 && (j % HW) == 0;
+  if (!BWD) {
+    const double mu = A / M;
+    double var = B / M - mu * mu;
+    if (var < 0.0) var = 0.0;
+    const float mean = (float)mu, invstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float scale = (gamma ? gamma[c] : 1.f) * invstd;
+    const float shift = (beta ? beta[c] : 0.f) - mean * scale;
+    if (writer) {
+      save_mean[c] = mean;
+      save_invstd[c] = invstd;
+      if (rmean != nullptr) {
+        const double unb = M > 1.0 ? var * M / (M - 1.0) : var;
+        rmean[c] = (float)((1.0 - momentum) * (double)rmean[c] + momentum * mu);
+        rvar[c] = (float)((1.0 - momentum) * (double)rvar[c] + momentum * unb);
+      }
+      if (nbt != nullptr && c == 0) nbt[0] += 1;
+    }
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const int n = g + k * kRowG;
+      if (n < N) {
+        const float z = fmaf(v[k], scale, shift) + d[k];
+        out[(int64_t)n * CHW + j] = relu ? fmaxf(z, 0.f) : z;
+      }
+    }
+  } else {
+    if (writer) {
+      if (dgamma) dgamma[c] = (float)B;
+      if (dbeta) dbeta[c] = (float)A;
+    }
+    const float k1 = (gamma ? gamma[c] : 1.f) * invstd_s;
+    const float mdz = (float)(A / M), mdzx = (float)(B / M);
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const int n = g + k * kRowG;
+      if (n < N) {
+        const float dz = (m[k] > 0.f) ? d[k] : 0.f;
+        const float xh = (v[k] - mean_s) * invstd_s;
+        const int64_t o = (int64_t)n * CHW + j;
+        out[o] = k1 * (dz - mdz - xh * mdzx);
+        if (dres) dres[o] = dz;
+      }
+    }
+  }
+}
+
+static bool bn_fused_ok(int N, int C, int HW) {
+  return (HW == 1 || HW == 2 || HW == 4) && N >= 1 && N <= kRowG * kFusedRows && (int64_t)N * C * HW < (1LL << 30);
+}
+
+template <int BWD>
+static void launch_small_fused(int HW, const float* x, const float* res, const float* dy, const float* yin,
+                               const float* gamma, const float* beta, float* rmean, float* rvar, int64_t* nbt,
+                               float* sm, float* si, float* dgamma, float* dbeta, float* out, float* dres, int N,
+                               int C, float eps, float momentum, int relu, hipStream_t s) {
+  const dim3 grid((unsigned)(((int64_t)C * HW + kColW - 1) / kColW));
+#define NDP_BN_FUSED(HWV)                                                                                           \
+  hipLaunchKernelGGL((bn_small_fused_kernel<HWV, BWD>), grid, dim3(kFusedThreads), 0, s, x, res, dy, yin, gamma, beta, \
+                     rmean, rvar, nbt, sm, si, dgamma, dbeta, out, dres, N, C, eps, momentum, relu)
+  switch (HW) {
+    case 1: NDP_BN_FUSED(1); break;
+    case 2: NDP_BN_FUSED(2); break;
+    default: NDP_BN_FUSED(4); break;
+  }
+#undef NDP_BN_FUSED
+}
+
 template <int HW>
 static void small_stats(const float* x, const float* dy, const float* y, const float* sm, const float* si,
                         double* part, int N, int C, int S, int bwd, int relu, hipStream_t s) {
@@ -469,7 +616,12 @@ int bn_slices(int N, int C, int HW) {
 void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamma, const float* beta,
                    float* rmean, float* rvar, int64_t* nbt, float* save_mean, float* save_invstd,
                    double* part, int N, int C, int HW, int S, float eps, float momentum, int relu,
-                   int training, hipStream_t s) {
+                   int training, int single, hipStream_t s) {
+  if (training && single && bn_fused_ok(N, C, HW)) {
+    launch_small_fused<0>(HW, x, res, nullptr, nullptr, gamma, beta, rmean, rvar, nbt, save_mean, save_invstd,
+                          nullptr, nullptr, y, nullptr, N, C, eps, momentum, relu, s);
+    return;
+  }
   if (training && bn_small_path(N, C, HW)) {
     const int Ss = bn_small_slices(N, C, HW);
     double* coef = part + (int64_t)C * Ss * 2;
@@ -498,7 +650,13 @@ void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamm
 
 void launch_bn_bwd(const float* dy, const float* y, const float* x, const float* gamma, const float* save_mean,
                    const float* save_invstd, float* dx, float* dres, float* dgamma, float* dbeta, double* part,
-                   int N, int C, int HW, int S, int relu, hipStream_t s) {
+                   int N, int C, int HW, int S, int relu, int single, hipStream_t s) {
+  if (single && bn_fused_ok(N, C, HW)) {
+    launch_small_fused<1>(HW, x, nullptr, dy, y, gamma, nullptr, nullptr, nullptr, nullptr,
+                          const_cast<float*>(save_mean), const_cast<float*>(save_invstd), dgamma, dbeta, dx, dres, N, C,
+                          0.f, 0.f, relu, s);
+    return;
+  }
   if (bn_small_path(N, C, HW)) {
     const int Ss = bn_small_slices(N, C, HW);
     double* coef = part + (int64_t)C * Ss * 2;

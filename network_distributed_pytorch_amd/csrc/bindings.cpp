@@ -257,7 +257,8 @@ void bn_fwd(torch::Tensor x, c10::optional<torch::Tensor> res, torch::Tensor y,
             c10::optional<torch::Tensor> gamma, c10::optional<torch::Tensor> beta,
             c10::optional<torch::Tensor> rmean, c10::optional<torch::Tensor> rvar,
             c10::optional<torch::Tensor> nbt, torch::Tensor save_mean, torch::Tensor save_invstd,
-            torch::Tensor part, double eps, double momentum, bool relu, bool training) {
+            torch::Tensor part, double eps, double momentum, bool relu, bool training,
+            bool single) {
   check_f32(x, "x"); check_f32(y, "y"); check_f32(save_mean, "save_mean"); check_f32(save_invstd, "save_invstd");
   check_dev(part, "part");
   TORCH_CHECK(x.dim() >= 2 && x.sizes() == y.sizes(), "bn_fwd: bad shapes");
@@ -278,14 +279,14 @@ void bn_fwd(torch::Tensor x, c10::optional<torch::Tensor> res, torch::Tensor y,
                      opt_f32(beta, "beta"), const_cast<float*>(opt_f32(rmean, "running_mean")),
                      const_cast<float*>(opt_f32(rvar, "running_var")), nb, save_mean.data_ptr<float>(),
                      save_invstd.data_ptr<float>(), part.data_ptr<double>(), N, C, HW, S, (float)eps,
-                     (float)momentum, relu ? 1 : 0, training ? 1 : 0, cur_stream());
+                     (float)momentum, relu ? 1 : 0, training ? 1 : 0, single ? 1 : 0, cur_stream());
   check_launch("launch_bn_fwd");
 }
 
 void bn_bwd(torch::Tensor dy, c10::optional<torch::Tensor> y, torch::Tensor x, c10::optional<torch::Tensor> gamma,
             torch::Tensor save_mean, torch::Tensor save_invstd, torch::Tensor dx, c10::optional<torch::Tensor> dres,
             c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta, torch::Tensor part,
-            bool relu) {
+            bool relu, bool single) {
   check_f32(dy, "dy"); check_f32(x, "x"); check_f32(dx, "dx"); check_dev(part, "part");
   TORCH_CHECK(dy.sizes() == x.sizes() && dx.sizes() == x.sizes(), "bn_bwd: bad shapes");
   TORCH_CHECK(!relu || y.has_value(), "bn_bwd: relu needs y");
@@ -298,8 +299,43 @@ void bn_bwd(torch::Tensor dy, c10::optional<torch::Tensor> y, torch::Tensor x, c
                      save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(), dx.data_ptr<float>(),
                      const_cast<float*>(opt_f32(dres, "dres")), const_cast<float*>(opt_f32(dgamma, "dgamma")),
                      const_cast<float*>(opt_f32(dbeta, "dbeta")), part.data_ptr<double>(), N, C, HW, S,
-                     relu ? 1 : 0, cur_stream());
+                     relu ? 1 : 0, single ? 1 : 0, cur_stream());
   check_launch("launch_bn_bwd");
+}
+
+// max-pool 2-D (stride/pad symmetric, dilation 1, floor mode): x [N, C, H, W] -> y, idx [N, C, OH, OW]
+static ndp::PoolGeom pool_geom(const torch::Tensor& x, const torch::Tensor& y, int64_t k, int64_t stride,
+                               int64_t pad) {
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && x.size(0) == y.size(0) && x.size(1) == y.size(1),
+              "maxpool: bad shapes");
+  TORCH_CHECK(k >= 1 && k * k <= 256 && stride >= 1 && pad >= 0 && 2 * pad <= k, "maxpool: bad window");
+  ndp::PoolGeom g;
+  g.H = (int)x.size(2); g.W = (int)x.size(3); g.OH = (int)y.size(2); g.OW = (int)y.size(3);
+  g.KH = g.KW = (int)k; g.stride = (int)stride; g.pad = (int)pad;
+  TORCH_CHECK(g.OH == (g.H + 2 * g.pad - g.KH) / g.stride + 1 && g.OW == (g.W + 2 * g.pad - g.KW) / g.stride + 1,
+              "maxpool: output size mismatch");
+  TORCH_CHECK(x.numel() < ((int64_t)1 << 31) - 256, "maxpool: tensor too large (32-bit indexing)");
+  return g;
+}
+
+void maxpool_fwd(torch::Tensor x, torch::Tensor y, torch::Tensor idx, int64_t k, int64_t stride, int64_t pad) {
+  check_f32(x, "x"); check_f32(y, "y"); check_dev(idx, "idx");
+  TORCH_CHECK(idx.scalar_type() == torch::kUInt8 && idx.sizes() == y.sizes() && idx.is_contiguous(),
+              "maxpool: idx must be contiguous uint8 shaped like y");
+  const ndp::PoolGeom g = pool_geom(x, y, k, stride, pad);
+  ndp::launch_maxpool_fwd(x.data_ptr<float>(), y.data_ptr<float>(), idx.data_ptr<uint8_t>(),
+                          (int)(x.size(0) * x.size(1)), g, cur_stream());
+  check_launch("launch_maxpool_fwd");
+}
+
+void maxpool_bwd(torch::Tensor dy, torch::Tensor idx, torch::Tensor dx, int64_t k, int64_t stride, int64_t pad) {
+  check_f32(dy, "dy"); check_f32(dx, "dx"); check_dev(idx, "idx");
+  TORCH_CHECK(idx.scalar_type() == torch::kUInt8 && idx.sizes() == dy.sizes() && idx.is_contiguous(),
+              "maxpool: idx must be contiguous uint8 shaped like dy");
+  const ndp::PoolGeom g = pool_geom(dx, dy, k, stride, pad);
+  ndp::launch_maxpool_bwd(dy.data_ptr<float>(), idx.data_ptr<uint8_t>(), dx.data_ptr<float>(),
+                          (int)(dx.size(0) * dx.size(1)), g, cur_stream());
+  check_launch("launch_maxpool_bwd");
 }
 
 int bn_slices(int N, int C, int HW) { return ndp::bn_slices(N, C, HW); }
@@ -497,6 +533,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd", &bn_bwd);
   m.def("bn_slices", &bn_slices);
   m.def("bn_part_numel", &bn_part_numel);
+  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_bwd", &maxpool_bwd);
   m.def("checksum", &checksum);
   m.def("toeplitz_expand", &toeplitz_expand);
   m.def("toeplitz_fold", &toeplitz_fold);

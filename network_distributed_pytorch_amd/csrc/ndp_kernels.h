@@ -105,14 +105,15 @@ namespace ndp {
 int bn_slices(int N, int C, int HW);
 // doubles of `part` scratch a (N, C, HW) BN needs (large-map slices or the small-map path)
 int64_t bn_part_numel(int N, int C, int HW);
-// part: C * S * 2 doubles of scratch; rmean/rvar/nbt may be null; training=0 uses running stats
+// part: C * S * 2 doubles of scratch; rmean/rvar/nbt may be null; training=0 uses running stats;
+// single: allow the one-launch small-map path (HW <= 4, N <= 512)
 void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamma, const float* beta,
                    float* rmean, float* rvar, int64_t* nbt, float* save_mean, float* save_invstd,
                    double* part, int N, int C, int HW, int S, float eps, float momentum, int relu,
-                   int training, hipStream_t s);
+                   int training, int single, hipStream_t s);
 void launch_bn_bwd(const float* dy, const float* y, const float* x, const float* gamma, const float* save_mean,
                    const float* save_invstd, float* dx, float* dres, float* dgamma, float* dbeta, double* part,
-                   int N, int C, int HW, int S, int relu, hipStream_t s);
+                   int N, int C, int HW, int S, int relu, int single, hipStream_t s);
 }  // namespace ndp
 
 // ---- convolutions, NCHW fp32 (conv.hip) -------------------------------------------------
@@ -149,4 +150,16 @@ void launch_attn_fwd(const float* q, const float* k, const float* v, const int32
 void launch_attn_bwd(const float* q, const float* k, const float* v, const int32_t* mask, const float* o,
                      const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv, int B,
                      int S, int H, float scale, const int32_t* seed, float p_drop, hipStream_t s);
+}  // namespace ndp
+
+// ---- max-pool 2-D, NCHW fp32, deterministic gather backward (pool.hip) ---------------
+namespace ndp {
+struct PoolGeom {
+  int32_t H, W, OH, OW;
+  int32_t KH, KW, stride, pad;
+};
+// idx: uint8 window offset (kh*KW + kw) of each output's maximum
+void launch_maxpool_fwd(const float* x, float* y, uint8_t* idx, int planes, const PoolGeom& g, hipStream_t s);
+void launch_maxpool_bwd(const float* dy, const uint8_t* idx, float* dx, int planes, const PoolGeom& g,
+                        hipStream_t s);
 }  // namespace ndp

@@ -26,6 +26,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.batchnorm import BatchNormAct2d
+from ..ops.pool import MaxPool2d
 from .conv_gemm import GemmConv2d
 
 __all__ = ["ResNet", "BasicBlock", "Bottleneck", "resnet18", "resnet34", "resnet50", "resnet101",
@@ -105,7 +106,8 @@ class ResNet(nn.Module):
         self.conv1 = GemmConv2d(3, 64, kernel_size=7, stride=2, padding=3, bias=False)
         self.bn1 = self.norm(64)
         self.relu = nn.ReLU(inplace=True)
-        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        # native deterministic pool when fused kernels are on (no params: state_dict unchanged)
+        self.maxpool = (MaxPool2d if fused_bn else nn.MaxPool2d)(kernel_size=3, stride=2, padding=1)
         self.layer1 = self._make_layer(block, 64, layers[0])
         self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
         self.layer3 = self._make_layer(block, 256, layers[2], stride=2)

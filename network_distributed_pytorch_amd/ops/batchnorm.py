@@ -24,7 +24,7 @@ __all__ = ["BatchNormAct2d", "bn_act"]
 
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, res, weight, bias, running_mean, running_var, nbt, part, eps, momentum, relu):
+    def forward(ctx, x, res, weight, bias, running_mean, running_var, nbt, part, eps, momentum, relu, sync=None):
         X = ext()
         x = x.contiguous()
         if res is not None:
@@ -34,8 +34,9 @@ class _BNActFn(torch.autograd.Function):
         save_mean = torch.empty(C, device=x.device, dtype=torch.float32)
         save_invstd = torch.empty(C, device=x.device, dtype=torch.float32)
         X.bn_fwd(x, res, y, weight, bias, running_mean, running_var, nbt, save_mean, save_invstd, part,
-                 float(eps), float(momentum), bool(relu), True)
+                 float(eps), float(momentum), bool(relu), True, sync)
         ctx.relu = bool(relu)
+        ctx.sync = sync
         ctx.has_res = res is not None
         ctx.has_w = weight is not None
         ctx.save_for_backward(x, y if relu else None, weight, save_mean, save_invstd, part)
@@ -50,12 +51,12 @@ class _BNActFn(torch.autograd.Function):
         dres = torch.empty_like(x) if ctx.has_res else None
         dgamma = torch.empty_like(weight) if ctx.has_w else None
         dbeta = torch.empty_like(weight) if ctx.has_w else None
-        ext().bn_bwd(dy, y, x, weight, save_mean, save_invstd, dx, dres, dgamma, dbeta, part, ctx.relu)
-        return dx, dres, dgamma, dbeta, None, None, None, None, None, None, None
+        ext().bn_bwd(dy, y, x, weight, save_mean, save_invstd, dx, dres, dgamma, dbeta, part, ctx.relu, ctx.sync)
+        return dx, dres, dgamma, dbeta, None, None, None, None, None, None, None, None
 
 
 def bn_act(x, weight, bias, running_mean, running_var, nbt, part, training, momentum, eps,
-           residual=None, relu=False):
+           residual=None, relu=False, sync=None):
     needs_grad = torch.is_grad_enabled() and (x.requires_grad or (weight is not None and weight.requires_grad)
                                               or (residual is not None and residual.requires_grad))
     if x.is_cuda and (training or not needs_grad):  # eval + autograd: differentiable torch path below
@@ -64,13 +65,13 @@ def bn_act(x, weight, bias, running_mean, running_var, nbt, part, training, mome
             residual = residual.float() if residual is not None else None
         if training:
             return _BNActFn.apply(x, residual, weight, bias, running_mean, running_var, nbt, part, eps,
-                                  momentum, relu)
+                                  momentum, relu, sync)
         y = torch.empty_like(x := x.contiguous())
         C = x.shape[1]
         sm = torch.empty(C, device=x.device)
         si = torch.empty(C, device=x.device)
         ext().bn_fwd(x, residual.contiguous() if residual is not None else None, y, weight, bias, running_mean,
-                     running_var, None, sm, si, part, float(eps), 0.0, bool(relu), False)
+                     running_var, None, sm, si, part, float(eps), 0.0, bool(relu), False, None)
         return y
     y = F.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps)
     if training and nbt is not None:
@@ -88,6 +89,8 @@ class BatchNormAct2d(nn.BatchNorm2d):
         # per-(channel, slice) fp64 partials: C * S * 2 with S <= ceil(1024 / C) (bn_slices)
         self.register_buffer("_part", torch.zeros((num_features + 1024) * 2, dtype=torch.float64),
                              persistent=False)
+        self._sync: Optional[torch.Tensor] = None
+        self.fused_small = True  # single-launch small-map kernels (HW <= 4)
 
     def _ensure_part(self, x: torch.Tensor) -> None:
         """Grow the fp64 partial-sum scratch to what this input shape needs (first call for
@@ -97,6 +100,11 @@ class BatchNormAct2d(nn.BatchNorm2d):
             need = int(ext().bn_part_numel(*key))
             if self._part.numel() < need or self._part.device != x.device:
                 self._part = torch.zeros(need, dtype=torch.float64, device=x.device)
+            # barrier words of the single-launch small-map path: zeroed once, they return to
+            # zero after every launch (csrc/batchnorm.hip, bn_small_fused_kernel)
+            nsync = int(ext().bn_sync_numel(*key))
+            if self._sync is None or self._sync.numel() < nsync or self._sync.device != x.device:
+                self._sync = torch.zeros(nsync, dtype=torch.int32, device=x.device)
             self._part_key = key
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, relu: bool = False):
@@ -110,4 +118,4 @@ class BatchNormAct2d(nn.BatchNorm2d):
             self._ensure_part(x)
         return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var,
                       self.num_batches_tracked if training else None, self._part, training, self.momentum,
-                      self.eps, residual, relu)
+                      self.eps, residual, relu, self._sync if (x.is_cuda and self.fused_small) else None)

@@ -14,7 +14,7 @@ os.environ.setdefault("PYTORCH_ROCM_ARCH", "gfx950")
 
 CSRC = os.path.join("network_distributed_pytorch_amd", "csrc")
 SOURCES = [os.path.join(CSRC, f) for f in ("bindings.cpp", "plan.cpp", "powersgd.hip", "orth.hip", "multitensor.hip", "batchnorm.hip", "attention.hip",
-                                                "conv.hip")]
+                                                "conv.hip", "pool.hip")]
 
 ext = CUDAExtension(
     name="network_distributed_pytorch_amd._C",

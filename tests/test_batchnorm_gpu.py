@@ -12,7 +12,7 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("shape", [(512, 64, 8, 8), (64, 128, 4, 4), (32, 512, 1, 1), (16, 24, 7, 7),
                                    (8, 64, 16, 16), (3, 5, 2, 3), (512, 256, 2, 2), (40, 96, 2, 1),
-                                   (7, 40, 2, 4)])
+                                   (7, 40, 2, 4), (8192, 64, 1, 1), (33, 300, 1, 1), (17, 70, 2, 2)])
 @pytest.mark.parametrize("res,relu", [(False, False), (False, True), (True, True)])
 def test_bn_act_train_fwd_bwd(device, shape, res, relu):
     assert ops.native_available()
@@ -80,3 +80,34 @@ def test_resnet18_fused_matches_unfused(device):
     for (n, a), b in zip(fused.named_parameters(), plain.parameters()):
         scale = b.grad.abs().max().item() + 1e-8
         assert torch.allclose(a.grad, b.grad, atol=2e-3 * scale, rtol=1e-2), n
+
+
+@pytest.mark.parametrize("shape", [(512, 512, 1, 1), (512, 256, 2, 2), (40, 96, 2, 1)])
+def test_bn_single_launch_small_path(device, shape):
+    """Single-launch small-map BN (grid barrier): equals the 3-kernel path bitwise, is
+    deterministic, and leaves its barrier words at rest (counters 0, error flag 0)."""
+    torch.manual_seed(2)
+    C = shape[1]
+    a = BatchNormAct2d(C).to(device)
+    b = BatchNormAct2d(C).to(device)
+    b.fused_small = False
+    b.load_state_dict(a.state_dict())
+    x = torch.randn(shape, device=device) * 1.5 + 0.2
+    r = torch.randn(shape, device=device)
+    g = torch.randn(shape, device=device)
+    outs = []
+    for m in (a, b, a):
+        xx = x.clone().requires_grad_(True)
+        rr = r.clone().requires_grad_(True)
+        y = m(xx, residual=rr, relu=True)
+        y.backward(g)
+        outs.append((y.detach(), xx.grad, rr.grad, m.weight.grad.clone(), m.bias.grad.clone()))
+        m.weight.grad = None
+        m.bias.grad = None
+    for t0, t1, t2 in zip(*outs):
+        assert torch.equal(t0, t2)              # deterministic
+        torch.testing.assert_close(t0, t1, rtol=1e-5, atol=1e-5)
+    torch.cuda.synchronize()
+    words = a._sync.cpu()
+    assert int(words[-1]) == 0, "barrier spin timed out"
+    assert all(int(v) == 0 for v in words[0:-1:2]), words
