@@ -91,7 +91,9 @@ def main():
     dev_index = local % max(1, torch.cuda.device_count())
     device = torch.device("cuda", dev_index)
     torch.cuda.set_device(device)
-    if world > 1:
+    # NDP_FORCE_COLLECTIVES=1: 1-rank process group whose collectives are still issued (a
+    # one-GPU rehearsal of the N > 1 RCCL path, parallel/comm.py Communicator.active)
+    if world > 1 or os.environ.get("NDP_FORCE_COLLECTIVES") == "1":
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=device)
         else:
@@ -243,7 +245,7 @@ def main():
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -12,11 +12,16 @@ MI355X additions:
     (``alpha + wire_bits / bandwidth``) by stalling the HIP stream with a wall-clock
     spin kernel (no root / ``tc`` on the GPU box) — the reference's README.md:2
     bandwidth experiments;
-  * collectives run on RCCL (``backend="nccl"`` is RCCL on ROCm) over xGMI; gloo for CPU.
+  * collectives run on RCCL (``backend="nccl"`` is RCCL on ROCm) over xGMI; gloo for CPU;
+  * ``NDP_FORCE_COLLECTIVES=1`` issues the collectives even in a 1-rank process group
+    (:attr:`Communicator.active`): a one-GPU rehearsal of the N > 1 RCCL path (async work
+    handles, bucket overlap hooks, eager collectives between graph segments) whose sums
+    are the identity, so results match the world-size-1 no-op path.
 """
 from __future__ import annotations
 
 import dataclasses
+import os
 import time
 from typing import List, Optional
 
@@ -145,6 +150,13 @@ class Communicator:
     def rank(self) -> int:
         return get_rank(self.group)
 
+    @property
+    def active(self) -> bool:
+        """Whether collectives are issued (world > 1, or forced for a 1-rank rehearsal)."""
+        if self.world_size > 1:
+            return True
+        return os.environ.get("NDP_FORCE_COLLECTIVES") == "1" and dist.is_available() and dist.is_initialized()
+
     def _pace(self, seconds: float, device_tensor: bool):
         if seconds <= 0:
             return
@@ -167,7 +179,7 @@ class Communicator:
 
     def all_reduce(self, t: torch.Tensor, async_op: bool = False, op=None):
         secs = self._account(t)
-        if self.world_size <= 1:
+        if not self.active:
             return _PacedWork(None, self, 0.0, t.is_cuda) if async_op else None
         kw = {"group": self.group}
         if op is not None:
@@ -181,17 +193,17 @@ class Communicator:
 
     def all_gather(self, out_list: List[torch.Tensor], t: torch.Tensor, async_op: bool = False):
         self._account(t)
-        if self.world_size <= 1:
+        if not self.active:
             assert len(out_list) == 1
             out_list[0].copy_(t)
             return None
         return dist.all_gather(out_list, t, group=self.group, async_op=async_op)
 
     def broadcast(self, t: torch.Tensor, src: int = 0):
-        if self.world_size <= 1:
+        if not self.active:
             return None
         return dist.broadcast(t, src=src, group=self.group)
 
     def barrier(self):
-        if self.world_size > 1:
+        if self.active:
             dist.barrier(group=self.group)

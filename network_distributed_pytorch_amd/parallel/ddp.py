@@ -90,7 +90,7 @@ class BucketedDataParallel:
         self._ready = [0] * len(self.buckets)
         self._works = [None] * len(self.buckets)
         self._launched = [False] * len(self.buckets)
-        self.overlap = overlap and self.comm.world_size > 1
+        self.overlap = overlap and self.comm.active
         self._hooks = []
         if self.overlap:
             for p in self.params:
@@ -103,7 +103,7 @@ class BucketedDataParallel:
 
     @property
     def collectives_per_step(self) -> int:
-        return len(self.buckets) if self.comm.world_size > 1 else 0
+        return len(self.buckets) if self.comm.active else 0
 
     def _flatten(self, b: int):
         _, _, ps = self.buckets[b]
@@ -119,7 +119,7 @@ class BucketedDataParallel:
 
     def _allreduce(self, b: int):
         s, e, _ = self.buckets[b]
-        if self.comm.world_size > 1:
+        if self.comm.active:
             self._works[b] = self.comm.all_reduce(self.g[s:e], async_op=True)
 
     def _launch(self, b: int):

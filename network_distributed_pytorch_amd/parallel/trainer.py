@@ -31,7 +31,7 @@ class PowerSGDSync:
                                      random_seed=seed, comm=comm, **kw)
         b = powersgd_bytes_per_step(list(model.parameters()), rank)
         self.bytes_per_step = b["total"]
-        self.collectives_per_step = 2 if comm.world_size > 1 else 0
+        self.collectives_per_step = 2 if comm.active else 0
 
     def zero_grad(self):
         self.opt.zero_grad()
@@ -67,7 +67,7 @@ class ReferencePowerSGDLoop:
         self.first = True
         self.bits = 0
         self.bytes_per_step = powersgd_bytes_per_step(self.params, rank)["total"]
-        self.collectives_per_step = 3 if comm.world_size > 1 else 0
+        self.collectives_per_step = 3 if comm.active else 0
 
     def zero_grad(self):
         for p in self.params:
@@ -100,7 +100,7 @@ class ReferenceDenseLoop:
         self.comm = comm
         self.opt = torch.optim.SGD(model.parameters(), lr=lr, momentum=momentum)
         self.bytes_per_step = 4 * sum(p.numel() for p in model.parameters())
-        self.collectives_per_step = len(list(model.parameters())) if comm.world_size > 1 else 0
+        self.collectives_per_step = len(list(model.parameters())) if comm.active else 0
 
     def zero_grad(self):
         self.opt.zero_grad()

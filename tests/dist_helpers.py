@@ -44,10 +44,15 @@ def reducer_rank_body(rank, world, out_dir, R):
 
 def train_rank_body(rank, world, out_dir, kind, steps, native):
     """Train a small CNN with a grad-sync strategy; dump final params + checksums."""
+    _init(rank, world)
+    _train(rank, world, out_dir, kind, steps, native)
+    dist.destroy_process_group()
+
+
+def _train(rank, world, out_dir, kind, steps, native, comm=None, tag=None):
     from network_distributed_pytorch_amd.parallel.comm import Communicator
     from network_distributed_pytorch_amd.parallel.trainer import build_grad_sync
 
-    _init(rank, world)
     dev = _dev()
     torch.manual_seed(1000 + rank)  # different init per rank: the sync must broadcast
     model = torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3), torch.nn.BatchNorm2d(8), torch.nn.ReLU(),
@@ -56,7 +61,7 @@ def train_rank_body(rank, world, out_dir, kind, steps, native):
         for p in model.parameters():  # reference has no broadcast: seed identically instead
             dist.broadcast(p.data, 0)
     kw = {"native": native} if kind == "powersgd" else {}
-    sync = build_grad_sync(kind, model, Communicator(), lr=0.05, momentum=0.9, rank=2, **kw)
+    sync = build_grad_sync(kind, model, comm or Communicator(), lr=0.05, momentum=0.9, rank=2, **kw)
     g = torch.Generator().manual_seed(7 + rank)
     losses = []
     for _ in range(steps):
@@ -68,8 +73,7 @@ def train_rank_body(rank, world, out_dir, kind, steps, native):
         sync.step()
         losses.append(float(loss))
     params = [p.detach().cpu().clone() for p in model.parameters()]
-    torch.save({"params": params, "losses": losses}, os.path.join(out_dir, f"{kind}_rank{rank}.pt"))
-    dist.destroy_process_group()
+    torch.save({"params": params, "losses": losses}, os.path.join(out_dir, f"{tag or kind}_rank{rank}.pt"))
 
 
 def checker_rank_body(rank, world, out_dir):
@@ -95,4 +99,28 @@ def checker_rank_body(rank, world, out_dir):
             caught = step
             break
     torch.save({"caught": caught, "fired": comm.fired}, os.path.join(out_dir, f"chk{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def forced_rank_body(rank, world, out_dir, kind, force):
+    """1-rank group: collectives issued (NDP_FORCE_COLLECTIVES=1) vs skipped."""
+    os.environ["NDP_FORCE_COLLECTIVES"] = "1" if force else "0"
+    from network_distributed_pytorch_amd.parallel.comm import Communicator
+
+    _init(rank, world)
+    comm = Communicator()
+    calls = []
+    orig = dist.all_reduce
+
+    def counting(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+
+    dist.all_reduce = counting
+    try:
+        _train(rank, world, out_dir, kind, 3, False, comm=comm, tag=f"{kind}_f{int(force)}")
+    finally:
+        dist.all_reduce = orig
+    torch.save({"calls": len(calls), "active": comm.active},
+               os.path.join(out_dir, f"{kind}_f{int(force)}_meta.pt"))
     dist.destroy_process_group()

@@ -87,3 +87,18 @@ def test_replica_checker_catches_corruption(tmp_path):
     r1 = torch.load(os.path.join(tmp_path, "chk1.pt"), weights_only=True)
     assert r1["fired"]
     assert r0["caught"] is not None and r0["caught"] == r1["caught"]
+
+
+@pytest.mark.parametrize("kind", ["powersgd", "dense"])
+def test_forced_collectives_rehearsal_is_identity(tmp_path, kind):
+    """NDP_FORCE_COLLECTIVES=1 (the one-GPU rehearsal of the N>1 path) issues the
+    collectives in a 1-rank group; results equal the skipped-collective run."""
+    for force in (False, True):
+        spawn(H.forced_rank_body, 1, args=(str(tmp_path), kind, force))
+    meta = {f: torch.load(os.path.join(tmp_path, f"{kind}_f{f}_meta.pt"), weights_only=True) for f in (0, 1)}
+    assert not meta[0]["active"] and meta[0]["calls"] == 0
+    assert meta[1]["active"] and meta[1]["calls"] > 0
+    a = torch.load(os.path.join(tmp_path, f"{kind}_f0_rank0.pt"), weights_only=True)
+    b = torch.load(os.path.join(tmp_path, f"{kind}_f1_rank0.pt"), weights_only=True)
+    for x, y in zip(a["params"], b["params"]):
+        assert torch.equal(x, y)
