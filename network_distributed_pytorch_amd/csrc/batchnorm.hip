@@ -419,31 +419,34 @@ __global__ __launch_bounds__(256) void bn_small_apply_kernel(
 // ---- single-launch small-map BN (column block x every image, register resident) ---------
 // The three small-map kernels above are each only a few µs of work on 1-2 MB tensors, so
 // a ResNet-18 step spends most of their ~300 µs in launch gaps.  This kernel does a whole
-// BN direction in ONE launch with no cross-workgroup traffic: a workgroup owns kColW
-// consecutive columns of the [N][C*HW] view (whole channels, since HW | kColW) for EVERY
-// image.  Its 512 threads are kColW columns x kRowG row groups; thread (g, col) keeps rows
-// g, g + kRowG, ... (<= kFusedRows of them) in registers, so the tensor is read once and
-// written once.  Per-channel sums: fp64 per thread -> xor shuffle over the HW lanes of a
-// channel -> fixed-order fold of the kRowG row-group partials through LDS (every thread
-// gets the bitwise-identical value; deterministic).  Each wave-wide load covers 4 rows x
-// kColW consecutive floats.  Used when N <= kRowG * kFusedRows (ResNet's per-GPU 512).
-constexpr int kColW = 16;
-constexpr int kRowG = 32;
-constexpr int kFusedRows = 16;
-constexpr int kFusedThreads = kColW * kRowG;
+// BN direction in ONE launch with no cross-workgroup traffic: a workgroup owns CW
+// consecutive columns of the [N][C*HW] view (whole channels, since HW | CW) for EVERY
+// image.  Its 512 threads are CW columns x RG = 512 / CW row groups; thread (g, col) keeps
+// rows g, g + RG, ... (<= 512 / RG of them) in registers, so the tensor is read once and
+// written once.  Per-channel sums (deterministic, every thread ends with the bitwise-same
+// value): fp64 per thread -> xor butterfly over the HW lanes of a channel and the row
+// groups inside the wave (commutative pairings: identical on every lane) -> fixed-order
+// fold of the 8 per-wave partials through LDS.  CW trades grid size (C*HW / CW workgroups;
+// 256 CUs to fill) against row-segment width per load (CW * 4 bytes): NDP_BN_COLW picks
+// it (tuning only), default by measurement.  Used when N <= 512 (ResNet's per-GPU batch).
+constexpr int kFusedThreads = 512;
+constexpr int kFusedMaxN = 512;
 
-template <int HW, int BWD>
+template <int HW, int BWD, int CW>
 __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
     const float* __restrict__ x, const float* __restrict__ res, const float* __restrict__ dy,
     const float* __restrict__ yin, const float* __restrict__ gamma, const float* __restrict__ beta,
     float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt, float* __restrict__ save_mean,
     float* __restrict__ save_invstd, float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ out,
     float* __restrict__ dres, int N, int C, float eps, float momentum, int relu) {
-  constexpr int NP = kFusedRows;
-  __shared__ double red[2][kRowG][kColW];
+  constexpr int RG = kFusedThreads / CW;
+  constexpr int NP = kFusedMaxN / RG;
+  constexpr int NW = kFusedThreads / 64;
+  static_assert(CW % HW == 0 && 64 % CW == 0, "bad column block");
+  __shared__ double red[2][NW][CW];
   const int CHW = C * HW;
-  const int col = threadIdx.x % kColW, g = threadIdx.x / kColW;
-  const int j = blockIdx.x * kColW + col;
+  const int col = threadIdx.x % CW, g = threadIdx.x / CW;
+  const int j = blockIdx.x * CW + col;
   const bool ok_col = j < CHW;
   const int c = ok_col ? j / HW : 0;
   float v[NP], d[NP], m[NP];
@@ -454,7 +457,7 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
   }
 #pragma unroll
   for (int k = 0; k < NP; ++k) {  // every load in flight before any use
-    const int n = g + k * kRowG;
+    const int n = g + k * RG;
     const bool ok = ok_col && n < N;
     const int64_t o = (int64_t)n * CHW + j;
     v[k] = ok ? x[o] : 0.f;
@@ -468,7 +471,7 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
   double a = 0.0, b = 0.0;
 #pragma unroll
   for (int k = 0; k < NP; ++k) {
-    if (g + k * kRowG < N) {
+    if (ok_col && g + k * RG < N) {
       if (!BWD) {
         a += (double)v[k];
         b += (double)v[k] * (double)v[k];
@@ -484,12 +487,20 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
     a += __shfl_xor(a, o, 64);
     b += __shfl_xor(b, o, 64);
   }
-  red[0][g][col] = a;
-  red[1][g][col] = b;
+#pragma unroll
+  for (int o = CW; o < 64; o <<= 1) {  // row groups inside the wave
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+  }
+  const int wave = threadIdx.x / 64;
+  if ((threadIdx.x % 64) < CW) {
+    red[0][wave][col] = a;
+    red[1][wave][col] = b;
+  }
   __syncthreads();
   double A = 0.0, B = 0.0;
 #pragma unroll
-  for (int k = 0; k < kRowG; ++k) {
+  for (int k = 0; k < NW; ++k) {
     A += red[0][k][col];
     B += red[1][k][col];
   }
@@ -515,7 +526,7 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
     }
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
-      const int n = g + k * kRowG;
+      const int n = g + k * RG;
       if (n < N) {
         const float z = fmaf(v[k], scale, shift) + d[k];
         out[(int64_t)n * CHW + j] = relu ? fmaxf(z, 0.f) : z;
@@ -530,7 +541,7 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
     const float mdz = (float)(A / M), mdzx = (float)(B / M);
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
-      const int n = g + k * kRowG;
+      const int n = g + k * RG;
       if (n < N) {
         const float dz = (m[k] > 0.f) ? d[k] : 0.f;
         const float xh = (v[k] - mean_s) * invstd_s;
@@ -543,7 +554,35 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
 }
 
 static bool bn_fused_ok(int N, int C, int HW) {
-  return (HW == 1 || HW == 2 || HW == 4) && N >= 1 && N <= kRowG * kFusedRows && (int64_t)N * C * HW < (1LL << 30);
+  return (HW == 1 || HW == 2 || HW == 4) && N >= 1 && N <= kFusedMaxN && (int64_t)N * C * HW < (1LL << 30);
+}
+
+// column-block width of the single-launch path (NDP_BN_COLW: 4 / 8 / 16, tuning only)
+static int bn_colw() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("NDP_BN_COLW");
+    v = e ? atoi(e) : 8;  // ResNet-18 step: 4 -> 2.221 ms, 8 -> 2.182 ms, 16 -> 2.202 ms (1x MI355X)
+    if (v != 4 && v != 8 && v != 16) v = 8;
+  }
+  return v;
+}
+
+template <int BWD, int CW>
+static void launch_small_fused_cw(int HW, const float* x, const float* res, const float* dy, const float* yin,
+                                  const float* gamma, const float* beta, float* rmean, float* rvar, int64_t* nbt,
+                                  float* sm, float* si, float* dgamma, float* dbeta, float* out, float* dres, int N,
+                                  int C, float eps, float momentum, int relu, hipStream_t s) {
+  const dim3 grid((unsigned)(((int64_t)C * HW + CW - 1) / CW));
+#define NDP_BN_FUSED(HWV)                                                                                          \
+  hipLaunchKernelGGL((bn_small_fused_kernel<HWV, BWD, CW>), grid, dim3(kFusedThreads), 0, s, x, res, dy, yin, gamma, \
+                     beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out, dres, N, C, eps, momentum, relu)
+  switch (HW) {
+    case 1: NDP_BN_FUSED(1); break;
+    case 2: NDP_BN_FUSED(2); break;
+    default: NDP_BN_FUSED(4); break;
+  }
+#undef NDP_BN_FUSED
 }
 
 template <int BWD>
@@ -551,16 +590,19 @@ static void launch_small_fused(int HW, const float* x, const float* res, const f
                                const float* gamma, const float* beta, float* rmean, float* rvar, int64_t* nbt,
                                float* sm, float* si, float* dgamma, float* dbeta, float* out, float* dres, int N,
                                int C, float eps, float momentum, int relu, hipStream_t s) {
-  const dim3 grid((unsigned)(((int64_t)C * HW + kColW - 1) / kColW));
-#define NDP_BN_FUSED(HWV)                                                                                           \
-  hipLaunchKernelGGL((bn_small_fused_kernel<HWV, BWD>), grid, dim3(kFusedThreads), 0, s, x, res, dy, yin, gamma, beta, \
-                     rmean, rvar, nbt, sm, si, dgamma, dbeta, out, dres, N, C, eps, momentum, relu)
-  switch (HW) {
-    case 1: NDP_BN_FUSED(1); break;
-    case 2: NDP_BN_FUSED(2); break;
-    default: NDP_BN_FUSED(4); break;
+  switch (bn_colw()) {
+    case 16:
+      launch_small_fused_cw<BWD, 16>(HW, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out,
+                                     dres, N, C, eps, momentum, relu, s);
+      break;
+    default:
+      launch_small_fused_cw<BWD, 8>(HW, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out,
+                                    dres, N, C, eps, momentum, relu, s);
+      break;
+    case 4:
+      launch_small_fused_cw<BWD, 4>(HW, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out,
+                                    dres, N, C, eps, momentum, relu, s);
   }
-#undef NDP_BN_FUSED
 }
 
 template <int HW>

@@ -11,6 +11,8 @@ normalisation, unbiased in ``running_var``, momentum 0.1).
 """
 from __future__ import annotations
 
+import os
+
 from typing import Optional
 
 import torch
@@ -24,7 +26,7 @@ __all__ = ["BatchNormAct2d", "bn_act"]
 
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, res, weight, bias, running_mean, running_var, nbt, part, eps, momentum, relu, sync=None):
+    def forward(ctx, x, res, weight, bias, running_mean, running_var, nbt, part, eps, momentum, relu, single=False):
         X = ext()
         x = x.contiguous()
         if res is not None:
@@ -34,9 +36,9 @@ class _BNActFn(torch.autograd.Function):
         save_mean = torch.empty(C, device=x.device, dtype=torch.float32)
         save_invstd = torch.empty(C, device=x.device, dtype=torch.float32)
         X.bn_fwd(x, res, y, weight, bias, running_mean, running_var, nbt, save_mean, save_invstd, part,
-                 float(eps), float(momentum), bool(relu), True, sync)
+                 float(eps), float(momentum), bool(relu), True, bool(single))
         ctx.relu = bool(relu)
-        ctx.sync = sync
+        ctx.single = bool(single)
         ctx.has_res = res is not None
         ctx.has_w = weight is not None
         ctx.save_for_backward(x, y if relu else None, weight, save_mean, save_invstd, part)
@@ -51,12 +53,12 @@ class _BNActFn(torch.autograd.Function):
         dres = torch.empty_like(x) if ctx.has_res else None
         dgamma = torch.empty_like(weight) if ctx.has_w else None
         dbeta = torch.empty_like(weight) if ctx.has_w else None
-        ext().bn_bwd(dy, y, x, weight, save_mean, save_invstd, dx, dres, dgamma, dbeta, part, ctx.relu, ctx.sync)
+        ext().bn_bwd(dy, y, x, weight, save_mean, save_invstd, dx, dres, dgamma, dbeta, part, ctx.relu, ctx.single)
         return dx, dres, dgamma, dbeta, None, None, None, None, None, None, None, None
 
 
 def bn_act(x, weight, bias, running_mean, running_var, nbt, part, training, momentum, eps,
-           residual=None, relu=False, sync=None):
+           residual=None, relu=False, single=False):
     needs_grad = torch.is_grad_enabled() and (x.requires_grad or (weight is not None and weight.requires_grad)
                                               or (residual is not None and residual.requires_grad))
     if x.is_cuda and (training or not needs_grad):  # eval + autograd: differentiable torch path below
@@ -65,13 +67,13 @@ def bn_act(x, weight, bias, running_mean, running_var, nbt, part, training, mome
             residual = residual.float() if residual is not None else None
         if training:
             return _BNActFn.apply(x, residual, weight, bias, running_mean, running_var, nbt, part, eps,
-                                  momentum, relu, sync)
+                                  momentum, relu, single)
         y = torch.empty_like(x := x.contiguous())
         C = x.shape[1]
         sm = torch.empty(C, device=x.device)
         si = torch.empty(C, device=x.device)
         ext().bn_fwd(x, residual.contiguous() if residual is not None else None, y, weight, bias, running_mean,
-                     running_var, None, sm, si, part, float(eps), 0.0, bool(relu), False, None)
+                     running_var, None, sm, si, part, float(eps), 0.0, bool(relu), False, False)
         return y
     y = F.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps)
     if training and nbt is not None:
@@ -89,8 +91,8 @@ class BatchNormAct2d(nn.BatchNorm2d):
         # per-(channel, slice) fp64 partials: C * S * 2 with S <= ceil(1024 / C) (bn_slices)
         self.register_buffer("_part", torch.zeros((num_features + 1024) * 2, dtype=torch.float64),
                              persistent=False)
-        self._sync: Optional[torch.Tensor] = None
-        self.fused_small = True  # single-launch small-map kernels (HW <= 4)
+        # single-launch small-map kernels (HW <= 4, N <= 512); NDP_BN_SINGLE=0: 3-kernel path (A/B)
+        self.fused_small = os.environ.get("NDP_BN_SINGLE", "1") != "0"
 
     def _ensure_part(self, x: torch.Tensor) -> None:
         """Grow the fp64 partial-sum scratch to what this input shape needs (first call for
@@ -100,11 +102,6 @@ class BatchNormAct2d(nn.BatchNorm2d):
             need = int(ext().bn_part_numel(*key))
             if self._part.numel() < need or self._part.device != x.device:
                 self._part = torch.zeros(need, dtype=torch.float64, device=x.device)
-            # barrier words of the single-launch small-map path: zeroed once, they return to
-            # zero after every launch (csrc/batchnorm.hip, bn_small_fused_kernel)
-            nsync = int(ext().bn_sync_numel(*key))
-            if self._sync is None or self._sync.numel() < nsync or self._sync.device != x.device:
-                self._sync = torch.zeros(nsync, dtype=torch.int32, device=x.device)
             self._part_key = key
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, relu: bool = False):
@@ -118,4 +115,4 @@ class BatchNormAct2d(nn.BatchNorm2d):
             self._ensure_part(x)
         return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var,
                       self.num_batches_tracked if training else None, self._part, training, self.momentum,
-                      self.eps, residual, relu, self._sync if (x.is_cuda and self.fused_small) else None)
+                      self.eps, residual, relu, x.is_cuda and self.fused_small)

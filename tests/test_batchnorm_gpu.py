@@ -82,10 +82,10 @@ def test_resnet18_fused_matches_unfused(device):
         assert torch.allclose(a.grad, b.grad, atol=2e-3 * scale, rtol=1e-2), n
 
 
-@pytest.mark.parametrize("shape", [(512, 512, 1, 1), (512, 256, 2, 2), (40, 96, 2, 1)])
+@pytest.mark.parametrize("shape", [(512, 512, 1, 1), (512, 256, 2, 2), (40, 96, 2, 1), (3, 20, 1, 1)])
 def test_bn_single_launch_small_path(device, shape):
-    """Single-launch small-map BN (grid barrier): equals the 3-kernel path bitwise, is
-    deterministic, and leaves its barrier words at rest (counters 0, error flag 0)."""
+    """Single-launch register-resident small-map BN: matches the 3-kernel path and is
+    deterministic (run twice, bitwise equal)."""
     torch.manual_seed(2)
     C = shape[1]
     a = BatchNormAct2d(C).to(device)
@@ -107,7 +107,3 @@ def test_bn_single_launch_small_path(device, shape):
     for t0, t1, t2 in zip(*outs):
         assert torch.equal(t0, t2)              # deterministic
         torch.testing.assert_close(t0, t1, rtol=1e-5, atol=1e-5)
-    torch.cuda.synchronize()
-    words = a._sync.cpu()
-    assert int(words[-1]) == 0, "barrier spin timed out"
-    assert all(int(v) == 0 for v in words[0:-1:2]), words
