@@ -553,8 +553,19 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
   }
 }
 
+// largest HW routed to the single-launch path (NDP_BN_SINGLE_MAX: 4 / 8 / 16, tuning only)
+static int bn_single_max() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("NDP_BN_SINGLE_MAX");
+    v = e ? atoi(e) : 16;  // ResNet-18 step: 4 -> 2.165 ms, 16 (layer2 too) -> 2.150 ms (1x MI355X)
+  }
+  return v;
+}
+
 static bool bn_fused_ok(int N, int C, int HW) {
-  return (HW == 1 || HW == 2 || HW == 4) && N >= 1 && N <= kFusedMaxN && (int64_t)N * C * HW < (1LL << 30);
+  return (HW == 1 || HW == 2 || HW == 4 || HW == 8 || HW == 16) && HW <= bn_single_max() && N >= 1 &&
+         N <= kFusedMaxN && (int64_t)N * C * HW < (1LL << 30);
 }
 
 // column-block width of the single-launch path (NDP_BN_COLW: 4 / 8 / 16, tuning only)
@@ -574,13 +585,16 @@ static void launch_small_fused_cw(int HW, const float* x, const float* res, cons
                                   float* sm, float* si, float* dgamma, float* dbeta, float* out, float* dres, int N,
                                   int C, float eps, float momentum, int relu, hipStream_t s) {
   const dim3 grid((unsigned)(((int64_t)C * HW + CW - 1) / CW));
-#define NDP_BN_FUSED(HWV)                                                                                          \
-  hipLaunchKernelGGL((bn_small_fused_kernel<HWV, BWD, CW>), grid, dim3(kFusedThreads), 0, s, x, res, dy, yin, gamma, \
-                     beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out, dres, N, C, eps, momentum, relu)
-  switch (HW) {
+#define NDP_BN_FUSED(HWV)                                                                                            \
+  if constexpr (CW % HWV == 0)                                                                                       \
+    hipLaunchKernelGGL((bn_small_fused_kernel<HWV, BWD, CW>), grid, dim3(kFusedThreads), 0, s, x, res, dy, yin, gamma, \
+                       beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out, dres, N, C, eps, momentum, relu)
+  switch (HW) {  // the caller picks CW >= HW
     case 1: NDP_BN_FUSED(1); break;
     case 2: NDP_BN_FUSED(2); break;
-    default: NDP_BN_FUSED(4); break;
+    case 4: NDP_BN_FUSED(4); break;
+    case 8: NDP_BN_FUSED(8); break;
+    default: NDP_BN_FUSED(16); break;
   }
 #undef NDP_BN_FUSED
 }
@@ -590,7 +604,7 @@ static void launch_small_fused(int HW, const float* x, const float* res, const f
                                const float* gamma, const float* beta, float* rmean, float* rvar, int64_t* nbt,
                                float* sm, float* si, float* dgamma, float* dbeta, float* out, float* dres, int N,
                                int C, float eps, float momentum, int relu, hipStream_t s) {
-  switch (bn_colw()) {
+  switch (bn_colw() > HW ? bn_colw() : HW) {
     case 16:
       launch_small_fused_cw<BWD, 16>(HW, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out,
                                      dres, N, C, eps, momentum, relu, s);

@@ -82,7 +82,8 @@ def test_resnet18_fused_matches_unfused(device):
         assert torch.allclose(a.grad, b.grad, atol=2e-3 * scale, rtol=1e-2), n
 
 
-@pytest.mark.parametrize("shape", [(512, 512, 1, 1), (512, 256, 2, 2), (40, 96, 2, 1), (3, 20, 1, 1)])
+@pytest.mark.parametrize("shape", [(512, 512, 1, 1), (512, 256, 2, 2), (40, 96, 2, 1), (3, 20, 1, 1),
+                                   (512, 128, 4, 4), (100, 64, 4, 2)])
 def test_bn_single_launch_small_path(device, shape):
     """Single-launch register-resident small-map BN: matches the 3-kernel path and is
     deterministic (run twice, bitwise equal)."""
