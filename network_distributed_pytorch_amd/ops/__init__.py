@@ -6,6 +6,8 @@ The PowerSGD grouped kernels are driven from
 """
 from __future__ import annotations
 
+import contextlib
+
 from typing import Sequence
 
 import torch
@@ -99,6 +101,9 @@ def upload(dev: torch.Tensor, host: torch.Tensor) -> None:
     assert dev.numel() >= n and dev.dtype == host.dtype
     if n == 0:
         return
+    if dev.is_cuda and capturing() and _UPLOADS.defer:
+        _UPLOADS.record(dev[:n], host.reshape(-1).clone())
+        return
     if dev.is_cuda and capturing():
         nbytes = n * host.element_size()
         pinned = _PINNED.take(nbytes).view(host.dtype)
@@ -107,7 +112,58 @@ def upload(dev: torch.Tensor, host: torch.Tensor) -> None:
     else:
         if dev.is_cuda:
             _PINNED.reserve()
+            _UPLOADS.generation += 1
         dev[:n].copy_(host)
+
+
+class _DeferredUploads:
+    """Capture-time table uploads applied ONCE after capture instead of as memcpy nodes.
+
+    A graph captured by :class:`utils.graph.StepRunner` always replays the capture-time
+    tables, so re-uploading them on every replay (one ~5 µs copy node per table, 5 per
+    PowerSGD step) is wasted.  Inside :meth:`capture_scope` uploads are recorded and, when
+    the scope ends, copied synchronously.  ``generation`` counts eager uploads: if an eager
+    step re-bound a table after capture, :meth:`ensure` restores the capture-time contents
+    before the next replay.
+    """
+
+    def __init__(self):
+        self.defer = False
+        self.generation = 0
+        self._pending = []
+
+    def record(self, dev: torch.Tensor, host: torch.Tensor):
+        for d, h in self._pending:
+            if d.data_ptr() == dev.data_ptr() and not (h.numel() == host.numel() and torch.equal(h, host)):
+                raise RuntimeError("table uploaded twice with different contents inside one capture; "
+                                   "capture without deferred uploads")
+        self._pending.append((dev, host))
+
+    @contextlib.contextmanager
+    def capture_scope(self):
+        """Yields the list that receives the recorded uploads (applied on exit)."""
+        self.defer, self._pending = True, []
+        try:
+            yield self._pending
+        finally:
+            self.defer = False
+        self.apply(self._pending)
+
+    def apply(self, uploads):
+        for d, h in uploads:
+            d.copy_(h)
+        if uploads:
+            torch.cuda.synchronize()
+        self.generation += 1  # the tables now hold the capture-time contents
+
+    def ensure(self, uploads, generation: int) -> int:
+        """Re-apply ``uploads`` if any eager upload happened since ``generation``."""
+        if generation != self.generation:
+            self.apply(uploads)
+        return self.generation
+
+
+_UPLOADS = _DeferredUploads()
 
 
 class SegPlan:

@@ -19,11 +19,17 @@ needs ``reuse_query=True`` (the reference default) because the query re-draw is 
 """
 from __future__ import annotations
 
+import contextlib
+import os
 from typing import Callable, List, Optional, Tuple
 
 import torch
 
+from ..ops import _UPLOADS
 from ..parallel.comm import world_size
+
+# NDP_DEFER_UPLOADS=0: capture-time table uploads stay memcpy nodes re-run on every replay
+_DEFER_UPLOADS = os.environ.get("NDP_DEFER_UPLOADS", "1") != "0"
 
 __all__ = ["StepRunner", "GraphedStep"]
 
@@ -42,6 +48,8 @@ class StepRunner:
         self.warmup = warmup
         self.segments: List[Tuple[Callable[[], None], bool]] = self._segments()
         self.graphs: Optional[list] = None
+        self._uploads: list = []
+        self._upload_gen = 0
         self.replays = 0
 
     def _segments(self):
@@ -83,15 +91,19 @@ class StepRunner:
         torch.cuda.synchronize()
         pool = torch.cuda.graph_pool_handle()
         graphs = []
-        for fn, cap in self.segments:
-            if cap:
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=pool):
-                    fn()
-                graphs.append(g)
-            else:
-                graphs.append(None)
+        scope = _UPLOADS.capture_scope() if _DEFER_UPLOADS else contextlib.nullcontext([])
+        with scope as uploads:  # table uploads: applied once after capture, not per replay
+            for fn, cap in self.segments:
+                if cap:
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, pool=pool):
+                        fn()
+                    graphs.append(g)
+                else:
+                    graphs.append(None)
         torch.cuda.synchronize()
+        self._uploads = uploads
+        self._upload_gen = _UPLOADS.generation
         self.graphs = graphs
         # the first replay below is the first real step after capture
 
@@ -101,6 +113,8 @@ class StepRunner:
             return
         if self.graphs is None:
             self.capture()
+        # an eager step since capture may have re-bound a table the graph reads
+        self._upload_gen = _UPLOADS.ensure(self._uploads, self._upload_gen)
         for (fn, _), g in zip(self.segments, self.graphs):
             if g is None:
                 fn()

@@ -78,8 +78,11 @@ def test_resnet18_native_convs_vs_fp64(device, mode):
         1.0, abs(losses[2]))
     for (n, pa), pb, pr in zip(a.named_parameters(), b.parameters(), ref.parameters()):
         g = pr.grad.flatten()
-        for p in (pa, pb):
+        for which, p in (("native", pa), ("miopen", pb)):
             d = p.grad.cpu().double().flatten()
             cos = torch.dot(d, g) / (d.norm() * g.norm() + 1e-300)
+            rel2 = (d - g).norm() / (g.norm() + 1e-300)
             rel = (d - g).abs().max() / (g.abs().max() + 1e-300)
-            assert cos > 0.999 and rel < 0.1, (n, float(cos), float(rel))
+            # one flipped ReLU in a batch-32 layer4 BN moved a single weight-grad row by
+            # 0.15 of the max (cos 0.9998) on MI355X: bound the L2 error, keep a gross cap
+            assert cos > 0.999 and rel2 < 0.05 and rel < 0.3, (which, n, float(cos), float(rel2), float(rel))

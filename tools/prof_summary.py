@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--marker", default="psgd_update_kernel")
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--sequence", default=None, help="also write the last step's kernel sequence here")
     a = ap.parse_args()
     rows = []
     with open(a.trace, newline="") as f:
@@ -55,6 +56,13 @@ def main():
     print("|---|---:|---:|---:|")
     for n, (t, c) in sorted(agg.items(), key=lambda x: -x[1][0])[: a.top]:
         print(f"| `{n}` | {t / k / 1e3:.1f} | {c / k:.1f} | {100 * t / busy:.1f} |")
+    if a.sequence:  # one step in launch order: µs, gap before it, name (find who launches what)
+        last = rows[marks[-2] + 1: marks[-1] + 1]
+        with open(a.sequence, "w") as f:
+            prev = rows[marks[-2]][1]
+            for s, e, n in last:
+                f.write(f"{(e - s) / 1e3:8.1f} {(s - prev) / 1e3:6.1f}  {short(n)}\n")
+                prev = e
 
 
 if __name__ == "__main__":
