@@ -5,16 +5,22 @@
     torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
         bench.py --gpus N --steps K --warmup W
 
-One process per GPU, RCCL over xGMI (backend "nccl" = RCCL on ROCm).  Each timed step is
-the full reference training step (ddp_powersgd_guide_cifar10/ddp_init.py:142-178):
-forward, cross-entropy, backward, EF pack, PowerSGD compress + 2 all-reduces,
-decompress, error memory, momentum, SGD update — fused by PowerSGDOptimizer into
-6 gfx950 kernels + 2 collectives.  fp32 everywhere (the reference's dtype), random-init
-weights, synthetic device-resident data.  Weak scaling: per-GPU batch fixed (default
-512 = the reference's global batch at N=1, ddp_powersgd_guide_cifar10/ddp_init.py:52).
+One process per GPU, RCCL over xGMI through the framework's native communicator
+(csrc/comm.cpp; c10d only bootstraps).  Each timed step is the full reference training
+step (ddp_powersgd_guide_cifar10/ddp_init.py:142-178): forward, cross-entropy, backward,
+EF pack, PowerSGD compress + all-reduces, decompress, error memory, momentum, SGD update.
+The whole step is ONE hipGraph; the PowerSGD group pipelines (gfx950 kernels + RCCL
+collectives) run on a side stream that overlaps backward.  fp32 everywhere (the
+reference's dtype), random-init weights, synthetic device-resident data.
 
-Rank 0 prints ONE JSON line.  `value` = whole-job samples/s (max step time over ranks).
-`bytes_per_step` = bytes all-reduced per rank per step with the reference's accounting.
+Scaling: **strong** by default for the CIFAR workloads, exactly like the reference — the
+global batch is fixed at 512 (PowerSGD, ddp_powersgd_guide_cifar10/ddp_init.py:52) and
+each of the N ranks trains on 512/N.  DistilBERT is weak in the reference (16 per rank,
+ddp_powersgd_distillBERT_IMDb/ddp_init.py:92).  For N > 1 strong runs the bench also
+times the weak configuration (512 per GPU) and reports it under ``weak_scaling``.
+
+Rank 0 prints ONE JSON line.  ``value`` = whole-job samples/s (max step time over ranks).
+``bytes_per_step`` = bytes all-reduced per rank per step with the reference's accounting.
 """
 from __future__ import annotations
 
@@ -32,15 +38,21 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 METRIC = "samples/sec + bytes/step all-reduced, ResNet18 CIFAR10 PowerSGD r=4, 1/2/4/8 GPU"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--model", default="resnet18", help="resnet18/34/50/101/152 | distilbert")
     ap.add_argument("--num-classes", type=int, default=None, help="default: 1000 (ResNet, reference head) / 2")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default=None,
+                    help="strong: global batch fixed, per-GPU = global/N (CIFAR default, the reference); "
+                         "weak: per-GPU batch fixed (DistilBERT default, the reference)")
+    ap.add_argument("--global-batch", type=int, default=512, help="strong scaling: global batch (reference 512)")
     ap.add_argument("--batch", type=int, default=None,
-                    help="per-GPU batch (weak scaling); default 512 ResNet, 16 DistilBERT (reference)")
+                    help="per-GPU batch; implies weak scaling. Default 512 ResNet, 16 DistilBERT (reference)")
+    ap.add_argument("--weak-too", choices=["auto", "on", "off"], default="auto",
+                    help="N>1 strong runs: also time the weak config (per-GPU 512) as an extra field")
     ap.add_argument("--seq-len", type=int, default=512)
     ap.add_argument("--reducer", choices=["powersgd", "dense", "dense-ref", "powersgd-ref", "powersgd-api"],
                     default="powersgd")
@@ -50,17 +62,28 @@ def parse():
     ap.add_argument("--no-fused-bn", action="store_true", help="use nn.BatchNorm2d + ReLU (MIOpen) instead")
     ap.add_argument("--no-gemm-convs", action="store_true", help="run every conv on MIOpen")
     ap.add_argument("--no-fused-attn", action="store_true", help="DistilBERT: explicit attention math")
+    ap.add_argument("--stock", action="store_true",
+                    help="stock PyTorch-ROCm model ops (MIOpen conv/BN, explicit attention): with "
+                         "--reducer powersgd-ref this is the eager reference-semantics arm")
     ap.add_argument("--amp", choices=["none", "bf16"], default="none",
                     help="opt-in bf16 autocast for model math (NOT the headline: the reference is fp32)")
     ap.add_argument("--link", default="none", help="none|1g|10g|100g link emulation")
-    ap.add_argument("--bucket-mb", type=float, default=25.0)
+    ap.add_argument("--emulate-world", type=int, default=None,
+                    help="charge the link model for an N-rank ring even on 1 GPU (bandwidth curves)")
+    ap.add_argument("--bucket-mb", type=float, default=None, help="dense arm bucket size (default 8 MB)")
+    ap.add_argument("--psgd-groups", type=int, default=None, help="PowerSGD overlap groups (default 4)")
+    ap.add_argument("--no-overlap", action="store_true", help="serial sync after backward (A/B)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--graph-mode", default="auto", choices=["auto", "full", "piecewise", "none"],
-                    help="hipGraph capture of the step: full (N=1 default), piecewise (collectives "
-                         "eager between captured compute; N>1 default), none")
-    a = ap.parse_args()
+                    help="hipGraph capture of the step: full (native RCCL / N=1), piecewise (collectives "
+                         "eager between captured compute; c10d data plane), none")
+    a = ap.parse_args(argv)
     bert = a.model.startswith("distilbert")
-    if a.batch is None:
+    if a.stock:
+        a.no_fused_bn = a.no_gemm_convs = a.no_fused_attn = True
+    if a.scaling is None:
+        a.scaling = "weak" if (bert or a.batch is not None) else "strong"
+    if a.batch is None and a.scaling == "weak":
         a.batch = 16 if bert else 512
     if a.lr is None:
         a.lr = 5e-5 if bert else 1e-3
@@ -77,12 +100,129 @@ def metric_name(args) -> str:
     return f"samples/sec + bytes/step all-reduced, {what} {red}"
 
 
-def main():
-    args = parse()
-    from network_distributed_pytorch_amd.models import build_model
-    from network_distributed_pytorch_amd.parallel.comm import LINK_PRESETS, Communicator
-    from network_distributed_pytorch_amd.parallel.trainer import build_grad_sync
+class Workload:
+    """Model + gradient sync + a timed-step factory for one per-GPU batch size."""
 
+    def __init__(self, args, device, world, rank):
+        from network_distributed_pytorch_amd.models import build_model
+        from network_distributed_pytorch_amd.parallel.comm import LINK_PRESETS, Communicator
+        from network_distributed_pytorch_amd.parallel.trainer import build_grad_sync
+
+        self.args, self.device, self.world, self.rank = args, device, world, rank
+        self.is_bert = args.model.startswith("distilbert")
+        self.model = build_model(args.model, args.num_classes, fused_bn=not args.no_fused_bn,
+                                 gemm_convs=not args.no_gemm_convs,
+                                 fused_attention=not args.no_fused_attn).to(device)
+        if args.channels_last:
+            self.model = self.model.to(memory_format=torch.channels_last)
+        link = None if args.link == "none" else LINK_PRESETS[args.link]
+        self.comm = Communicator(link=link, emulate_world=args.emulate_world, device=device)
+        kw = {}
+        if args.reducer == "powersgd":
+            if args.no_overlap:
+                kw["overlap"] = False
+            if args.psgd_groups is not None:
+                kw["groups"] = args.psgd_groups
+        self.sync = build_grad_sync(args.reducer, self.model, self.comm, lr=args.lr, momentum=0.9,
+                                    rank=args.rank, bucket_mb=args.bucket_mb, **kw)
+        if args.reducer == "dense" and args.no_overlap:
+            self.sync.ddp.overlap = False
+        self.crit = torch.nn.CrossEntropyLoss()
+        self.loss_acc = torch.zeros((), device=device)
+        self.graph_mode = None
+
+    def make_step(self, batch: int):
+        args, device, model = self.args, self.device, self.model
+        g = torch.Generator(device=device)
+        g.manual_seed(1234 + self.rank)
+        n_pool = 4
+        if self.is_bert:
+            from network_distributed_pytorch_amd.utils.data import SyntheticIMDb
+
+            ds = SyntheticIMDb(n=n_pool * batch, seq_len=args.seq_len, seed=1234 + self.rank, device=device)
+            pool = [{k: v[i * batch:(i + 1) * batch].contiguous() for k, v in ds.columns.items()}
+                    for i in range(n_pool)]
+
+            def loss_of(b):
+                return model(b["input_ids"], attention_mask=b["attention_mask"], labels=b["labels"])[0]
+        else:
+            # CIFAR-10-shape images in [-1, 1] (what ToTensor+Normalize(0.5, 0.5) yields)
+            xs = (torch.rand(n_pool, batch, 3, 32, 32, device=device, generator=g) * 2 - 1)
+            if args.channels_last:
+                xs = torch.stack([x.contiguous(memory_format=torch.channels_last) for x in xs])
+            ys = torch.randint(0, 10, (n_pool, batch), device=device, generator=g)
+            pool = [{"x": xs[i], "y": ys[i]} for i in range(n_pool)]
+
+            def loss_of(b):
+                return self.crit(model(b["x"]), b["y"])
+
+        if args.amp == "bf16":  # opt-in mixed precision: bf16 model math, fp32 params/grads/reducer
+            fp32_loss_of = loss_of
+
+            def loss_of(b):
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    return fp32_loss_of(b).float()
+
+        sync, loss_acc = self.sync, self.loss_acc
+        graph_mode = args.graph_mode
+        if graph_mode == "auto" and "ref" in args.reducer:
+            graph_mode = "none"  # reference-semantics arms are eager by definition
+        if graph_mode != "none":
+            from network_distributed_pytorch_amd.utils.graph import StepRunner
+
+            static = {k: v.clone() for k, v in pool[0].items()}
+            loss_static = torch.zeros((), device=device)
+
+            def pre():
+                sync.zero_grad()
+                loss = loss_of(static)
+                loss.backward()
+                loss_static.copy_(loss.detach())
+
+            def post():
+                loss_acc.add_(loss_static)
+
+            runner = StepRunner(pre, sync, mode=graph_mode, warmup=3, post=post,
+                                state_tensors=list(model.buffers()))
+            graph_mode = runner.mode
+
+            def step(i):
+                for k, v in pool[i % n_pool].items():
+                    static[k].copy_(v, non_blocking=True)
+                runner()
+        else:
+            def step(i):
+                sync.zero_grad()
+                loss = loss_of(pool[i % n_pool])
+                loss.backward()
+                sync.step()
+                loss_acc.add_(loss.detach())
+        self.graph_mode = graph_mode
+        return step
+
+    def time(self, step, steps: int, warmup: int) -> float:
+        for i in range(warmup):
+            step(i)
+        if self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        self.comm.stats.reset()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            step(i)
+        torch.cuda.synchronize()
+        if self.world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        if self.world > 1:
+            t = torch.tensor([elapsed], device=self.device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        return elapsed
+
+
+def main(argv=None):
+    args = parse(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -101,111 +241,35 @@ def main():
     torch.manual_seed(714)
     torch.backends.cudnn.benchmark = True
 
-    model = build_model(args.model, args.num_classes, fused_bn=not args.no_fused_bn,
-                        gemm_convs=not args.no_gemm_convs,
-                        fused_attention=not args.no_fused_attn).to(device)
-    if args.channels_last:
-        model = model.to(memory_format=torch.channels_last)
-    link = None if args.link == "none" else LINK_PRESETS[args.link]
-    comm = Communicator(link=link)
-    sync = build_grad_sync(args.reducer, model, comm, lr=args.lr, momentum=0.9, rank=args.rank,
-                           bucket_mb=args.bucket_mb)
-    crit = torch.nn.CrossEntropyLoss()
-    is_bert = args.model.startswith("distilbert")
-
-    # synthetic data pools (device-resident): CIFAR-10-shape images in [-1, 1] (what
-    # ToTensor+Normalize(0.5, 0.5) yields) or IMDb-shape token batches (512 tokens, masks)
-    g = torch.Generator(device=device)
-    g.manual_seed(1234 + rank)
-    n_pool = 4
-    if is_bert:
-        from network_distributed_pytorch_amd.utils.data import SyntheticIMDb
-
-        ds = SyntheticIMDb(n=n_pool * args.batch, seq_len=args.seq_len, seed=1234 + rank, device=device)
-        pool = [{k: v[i * args.batch:(i + 1) * args.batch].contiguous() for k, v in ds.columns.items()}
-                for i in range(n_pool)]
-
-        def loss_of(b):
-            return model(b["input_ids"], attention_mask=b["attention_mask"], labels=b["labels"])[0]
+    if args.scaling == "strong":
+        assert args.global_batch % world == 0, "global batch must divide by the world size"
+        per_gpu = args.global_batch // world   # reference: bsz = int(512 / float(size))
     else:
-        xs = (torch.rand(n_pool, args.batch, 3, 32, 32, device=device, generator=g) * 2 - 1)
-        if args.channels_last:
-            xs = torch.stack([x.contiguous(memory_format=torch.channels_last) for x in xs])
-        ys = torch.randint(0, 10, (n_pool, args.batch), device=device, generator=g)
-        pool = [{"x": xs[i], "y": ys[i]} for i in range(n_pool)]
+        per_gpu = args.batch
+    wl = Workload(args, device, world, rank)
+    step = wl.make_step(per_gpu)
+    elapsed = wl.time(step, args.steps, args.warmup)
+    graph_mode = wl.graph_mode
+    comm_stats = wl.comm.stats.as_dict()
+    final_loss = float(wl.loss_acc.item()) / max(1, args.warmup + args.steps)
 
-        def loss_of(b):
-            return crit(model(b["x"]), b["y"])
-
-    if args.amp == "bf16":  # opt-in mixed precision: bf16 model math, fp32 params/grads/reducer
-        fp32_loss_of = loss_of
-
-        def loss_of(b):
-            with torch.autocast("cuda", dtype=torch.bfloat16):
-                return fp32_loss_of(b).float()
-
-    loss_acc = torch.zeros((), device=device)
-
-    graph_mode = args.graph_mode
-    if graph_mode == "auto" and "ref" in args.reducer:
-        graph_mode = "none"  # reference-semantics arms are eager by definition
-    if graph_mode == "auto" and world > 1 and backend != "nccl":
-        # gloo-on-device (test rehearsal of N ranks on one GPU): gloo's host thread waits on
-        # events behind unsynchronised graph replays and stalls for seconds per step
-        # (tools/piecewise_diag.py shows the segments themselves are fine)
-        graph_mode = "none"
-    if graph_mode != "none":
-        from network_distributed_pytorch_amd.utils.graph import StepRunner
-
-        static = {k: v.clone() for k, v in pool[0].items()}
-        loss_static = torch.zeros((), device=device)
-
-        def pre():
-            sync.zero_grad()
-            loss = loss_of(static)
-            loss.backward()
-            loss_static.copy_(loss.detach())
-
-        def post():
-            loss_acc.add_(loss_static)
-
-        runner = StepRunner(pre, sync, mode=graph_mode, warmup=3, post=post)
-        graph_mode = runner.mode
-
-        def step(i):
-            for k, v in pool[i % n_pool].items():
-                static[k].copy_(v, non_blocking=True)
-            runner()
-    else:
-        def step(i):
-            sync.zero_grad()
-            loss = loss_of(pool[i % n_pool])
-            loss.backward()
-            sync.step()
-            loss_acc.add_(loss.detach())
-
-    for i in range(args.warmup):
-        step(i)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    comm.stats.reset()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    final_loss = float(loss_acc.item()) / max(1, args.warmup + args.steps)
+    weak = None
+    want_weak = args.weak_too == "on" or (args.weak_too == "auto" and world > 1)
+    if args.scaling == "strong" and want_weak and not wl.is_bert:
+        try:
+            wb = args.global_batch  # per-GPU batch of the N=1 config, fixed as N grows
+            wstep = wl.make_step(wb)
+            we = wl.time(wstep, args.steps, args.warmup)
+            weak = {"value": round(wb * world * args.steps / we, 2), "unit": "samples/s",
+                    "ms_per_step": round(1e3 * we / args.steps, 4), "per_gpu_batch": wb,
+                    "global_batch": wb * world}
+        except Exception as e:  # the extra arm must never cost the headline line
+            weak = {"error": repr(e)[:200]}
 
     if rank == 0:
-        global_batch = args.batch * world
+        global_batch = per_gpu * world
         sps = global_batch * args.steps / elapsed
+        is_bert = wl.is_bert
         rec = {
             "metric": metric_name(args),
             "value": round(sps, 2),
@@ -215,36 +279,44 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "fp32" if args.amp == "none" else "bf16-autocast (fp32 params/grads/reducer)",
             "data": ("synthetic IMDb-shape (512-token ids + masks, 2 labels)" if is_bert else
                      "synthetic CIFAR-10-shape (3x32x32, 10 labels)") + ", random-init weights",
-            "bytes_per_step": sync.bytes_per_step,
-            "dense_bytes_per_step": 4 * sum(p.numel() for p in model.parameters()),
-            "collectives_per_step": sync.collectives_per_step,
+            "bytes_per_step": wl.sync.bytes_per_step,
+            "dense_bytes_per_step": 4 * sum(p.numel() for p in wl.model.parameters()),
+            "collectives_per_step": wl.sync.collectives_per_step,
+            "comm_backend": wl.comm.backend,
             "config": {
                 "model": args.model,
                 "num_classes": args.num_classes if args.num_classes is not None else (2 if is_bert else 1000),
                 "global_batch": global_batch,
-                "per_gpu_batch": args.batch,
+                "per_gpu_batch": per_gpu,
                 "seq_len": args.seq_len if is_bert else None,
                 "image": None if is_bert else [3, 32, 32],
                 "parallelism": f"dp{world}",
                 "reducer": args.reducer,
                 "powersgd_rank": args.rank if "powersgd" in args.reducer else None,
+                "overlap": getattr(getattr(wl.sync, "opt", getattr(wl.sync, "ddp", None)), "overlap", None),
                 "link_emulation": args.link,
+                "emulate_world": args.emulate_world,
                 "channels_last": args.channels_last,
+                "stock_model_ops": bool(args.no_fused_bn and args.no_gemm_convs),
                 "hip_graph": graph_mode,
                 "fused_attention": (not args.no_fused_attn) if is_bert else None,
             },
+            "comm_stats_timed": comm_stats,
             "mean_loss": round(final_loss, 5),
         }
+        if weak is not None:
+            rec["weak_scaling"] = weak
         line = json.dumps(rec)
         print(line, flush=True)
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
+    wl.comm.close()
     if dist.is_initialized():
         dist.destroy_process_group()
 

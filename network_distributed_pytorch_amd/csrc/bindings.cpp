@@ -62,6 +62,21 @@ py::dict build_plan(const std::vector<std::pair<int64_t, int64_t>>& shapes, int 
   d["pp_total"] = pl.pp_total;
   d["qp_total"] = pl.qp_total;
   d["max_rank"] = pl.max_rank;
+  // first work item of every matrix (+ sentinel) in each list: a PowerSGD group of
+  // matrices [lo, hi) launches the contiguous item slice [start[lo], start[hi])
+  auto starts = [&](auto const& items) {
+    py::list out;
+    size_t k = 0;
+    for (size_t i = 0; i <= pl.geom.size(); ++i) {
+      while (k < items.size() && (size_t)items[k].mat < i) ++k;
+      out.append((int64_t)k);
+    }
+    return out;
+  };
+  d["p_item_start"] = starts(pl.p_items);
+  d["q_item_start"] = starts(pl.q_items);
+  d["u_item_start"] = starts(pl.u_items);
+  d["orth_item_start"] = starts(pl.orth_items);
   py::list rs, poff, qoff, ppoff, qpoff, pch, qch, qrows;
   for (size_t i = 0; i < pl.geom.size(); ++i) {
     rs.append(pl.geom[i].r);
@@ -172,19 +187,25 @@ void psgd_q(torch::Tensor geom, torch::Tensor ptrs, torch::Tensor items, torch::
 
 // scratch: float32 tensor of >= 2*n_items*kMaxRank partials; ctr: int32 tensor of
 // >= n_mats + 1 words (counters, then the error word at index n_mats)
+// items may be a slice of the plan's full item list (one PowerSGD group); n_items_total
+// (the full list's length, -1 = this slice) fixes the double-buffered slab layout
 void psgd_orth(torch::Tensor geom, torch::Tensor items, torch::Tensor p, double p_div, double eps,
-               int max_rank, torch::Tensor scratch, torch::Tensor ctr) {
+               int max_rank, torch::Tensor scratch, torch::Tensor ctr, int64_t n_items_total,
+               int64_t max_spins) {
   check_dev(geom, "geom"); check_dev(items, "items"); check_f32(p, "p"); check_f32(scratch, "scratch");
   check_dev(ctr, "ctr");
   const int n_items = (int)n_of(items, sizeof(ndp::OrthItem));
+  const int n_total = n_items_total < 0 ? n_items : (int)n_items_total;
+  TORCH_CHECK(n_total >= n_items, "orth: n_items_total smaller than the item slice");
   const int n_mats = (int)n_of(geom, sizeof(MatGeom));
-  TORCH_CHECK(scratch.numel() >= 2LL * n_items * ndp::kMaxRank, "orth scratch too small");
+  TORCH_CHECK(scratch.numel() >= 2LL * n_total * ndp::kMaxRank, "orth scratch too small");
   TORCH_CHECK(ctr.numel() * ctr.element_size() >= 4LL * (n_mats + 1), "orth counters too small");
   auto* c = reinterpret_cast<unsigned*>(ctr.data_ptr());
   ndp::launch_psgd_orth(reinterpret_cast<const MatGeom*>(geom.data_ptr()),
                         reinterpret_cast<const ndp::OrthItem*>(items.data_ptr()), n_items, n_mats,
                         p.data_ptr<float>(), (float)p_div, (float)eps, max_rank,
-                        scratch.data_ptr<float>(), c, c + n_mats, cur_stream());
+                        scratch.data_ptr<float>(), c, c + n_mats, n_total,
+                        max_spins < 0 ? ndp::kOrthMaxSpins : (unsigned)max_spins, cur_stream());
   check_launch("launch_psgd_orth");
 }
 
@@ -509,6 +530,8 @@ void attn_bwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, c10::optional<t
 
 }  // namespace
 
+void register_comm(py::module& m);  // comm.cpp
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "network_distributed_pytorch_amd native gfx950 kernels + plan builder";
   m.attr("SIZEOF_MATGEOM") = (int)sizeof(MatGeom);
@@ -522,7 +545,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("make_orth_geom", &make_orth_geom);
   m.def("psgd_p", &psgd_p);
   m.def("psgd_q", &psgd_q);
-  m.def("psgd_orth", &psgd_orth);
+  m.def("psgd_orth", &psgd_orth, py::arg("geom"), py::arg("items"), py::arg("p"), py::arg("p_div"),
+        py::arg("eps"), py::arg("max_rank"), py::arg("scratch"), py::arg("ctr"), py::arg("n_items_total") = -1,
+        py::arg("max_spins") = -1);
+  m.def("orth_coresident_cap", &ndp::orth_coresident_cap);
   m.def("psgd_update", &psgd_update);
   m.def("rank1_step", &rank1_step);
   m.def("seg_reduce", &seg_reduce);
@@ -544,4 +570,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_wgrad", &conv_wgrad);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
+  register_comm(m);
 }

@@ -18,9 +18,14 @@
 //  * Partial slabs are double-buffered by barrier parity (a fast workgroup can be at most
 //    one barrier ahead); counters are zeroed by a memset node before each launch; spins are
 //    bounded and report through an error word instead of hanging the GPU.
-//  * Residency: the plan keeps the grid small (<= a few hundred 256-thread workgroups, a
-//    fraction of 256 CUs x 8), and the kernel runs alone on its stream after the P
-//    all-reduce, so all workgroups of a matrix are co-resident.
+//  * Residency: workgroups are dispatched in grid order, so the barrier can only
+//    deadlock if ONE matrix needs more workgroups than the device holds at once.  The
+//    plan checks every matrix's workgroup count against orth_coresident_cap() =
+//    hipOccupancyMaxActiveBlocksPerMultiprocessor x CUs / 2 (half the device is left to
+//    kernels of other streams: backward, RCCL).  A spin that still exceeds `max_spins`
+//    sets the error word AND poisons the workgroup's rows of P-hat with NaN, so a
+//    timed-out barrier can never silently yield a plausible-but-wrong P-hat; the Python
+//    layer reads the error word at its check cadence and raises.
 #include <hip/hip_runtime.h>
 #include "ndp_kernels.h"
 
@@ -52,12 +57,13 @@ struct OrthCtx {
   unsigned* ctr;      // [n_mats]
   unsigned* err;      // [1]
   int n_items;
+  unsigned max_spins; // barrier spin bound (s_sleep 2 each) before reporting a timeout
 };
 
 // Sum v[] over all workgroups of the matrix (deterministic, identical everywhere).
 template <int K>
 __device__ __forceinline__ void group_sum(float (&v)[K], float* red, const OrthItem& it, const OrthCtx& cx,
-                                          int& bar) {
+                                          int& bar, int* bad) {
   block_sum_o<K>(v, red);
   if (it.nwg == 1) return;
   float* slab = cx.partial + ((size_t)(bar & 1) * cx.n_items + it.slab0) * kMaxRank;
@@ -76,8 +82,9 @@ __device__ __forceinline__ void group_sum(float (&v)[K], float* red, const OrthI
     unsigned spins = 0;
     while (__hip_atomic_load(cx.ctr + it.mat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1u << 25)) {  // ~seconds: report instead of hanging
+      if (++spins > cx.max_spins) {  // report (and poison, below) instead of hanging
         __hip_atomic_fetch_or(cx.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *bad = 1;
         break;
       }
     }
@@ -100,6 +107,8 @@ __global__ __launch_bounds__(256) void psgd_orth_mw_kernel(const MatGeom* __rest
                                                            float* __restrict__ p, float p_div,
                                                            float eps, OrthCtx cx) {
   __shared__ float red[4 * RMAX];
+  __shared__ int bad;
+  if (threadIdx.x == 0) bad = 0;  // published by group_sum's barriers before any read
   const OrthItem it = items[blockIdx.x];
   const MatGeom g = geom[it.mat];
   const int r = g.r;
@@ -123,7 +132,7 @@ __global__ __launch_bounds__(256) void psgd_orth_mw_kernel(const MatGeom* __rest
 #pragma unroll
       for (int c = 0; c < RMAX; ++c)
         if (c == i) s[0] += v[k][c] * v[k][c];
-    group_sum<1>(s, red, it, cx, bar);
+    group_sum<1>(s, red, it, cx, bar, &bad);
     const float nrm = sqrtf(s[0]) + eps;
     float vi[RPT];
 #pragma unroll
@@ -145,7 +154,7 @@ __global__ __launch_bounds__(256) void psgd_orth_mw_kernel(const MatGeom* __rest
       for (int k = 0; k < RPT; ++k)
         if (j > i) d[j] += vi[k] * v[k][j];
     }
-    group_sum<RMAX>(d, red, it, cx, bar);
+    group_sum<RMAX>(d, red, it, cx, bar, &bad);
 #pragma unroll
     for (int k = 0; k < RPT; ++k)
 #pragma unroll
@@ -153,13 +162,15 @@ __global__ __launch_bounds__(256) void psgd_orth_mw_kernel(const MatGeom* __rest
         if (j > i && j < r) v[k][j] = v[k][j] - d[j] * vi[k];
   }
 
+  __syncthreads();
+  const bool poison = bad != 0;
 #pragma unroll
   for (int k = 0; k < RPT; ++k) {
     const int a = it.row0 + tid + 256 * k;
     if (a < it.row1) {
 #pragma unroll
       for (int c = 0; c < RMAX; ++c)
-        if (c < r) P[(int64_t)a * r + c] = v[k][c];
+        if (c < r) P[(int64_t)a * r + c] = poison ? __builtin_nanf("") : v[k][c];
     }
   }
 }
@@ -173,10 +184,10 @@ int orth_rows_per_thread(int max_rank) {
 
 void launch_psgd_orth(const MatGeom* geom, const OrthItem* items, int n_items, int n_mats, float* p,
                       float p_div, float eps, int max_rank, float* partial, unsigned* counters,
-                      unsigned* err, hipStream_t s) {
+                      unsigned* err, int n_items_total, unsigned max_spins, hipStream_t s) {
   if (n_items <= 0) return;
   (void)hipMemsetAsync(counters, 0, sizeof(unsigned) * (size_t)n_mats, s);
-  OrthCtx cx{partial, counters, err, n_items};
+  OrthCtx cx{partial, counters, err, n_items_total, max_spins};
   if (max_rank <= 4)
     hipLaunchKernelGGL((psgd_orth_mw_kernel<4, 8>), dim3(n_items), dim3(256), 0, s, geom, items, p, p_div, eps, cx);
   else if (max_rank <= 8)
@@ -187,6 +198,26 @@ void launch_psgd_orth(const MatGeom* geom, const OrthItem* items, int n_items, i
     hipLaunchKernelGGL((psgd_orth_mw_kernel<32, 2>), dim3(n_items), dim3(256), 0, s, geom, items, p, p_div, eps, cx);
   else
     hipLaunchKernelGGL((psgd_orth_mw_kernel<64, 1>), dim3(n_items), dim3(256), 0, s, geom, items, p, p_div, eps, cx);
+}
+
+static int occ(const void* fn) {
+  int blocks = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, 256, 0) != hipSuccess) blocks = 1;
+  return blocks < 1 ? 1 : blocks;
+}
+
+int orth_coresident_cap(int max_rank) {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    return -1;  // no device: the caller falls back to a conservative constant
+  int per_cu;
+  if (max_rank <= 4) per_cu = occ(reinterpret_cast<const void*>(psgd_orth_mw_kernel<4, 8>));
+  else if (max_rank <= 8) per_cu = occ(reinterpret_cast<const void*>(psgd_orth_mw_kernel<8, 8>));
+  else if (max_rank <= 16) per_cu = occ(reinterpret_cast<const void*>(psgd_orth_mw_kernel<16, 4>));
+  else if (max_rank <= 32) per_cu = occ(reinterpret_cast<const void*>(psgd_orth_mw_kernel<32, 2>));
+  else per_cu = occ(reinterpret_cast<const void*>(psgd_orth_mw_kernel<64, 1>));
+  return (per_cu * cus) / 2;
 }
 
 }  // namespace ndp

@@ -114,11 +114,14 @@ std::vector<OrthItem> build_orth_items(const std::vector<MatGeom>& geom, int max
       items.push_back(it);
     }
   }
-  // every workgroup of a matrix must be co-resident (spin barriers): the kernel fits
-  // >= 3 workgroups per CU for RMAX <= 32 and 1 for RMAX = 64 (kernel-resource-usage),
-  // so stay well below 256 CUs x that
-  const size_t cap = max_rank <= 32 ? 512 : 192;
-  if (items.size() > cap) throw std::invalid_argument("orthogonalisation grid too large for co-residency");
+  // every workgroup of ONE matrix must be co-resident (spin barriers; grid-order dispatch
+  // means other matrices' workgroups always drain): check against the measured occupancy
+  // of the kernel instance (orth.hip), or a conservative constant without a device
+  int cap = orth_coresident_cap(max_rank);
+  if (cap <= 0) cap = 64;
+  for (const OrthItem& it : items)
+    if (it.nwg > cap)
+      throw std::invalid_argument("orthogonalisation: a matrix needs more workgroups than can be co-resident");
   return items;
 }
 

@@ -48,7 +48,7 @@ def default_config(**over) -> Dict[str, Any]:
         # additions
         task="cifar", model="resnet18", num_classes=1000, global_batch=512, grad_sync="powersgd",
         dataset_size=None, data_seed=0, max_steps_per_epoch=None, graph_mode="none", link="none",
-        bucket_mb=25.0, checkpoint_dir=None, resume=None, log_file=None, check_replicas_every=0,
+        bucket_mb=None, checkpoint_dir=None, resume=None, log_file=None, check_replicas_every=0,
         write_grad=False, verbose=True, trace_phases=False,
     )
     cfg.update(over)
@@ -186,7 +186,7 @@ def run_task(config) -> Dict[str, Any]:
     comm = Communicator(link=link)
     sync = build_grad_sync(config["grad_sync"], model, comm, lr=config["learning_rate"],
                            momentum=config["momentum"], rank=config["reducer_rank"],
-                           bucket_mb=config.get("bucket_mb", 25.0), seed=config["seed"],
+                           bucket_mb=config.get("bucket_mb"), seed=config["seed"],
                            **({"write_grad": config.get("write_grad", False)} if config["grad_sync"] == "powersgd" else {}))
     start_epoch = 0
     if config.get("resume"):

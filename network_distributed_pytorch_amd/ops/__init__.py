@@ -26,6 +26,7 @@ __all__ = [
     "capturing",
     "upload",
     "SegPlan",
+    "upload_epoch",
 ]
 
 
@@ -125,11 +126,17 @@ class _DeferredUploads:
     the scope ends, copied synchronously.  ``generation`` counts eager uploads: if an eager
     step re-bound a table after capture, :meth:`ensure` restores the capture-time contents
     before the next replay.
+
+    ``epoch`` counts :meth:`apply` calls.  Every Python-side table cache (``SegPlan``,
+    ``_PlanBuffers``, the optimizers' pointer tables) puts the epoch into its cache key:
+    after the capture-time tables were (re)applied, the next eager bind always re-uploads
+    instead of trusting an address key that no longer describes the device table.
     """
 
     def __init__(self):
         self.defer = False
         self.generation = 0
+        self.epoch = 0
         self._pending = []
 
     def record(self, dev: torch.Tensor, host: torch.Tensor):
@@ -155,6 +162,7 @@ class _DeferredUploads:
         if uploads:
             torch.cuda.synchronize()
         self.generation += 1  # the tables now hold the capture-time contents
+        self.epoch += 1       # ... so every eager-side cache key is stale
 
     def ensure(self, uploads, generation: int) -> int:
         """Re-apply ``uploads`` if any eager upload happened since ``generation``."""
@@ -164,6 +172,11 @@ class _DeferredUploads:
 
 
 _UPLOADS = _DeferredUploads()
+
+
+def upload_epoch() -> int:
+    """Current table-restore epoch (include it in any device-table cache key)."""
+    return _UPLOADS.epoch
 
 
 class SegPlan:
@@ -196,14 +209,15 @@ class SegPlan:
 
     def set(self, specs: Sequence[tuple]) -> None:
         specs = list(specs)
-        key = tuple((s.data_ptr(), d.data_ptr(), d.numel(), int(c), int(st), float(dv)) for s, d, c, st, dv in specs)
+        key = (_UPLOADS.epoch,) + tuple((s.data_ptr(), d.data_ptr(), d.numel(), int(c), int(st), float(dv))
+                                        for s, d, c, st, dv in specs)
         self.specs = specs
         if key == self._key:
             return
         self._key = key
         if self.device.type != "cuda" or not specs:
             return
-        rows = [(a, b, n, st, c, dv) for a, b, n, c, st, dv in key]
+        rows = [(a, b, n, st, c, dv) for a, b, n, c, st, dv in key[1:]]
         ent, prefix, n_ent, n_blocks = ext().make_seg_table(rows)
         if n_ent > self._cap:
             assert not capturing(), "SegPlan must be sized before graph capture"

@@ -2,8 +2,9 @@
 
 Policy: device (HIP) tensors ALWAYS go through the native kernels; if the extension is
 missing on a GPU box every op raises instead of silently falling back to eager PyTorch.
-CPU tensors (gloo unit tests, no GPU in the build container) use the pure-torch
-implementations in :mod:`network_distributed_pytorch_amd.ops.reference`.
+CPU tensors (gloo unit tests, no GPU in the build container) take the pure-torch branches
+written next to each op (``ops/__init__.py``, ``ops/conv.py``, ...; ``parallel/powersgd.py``
+``_step_torch`` / ``_reduce_torch``).
 """
 from __future__ import annotations
 

@@ -1,29 +1,39 @@
-"""Collective layer: world-size-guarded collectives, byte accounting, link emulation.
+"""Collective layer: world-size-guarded collectives, byte accounting, link emulation, and the
+native RCCL data plane.
 
 Reference behaviour kept:
   * ``all_reduce`` / ``all_gather`` are no-ops at world size 1
     (ddp_powersgd_guide_cifar10/reducer.py:193-195, tensor_buffer.py:59-69);
   * ``n_bits(t) = 8 * numel * element_size`` (reducer.py:197-198).
 
-MI355X additions:
+MI355X design:
+  * **Data plane = native RCCL** (``csrc/comm.cpp``, :class:`RcclComm`): c10d only
+    bootstraps.  Rank 0's ``ncclUniqueId`` goes through the c10d store, every rank calls
+    ``ncclCommInitRank``, and collectives are enqueued straight onto a HIP stream: the
+    framework-owned high-priority side stream (``csrc/comm.cpp`` SideStream), ordered
+    against the compute stream with hipEvents (:meth:`Communicator.side_launch`), so
+    bucket / PowerSGD-group work overlaps backward — eagerly, or as comm graphs launched
+    between the segments of a captured step (utils/graph.py).  c10d (``ProcessGroupNCCL`` = RCCL, or gloo for
+    CPU tests) is the fallback data plane.
   * every collective is accounted (calls, payload bytes, modelled ring wire bytes
     2(N-1)/N * S) so the bytes/step metric is measured, not only derived;
   * :class:`LinkModel` paces each collective to an emulated 1/10/100 Gb link
-    (``alpha + wire_bits / bandwidth``) by stalling the HIP stream with a wall-clock
-    spin kernel (no root / ``tc`` on the GPU box) — the reference's README.md:2
-    bandwidth experiments;
-  * collectives run on RCCL (``backend="nccl"`` is RCCL on ROCm) over xGMI; gloo for CPU;
+    (``alpha + wire_bits / bandwidth``) by stalling the stream that carries the collective
+    with a wall-clock spin kernel (no root / ``tc`` on the GPU box) — the reference's
+    README.md:2 bandwidth experiments.  ``emulate_world=N`` charges the N-rank ring time
+    even in a 1-GPU run (one-GPU rehearsal of an N-GPU bandwidth curve);
   * ``NDP_FORCE_COLLECTIVES=1`` issues the collectives even in a 1-rank process group
-    (:attr:`Communicator.active`): a one-GPU rehearsal of the N > 1 RCCL path (async work
-    handles, bucket overlap hooks, eager collectives between graph segments) whose sums
+    (:attr:`Communicator.active`): a one-GPU rehearsal of the N > 1 RCCL path whose sums
     are the identity, so results match the world-size-1 no-op path.
+  * ``NDP_NATIVE_COMM=0`` forces the c10d data plane.
 """
 from __future__ import annotations
 
+import contextlib
 import dataclasses
 import os
 import time
-from typing import List, Optional
+from typing import List, Optional, Sequence
 
 import torch
 import torch.distributed as dist
@@ -38,6 +48,7 @@ __all__ = [
     "CommStats",
     "Communicator",
     "LINK_PRESETS",
+    "create_native_comm",
 ]
 
 
@@ -76,7 +87,7 @@ def all_gather(out_list: List[torch.Tensor], in_tensor: torch.Tensor, **kwargs):
 
 @dataclasses.dataclass
 class LinkModel:
-    """Emulated point-to-point link: time(S) = alpha + 8*wire(S)/bandwidth_bps."""
+    """Emulated point-to-point link: time(S) = alpha + 8*wire(S)/bandwidth_bps (ring)."""
 
     bandwidth_bps: float
     alpha_s: float = 25e-6
@@ -116,7 +127,7 @@ class CommStats:
 
 
 class _PacedWork:
-    """Async handle that applies link pacing when waited on."""
+    """Async handle that applies link pacing when waited on (c10d data plane)."""
 
     def __init__(self, work, comm: "Communicator", seconds: float, device_tensor: bool):
         self._work = work
@@ -134,14 +145,94 @@ class _PacedWork:
         return self._work is None or self._work.is_completed()
 
 
-class Communicator:
-    """Accounting + pacing front-end over a c10d process group (RCCL or gloo)."""
+class _StreamWork:
+    """Handle of a stream-ordered (native RCCL) collective: already ordered on its stream."""
 
-    def __init__(self, group=None, link: Optional[LinkModel] = None):
+    def wait(self):
+        return True
+
+    def is_completed(self):
+        return True
+
+
+_SIDE_LINKS = {}
+_KEEPALIVE = []
+
+
+def _side_link(device_index: int):
+    """One framework-owned side stream (+ its events) per device and process.  Never
+    destroyed: captured graphs hold its events and stream for their whole lifetime, and
+    Python's cycle collector frees graphs and streams in no particular order."""
+    if device_index not in _SIDE_LINKS:
+        from ..ops import ext
+
+        link = ext().SideStream(device_index)
+        _SIDE_LINKS[device_index] = (link, torch.cuda.ExternalStream(link.handle,
+                                                                      device=torch.device("cuda", device_index)))
+    return _SIDE_LINKS[device_index]
+
+
+def _native_wanted() -> bool:
+    return os.environ.get("NDP_NATIVE_COMM", "1") != "0"
+
+
+def create_native_comm(group=None, device: Optional[torch.device] = None):
+    """Bootstrap an :class:`RcclComm` over ``group`` (collective: every rank must call it).
+
+    Rank 0 of the group draws the ``ncclUniqueId``; its 128 bytes are exchanged through the
+    default c10d store under a per-group, per-call key.  Returns None when the native data
+    plane is unavailable (no device, no extension, not an nccl group, or disabled).
+    """
+    if not (_native_wanted() and dist.is_available() and dist.is_initialized() and torch.cuda.is_available()):
+        return None
+    try:
+        if dist.get_backend(group) != "nccl":
+            return None
+    except Exception:
+        return None
+    from ..ops import native_available, ext
+
+    if not native_available():
+        return None
+    X = ext()
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    store = dist.distributed_c10d._get_default_store()
+    create_native_comm._n = getattr(create_native_comm, "_n", 0) + 1
+    ranks = dist.get_process_group_ranks(group) if group is not None else list(range(dist.get_world_size()))
+    key = "ndp_rccl_uid/{}/{}".format("-".join(map(str, ranks)), create_native_comm._n)
+    rank = dist.get_rank(group)
+    if rank == 0:
+        store.set(key, X.rccl_unique_id())
+    uid = store.get(key)
+    return X.RcclComm(uid, len(ranks), rank, dev.index if dev.index is not None else 0)
+
+
+class Communicator:
+    """Accounting + pacing front-end over the native RCCL communicator or a c10d group.
+
+    Stream-ordered API (device tensors) used by the overlapped gradient-sync engines:
+    :meth:`fork` (side stream waits for the compute stream), :meth:`on_side` (context that
+    makes the side stream current), :meth:`join` (compute stream waits for the side stream).
+    """
+
+    def __init__(self, group=None, link: Optional[LinkModel] = None, native: Optional[bool] = None,
+                 emulate_world: Optional[int] = None, device: Optional[torch.device] = None):
         self.group = group
         self.link = link
+        self.emulate_world = emulate_world
         self.stats = CommStats()
+        self._native = None
+        self._side = None
+        self._deferred = None
+        self._split = None
+        self._captured = False
+        self._device = device
+        if native is not False and self.active:
+            self._native = create_native_comm(group, device)
+            if native is True and self._native is None:
+                raise RuntimeError("native RCCL communicator requested but unavailable")
 
+    # -- topology ---------------------------------------------------------------------------
     @property
     def world_size(self) -> int:
         return world_size(self.group)
@@ -157,6 +248,99 @@ class Communicator:
             return True
         return os.environ.get("NDP_FORCE_COLLECTIVES") == "1" and dist.is_available() and dist.is_initialized()
 
+    @property
+    def backend(self) -> str:
+        if self._native is not None:
+            return "rccl-native"
+        if not self.active:
+            return "none"
+        try:
+            return "c10d-" + str(dist.get_backend(self.group))
+        except Exception:
+            return "c10d"
+
+    @property
+    def native(self):
+        return self._native
+
+    @property
+    def stream_ordered(self) -> bool:
+        """True if device collectives are ordered on HIP streams (no host blocking), i.e.
+        the overlapped / graph-captured step is possible: native RCCL, or nothing to issue."""
+        return self._native is not None or not self.active
+
+    @property
+    def paced_world(self) -> int:
+        return self.emulate_world if self.emulate_world else self.world_size
+
+    # -- side stream (framework-owned HIP stream, csrc/comm.cpp SideStream) --------------------
+    def _link(self):
+        if self._side is None:
+            dev = self._device or torch.device("cuda", torch.cuda.current_device())
+            idx = dev.index if dev.index is not None else torch.cuda.current_device()
+            self._side = _side_link(idx)
+        return self._side
+
+    def side_stream(self):
+        return self._link()[1]
+
+    def fork(self):
+        """The side stream waits for all work enqueued so far on the current stream."""
+        self._link()[0].fork()
+
+    def join(self):
+        """The current stream waits for all work enqueued so far on the side stream."""
+        self._link()[0].join()
+
+    @contextlib.contextmanager
+    def on_side(self):
+        with torch.cuda.stream(self.side_stream()):
+            yield
+
+    def side_launch(self, fn):
+        """Run ``fn`` (kernels + collectives) on the side stream after the work enqueued so
+        far on the current stream.  Eagerly: event fork + run.  While a step is being
+        captured in segments (:meth:`defer_side`): the current compute-graph segment is
+        closed (the split callback) and ``fn`` is kept, to be captured as its own comm
+        graph that the runner launches on the side stream right after that segment."""
+        if self._deferred is not None:
+            if self._split() or not self._deferred:
+                self._deferred.append([fn])
+            else:  # nothing was captured since the last split: same comm graph
+                self._deferred[-1].append(fn)
+            return
+        self.fork()
+        with self.on_side():
+            fn()
+
+    def side_join(self):
+        """Current stream waits for the side stream (deferred in segmented capture: the
+        runner joins after launching the last comm graph)."""
+        if self._deferred is None:
+            self.join()
+
+    def record_event(self, i: int):
+        """Numbered event recorded on the current stream (an event-record node if capturing)."""
+        self._link()[0].record(i)
+
+    def wait_event(self, i: int):
+        """Current stream waits on numbered event i (an event-wait node if capturing)."""
+        self._link()[0].wait(i)
+
+    @contextlib.contextmanager
+    def defer_side(self, split):
+        """Segmented-capture scope: ``split()`` is called at every side launch; it ends the
+        compute-graph segment being captured and begins the next, returning False (and
+        splitting nothing) if the segment is still empty.  Yields the list that collects
+        the side work: one list of callables per comm graph."""
+        assert self._deferred is None, "nested defer_side"
+        self._deferred, self._split = [], split
+        try:
+            yield self._deferred
+        finally:
+            self._deferred, self._split = None, None
+
+    # -- pacing / accounting --------------------------------------------------------------------
     def _pace(self, seconds: float, device_tensor: bool):
         if seconds <= 0:
             return
@@ -168,7 +352,7 @@ class Communicator:
             time.sleep(seconds)
 
     def _account(self, t: torch.Tensor) -> float:
-        n = self.world_size
+        n = self.paced_world
         payload = t.nelement() * t.element_size()
         self.stats.calls += 1
         self.stats.payload_bytes += payload
@@ -177,10 +361,20 @@ class Communicator:
         self.stats.emulated_seconds += secs
         return secs
 
+    def pace_seconds(self, payload_bytes: int) -> float:
+        return self.link.seconds(payload_bytes, self.paced_world) if self.link is not None else 0.0
+
+    # -- collectives ----------------------------------------------------------------------------
     def all_reduce(self, t: torch.Tensor, async_op: bool = False, op=None):
         secs = self._account(t)
         if not self.active:
+            self._pace(secs, t.is_cuda)  # emulated world on a 1-GPU run: charge the link only
             return _PacedWork(None, self, 0.0, t.is_cuda) if async_op else None
+        if self._native is not None and t.is_cuda:
+            self._captured |= torch.cuda.is_current_stream_capturing()
+            self._native.all_reduce(t, _op_name(op))
+            self._pace(secs, True)
+            return _StreamWork() if async_op else None
         kw = {"group": self.group}
         if op is not None:
             kw["op"] = op
@@ -191,19 +385,72 @@ class Communicator:
         self._pace(secs, t.is_cuda)
         return None
 
+    def all_reduce_many(self, ts: Sequence[torch.Tensor]):
+        """Several SUM all-reduces; ONE fused RCCL launch on the native data plane."""
+        ts = [t for t in ts if t.numel()]
+        if not ts:
+            return
+        if self._native is not None and self.active and all(t.is_cuda for t in ts):
+            secs = sum(self._account(t) for t in ts)
+            self._captured |= torch.cuda.is_current_stream_capturing()
+            self._native.all_reduce_many(ts)
+            self._pace(secs, True)
+            return
+        for t in ts:
+            self.all_reduce(t)
+
     def all_gather(self, out_list: List[torch.Tensor], t: torch.Tensor, async_op: bool = False):
         self._account(t)
         if not self.active:
             assert len(out_list) == 1
-            out_list[0].copy_(t)
-            return None
+            out_list[0].copy_(t)  # a copy, not the reference's alias (tensor_buffer.py:69):
+            return None           # callers own out_list storage (TensorBuffer.all_gather)
+        if self._native is not None and t.is_cuda:
+            flat = torch.empty(len(out_list) * t.numel(), dtype=t.dtype, device=t.device)
+            self._native.all_gather(flat, t.contiguous())
+            for i, o in enumerate(out_list):
+                o.copy_(flat[i * t.numel(): (i + 1) * t.numel()].view_as(o))
+            return _StreamWork() if async_op else None
         return dist.all_gather(out_list, t, group=self.group, async_op=async_op)
 
     def broadcast(self, t: torch.Tensor, src: int = 0):
         if not self.active:
+            return None
+        if self._native is not None and t.is_cuda and t.is_contiguous():
+            self._native.broadcast(t, src)
             return None
         return dist.broadcast(t, src=src, group=self.group)
 
     def barrier(self):
         if self.active:
             dist.barrier(group=self.group)
+
+    def check(self):
+        """Raise if the native communicator reported an asynchronous RCCL error."""
+        if self._native is not None:
+            self._native.check()
+
+    def close(self):
+        """Destroy the native communicator — unless a captured graph contains its
+        collectives (RCCL ties graph-owned resources to the communicator; destroying it
+        before the graph is freed aborts the process), in which case it is kept alive."""
+        if self._native is not None:
+            if self._captured:
+                _KEEPALIVE.append(self._native)
+            else:
+                self._native.destroy()
+            self._native = None
+
+
+def _op_name(op) -> str:
+    if op is None or op == dist.ReduceOp.SUM:
+        return "sum"
+    if op == dist.ReduceOp.MAX:
+        return "max"
+    if op == dist.ReduceOp.MIN:
+        return "min"
+    if op == dist.ReduceOp.PRODUCT:
+        return "prod"
+    if op == dist.ReduceOp.AVG:
+        return "avg"
+    raise ValueError(f"unsupported reduce op {op}")

@@ -31,12 +31,13 @@ Q8 decompression writes parameter-shaped output directly.
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
 
-from ..ops import SegPlan, capturing, ext, upload
+from ..ops import SegPlan, capturing, ext, upload, upload_epoch
 from .comm import Communicator, n_bits
 
 __all__ = [
@@ -158,6 +159,7 @@ class _PlanBuffers:
             self.p_chunks, self.q_chunks = d["p_chunks"], d["q_chunks"]
             self.counts = {k: d[k] for k in ("n_p_items", "n_q_items", "n_u_items", "n_orth_items", "pp_total",
                                              "qp_total")}
+            self.item_start = {k: d[k + "_item_start"] for k in ("p", "q", "u", "orth")}
             self.orth_items = d["orth_items"].to(device)
             self.orth_scratch = torch.zeros(max(1, 2 * d["n_orth_items"] * X.MAX_RANK), **f32)
             self.orth_ctr = torch.zeros(len(shapes) + 1, dtype=torch.int32, device=device)
@@ -165,27 +167,52 @@ class _PlanBuffers:
             self.geom = torch.zeros(nb, dtype=torch.uint8, device=device)
             self.ptrs = torch.zeros(nb, dtype=torch.uint8, device=device)
             self._bind_key = None
-            self.q_seg = SegPlan(
-                [(self.q_part[o:], self.q_memory[qo: qo + m * r], c, m * r, 1.0)
-                 for (n, m), r, o, qo, c in zip(shapes, self.ranks, self.qp_offs, self.q_offs, self.q_chunks)],
-                device)
+            self.q_seg = SegPlan(self.q_seg_specs(0, len(shapes)), device)
 
-    def p_seg_specs(self):
-        return [(self.p_part[o:], self.p_memory[po: po + n * r], c, n * r, 1.0)
-                for (n, m), r, o, po, c in zip(self.shapes, self.ranks, self.pp_offs, self.p_offs, self.p_chunks)]
+    # -- per-matrix-range views (a PowerSGD overlap group = matrices [lo, hi)) ----------------
+    def p_seg_specs(self, lo: int = 0, hi: Optional[int] = None):
+        hi = len(self.shapes) if hi is None else hi
+        return [(self.p_part[self.pp_offs[i]:], self.p_memory[self.p_offs[i]: self.p_offs[i] + n * r],
+                 self.p_chunks[i], n * r, 1.0)
+                for i, ((n, m), r) in enumerate(zip(self.shapes, self.ranks)) if lo <= i < hi]
 
-    def orth(self, p_div: float, eps: float):
-        """P-hat = MGS(P / p_div) for every matrix, one multi-workgroup launch."""
-        ext().psgd_orth(self.geom, self.orth_items, self.comm_buf, p_div, eps, self.max_rank,
-                        self.orth_scratch, self.orth_ctr)
+    def q_seg_specs(self, lo: int, hi: int):
+        return [(self.q_part[self.qp_offs[i]:], self.q_memory[self.q_offs[i]: self.q_offs[i] + m * r],
+                 self.q_chunks[i], m * r, 1.0)
+                for i, ((n, m), r) in enumerate(zip(self.shapes, self.ranks)) if lo <= i < hi]
+
+    def items(self, kind: str, lo: int, hi: int) -> torch.Tensor:
+        """Byte slice of a work-item table covering matrices [lo, hi)."""
+        size = {"p": 32, "q": 32, "u": 16, "orth": 32}[kind]  # sizeof PItem / QItem / UItem / OrthItem
+        table = {"p": self.p_items, "q": self.q_items, "u": self.u_items, "orth": self.orth_items}[kind]
+        st = self.item_start[kind]
+        return table[st[lo] * size: st[hi] * size]
+
+    def p_range(self, lo: int, hi: int) -> Tuple[int, int]:
+        end = self.p_offs[hi - 1] + self.shapes[hi - 1][0] * self.ranks[hi - 1]
+        return self.p_offs[lo], end
+
+    def q_range(self, lo: int, hi: int) -> Tuple[int, int]:
+        end = self.q_offs[hi - 1] + self.shapes[hi - 1][1] * self.ranks[hi - 1]
+        return self.q_offs[lo], end
+
+    def orth(self, p_div: float, eps: float, items: Optional[torch.Tensor] = None, max_spins: int = -1):
+        """P-hat = MGS(P / p_div) for every matrix (or a group's item slice), one launch."""
+        ext().psgd_orth(self.geom, self.orth_items if items is None else items, self.comm_buf, p_div, eps,
+                        self.max_rank, self.orth_scratch, self.orth_ctr, self.counts["n_orth_items"], max_spins)
 
     def orth_error(self) -> int:
-        """Non-zero if a cross-workgroup barrier of the MGS kernel ever timed out."""
+        """Non-zero if a cross-workgroup barrier of the MGS kernel ever timed out (host sync)."""
         return int(self.orth_ctr[-1].item())
+
+    def check_orth(self):
+        if self.native and self.orth_error():
+            raise RuntimeError("PowerSGD orthogonalisation: a cross-workgroup barrier timed out; P-hat "
+                               "was poisoned with NaN (co-residency violated)")
 
     def bind(self, rows: List[List[int]], vec: List[int]) -> bool:
         """Point the grouped kernels at new tensors; returns True if the tables changed."""
-        key = (tuple(map(tuple, rows)), tuple(vec))
+        key = (upload_epoch(), tuple(map(tuple, rows)), tuple(vec))
         if key == self._bind_key:
             return False
         X = ext()
@@ -193,6 +220,17 @@ class _PlanBuffers:
         upload(self.ptrs, X.make_mat_ptrs(rows))
         self._bind_key = key
         return True
+
+    def bind_range(self, lo: int, rows: List[List[int]], vec: List[int]):
+        """Upload geometry + pointer rows of matrices [lo, lo + len(rows)) only."""
+        X = ext()
+        sz = X.SIZEOF_MATGEOM
+        hi = lo + len(rows)
+        geom = self._geom_host[lo * sz: hi * sz].clone()
+        gi = geom.view(torch.int32).view(hi - lo, sz // 4)
+        gi[:, 3] = torch.tensor(vec, dtype=torch.int32)  # MatGeom.vec
+        upload(self.geom[lo * sz: hi * sz], geom)
+        upload(self.ptrs[lo * X.SIZEOF_MATPTRS: hi * X.SIZEOF_MATPTRS], X.make_mat_ptrs(rows))
 
     def p_view(self, i):
         n, _ = self.shapes[i]
@@ -339,6 +377,21 @@ class PowerSGDReducer(Reducer):
             off += o.numel()
 
 
+class _Group:
+    """One overlap group: high-rank matrices [lo, hi) (contiguous in parameter order, so
+    their P / Q payloads are contiguous slices of the reference-order buffers)."""
+
+    def __init__(self, idx: int, lo: int, hi: int, params: List[torch.nn.Parameter]):
+        self.idx, self.lo, self.hi = idx, lo, hi
+        self.params = params
+        self.numel = sum(p.numel() for p in params)
+        self.ready = 0
+        self.launched = False
+        self.key = None
+        self.p_seg: Optional[SegPlan] = None
+        self.q_seg: Optional[SegPlan] = None
+
+
 class PowerSGDOptimizer:
     """Fused EF-SGD-with-momentum PowerSGD step (ddp_init.py:121-178) over flat arenas.
 
@@ -350,6 +403,22 @@ class PowerSGDOptimizer:
     when an address changes (hipGraph-capture safe).  ``step()`` returns the bits
     communicated (reducer.py:170).
 
+    **Overlap with backward** (``overlap=True``, the default on a device with a
+    stream-ordered data plane — native RCCL, or nothing to communicate).  The high-rank
+    matrices are cut, in backward order, into ``groups`` contiguous groups.  A
+    post-accumulate-grad hook launches a group's whole pipeline on the communicator's side
+    stream as soon as its last gradient lands, in group order on every rank:
+
+        psgd_p -> split-K sum -> all_reduce(P_g) -> MGS -> psgd_q -> split-K sum
+               -> all_reduce(Q_g) -> fused decompress / EF / momentum / SGD update
+
+    so compression, both collectives and the update of the late layers run while backward
+    is still computing the early layers.  ``step()`` launches what is left (the rank-1
+    group: pack, all-reduce, momentum/SGD) and joins the side stream.  Per-matrix work
+    items, split-K slab order and the MGS reduction order are exactly those of the serial
+    path, so the result is bitwise identical to ``overlap=False`` (tests/test_overlap_gpu.py);
+    the byte count is unchanged, the collective count becomes 2 * groups + 1.
+
     ``write_grad=True`` also leaves ``p.grad = out + m`` exactly like the reference loop
     (ddp_init.py:172); it costs one extra write pass and is off by default.
     """
@@ -358,7 +427,7 @@ class PowerSGDOptimizer:
                  random_seed: int = 714, reuse_query: bool = True,
                  comm: Optional[Communicator] = None, write_grad: bool = False,
                  broadcast_params: bool = True, rng_compat: bool = False, eps: float = 1e-8,
-                 native: Optional[bool] = None):
+                 native: Optional[bool] = None, overlap: Optional[bool] = None, groups: Optional[int] = None):
         self.params: List[torch.nn.Parameter] = [p for p in params]
         assert self.params, "no parameters"
         self.lr = float(lr)
@@ -378,6 +447,8 @@ class PowerSGDOptimizer:
                 left -= k
         self.step_count = 0
         self.bits_communicated = 0
+        self._q_ready = False
+        self.orth_max_spins = -1  # < 0: kernel default (debug / tests may lower it)
 
         hi = [p for p in self.params if p.dim() > 1]
         r1 = [p for p in self.params if p.dim() <= 1]
@@ -413,7 +484,147 @@ class PowerSGDOptimizer:
         self.native = self.buf.native
         self._p_seg = SegPlan([], self.device, capacity=len(shapes) + len(r1) + 1) if self.native else None
         self._r1_out = SegPlan([], self.device, capacity=len(r1) + 1) if self.native else None
+        self._r1_pack = SegPlan([], self.device, capacity=len(r1) + 1) if self.native else None
         self._grad_key = None
+        self._r1_key = None
+
+        want = overlap if overlap is not None else os.environ.get("NDP_PSGD_OVERLAP", "1") != "0"
+        self.overlap = bool(want) and self.native and self.comm.stream_ordered and bool(hi)
+        if overlap and not self.overlap:
+            raise ValueError("overlap=True needs device tensors, the native extension and a stream-ordered "
+                             "communicator (native RCCL or world size 1)")
+        self.groups: List[_Group] = []
+        self._group_of = {}
+        self._hooks = []
+        self._next_group = 0
+        if self.overlap:
+            n_groups = groups if groups is not None else int(os.environ.get("NDP_PSGD_GROUPS", "4"))
+            self._build_groups(max(1, n_groups))
+            for p in self.params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+
+    # -- overlap groups ------------------------------------------------------------------------
+    def _build_groups(self, n_groups: int):
+        """Cut the high-rank matrices, in backward (reverse parameter) order, into groups of
+        about total/n_groups elements; the last group to be produced (the first layers) is
+        whatever is left, so the exposed post-backward tail stays small."""
+        total = sum(p.numel() for p in self.high)
+        target = total / n_groups
+        bounds = []  # (lo, hi) in forward index space, built from the back
+        hi_idx = len(self.high)
+        acc = 0
+        for i in range(len(self.high) - 1, -1, -1):
+            acc += self.high[i].numel()
+            if acc >= target and len(bounds) < n_groups - 1 and i > 0:
+                bounds.append((i, hi_idx))
+                hi_idx, acc = i, 0
+        bounds.append((0, hi_idx))
+        for gi, (lo, hi) in enumerate(bounds):
+            g = _Group(gi, lo, hi, self.high[lo:hi])
+            g.p_seg = SegPlan([], self.device, capacity=hi - lo + 1)
+            g.q_seg = SegPlan(self.buf.q_seg_specs(lo, hi), self.device)
+            self.groups.append(g)
+            for p in g.params:
+                self._group_of[id(p)] = g
+
+    def _on_grad(self, p):
+        if not self.overlap:
+            return
+        g = self._group_of.get(id(p))
+        if g is None:
+            return  # rank-1 parameters are handled in step()
+        g.ready += 1
+        # launch in group order on every rank (identical collective sequence everywhere)
+        while self._next_group < len(self.groups):
+            nxt = self.groups[self._next_group]
+            if nxt.launched or nxt.ready < len(nxt.params):
+                break
+            self._launch_group(nxt)
+            self._next_group += 1
+
+    def _bind_group(self, g: _Group):
+        B = self.buf
+        grads = [p.grad for p in g.params]
+        key = (upload_epoch(),) + tuple(t.data_ptr() for t in grads)
+        if key == g.key:
+            return
+        rows, vec = [], []
+        for p, gr, (n, m) in zip(g.params, grads, B.shapes[g.lo:g.hi]):
+            assert gr.is_contiguous() and gr.dtype == torch.float32, "PowerSGD needs dense fp32 grads"
+            s = self.offsets[id(p)]
+            e, mo, x = (t[s:].data_ptr() for t in (self.e, self.m, self.x))
+            row = [gr.data_ptr(), e, e, 0, 0, mo, x, gr.data_ptr()]
+            rows.append(row)
+            vec.append(_vec_ok(m, row))
+        B.bind_range(g.lo, rows, vec)
+        g.p_seg.set(B.p_seg_specs(g.lo, g.hi))
+        g.key = key
+
+    @torch.no_grad()
+    def _launch_group(self, g: _Group):
+        B = self.buf
+        X = ext()
+        N = self.comm.world_size
+        self._ensure_queries()
+        for p in g.params:
+            if p.grad is None:  # parameter unused this step: zero gradient
+                p.grad = torch.zeros_like(p)
+        self._bind_group(g)  # table uploads on the compute stream, before the fork
+        p0, p1 = B.p_range(g.lo, g.hi)
+        q0, q1 = B.q_range(g.lo, g.hi)
+        mode, lr, mom, spins = 2 if self.write_grad else 1, self.lr, self.momentum, self.orth_max_spins
+
+        def pipeline():
+            X.psgd_p(B.geom, B.ptrs, B.items("p", g.lo, g.hi), B.q_warm, B.p_part, True, B.max_rank)
+            g.p_seg.run()
+            self.comm.all_reduce(B.comm_buf[p0:p1])                       # reducer.py:126 (group g)
+            B.orth(float(N), self.eps, B.items("orth", g.lo, g.hi), spins)
+            X.psgd_q(B.geom, B.ptrs, B.items("q", g.lo, g.hi), B.comm_buf, B.q_part, B.max_rank)
+            g.q_seg.run()
+            self.comm.all_reduce(B.q_memory[q0:q1])                       # reducer.py:145 (group g)
+            X.psgd_update(B.geom, B.ptrs, B.items("u", g.lo, g.hi), B.comm_buf, B.q_memory, float(N),
+                          B.q_warm, mode, lr, mom)
+        self.comm.side_launch(pipeline)
+        g.launched = True
+
+    def _finish_overlapped(self):
+        """After backward: launch groups whose hooks did not fire (unused parameters / hooks
+        bypassed), run the rank-1 group on the side stream, join."""
+        for g in self.groups[self._next_group:]:
+            if not g.launched:
+                self._launch_group(g)
+        self._next_group = len(self.groups)
+        B = self.buf
+        N = self.comm.world_size
+        if self.r1_numel:
+            grads = []
+            for p in self.rank1:
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
+                grads.append(p.grad)
+            key = (upload_epoch(),) + tuple(t.data_ptr() for t in grads)
+            if key != self._r1_key:
+                specs, outs = [], []
+                for p, gr in zip(self.rank1, grads):
+                    s = self.offsets[id(p)] - self.r1_start
+                    specs.append((gr.view(-1), B.rank1_buf[s: s + p.numel()], 1, 0, 1.0))
+                    if self.write_grad:
+                        outs.append((self.r1_upd[s: s + p.numel()], gr.view(-1), 1, 0, 1.0))
+                self._r1_pack.set(specs)
+                self._r1_out.set(outs)
+                self._r1_key = key
+            r1 = slice(self.r1_start, self.arena_numel)
+            lr, mom = self.lr, self.momentum
+
+            def rank1():
+                self._r1_pack.run()
+                self.comm.all_reduce(B.rank1_buf)                           # reducer.py:132
+                ext().rank1_step(B.rank1_buf, float(N), self.m[r1], self.x[r1],
+                                 self.r1_upd if self.write_grad else None, lr, mom)
+                if self.write_grad:
+                    self._r1_out.run()
+            self.comm.side_launch(rank1)
+        self.comm.side_join()
 
     # -- helpers -------------------------------------------------------------------------
     def zero_grad(self, set_to_none: bool = True):
@@ -422,6 +633,13 @@ class PowerSGDOptimizer:
                 p.grad = None
             elif p.grad is not None:
                 p.grad.zero_()
+        self._reset_groups()
+
+    def _reset_groups(self):
+        for g in self.groups:
+            g.ready = 0
+            g.launched = False
+        self._next_group = 0
 
     def _view(self, t, p):
         s = self.offsets[id(p)]
@@ -439,7 +657,7 @@ class PowerSGDOptimizer:
 
     def _bind(self):
         gmap = {id(p): p.grad for p in self.params}
-        key = tuple(g.data_ptr() for g in gmap.values())
+        key = (upload_epoch(),) + tuple(g.data_ptr() for g in gmap.values())
         if key == self._grad_key:
             return
         B = self.buf
@@ -471,22 +689,42 @@ class PowerSGDOptimizer:
             gen.manual_seed(int(self.rng.randint(1_000_000_000)))
             q.copy_(torch.randn(*q.shape, generator=gen, device=q.device, dtype=q.dtype))
 
+    def _ensure_queries(self):
+        """Draw the Q init once (reuse_query=True, reducer.py:101-111) or every step."""
+        if self._q_ready:
+            return
+        assert not capturing(), \
+            "run one eager step before capturing; reuse_query=False is not graph-capturable"
+        self._init_queries()
+        self._q_ready = True
+
     @property
     def bits_per_step(self) -> int:
         B = self.buf
         return 32 * (B.p_total + B.r1_numel + B.q_total)
 
+    @property
+    def collectives_per_step(self) -> int:
+        if not self.comm.active:
+            return 0
+        if self.overlap:
+            return 2 * len(self.groups) + (1 if self.r1_numel else 0)
+        return 2 if self.buf.shapes else 1
+
+    def check_errors(self):
+        """Host-synchronising health check (call at a low cadence: epoch / replica check):
+        raises on a timed-out MGS barrier or an asynchronous RCCL error."""
+        self.buf.check_orth()
+        self.comm.check()
+
     # -- the step --------------------------------------------------------------------------
-    # step() = phase_p -> comm_p -> phase_q -> comm_q -> phase_update.  The phases are
-    # exposed separately so a piecewise hipGraph can capture the compute phases and run
-    # the two collectives eagerly in between (utils/graph.py).
+    # Serial path: step() = phase_p -> comm_p -> phase_q -> comm_q -> phase_update.  The
+    # phases are exposed separately so a piecewise hipGraph can capture the compute phases
+    # and run the two collectives eagerly in between (utils/graph.py, c10d data plane).
     @torch.no_grad()
     def phase_p(self):
         B = self.buf
-        if self.step_count == 0 or not self.reuse_query:
-            assert not capturing(), \
-                "run one eager step before capturing; reuse_query=False is not graph-capturable"
-            self._init_queries()
+        self._ensure_queries()
         self._grads()
         if not self.native:
             return
@@ -505,7 +743,7 @@ class PowerSGDOptimizer:
         B = self.buf
         if self.native and B.shapes:
             X = ext()
-            B.orth(float(self.comm.world_size), self.eps)
+            B.orth(float(self.comm.world_size), self.eps, max_spins=self.orth_max_spins)
             X.psgd_q(B.geom, B.ptrs, B.q_items, B.comm_buf, B.q_part, B.max_rank)
             B.q_seg.run()
 
@@ -539,8 +777,16 @@ class PowerSGDOptimizer:
             return
         self.step_count += 1
         self.bits_communicated += self.bits_per_step
+        if not self.reuse_query:
+            self._q_ready = False
 
+    @torch.no_grad()
     def step(self) -> int:
+        if self.overlap:
+            self._finish_overlapped()
+            self._reset_groups()
+            self.count_step()
+            return self.bits_per_step
         self.phase_p()
         self.comm_p()
         self.phase_q()
@@ -549,9 +795,17 @@ class PowerSGDOptimizer:
         return self.bits_per_step
 
     def phases(self):
-        """[(fn, is_collective)] in execution order (for piecewise graph capture)."""
+        """[(fn, is_collective)] in execution order (for piecewise graph capture).  Piecewise
+        capture runs the collectives eagerly between segments, so the hooks are disabled."""
+        self.set_overlap(False)
         return [(self.phase_p, False), (self.comm_p, True), (self.phase_q, False), (self.comm_q, True),
                 (self.phase_update, False)]
+
+    def set_overlap(self, on: bool):
+        if on and not self.groups:
+            raise ValueError("optimizer was built without overlap groups")
+        self.overlap = on
+        self._reset_groups()
 
     def _step_torch(self, N, grads):
         B = self.buf
@@ -597,6 +851,27 @@ class PowerSGDOptimizer:
                     s = self.offsets[id(p)] - self.r1_start
                     gmap[id(p)].copy_(upd[s: s + p.numel()].view_as(p))
 
+    # -- training-state snapshot (graph warm-up must not change training) -------------------
+    def prepare(self):
+        """Draw the initial queries now (before a graph warm-up snapshot)."""
+        with torch.no_grad():
+            self._ensure_queries()
+
+    def snapshot(self):
+        return {"x": self.x.clone(), "e": self.e.clone(), "m": self.m.clone(), "q": self.buf.q_warm.clone(),
+                "step_count": self.step_count, "bits": self.bits_communicated, "q_ready": self._q_ready,
+                "rng": self.rng.get_state()}
+
+    def restore(self, snap):
+        self.x.copy_(snap["x"])
+        self.e.copy_(snap["e"])
+        self.m.copy_(snap["m"])
+        self.buf.q_warm.copy_(snap["q"])
+        self.step_count = snap["step_count"]
+        self.bits_communicated = snap["bits"]
+        self._q_ready = snap["q_ready"]
+        self.rng.set_state(snap["rng"])
+
     # -- checkpoint / resume ---------------------------------------------------------------
     def state_dict(self):
         return {
@@ -605,6 +880,7 @@ class PowerSGDOptimizer:
             "error": self.e.detach().cpu().clone(),
             "momentum": self.m.detach().cpu().clone(),
             "q_warm": self.buf.q_warm.detach().cpu().clone(),
+            "q_ready": self._q_ready,
             "rng_state": _rng_state_to_dict(self.rng.get_state()),
             "lr": self.lr,
             "momentum_coef": self.momentum,
@@ -618,6 +894,7 @@ class PowerSGDOptimizer:
         self.e.copy_(sd["error"])
         self.m.copy_(sd["momentum"])
         self.buf.q_warm.copy_(sd["q_warm"])
+        self._q_ready = bool(sd.get("q_ready", self.step_count > 0)) and self.reuse_query
         self.rng.set_state(_rng_state_from_dict(sd["rng_state"]))
         self.lr = float(sd["lr"])
         self.momentum = float(sd["momentum_coef"])

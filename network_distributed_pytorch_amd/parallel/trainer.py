@@ -4,7 +4,8 @@
 
 =================  ===========================================================================
 ``powersgd``       fused native engine (:class:`PowerSGDOptimizer`): EF + PowerSGD + momentum
-                   + SGD over flat arenas, 6 gfx950 launches + 2 collectives per step.
+                   + SGD over flat arenas; on a device the per-group pipelines (6 gfx950
+                   launches + 2 collectives each) overlap backward on the side stream.
 ``powersgd-ref``   reference semantics, eager per-tensor loops (ddp_init.py:149-178 with the
                    reducer's torch path) — the "eager reference" comparison arm.
 ``dense``          bucketed all-reduce overlapped with backward + fused SGD-momentum kernel.
@@ -31,7 +32,14 @@ class PowerSGDSync:
                                      random_seed=seed, comm=comm, **kw)
         b = powersgd_bytes_per_step(list(model.parameters()), rank)
         self.bytes_per_step = b["total"]
-        self.collectives_per_step = 2 if comm.active else 0
+
+    @property
+    def collectives_per_step(self):
+        return self.opt.collectives_per_step
+
+    @property
+    def comm(self):
+        return self.opt.comm
 
     def zero_grad(self):
         self.opt.zero_grad()
@@ -44,6 +52,18 @@ class PowerSGDSync:
 
     def count_step(self):
         self.opt.count_step()
+
+    def prepare(self):
+        self.opt.prepare()
+
+    def snapshot(self):
+        return self.opt.snapshot()
+
+    def restore(self, snap):
+        self.opt.restore(snap)
+
+    def check_errors(self):
+        self.opt.check_errors()
 
     def state_dict(self):
         return self.opt.state_dict()
@@ -115,7 +135,23 @@ class _DenseSync:
     def __init__(self, model, comm, lr, momentum, bucket_mb):
         self.ddp = BucketedDataParallel(model, comm, lr=lr, momentum=momentum, bucket_mb=bucket_mb)
         self.bytes_per_step = self.ddp.bytes_per_step
-        self.collectives_per_step = self.ddp.collectives_per_step
+
+    @property
+    def collectives_per_step(self):
+        return self.ddp.collectives_per_step
+
+    @property
+    def comm(self):
+        return self.ddp.comm
+
+    def snapshot(self):
+        return self.ddp.snapshot()
+
+    def restore(self, snap):
+        self.ddp.restore(snap)
+
+    def check_errors(self):
+        self.ddp.comm.check()
 
     def zero_grad(self):
         self.ddp.zero_grad()
@@ -137,7 +173,8 @@ class _DenseSync:
 
 
 def build_grad_sync(kind: str, model: torch.nn.Module, comm: Optional[Communicator] = None, lr: float = 1e-3,
-                    momentum: float = 0.9, rank: int = 4, bucket_mb: float = 25.0, seed: int = 714, **kw):
+                    momentum: float = 0.9, rank: int = 4, bucket_mb: Optional[float] = None, seed: int = 714,
+                    **kw):
     comm = comm if comm is not None else Communicator()
     if kind == "powersgd":
         return PowerSGDSync(model, comm, lr, momentum, rank, seed=seed, **kw)

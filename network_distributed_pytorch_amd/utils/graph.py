@@ -1,56 +1,100 @@
 """hipGraph step runner (HIP graphs instead of a tracing compiler).
 
-ResNet-18 on 32x32 inputs launches ~300 small kernels per training step; eager launch
+ResNet-18 on 32x32 inputs launches ~200 small kernels per training step; eager launch
 overhead leaves the GPU idle for ~25 % of the step (profiles/).  :class:`StepRunner`
 warms a training step up on a side stream (MIOpen find, RCCL communicator init, the
 native table uploads), then captures it and replays it every step:
 
-* ``full``      — forward + backward + the fused PowerSGD / SGD update (and, for N > 1,
-                  the collectives) in ONE graph;
+* ``full``      — the whole step (forward + backward + gradient sync + update) captured.
+                  With a stream-ordered data plane (native RCCL communicator, or world
+                  size 1) the sync's post-accumulate-grad hooks hand bucket / PowerSGD-group
+                  work (kernels AND collectives) to the communicator's side stream
+                  (``Communicator.side_launch``).  The step is then captured in SEGMENTS:
+                  at every side launch the compute graph being captured is closed and the
+                  next one begun (in the autograd thread, mid-backward), and the side work
+                  becomes its own comm graph.  Replay launches compute segment i, forks the
+                  side stream, launches comm graph i there, and so on; one join at the end.
+                  Every graph is linear (the HIP runtime executes a graph with parallel
+                  branches node by node over internal streams — measured 2.50 vs 2.13 ms per
+                  step), and each comm graph is enqueued as soon as its compute segment has
+                  been launched, not after the whole step graph (launching a ~200-node graph
+                  costs the host about as long as the GPU takes to run it, so a comm graph
+                  launched after one monolithic compute graph started ~1.3 ms late).
 * ``piecewise`` — the compute phases are captured, the collectives run eagerly between
-                  graph replays (``sync.phases()``): robust for RCCL at N > 1 while still
-                  removing every compute-kernel launch from the host path;
-* ``none``      — plain eager execution.
+                  graph replays (``sync.phases()``): the c10d data plane (``NDP_NATIVE_COMM=0``).
+* ``none``      — plain eager execution (gloo: its host thread blocks on collectives).
 
-``auto`` = ``full`` at world size 1, ``piecewise`` otherwise.  The step must read its
-inputs from static tensors (copy each batch into them before calling the runner).
-Requirements: all ops capture-safe (the native kernels and ``ops.upload`` are); PowerSGD
-needs ``reuse_query=True`` (the reference default) because the query re-draw is host-side.
+``auto`` = ``full`` when the sync's communicator is stream-ordered, ``piecewise`` for a
+c10d-nccl group, ``none`` for gloo / CPU.
+
+Warm-up does not change training: the sync's training state (parameters, error memory,
+momentum, warm-start Q, step counter — ``sync.snapshot()``) and any ``state_tensors``
+(e.g. BatchNorm running statistics) are saved before the warm-up steps and restored after
+capture, so the first replay is the first real step (graph mode used to apply
+``warmup`` extra optimizer updates to batch 0).
+
+The step must read its inputs from static tensors (copy each batch into them before
+calling the runner).  Requirements: all ops capture-safe (the native kernels and
+``ops.upload`` are); PowerSGD needs ``reuse_query=True`` (the reference default) because
+the query re-draw is host-side.
 """
 from __future__ import annotations
 
 import contextlib
+import gc
 import os
-from typing import Callable, List, Optional, Tuple
+import time
+from typing import Callable, List, Optional, Sequence, Tuple
 
 import torch
+import torch.distributed as dist
 
-from ..ops import _UPLOADS
+from ..ops import _UPLOADS, ext
 from ..parallel.comm import world_size
 
 # NDP_DEFER_UPLOADS=0: capture-time table uploads stay memcpy nodes re-run on every replay
 _DEFER_UPLOADS = os.environ.get("NDP_DEFER_UPLOADS", "1") != "0"
 
-__all__ = ["StepRunner", "GraphedStep"]
+__all__ = ["StepRunner", "GraphedStep", "auto_mode"]
+
+
+def auto_mode(sync) -> str:
+    """Pick the capture mode for a gradient-sync object (see module docstring)."""
+    if not torch.cuda.is_available():
+        return "none"
+    comm = getattr(sync, "comm", None)
+    if comm is None:
+        return "full" if world_size() <= 1 else "piecewise"
+    if getattr(comm, "stream_ordered", False):
+        return "full"
+    try:
+        backend = dist.get_backend(comm.group)
+    except Exception:
+        backend = "gloo"
+    return "piecewise" if backend == "nccl" else "none"
 
 
 class StepRunner:
     def __init__(self, pre: Callable[[], None], sync, mode: str = "auto", warmup: int = 3,
-                 post: Optional[Callable[[], None]] = None):
+                 post: Optional[Callable[[], None]] = None, state_tensors: Sequence[torch.Tensor] = ()):
         self.pre = pre
         self.sync = sync
         self.post = post or (lambda: None)
         if mode == "auto":
-            mode = "full" if world_size() <= 1 else "piecewise"
+            mode = auto_mode(sync)
         if not torch.cuda.is_available():
             mode = "none"
         self.mode = mode
         self.warmup = warmup
+        self.state_tensors = [t for t in state_tensors if t is not None]
         self.segments: List[Tuple[Callable[[], None], bool]] = self._segments()
         self.graphs: Optional[list] = None
         self._uploads: list = []
         self._upload_gen = 0
         self.replays = 0
+        self.side_graphs = []
+        self._comm = None
+        self.host_launch_s = [0.0, 0.0]  # host time inside replay() of compute / comm graphs
 
     def _segments(self):
         if self.mode in ("none", "full"):
@@ -81,7 +125,21 @@ class StepRunner:
         for fn, _ in self.segments:
             fn()
 
+    def _snapshot(self):
+        snap = self.sync.snapshot() if hasattr(self.sync, "snapshot") else None
+        return snap, [t.clone() for t in self.state_tensors]
+
+    def _restore(self, saved):
+        snap, tensors = saved
+        if snap is not None:
+            self.sync.restore(snap)
+        for t, s in zip(self.state_tensors, tensors):
+            t.copy_(s)
+
     def capture(self):
+        if hasattr(self.sync, "prepare"):
+            self.sync.prepare()  # e.g. draw PowerSGD's initial queries BEFORE the snapshot
+        saved = self._snapshot()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -89,23 +147,65 @@ class StepRunner:
                 self._run_eager()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+        # no cyclic GC while capturing: a collected graph / stream / event of an earlier
+        # runner would call a HIP API that is illegal during capture (abort in a destructor)
+        gc.collect()
+        gc_was_enabled = gc.isenabled()
+        gc.disable()
+        try:
+            self._capture_graphs()
+        finally:
+            if gc_was_enabled:
+                gc.enable()
+        self._restore(saved)  # warm-up steps leave no trace: the first replay is step 1
+        torch.cuda.synchronize()
+
+    def _capture_graphs(self):
         pool = torch.cuda.graph_pool_handle()
         graphs = []
+        comm = getattr(self.sync, "comm", None)
+        segmented = self.mode == "full" and comm is not None and hasattr(comm, "defer_side")
+        self.side_graphs = []
         scope = _UPLOADS.capture_scope() if _DEFER_UPLOADS else contextlib.nullcontext([])
         with scope as uploads:  # table uploads: applied once after capture, not per replay
-            for fn, cap in self.segments:
-                if cap:
+            if segmented:
+                # compute graph: forward + backward with an external event-record node at
+                # every side launch; comm graphs: wait node + the side work (one per launch)
+                (fn, _), = self.segments
+                side_items = []
+                with comm.defer_side(lambda: self._record_split(comm, side_items)) as items:
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g, pool=pool):
                         fn()
                     graphs.append(g)
-                else:
-                    graphs.append(None)
+                side_pool = torch.cuda.graph_pool_handle()
+                side_cap = torch.cuda.Stream()
+                gs = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gs, pool=side_pool, stream=side_cap):
+                    for i, item in enumerate(items):
+                        comm.wait_event(i)
+                        for f in item:
+                            f()
+                self.side_graphs.append(gs)
+                self._comm = comm
+            else:
+                for fn, cap in self.segments:
+                    if cap:
+                        g = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(g, pool=pool):
+                            fn()
+                        graphs.append(g)
+                    else:
+                        graphs.append(None)
         torch.cuda.synchronize()
         self._uploads = uploads
         self._upload_gen = _UPLOADS.generation
         self.graphs = graphs
-        # the first replay below is the first real step after capture
+
+    @staticmethod
+    def _record_split(comm, _items):
+        comm.record_event(len(comm._deferred))
+        return True
 
     def __call__(self):
         if self.mode == "none":
@@ -115,11 +215,25 @@ class StepRunner:
             self.capture()
         # an eager step since capture may have re-bound a table the graph reads
         self._upload_gen = _UPLOADS.ensure(self._uploads, self._upload_gen)
-        for (fn, _), g in zip(self.segments, self.graphs):
-            if g is None:
-                fn()
-            else:
-                g.replay()
+        if self.side_graphs:
+            comm = self._comm
+            t0 = time.perf_counter()
+            self.graphs[0].replay()
+            t1 = time.perf_counter()
+            with comm.on_side():
+                self.side_graphs[0].replay()  # its wait nodes order it after the record nodes
+            t2 = time.perf_counter()
+            comm.join()
+            self.host_launch_s[0] += t1 - t0
+            self.host_launch_s[1] += t2 - t1
+        else:
+            t0 = time.perf_counter()
+            for (fn, _), g in zip(self.segments, self.graphs):
+                if g is None:
+                    fn()
+                else:
+                    g.replay()
+            self.host_launch_s[0] += time.perf_counter() - t0
         self.replays += 1
         count = getattr(self.sync, "count_step", None)
         if count is not None:  # host bookkeeping skipped by the replayed Python

@@ -7,19 +7,27 @@ box with the snapshot; nothing is installed into site-packages).
 """
 import os
 
+import torch
 from setuptools import find_packages, setup
 from torch.utils.cpp_extension import BuildExtension, CUDAExtension
 
 os.environ.setdefault("PYTORCH_ROCM_ARCH", "gfx950")
 
 CSRC = os.path.join("network_distributed_pytorch_amd", "csrc")
-SOURCES = [os.path.join(CSRC, f) for f in ("bindings.cpp", "plan.cpp", "powersgd.hip", "orth.hip", "multitensor.hip", "batchnorm.hip", "attention.hip",
-                                                "conv.hip", "pool.hip")]
+SOURCES = [os.path.join(CSRC, f) for f in ("bindings.cpp", "plan.cpp", "comm.cpp", "powersgd.hip", "orth.hip",
+                                                "multitensor.hip", "batchnorm.hip", "attention.hip", "conv.hip",
+                                                "pool.hip")]
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+# RCCL: link the copy torch already loads (SONAME librccl.so.1), so the process holds ONE
+# RCCL whether c10d or the native communicator (csrc/comm.cpp) creates a communicator
+TORCH_LIB = os.path.join(os.path.dirname(torch.__file__), "lib")
 
 ext = CUDAExtension(
     name="network_distributed_pytorch_amd._C",
     sources=SOURCES,
-    include_dirs=[os.path.abspath(CSRC)],
+    include_dirs=[os.path.abspath(CSRC), os.path.join(ROCM, "include")],
+    library_dirs=[TORCH_LIB],
+    libraries=["rccl"],
     extra_compile_args={
         "cxx": ["-O3", "-std=c++17"],
         "nvcc": ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=fast"],
