@@ -19,6 +19,7 @@
 #include <torch/extension.h>
 #include <rccl/rccl.h>
 
+#include <cstdlib>
 #include <memory>
 #include <string>
 #include <vector>
@@ -197,15 +198,15 @@ hipStream_t cur() { return at::hip::getCurrentHIPStream().stream(); }
 // run it.  Hence the segmented capture in utils/graph.py.
 class SideStream {
  public:
-  explicit SideStream(int device) : device_(device) {
+  SideStream(int device, bool high_priority) : device_(device) {
     NDP_HIP_CHECK(hipSetDevice(device));
     int lo = 0, hi = 0;
     NDP_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    // highest priority: reducer / collective work issued mid-backward is dispatched ahead
-    // of the compute stream's queued workgroups, which shortens the post-backward tail
-    NDP_HIP_CHECK(hipStreamCreateWithPriority(&side_, hipStreamNonBlocking, hi));
+    // high priority: reducer / collective work issued mid-backward is dispatched ahead of
+    // the compute stream's queued workgroups, which shortens the post-backward tail
+    NDP_HIP_CHECK(hipStreamCreateWithPriority(&side_, hipStreamNonBlocking, high_priority ? hi : lo));
     ring_.resize(kRing);
-    for (auto& e : ring_) NDP_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto& e : ring_) NDP_HIP_CHECK(hipEventCreateWithFlags(&e, event_flags()));
   }
   ~SideStream() {
     for (auto& e : ring_) (void)hipEventDestroy(e);
@@ -254,6 +255,10 @@ class SideStream {
 
  private:
   static constexpr int kRing = 64;
+  static unsigned event_flags() {
+    const char* v = std::getenv("NDP_EVENT_FLAGS");
+    return v ? (unsigned)std::atoi(v) : hipEventDisableTiming;
+  }
   static void insert_node(hipStream_t s, hipEvent_t e, bool record) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     unsigned long long id = 0;
@@ -278,7 +283,7 @@ class SideStream {
     TORCH_CHECK(i >= 0 && i < 4096, "SideStream: event index out of range");
     while ((int)named_.size() <= i) {
       hipEvent_t e;
-      NDP_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      NDP_HIP_CHECK(hipEventCreateWithFlags(&e, event_flags()));
       named_.push_back(e);
     }
     return named_[i];
@@ -328,7 +333,7 @@ void register_comm(py::module& m) {
       .def("destroy", &RcclComm::destroy)
       .def_property_readonly("alive", &RcclComm::alive);
   py::class_<SideStream, std::shared_ptr<SideStream>>(m, "SideStream")
-      .def(py::init<int>(), py::arg("device"))
+      .def(py::init<int, bool>(), py::arg("device"), py::arg("high_priority") = true)
       .def_property_readonly("handle", &SideStream::handle)
       .def_property_readonly("device", &SideStream::device)
       .def("fork", &SideStream::fork, py::arg("from_stream") = 0)

@@ -47,8 +47,9 @@ def default_config(**over) -> Dict[str, Any]:
         learning_rate=1e-3, momentum=0.9, nesterov=False, training_epochs=1, batch_size=32, reducer_rank=4,
         # additions
         task="cifar", model="resnet18", num_classes=1000, global_batch=512, grad_sync="powersgd",
-        dataset_size=None, data_seed=0, max_steps_per_epoch=None, graph_mode="none", link="none",
-        bucket_mb=None, checkpoint_dir=None, resume=None, log_file=None, check_replicas_every=0,
+        dataset_size=None, data_seed=0, max_steps_per_epoch=None, graph_mode="auto", link="none",
+        emulate_world=None, bucket_mb=None, reuse_query=True, overlap=None, psgd_groups=None,
+        checkpoint_dir=None, resume=None, log_file=None, log_every=1, check_replicas_every=0,
         write_grad=False, verbose=True, trace_phases=False,
     )
     cfg.update(over)
@@ -170,12 +171,9 @@ def run_task(config) -> Dict[str, Any]:
     device = device_for(config)
     world, rank = _world()
     part, bsz, _val = _build_data(config, device, world, rank)
-    graph_mode = config.get("graph_mode", "none")
+    graph_mode = config.get("graph_mode", "auto")
     if device.type != "cuda":
         graph_mode = "none"
-    loader = DeviceLoader(part, bsz, shuffle=True, seed=config["seed"] + rank, device=device,
-                          drop_last=graph_mode != "none")
-    num_batches = math.ceil(len(part) / float(bsz))
 
     model_name = config["model"] if config["task"] != "imdb" else "distilbert"
     if config["task"] == "mlp":
@@ -183,17 +181,29 @@ def run_task(config) -> Dict[str, Any]:
     model = build_model(model_name, config["num_classes"] if config["task"] != "imdb" else 2).to(device)
     crit = torch.nn.CrossEntropyLoss().to(device)
     link = None if config.get("link", "none") == "none" else LINK_PRESETS[config["link"]]
-    comm = Communicator(link=link)
+    comm = Communicator(link=link, emulate_world=config.get("emulate_world"),
+                        device=device if device.type == "cuda" else None)
+    extra = {}
+    if config["grad_sync"] == "powersgd":
+        extra = {"write_grad": config.get("write_grad", False), "reuse_query": config.get("reuse_query", True),
+                 "overlap": config.get("overlap"), "groups": config.get("psgd_groups")}
+        if not extra["reuse_query"]:
+            graph_mode = "none"  # the per-step query re-draw is host-side (not capturable)
     sync = build_grad_sync(config["grad_sync"], model, comm, lr=config["learning_rate"],
                            momentum=config["momentum"], rank=config["reducer_rank"],
-                           bucket_mb=config.get("bucket_mb"), seed=config["seed"],
-                           **({"write_grad": config.get("write_grad", False)} if config["grad_sync"] == "powersgd" else {}))
+                           bucket_mb=config.get("bucket_mb"), seed=config["seed"], **extra)
     start_epoch = 0
+    step = 0
     if config.get("resume"):
         info = load_checkpoint(config["resume"], model, sync)
         start_epoch = info["epoch"] + 1
-        loader.set_epoch(start_epoch)
-    logger = JsonlLogger(config.get("log_file"), rank)
+        step = info["step"]
+    log_path = config.get("log_file")
+    if log_path and "{rank}" in log_path:  # one file per rank
+        logger = JsonlLogger(log_path.format(rank=rank), rank, all_ranks=True)
+    else:
+        logger = JsonlLogger(log_path, rank)
+    log_every = int(config.get("log_every") or 0) if logger.enabled else 0
     flat = getattr(getattr(sync, "opt", None), "x", None)
     if flat is None:
         flat = getattr(getattr(sync, "ddp", None), "x", None)
@@ -213,13 +223,21 @@ def run_task(config) -> Dict[str, Any]:
             loss = loss_fn(static["batch"])
             loss.backward()
             loss_static.copy_(loss.detach())
-        runner = StepRunner(pre, sync, mode=graph_mode)
+        runner = StepRunner(pre, sync, mode=graph_mode, state_tensors=list(model.buffers()))
+        graph_mode = runner.mode
+        if graph_mode == "none":
+            runner = None
+    # a captured step needs a fixed batch shape: drop the ragged last batch in graph mode
+    loader = DeviceLoader(part, bsz, shuffle=True, seed=config["seed"] + rank, device=device,
+                          drop_last=runner is not None)
+    loader.set_epoch(start_epoch)
+    num_batches = math.ceil(len(part) / float(bsz))
 
     timer = PhaseTimer() if (config.get("trace_phases") and runner is None) else None
     losses = []
-    step = 0
     t_start = time.perf_counter()
     samples = 0
+    last_log = (time.perf_counter(), comm.stats.payload_bytes, comm.stats.wire_bytes, step)
     for epoch in range(start_epoch, config["training_epochs"]):
         _log(config, ">>>>> Rank ", rank, ", epoch ", epoch, " Started...")
         epoch_loss = torch.zeros((), device=device, dtype=torch.float64)
@@ -259,7 +277,24 @@ def run_task(config) -> Dict[str, Any]:
             samples += bsz * world
             if checker is not None:
                 checker.check(step)
+            if log_every and step % log_every == 0:  # per-step record (host sync at this cadence)
+                loss_now = float((loss_static if runner is not None else loss.detach()).item())
+                now = time.perf_counter()
+                t_prev, pay_prev, wire_prev, step_prev = last_log
+                n = max(1, step - step_prev)
+                logger.log(kind="step", epoch=epoch, step=step, loss=loss_now,
+                           step_ms=1e3 * (now - t_prev) / n,
+                           samples_per_s=bsz * world * n / max(now - t_prev, 1e-9),
+                           payload_bytes=(comm.stats.payload_bytes - pay_prev) / n
+                           if runner is None or graph_mode == "piecewise" else getattr(sync, "bytes_per_step", None),
+                           wire_bytes=(comm.stats.wire_bytes - wire_prev) / n
+                           if runner is None or graph_mode == "piecewise" else
+                           _ring_wire(getattr(sync, "bytes_per_step", 0) or 0, comm.paced_world),
+                           bytes_per_step=getattr(sync, "bytes_per_step", None))
+                last_log = (now, comm.stats.payload_bytes, comm.stats.wire_bytes, step)
         mean = float(epoch_loss.item()) / max(1, i)
+        if hasattr(sync, "check_errors"):
+            sync.check_errors()  # MGS barrier timeouts / RCCL async errors (epoch cadence)
         losses.append(mean)
         if config.get("verbose", True):
             print_epoch(rank, epoch, mean)
@@ -268,21 +303,32 @@ def run_task(config) -> Dict[str, Any]:
                    bytes_per_step=getattr(sync, "bytes_per_step", None), comm=comm.stats.as_dict(),
                    phase_ms=timer.summary() if timer is not None else None)
         if config.get("checkpoint_dir"):
-            save_checkpoint(os.path.join(config["checkpoint_dir"], "last.pt"), model, sync, epoch=epoch, step=step)
+            save_checkpoint(os.path.join(config["checkpoint_dir"], "last.pt"), model, sync, epoch=epoch, step=step,
+                            rank=rank, world=world)
     if device.type == "cuda":
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     _log(config, "All Task Finished")
     _log(config, "==============================\n")
+    flat = getattr(getattr(sync, "opt", None), "x", None)
+    if flat is None:
+        flat = getattr(getattr(sync, "ddp", None), "x", None)
+    if flat is None:
+        flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
     summary = {"epoch_losses": losses, "steps": step, "elapsed_s": elapsed,
                "samples_per_s": samples / elapsed if elapsed > 0 else None,
                "bytes_per_step": getattr(sync, "bytes_per_step", None), "comm": comm.stats.as_dict(),
-               "world_size": world, "per_rank_batch": bsz, "graph_mode": graph_mode}
+               "comm_backend": comm.backend, "world_size": world, "per_rank_batch": bsz, "graph_mode": graph_mode,
+               "param_checksum": float(flat.double().sum().item())}
     logger.log(kind="summary", **{k: v for k, v in summary.items()})
     logger.close()
     summary["model"] = model
     summary["sync"] = sync
     return summary
+
+
+def _ring_wire(payload: int, n: int) -> float:
+    return 0.0 if n <= 1 else 2.0 * (n - 1) / n * payload
 
 
 def _clone_batch(b):

@@ -155,6 +155,7 @@ class _StreamWork:
         return True
 
 
+_DEBUG_SIDE = os.environ.get("NDP_DEBUG_SIDE") == "1"
 _SIDE_LINKS = {}
 _KEEPALIVE = []
 
@@ -166,7 +167,7 @@ def _side_link(device_index: int):
     if device_index not in _SIDE_LINKS:
         from ..ops import ext
 
-        link = ext().SideStream(device_index)
+        link = ext().SideStream(device_index, os.environ.get("NDP_SIDE_PRIORITY", "high") == "high")
         _SIDE_LINKS[device_index] = (link, torch.cuda.ExternalStream(link.handle,
                                                                       device=torch.device("cuda", device_index)))
     return _SIDE_LINKS[device_index]
@@ -304,6 +305,11 @@ class Communicator:
         closed (the split callback) and ``fn`` is kept, to be captured as its own comm
         graph that the runner launches on the side stream right after that segment."""
         if self._deferred is not None:
+            if _DEBUG_SIDE:
+                from ..ops import ext
+                print(f"[side_launch] item={len(self._deferred)} stream={torch.cuda.current_stream()} "
+                      f"capturing={torch.cuda.is_current_stream_capturing()} "
+                      f"nodes={ext().capture_node_count()}", flush=True)
             if self._split() or not self._deferred:
                 self._deferred.append([fn])
             else:  # nothing was captured since the last split: same comm graph

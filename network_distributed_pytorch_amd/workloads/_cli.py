@@ -6,7 +6,9 @@ workload — quirk Q12 fixed: the CIFAR scripts hard-code ``n_workers = 4``, whi
 default).  Additions: ``-spawn`` launches all ranks locally (127.0.0.1 rendezvous),
 ``-epochs``, ``-steps`` (max steps per epoch), ``-model``, ``-grad_sync``, ``-rank_r``
 (PowerSGD rank), ``-batch`` (global batch), ``-graph_mode``, ``-link``, ``-backend``,
-``-checkpoint_dir``, ``-resume``, ``-log_file``, ``-dataset_size``, ``-check_replicas``.
+``-checkpoint_dir``, ``-resume``, ``-log_file`` (``{rank}`` in the path = one file per rank),
+``-log_every``, ``-dataset_size``, ``-check_replicas``, ``-bucket_mb``, ``-reuse_query``,
+``-overlap``, ``-psgd_groups``, ``-emulate_world``.
 """
 from __future__ import annotations
 
@@ -42,6 +44,15 @@ def build_parser(default_world: int, world_required: bool = False) -> argparse.A
     p.add_argument("-dataset_size", type=int, default=None)
     p.add_argument("-check_replicas", type=int, default=None, help="replica checksum every N steps")
     p.add_argument("-toy_steps", type=int, default=None, help="ddp_guide: toy-MLP dense-DP steps")
+    p.add_argument("-bucket_mb", type=float, default=None, help="dense arm: all-reduce bucket size (MB)")
+    p.add_argument("-reuse_query", type=int, default=None, choices=[None, 0, 1],
+                   help="PowerSGD warm-start query (reducer.py reuse_query; 0 redraws Q every step)")
+    p.add_argument("-overlap", type=int, default=None, choices=[None, 0, 1],
+                   help="launch the gradient sync from grad hooks during backward (default 1 on GPU)")
+    p.add_argument("-psgd_groups", type=int, default=None, help="PowerSGD overlap groups")
+    p.add_argument("-emulate_world", type=int, default=None, help="link emulation: charge an N-rank ring")
+    p.add_argument("-log_every", type=int, default=None, help="per-step JSONL record cadence (0 = off)")
+    p.add_argument("-seq_len", type=int, default=None, help="DistilBERT sequence length (reference 512)")
     p.add_argument("-trace", action="store_true", help="per-phase HIP-event timings into the JSONL log")
     p.add_argument("-quiet", action="store_true")
     return p
@@ -51,7 +62,9 @@ _MAP = {"epochs": "training_epochs", "steps": "max_steps_per_epoch", "model": "m
         "grad_sync": "grad_sync", "rank_r": "reducer_rank", "batch": "global_batch", "lr": "learning_rate",
         "graph_mode": "graph_mode", "link": "link", "backend": "distributed_backend",
         "checkpoint_dir": "checkpoint_dir", "resume": "resume", "log_file": "log_file",
-        "dataset_size": "dataset_size", "check_replicas": "check_replicas_every", "toy_steps": "toy_mlp_steps"}
+        "dataset_size": "dataset_size", "check_replicas": "check_replicas_every", "toy_steps": "toy_mlp_steps",
+        "bucket_mb": "bucket_mb", "psgd_groups": "psgd_groups", "emulate_world": "emulate_world",
+        "log_every": "log_every", "seq_len": "seq_len"}
 
 
 def apply_args(ddp_init: ModuleType, args, rank: int, world: int, cuda: Optional[int]):
@@ -67,6 +80,10 @@ def apply_args(ddp_init: ModuleType, args, rank: int, world: int, cuda: Optional
         v = getattr(args, a)
         if v is not None:
             c[k] = v
+    if args.reuse_query is not None:
+        c["reuse_query"] = bool(args.reuse_query)
+    if args.overlap is not None:
+        c["overlap"] = bool(args.overlap)
     if args.quiet:
         c["verbose"] = False
     if args.trace:

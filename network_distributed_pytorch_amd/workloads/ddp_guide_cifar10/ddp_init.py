@@ -33,7 +33,7 @@ config = dict(
     num_classes=1000,
     global_batch=256,
     grad_sync="dense",
-    graph_mode="none",
+    graph_mode="auto",  # hipGraph on GPU (full / piecewise by data plane), eager on CPU
 )
 
 

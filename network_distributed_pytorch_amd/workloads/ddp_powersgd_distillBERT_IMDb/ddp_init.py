@@ -34,7 +34,7 @@ config = dict(
     global_batch=None,  # None -> 16 * world (reference)
     seq_len=512,
     grad_sync="powersgd",
-    graph_mode="none",
+    graph_mode="auto",  # hipGraph on GPU (full / piecewise by data plane), eager on CPU
 )
 
 

@@ -35,7 +35,7 @@ config = dict(
     num_classes=1000,
     global_batch=512,
     grad_sync="powersgd",
-    graph_mode="none",
+    graph_mode="auto",  # hipGraph on GPU (full / piecewise by data plane), eager on CPU
 )
 
 

@@ -1,6 +1,6 @@
 """GPU probe: when do comm-graph event-wait nodes resolve against compute-graph record nodes?
-Compute graph: 12 x 100 us delay kernels, record events after kernels 3, 6, 9.
-Comm graph: wait e_i -> tiny delay kernel (10+i us).  Run under rocprofv3 --kernel-trace."""
+Compute graph: N delay kernels of D us, records after kernels in RECS.
+Comm graph: wait e_i -> tiny delay kernel.  Run under rocprofv3 --kernel-trace."""
 import os
 import sys
 import time
@@ -13,31 +13,51 @@ from network_distributed_pytorch_amd.parallel.comm import Communicator  # noqa: 
 
 
 def main():
+    n, d = int(sys.argv[1]), int(sys.argv[2])
+    recs = [int(x) for x in sys.argv[3].split(",")]
+    mode = sys.argv[4] if len(sys.argv) > 4 else "graph"
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     comm = Communicator(device=dev)
-    gM, gS = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-    with torch.cuda.graph(gM):
-        for k in range(12):
-            delay_ns(100_000 + 1000 * k)
-            if k in (3, 6, 9):
-                comm.record_event(k // 3 - 1)
-    with torch.cuda.graph(gS, stream=torch.cuda.Stream()):
-        for i in range(3):
+    x = torch.zeros(1 << 20, device=dev)
+
+    def body_m():
+        for k in range(n):
+            delay_ns(d * 1000)
+            if k % 7 == 3:
+                x.add_(1.0)  # a torch elementwise kernel
+            if k in recs:
+                comm.record_event(recs.index(k))
+
+    def body_s():
+        for i in range(len(recs)):
             comm.wait_event(i)
-            delay_ns(10_000 + 1000 * i)
+            delay_ns(3000 + 1000 * i)
+
+    if mode == "graph":
+        gM, gS = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gM):
+            body_m()
+        with torch.cuda.graph(gS, stream=torch.cuda.Stream()):
+            body_s()
+
+        def step():
+            gM.replay()
+            with comm.on_side():
+                gS.replay()
+            comm.join()
+    else:
+        def step():
+            body_m()
+            with comm.on_side():
+                body_s()
+            comm.join()
     for _ in range(5):
-        gM.replay()
-        with comm.on_side():
-            gS.replay()
-        comm.join()
+        step()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(10):
-        gM.replay()
-        with comm.on_side():
-            gS.replay()
-        comm.join()
+        step()
     torch.cuda.synchronize()
     print("ms/step", (time.perf_counter() - t0) / 10 * 1e3, flush=True)
 
