@@ -307,6 +307,11 @@ def main(argv=None):
                 "fused_attention": (not args.no_fused_attn) if is_bert else None,
             },
             "comm_stats_timed": comm_stats,
+            "collective_payloads": wl.sync.collective_payloads() if hasattr(wl.sync, "collective_payloads") else None,
+            "link_model_s_per_step": (sum(wl.comm.link.seconds(b, wl.comm.paced_world)
+                                          for b in wl.sync.collective_payloads())
+                                      if wl.comm.link is not None and hasattr(wl.sync, "collective_payloads")
+                                      else None),
             "mean_loss": round(final_loss, 5),
         }
         if weak is not None:

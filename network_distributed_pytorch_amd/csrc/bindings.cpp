@@ -367,6 +367,24 @@ void delay_ns(int64_t ns) {
   check_launch("launch_delay_ns");
 }
 
+// flags: int32 device tensor; indices are element offsets
+void flag_signal(torch::Tensor flags, int64_t i) {
+  check_dev(flags, "flags");
+  TORCH_CHECK(flags.scalar_type() == torch::kInt32 && i >= 0 && i < flags.numel(), "flag_signal: bad flag");
+  ndp::launch_flag_signal(reinterpret_cast<unsigned*>(flags.data_ptr<int32_t>()) + i, cur_stream());
+  check_launch("launch_flag_signal");
+}
+
+void flag_wait(torch::Tensor flags, int64_t i, int64_t seen, int64_t err, int64_t max_spins) {
+  check_dev(flags, "flags");
+  TORCH_CHECK(flags.scalar_type() == torch::kInt32 && i >= 0 && i < flags.numel() && seen >= 0 &&
+                  seen < flags.numel() && err >= 0 && err < flags.numel(),
+              "flag_wait: bad flag indices");
+  auto* f = reinterpret_cast<unsigned*>(flags.data_ptr<int32_t>());
+  ndp::launch_flag_wait(f + i, f + seen, f + err, (unsigned)max_spins, cur_stream());
+  check_launch("launch_flag_wait");
+}
+
 void checksum(torch::Tensor x, torch::Tensor out) {
   check_f32(x, "x");
   check_dev(out, "out");
@@ -562,6 +580,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("checksum", &checksum);
+  m.def("flag_signal", &flag_signal);
+  m.def("flag_wait", &flag_wait);
   m.def("toeplitz_expand", &toeplitz_expand);
   m.def("toeplitz_fold", &toeplitz_fold);
   m.def("conv_plan", &conv_plan);

@@ -124,6 +124,46 @@ __global__ void delay_kernel(int64_t ticks) {
   while ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) < ticks) __builtin_amdgcn_s_sleep(8);
 }
 
+// ---- device-flag ordering between the compute and comm graphs (utils/graph.py) -------
+// A cross-queue hipEvent wait is re-evaluated late when the producing queue runs a long
+// train of short kernels (measured: comm-graph work started only after the whole compute
+// graph).  Instead, the compute graph bumps a counter with one single-lane kernel and the
+// comm graph's first kernel of each piece spins on it (agent-scope acquire, s_sleep), so
+// the comm queue reacts within microseconds.  Each wait consumes exactly one bump
+// (`seen` is private to the waiting queue), so the same captured graphs replay forever.
+// A bounded spin reports through `err` instead of hanging (e.g. if both streams ever
+// shared one hardware queue).
+__global__ void flag_signal_kernel(unsigned* ctr) {
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__global__ void flag_wait_kernel(unsigned* ctr, unsigned* seen, unsigned* err, unsigned max_spins) {
+  if (threadIdx.x == 0) {
+    const unsigned want = __hip_atomic_load(seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    unsigned spins = 0;
+    while ((int)(__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > max_spins) {
+        __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __hip_atomic_store(seen, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+}
+
+void launch_flag_signal(unsigned* ctr, hipStream_t s) {
+  hipLaunchKernelGGL(flag_signal_kernel, dim3(1), dim3(64), 0, s, ctr);
+}
+
+void launch_flag_wait(unsigned* ctr, unsigned* seen, unsigned* err, unsigned max_spins, hipStream_t s) {
+  hipLaunchKernelGGL(flag_wait_kernel, dim3(1), dim3(64), 0, s, ctr, seen, err, max_spins);
+}
+
 constexpr int kCkBlocks = 256;
 
 __global__ __launch_bounds__(256) void checksum_partial_kernel(const float* __restrict__ x,

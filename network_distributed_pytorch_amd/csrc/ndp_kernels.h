@@ -99,6 +99,10 @@ void launch_sgd_momentum(float* x, const float* g, float* buf, int64_t n, float 
 void launch_add(const float* a, const float* b, float* out, int64_t n, hipStream_t s);
 // spin the stream for `ns` nanoseconds of wall time (link-emulation pacing)
 void launch_delay_ns(int64_t ns, hipStream_t s);
+// device-flag ordering between two queues: signal bumps *ctr; wait spins until *ctr has
+// been bumped once more than *seen records (then records it); err |= 1 on spin timeout
+void launch_flag_signal(unsigned* ctr, hipStream_t s);
+void launch_flag_wait(unsigned* ctr, unsigned* seen, unsigned* err, unsigned max_spins, hipStream_t s);
 // deterministic fp64-accumulated checksum of a flat buffer (replica divergence detector)
 void launch_checksum(const float* x, int64_t n, double* out, hipStream_t s);
 

@@ -276,6 +276,8 @@ def run_task(config) -> Dict[str, Any]:
             step += 1
             samples += bsz * world
             if checker is not None:
+                if runner is not None and step % checker.every == 0:
+                    runner.join()
                 checker.check(step)
             if log_every and step % log_every == 0:  # per-step record (host sync at this cadence)
                 loss_now = float((loss_static if runner is not None else loss.detach()).item())
@@ -292,6 +294,8 @@ def run_task(config) -> Dict[str, Any]:
                            _ring_wire(getattr(sync, "bytes_per_step", 0) or 0, comm.paced_world),
                            bytes_per_step=getattr(sync, "bytes_per_step", None))
                 last_log = (now, comm.stats.payload_bytes, comm.stats.wire_bytes, step)
+        if runner is not None:
+            runner.join()  # parameters / sync state are read below (checks, checkpoint)
         mean = float(epoch_loss.item()) / max(1, i)
         if hasattr(sync, "check_errors"):
             sync.check_errors()  # MGS barrier timeouts / RCCL async errors (epoch cadence)

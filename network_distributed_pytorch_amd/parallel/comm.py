@@ -12,8 +12,8 @@ MI355X design:
     ``ncclCommInitRank``, and collectives are enqueued straight onto a HIP stream: the
     framework-owned high-priority side stream (``csrc/comm.cpp`` SideStream), ordered
     against the compute stream with hipEvents (:meth:`Communicator.side_launch`), so
-    bucket / PowerSGD-group work overlaps backward — eagerly, or as comm graphs launched
-    between the segments of a captured step (utils/graph.py).  c10d (``ProcessGroupNCCL`` = RCCL, or gloo for
+    bucket / PowerSGD-group work overlaps backward — eagerly, or as the comm graph of a
+    captured step, ordered against the compute graph by device flags (utils/graph.py).  c10d (``ProcessGroupNCCL`` = RCCL, or gloo for
     CPU tests) is the fallback data plane.
   * every collective is accounted (calls, payload bytes, modelled ring wire bytes
     2(N-1)/N * S) so the bytes/step metric is measured, not only derived;
@@ -155,7 +155,9 @@ class _StreamWork:
         return True
 
 
-_DEBUG_SIDE = os.environ.get("NDP_DEBUG_SIDE") == "1"
+_MAX_FLAGS = 256
+_DONE, _ERR = 2 * _MAX_FLAGS, 2 * _MAX_FLAGS + 2
+_SPINS = 1 << 25  # ~2 s of s_sleep 2 before a wait reports a timeout instead of hanging
 _SIDE_LINKS = {}
 _KEEPALIVE = []
 
@@ -225,7 +227,7 @@ class Communicator:
         self._native = None
         self._side = None
         self._deferred = None
-        self._split = None
+        self._flags = None
         self._captured = False
         self._device = device
         if native is not False and self.active:
@@ -300,51 +302,73 @@ class Communicator:
 
     def side_launch(self, fn):
         """Run ``fn`` (kernels + collectives) on the side stream after the work enqueued so
-        far on the current stream.  Eagerly: event fork + run.  While a step is being
-        captured in segments (:meth:`defer_side`): the current compute-graph segment is
-        closed (the split callback) and ``fn`` is kept, to be captured as its own comm
-        graph that the runner launches on the side stream right after that segment."""
+        far on the current stream.  Eagerly: hipEvent fork + run.  While a step is being
+        captured (:meth:`defer_side`): a device-flag signal kernel goes into the compute
+        graph and ``fn`` is kept, to be captured into the comm graph behind a matching
+        device-flag wait (:meth:`graph_wait`)."""
         if self._deferred is not None:
-            if _DEBUG_SIDE:
-                from ..ops import ext
-                print(f"[side_launch] item={len(self._deferred)} stream={torch.cuda.current_stream()} "
-                      f"capturing={torch.cuda.is_current_stream_capturing()} "
-                      f"nodes={ext().capture_node_count()}", flush=True)
-            if self._split() or not self._deferred:
-                self._deferred.append([fn])
-            else:  # nothing was captured since the last split: same comm graph
-                self._deferred[-1].append(fn)
+            i = len(self._deferred)
+            assert i < _MAX_FLAGS, "too many side launches in one captured step"
+            self._flag_ext().flag_signal(self._flag_buf(), i)
+            self._deferred.append([fn])
             return
         self.fork()
         with self.on_side():
             fn()
 
     def side_join(self):
-        """Current stream waits for the side stream (deferred in segmented capture: the
-        runner joins after launching the last comm graph)."""
+        """Current stream waits for the side stream (skipped while capturing the compute
+        graph: the comm graph signals the next step's compute graph through a flag)."""
         if self._deferred is None:
             self.join()
 
-    def record_event(self, i: int):
-        """Numbered event recorded on the current stream (an event-record node if capturing)."""
-        self._link()[0].record(i)
-
-    def wait_event(self, i: int):
-        """Current stream waits on numbered event i (an event-wait node if capturing)."""
-        self._link()[0].wait(i)
-
     @contextlib.contextmanager
-    def defer_side(self, split):
-        """Segmented-capture scope: ``split()`` is called at every side launch; it ends the
-        compute-graph segment being captured and begins the next, returning False (and
-        splitting nothing) if the segment is still empty.  Yields the list that collects
-        the side work: one list of callables per comm graph."""
+    def defer_side(self):
+        """Capture scope of the compute graph: yields the list that collects the side work
+        (one list of callables per signal)."""
         assert self._deferred is None, "nested defer_side"
-        self._deferred, self._split = [], split
+        self._flag_buf()  # allocate NOW: inside a capture it would come from the graph's pool
+        self._deferred = []
         try:
             yield self._deferred
         finally:
-            self._deferred, self._split = None, None
+            self._deferred = None
+
+    # device-flag protocol between the compute graph (current stream) and the comm graph
+    # (side stream); csrc/multitensor.hip flag_signal / flag_wait.  Layout of the int32
+    # flag buffer: [0, MAX) signal counters, [MAX, 2 MAX) their "seen" words, then
+    # DONE counter, DONE seen, error word.
+    def _flag_ext(self):
+        from ..ops import ext
+        return ext()
+
+    def _flag_buf(self):
+        if self._flags is None:
+            assert not torch.cuda.is_current_stream_capturing(), "flag buffer must exist before capture"
+            dev = self._device or torch.device("cuda", torch.cuda.current_device())
+            self._flags = torch.zeros(2 * _MAX_FLAGS + 3, dtype=torch.int32, device=dev)
+        return self._flags
+
+    def graph_prologue(self):
+        """First node of the compute graph: wait until the previous step's comm graph is done."""
+        self._flag_ext().flag_wait(self._flag_buf(), _DONE, _DONE + 1, _ERR, _SPINS)
+
+    def graph_wait(self, i: int):
+        """Comm graph: wait for the compute graph's i-th signal."""
+        self._flag_ext().flag_wait(self._flag_buf(), i, _MAX_FLAGS + i, _ERR, _SPINS)
+
+    def graph_epilogue(self):
+        """Last node of the comm graph: release the next step's compute graph."""
+        self._flag_ext().flag_signal(self._flag_buf(), _DONE)
+
+    def reset_flags(self):
+        """Before the first replay: counters zero, DONE pre-signalled once."""
+        f = self._flag_buf()
+        f.zero_()
+        f[_DONE] = 1
+
+    def flag_error(self) -> int:
+        return int(self._flags[_ERR].item()) if self._flags is not None else 0
 
     # -- pacing / accounting --------------------------------------------------------------------
     def _pace(self, seconds: float, device_tensor: bool):
@@ -432,9 +456,13 @@ class Communicator:
             dist.barrier(group=self.group)
 
     def check(self):
-        """Raise if the native communicator reported an asynchronous RCCL error."""
+        """Raise if the native communicator reported an asynchronous RCCL error, or a
+        compute/comm graph flag wait timed out (host sync: call at a low cadence)."""
         if self._native is not None:
             self._native.check()
+        if self.flag_error():
+            raise RuntimeError("compute/comm graph ordering: a device-flag wait timed out "
+                               "(the two streams may share a hardware queue); results of that step are unordered")
 
     def close(self):
         """Destroy the native communicator — unless a captured graph contains its

@@ -124,6 +124,10 @@ class BucketedDataParallel:
     def collectives_per_step(self) -> int:
         return len(self.buckets) if self.comm.active else 0
 
+    def collective_payloads(self):
+        """Bytes of every bucket all-reduce of one step (link-model input)."""
+        return [4 * (e - s) for s, e, _ in self.buckets]
+
     def _bind(self, b: int):
         _, _, ps = self.buckets[b]
         specs = []

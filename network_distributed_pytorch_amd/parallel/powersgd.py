@@ -711,6 +711,20 @@ class PowerSGDOptimizer:
             return 2 * len(self.groups) + (1 if self.r1_numel else 0)
         return 2 if self.buf.shapes else 1
 
+    def collective_payloads(self) -> List[int]:
+        """Bytes of every collective of one step, in issue order (link-model input)."""
+        B = self.buf
+        if self.overlap:
+            out = []
+            for g in self.groups:
+                p0, p1 = B.p_range(g.lo, g.hi)
+                q0, q1 = B.q_range(g.lo, g.hi)
+                out += [4 * (p1 - p0), 4 * (q1 - q0)]
+            if self.r1_numel:
+                out.append(4 * self.r1_numel)
+            return out
+        return [4 * (B.p_total + self.r1_numel)] + ([4 * B.q_total] if B.shapes else [])
+
     def check_errors(self):
         """Host-synchronising health check (call at a low cadence: epoch / replica check):
         raises on a timed-out MGS barrier or an asynchronous RCCL error."""

@@ -41,6 +41,9 @@ class PowerSGDSync:
     def comm(self):
         return self.opt.comm
 
+    def collective_payloads(self):
+        return self.opt.collective_payloads()
+
     def zero_grad(self):
         self.opt.zero_grad()
 
@@ -86,8 +89,13 @@ class ReferencePowerSGDLoop:
         self.momenta = [torch.empty_like(p) for p in self.params]
         self.first = True
         self.bits = 0
-        self.bytes_per_step = powersgd_bytes_per_step(self.params, rank)["total"]
+        b = powersgd_bytes_per_step(self.params, rank)
+        self.bytes_per_step = b["total"]
+        self._payloads = [b["p"], b["rank1"], b["q"]]  # reducer.py:126, :132, :145
         self.collectives_per_step = 3 if comm.active else 0
+
+    def collective_payloads(self):
+        return list(self._payloads)
 
     def zero_grad(self):
         for p in self.params:
@@ -120,7 +128,11 @@ class ReferenceDenseLoop:
         self.comm = comm
         self.opt = torch.optim.SGD(model.parameters(), lr=lr, momentum=momentum)
         self.bytes_per_step = 4 * sum(p.numel() for p in model.parameters())
+        self._payloads = [4 * p.numel() for p in model.parameters()]  # ddp_init.py:61, one per param
         self.collectives_per_step = len(list(model.parameters())) if comm.active else 0
+
+    def collective_payloads(self):
+        return list(self._payloads)
 
     def zero_grad(self):
         self.opt.zero_grad()
@@ -143,6 +155,9 @@ class _DenseSync:
     @property
     def comm(self):
         return self.ddp.comm
+
+    def collective_payloads(self):
+        return self.ddp.collective_payloads()
 
     def snapshot(self):
         return self.ddp.snapshot()

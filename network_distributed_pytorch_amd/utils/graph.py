@@ -9,17 +9,19 @@ native table uploads), then captures it and replays it every step:
                   With a stream-ordered data plane (native RCCL communicator, or world
                   size 1) the sync's post-accumulate-grad hooks hand bucket / PowerSGD-group
                   work (kernels AND collectives) to the communicator's side stream
-                  (``Communicator.side_launch``).  The step is then captured in SEGMENTS:
-                  at every side launch the compute graph being captured is closed and the
-                  next one begun (in the autograd thread, mid-backward), and the side work
-                  becomes its own comm graph.  Replay launches compute segment i, forks the
-                  side stream, launches comm graph i there, and so on; one join at the end.
-                  Every graph is linear (the HIP runtime executes a graph with parallel
-                  branches node by node over internal streams — measured 2.50 vs 2.13 ms per
-                  step), and each comm graph is enqueued as soon as its compute segment has
-                  been launched, not after the whole step graph (launching a ~200-node graph
-                  costs the host about as long as the GPU takes to run it, so a comm graph
-                  launched after one monolithic compute graph started ~1.3 ms late).
+                  (``Communicator.side_launch``).  The step is then captured as TWO linear
+                  graphs: the compute graph (forward + backward) with a one-lane
+                  "flag signal" kernel at every hook point, and the comm graph with a
+                  matching "flag wait" kernel before each piece of side work.  Replay
+                  launches the compute graph on the current stream and the comm graph on
+                  the side stream; the comm graph ends by signalling a DONE flag that the
+                  next compute graph waits on first.  Measured reasons for this shape
+                  (profiles/overlap_r2.md): one graph with a parallel branch is executed by
+                  the HIP runtime node by node across internal streams (2.50 vs 2.13 ms per
+                  step), and hipEvent waits between the two graphs were re-evaluated only
+                  after the producing queue drained its kernel train (the comm work started
+                  after the whole backward).  The device flags react within microseconds.
+                  ``runner.join()`` orders the current stream after the last comm graph.
 * ``piecewise`` — the compute phases are captured, the collectives run eagerly between
                   graph replays (``sync.phases()``): the c10d data plane (``NDP_NATIVE_COMM=0``).
 * ``none``      — plain eager execution (gloo: its host thread blocks on collectives).
@@ -95,6 +97,7 @@ class StepRunner:
         self.side_graphs = []
         self._comm = None
         self.host_launch_s = [0.0, 0.0]  # host time inside replay() of compute / comm graphs
+        self._joined = True
 
     def _segments(self):
         if self.mode in ("none", "full"):
@@ -122,6 +125,7 @@ class StepRunner:
         return [(chain(f), cap) for f, cap in segs]
 
     def _run_eager(self):
+        self.join()  # an eager step after a replay reads what the comm graph writes
         for fn, _ in self.segments:
             fn()
 
@@ -169,25 +173,27 @@ class StepRunner:
         scope = _UPLOADS.capture_scope() if _DEFER_UPLOADS else contextlib.nullcontext([])
         with scope as uploads:  # table uploads: applied once after capture, not per replay
             if segmented:
-                # compute graph: forward + backward with an external event-record node at
-                # every side launch; comm graphs: wait node + the side work (one per launch)
+                # compute graph: wait(DONE) + forward + backward, one flag-signal kernel at
+                # every side launch; comm graph: flag-wait + side work per signal, then
+                # signal(DONE) for the next step's compute graph
                 (fn, _), = self.segments
-                side_items = []
-                with comm.defer_side(lambda: self._record_split(comm, side_items)) as items:
+                with comm.defer_side() as items:
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g, pool=pool):
+                        comm.graph_prologue()
                         fn()
                     graphs.append(g)
-                side_pool = torch.cuda.graph_pool_handle()
-                side_cap = torch.cuda.Stream()
-                gs = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gs, pool=side_pool, stream=side_cap):
-                    for i, item in enumerate(items):
-                        comm.wait_event(i)
-                        for f in item:
-                            f()
-                self.side_graphs.append(gs)
-                self._comm = comm
+                if items:
+                    gs = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(gs, pool=torch.cuda.graph_pool_handle(), stream=torch.cuda.Stream()):
+                        for i, item in enumerate(items):
+                            comm.graph_wait(i)
+                            for f in item:
+                                f()
+                        comm.graph_epilogue()
+                    self.side_graphs.append(gs)
+                    self._comm = comm
+                    comm.reset_flags()
             else:
                 for fn, cap in self.segments:
                     if cap:
@@ -202,10 +208,12 @@ class StepRunner:
         self._upload_gen = _UPLOADS.generation
         self.graphs = graphs
 
-    @staticmethod
-    def _record_split(comm, _items):
-        comm.record_event(len(comm._deferred))
-        return True
+    def join(self):
+        """Make the current stream wait for the last replay's comm graph (call before
+        reading parameters / sync state on the host side: checkpoint, eval, checks)."""
+        if self.side_graphs and not self._joined:
+            self._comm.join()
+            self._joined = True
 
     def __call__(self):
         if self.mode == "none":
@@ -216,16 +224,14 @@ class StepRunner:
         # an eager step since capture may have re-bound a table the graph reads
         self._upload_gen = _UPLOADS.ensure(self._uploads, self._upload_gen)
         if self.side_graphs:
-            comm = self._comm
             t0 = time.perf_counter()
-            self.graphs[0].replay()
+            self.graphs[0].replay()          # waits (device flag) for the previous comm graph
             t1 = time.perf_counter()
-            with comm.on_side():
-                self.side_graphs[0].replay()  # its wait nodes order it after the record nodes
-            t2 = time.perf_counter()
-            comm.join()
+            with self._comm.on_side():
+                self.side_graphs[0].replay()  # each piece waits for its compute-graph signal
             self.host_launch_s[0] += t1 - t0
-            self.host_launch_s[1] += t2 - t1
+            self.host_launch_s[1] += time.perf_counter() - t1
+            self._joined = False
         else:
             t0 = time.perf_counter()
             for (fn, _), g in zip(self.segments, self.graphs):

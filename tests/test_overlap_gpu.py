@@ -248,3 +248,25 @@ def test_tables_reuploaded_after_graph_restore(device):
         torch.cuda.synchronize()
         got = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
     assert torch.equal(ref, got), (ref - got).abs().max()
+
+
+@pytest.mark.parametrize("link", ["100g", "10g"])
+def test_link_pacing_matches_model(device, link):
+    """1-GPU link emulation: the stall charged on the stream for an
+    emulated 8-rank ring equals LinkModel.seconds within 10%."""
+    from network_distributed_pytorch_amd.parallel.comm import LINK_PRESETS
+
+    comm = Communicator(link=LINK_PRESETS[link], emulate_world=8, device=device)
+    t = torch.zeros(1 << 20, device=device)  # 4 MiB payload
+    expected = comm.link.seconds(t.numel() * 4, 8)
+    comm.all_reduce(t)  # warm-up
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(4):
+        comm.all_reduce(t)
+    b.record()
+    torch.cuda.synchronize()
+    got = a.elapsed_time(b) / 1e3 / 4
+    assert abs(got - expected) <= 0.1 * expected, (got, expected)
+    assert comm.stats.emulated_seconds == pytest.approx(5 * expected)

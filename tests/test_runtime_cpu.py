@@ -1,5 +1,6 @@
 """Runtime pieces on CPU: comm accounting + link model, plan builder coverage, checkpoint
 resume equivalence, the training engine (all tasks), the orthogonalizer and Q seeding."""
+import json
 import os
 
 import numpy as np
@@ -145,7 +146,8 @@ def test_engine_tasks(tmp_path, task, grad_sync, extra):
     out = engine.run_task(cfg)
     assert len(out["epoch_losses"]) == 2 and all(np.isfinite(out["epoch_losses"]))
     assert os.path.exists(tmp_path / "ck" / "last.pt")
-    assert (tmp_path / "log.jsonl").read_text().count("\n") == 3
+    kinds = [json.loads(ln)["kind"] for ln in (tmp_path / "log.jsonl").read_text().splitlines()]
+    assert kinds.count("step") == 4 and kinds.count("epoch") == 2 and kinds[-1] == "summary"
 
 
 def test_batchnorm_act_cpu_matches_torch():
