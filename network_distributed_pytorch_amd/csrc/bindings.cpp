@@ -375,13 +375,13 @@ void flag_signal(torch::Tensor flags, int64_t i) {
   check_launch("launch_flag_signal");
 }
 
-void flag_wait(torch::Tensor flags, int64_t i, int64_t seen, int64_t err, int64_t max_spins) {
+void flag_wait(torch::Tensor flags, int64_t i, int64_t seen, int64_t err, int64_t timeout_us) {
   check_dev(flags, "flags");
   TORCH_CHECK(flags.scalar_type() == torch::kInt32 && i >= 0 && i < flags.numel() && seen >= 0 &&
                   seen < flags.numel() && err >= 0 && err < flags.numel(),
               "flag_wait: bad flag indices");
   auto* f = reinterpret_cast<unsigned*>(flags.data_ptr<int32_t>());
-  ndp::launch_flag_wait(f + i, f + seen, f + err, (unsigned)max_spins, cur_stream());
+  ndp::launch_flag_wait(f + i, f + seen, f + err, timeout_us, cur_stream());
   check_launch("launch_flag_wait");
 }
 

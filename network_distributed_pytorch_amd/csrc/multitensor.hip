@@ -131,8 +131,8 @@ __global__ void delay_kernel(int64_t ticks) {
 // comm graph's first kernel of each piece spins on it (agent-scope acquire, s_sleep), so
 // the comm queue reacts within microseconds.  Each wait consumes exactly one bump
 // (`seen` is private to the waiting queue), so the same captured graphs replay forever.
-// A bounded spin reports through `err` instead of hanging (e.g. if both streams ever
-// shared one hardware queue).
+// A wall-clock-bounded spin (s_memrealtime, 100 MHz) reports through `err` instead of
+// hanging (e.g. if both streams ever shared one hardware queue, or a wait has no signaller).
 __global__ void flag_signal_kernel(unsigned* ctr) {
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -140,13 +140,13 @@ __global__ void flag_signal_kernel(unsigned* ctr) {
   }
 }
 
-__global__ void flag_wait_kernel(unsigned* ctr, unsigned* seen, unsigned* err, unsigned max_spins) {
+__global__ void flag_wait_kernel(unsigned* ctr, unsigned* seen, unsigned* err, uint64_t max_ticks) {
   if (threadIdx.x == 0) {
     const unsigned want = __hip_atomic_load(seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-    unsigned spins = 0;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while ((int)(__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
       __builtin_amdgcn_s_sleep(2);
-      if (++spins > max_spins) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > max_ticks) {
         __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
@@ -160,8 +160,9 @@ void launch_flag_signal(unsigned* ctr, hipStream_t s) {
   hipLaunchKernelGGL(flag_signal_kernel, dim3(1), dim3(64), 0, s, ctr);
 }
 
-void launch_flag_wait(unsigned* ctr, unsigned* seen, unsigned* err, unsigned max_spins, hipStream_t s) {
-  hipLaunchKernelGGL(flag_wait_kernel, dim3(1), dim3(64), 0, s, ctr, seen, err, max_spins);
+void launch_flag_wait(unsigned* ctr, unsigned* seen, unsigned* err, int64_t timeout_us, hipStream_t s) {
+  const uint64_t ticks = (uint64_t)(timeout_us > 0 ? timeout_us : 0) * 100u;  // 100 MHz clock
+  hipLaunchKernelGGL(flag_wait_kernel, dim3(1), dim3(64), 0, s, ctr, seen, err, ticks);
 }
 
 constexpr int kCkBlocks = 256;

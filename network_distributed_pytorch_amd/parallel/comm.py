@@ -157,7 +157,7 @@ class _StreamWork:
 
 _MAX_FLAGS = 256
 _DONE, _ERR = 2 * _MAX_FLAGS, 2 * _MAX_FLAGS + 2
-_SPINS = 1 << 25  # ~2 s of s_sleep 2 before a wait reports a timeout instead of hanging
+_WAIT_US = 2_000_000  # a flag wait reports a timeout after 2 s (device wall clock) instead of hanging
 _SIDE_LINKS = {}
 _KEEPALIVE = []
 
@@ -230,6 +230,7 @@ class Communicator:
         self._flags = None
         self._captured = False
         self._device = device
+        self.side_launches = 0  # eager side launches so far (StepRunner: does a step use the side stream?)
         if native is not False and self.active:
             self._native = create_native_comm(group, device)
             if native is True and self._native is None:
@@ -312,6 +313,7 @@ class Communicator:
             self._flag_ext().flag_signal(self._flag_buf(), i)
             self._deferred.append([fn])
             return
+        self.side_launches += 1
         self.fork()
         with self.on_side():
             fn()
@@ -351,11 +353,11 @@ class Communicator:
 
     def graph_prologue(self):
         """First node of the compute graph: wait until the previous step's comm graph is done."""
-        self._flag_ext().flag_wait(self._flag_buf(), _DONE, _DONE + 1, _ERR, _SPINS)
+        self._flag_ext().flag_wait(self._flag_buf(), _DONE, _DONE + 1, _ERR, _WAIT_US)
 
     def graph_wait(self, i: int):
         """Comm graph: wait for the compute graph's i-th signal."""
-        self._flag_ext().flag_wait(self._flag_buf(), i, _MAX_FLAGS + i, _ERR, _SPINS)
+        self._flag_ext().flag_wait(self._flag_buf(), i, _MAX_FLAGS + i, _ERR, _WAIT_US)
 
     def graph_epilogue(self):
         """Last node of the comm graph: release the next step's compute graph."""

@@ -146,9 +146,14 @@ class StepRunner:
         saved = self._snapshot()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
+        comm = getattr(self.sync, "comm", None)
         with torch.cuda.stream(s):
             for _ in range(self.warmup):
+                n0 = getattr(comm, "side_launches", 0)
                 self._run_eager()
+        # split compute / comm graphs only if the step hands work to the side stream (the
+        # compute graph's DONE wait would otherwise have no signaller)
+        self._uses_side = getattr(comm, "side_launches", 0) > n0 if self.warmup > 0 else True
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         # no cyclic GC while capturing: a collected graph / stream / event of an earlier
@@ -168,7 +173,8 @@ class StepRunner:
         pool = torch.cuda.graph_pool_handle()
         graphs = []
         comm = getattr(self.sync, "comm", None)
-        segmented = self.mode == "full" and comm is not None and hasattr(comm, "defer_side")
+        segmented = (self.mode == "full" and comm is not None and hasattr(comm, "defer_side")
+                     and getattr(self, "_uses_side", True))
         self.side_graphs = []
         scope = _UPLOADS.capture_scope() if _DEFER_UPLOADS else contextlib.nullcontext([])
         with scope as uploads:  # table uploads: applied once after capture, not per replay
@@ -183,6 +189,9 @@ class StepRunner:
                         comm.graph_prologue()
                         fn()
                     graphs.append(g)
+                if not items:
+                    raise RuntimeError("captured compute graph waits for a comm graph, but the step "
+                                       "launched no side work during capture (it did during warm-up)")
                 if items:
                     gs = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(gs, pool=torch.cuda.graph_pool_handle(), stream=torch.cuda.Stream()):

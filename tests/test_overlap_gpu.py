@@ -163,6 +163,7 @@ def _train(device, kind, sync_kind, mode, overlap, steps=3, rank=4, groups=3):
         static[1].copy_(y)
         runner()
     torch.cuda.synchronize()
+    assert comm.flag_error() == 0, "a compute/comm graph flag wait timed out"
     out = torch.cat([p.detach().reshape(-1) for p in model.parameters()]).clone()
     n_coll = sync.collectives_per_step
     comm.close()
@@ -200,6 +201,20 @@ def test_dense_overlap_bitwise(device, mode):
     assert n_coll >= 2
     assert torch.equal(serial, over), (serial - over).abs().max()
     assert torch.equal(serial, rccl), (serial - rccl).abs().max()
+
+
+@pytest.mark.parametrize("sync_kind", ["powersgd", "dense"])
+def test_serial_full_graph_no_side_stream(device, sync_kind):
+    """overlap=False under full capture: no side work, so no compute/comm graph split (a
+    DONE wait without a signaller used to stall every replay until its timeout)."""
+    import time
+
+    with deterministic():
+        serial, _ = _train(device, "resnet", sync_kind, "none", overlap=False)
+        t0 = time.perf_counter()
+        graphed, _ = _train(device, "resnet", sync_kind, "full", overlap=False)
+        assert time.perf_counter() - t0 < 30
+    assert torch.equal(serial, graphed), (serial - graphed).abs().max()
 
 
 def test_orth_barrier_timeout_poisons_and_raises(device):
