@@ -72,12 +72,17 @@ def parse(argv=None):
                     help="charge the link model for an N-rank ring even on 1 GPU (bandwidth curves)")
     ap.add_argument("--bucket-mb", type=float, default=None, help="dense arm bucket size (default 8 MB)")
     ap.add_argument("--psgd-groups", type=int, default=None, help="PowerSGD overlap groups (default 4)")
-    ap.add_argument("--no-overlap", action="store_true", help="serial sync after backward (A/B)")
+    ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
+                    help="gradient sync overlapped with backward on the side stream (auto: when N > 1 or a "
+                         "link is emulated)")
+    ap.add_argument("--no-overlap", action="store_true", help="= --overlap off")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--graph-mode", default="auto", choices=["auto", "full", "piecewise", "none"],
                     help="hipGraph capture of the step: full (native RCCL / N=1), piecewise (collectives "
                          "eager between captured compute; c10d data plane), none")
     a = ap.parse_args(argv)
+    if a.no_overlap:
+        a.overlap = "off"
     bert = a.model.startswith("distilbert")
     if a.stock:
         a.no_fused_bn = a.no_gemm_convs = a.no_fused_attn = True
@@ -118,15 +123,13 @@ class Workload:
         link = None if args.link == "none" else LINK_PRESETS[args.link]
         self.comm = Communicator(link=link, emulate_world=args.emulate_world, device=device)
         kw = {}
-        if args.reducer == "powersgd":
-            if args.no_overlap:
-                kw["overlap"] = False
-            if args.psgd_groups is not None:
+        if args.reducer in ("powersgd", "dense"):
+            if args.overlap != "auto":  # auto: overlap when a step has wire time (N > 1 / link emulation)
+                kw["overlap"] = args.overlap == "on"
+            if args.psgd_groups is not None and args.reducer == "powersgd":
                 kw["groups"] = args.psgd_groups
         self.sync = build_grad_sync(args.reducer, self.model, self.comm, lr=args.lr, momentum=0.9,
                                     rank=args.rank, bucket_mb=args.bucket_mb, **kw)
-        if args.reducer == "dense" and args.no_overlap:
-            self.sync.ddp.overlap = False
         self.crit = torch.nn.CrossEntropyLoss()
         self.loss_acc = torch.zeros((), device=device)
         self.graph_mode = None

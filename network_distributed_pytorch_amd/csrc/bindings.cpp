@@ -418,6 +418,32 @@ void toeplitz_expand(torch::Tensor w, torch::Tensor wb, const std::vector<int64_
   check_launch("launch_toeplitz_expand");
 }
 
+// entries: [(w, w_big, geom)] -> every W_big^T in one launch
+void toeplitz_expand_many(const std::vector<std::tuple<torch::Tensor, torch::Tensor, std::vector<int64_t>>>& entries) {
+  TORCH_CHECK(!entries.empty() && (int)entries.size() <= ndp::kMaxExpand, "toeplitz_expand_many: 1..",
+              ndp::kMaxExpand, " layers");
+  ndp::ExpandBatch b{};
+  int64_t acc = 0;
+  for (const auto& en : entries) {
+    const torch::Tensor& w = std::get<0>(en);
+    const torch::Tensor& wb = std::get<1>(en);
+    check_f32(w, "w"); check_f32(wb, "w_big");
+    const ndp::ConvGeom g = conv_geom(std::get<2>(en));
+    TORCH_CHECK(w.numel() == (int64_t)g.Co * g.C * g.KH * g.KW, "toeplitz_expand_many: weight size");
+    const int64_t nk = (int64_t)g.C * g.H * g.W * g.Co * g.OH * g.OW;
+    TORCH_CHECK(wb.numel() == nk, "toeplitz_expand_many: w_big size");
+    b.w[b.n] = w.data_ptr<float>();
+    b.wt[b.n] = wb.data_ptr<float>();
+    b.g[b.n] = g;
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(b.wt[b.n]) & 15) == 0, "toeplitz_expand_many: w_big not 16-B aligned");
+    acc += (int64_t)g.Co * g.OH * g.OW;
+    b.end[b.n] = acc;
+    ++b.n;
+  }
+  ndp::launch_toeplitz_expand_many(b, cur_stream());
+  check_launch("launch_toeplitz_expand_many");
+}
+
 void toeplitz_fold(torch::Tensor dwb, torch::Tensor dw, const std::vector<int64_t>& geom) {
   check_f32(dwb, "dw_big"); check_f32(dw, "dw");
   const ndp::ConvGeom g = conv_geom(geom);
@@ -428,11 +454,23 @@ void toeplitz_fold(torch::Tensor dwb, torch::Tensor dw, const std::vector<int64_
 }
 
 // (class, fwd images per workgroup, grad-W images per slice, grad-x direct) or class -1
-py::tuple conv_plan(const std::vector<int64_t>& geom) {
+// (class, fwd images per workgroup, grad-W images per slice, grad-x direct, fwd split-K,
+// grad-x split-K) for batch B, or class -1
+py::tuple conv_plan(const std::vector<int64_t>& geom, int64_t B) {
   const ndp::ConvGeom g = conv_geom(geom);
   const int cls = ndp::conv_direct_class(g);
-  if (cls < 0) return py::make_tuple(-1, 0, 0, false);
-  return py::make_tuple(cls, ndp::conv_fwd_imgs(cls), ndp::conv_wgrad_imgs(cls), ndp::conv_dgrad_direct(cls));
+  if (cls < 0 || B <= 0 || B % ndp::conv_fwd_imgs(cls)) return py::make_tuple(-1, 0, 0, false, 1, 1);
+  return py::make_tuple(cls, ndp::conv_fwd_imgs(cls), ndp::conv_wgrad_imgs(cls, g, (int)B),
+                        ndp::conv_dgrad_direct(cls), ndp::conv_ksplit(cls, g, (int)B, false),
+                        ndp::conv_ksplit(cls, g, (int)B, true));
+}
+
+float* conv_part(const c10::optional<torch::Tensor>& part, int ks, int64_t out_numel, const char* who) {
+  if (ks <= 1) return nullptr;
+  TORCH_CHECK(part.has_value(), who, ": split-K needs a part scratch tensor");
+  check_f32(*part, "part");
+  TORCH_CHECK(part->numel() >= ks * out_numel, who, ": part scratch too small");
+  return part->data_ptr<float>();
 }
 
 void conv_check(const torch::Tensor& t, const char* n, int64_t b, int64_t c, int64_t h, int64_t w) {
@@ -448,17 +486,21 @@ int conv_batch(const torch::Tensor& t, const ndp::ConvGeom& g, int imgs) {
   return B;
 }
 
-void conv_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, const std::vector<int64_t>& geom) {
+void conv_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, const std::vector<int64_t>& geom,
+              c10::optional<torch::Tensor> part) {
   const ndp::ConvGeom g = conv_geom(geom);
-  const int B = conv_batch(x, g, ndp::conv_fwd_imgs(ndp::conv_direct_class(g)));
+  const int cls = ndp::conv_direct_class(g);
+  const int B = conv_batch(x, g, ndp::conv_fwd_imgs(cls));
   conv_check(x, "x", B, g.C, g.H, g.W);
   conv_check(w, "w", g.Co, g.C, g.KH, g.KW);
   conv_check(y, "y", B, g.Co, g.OH, g.OW);
-  ndp::launch_conv_fwd(x.data_ptr<float>(), w.data_ptr<float>(), y.data_ptr<float>(), B, g, cur_stream());
+  float* pp = conv_part(part, ndp::conv_ksplit(cls, g, B, false), y.numel(), "conv_fwd");
+  ndp::launch_conv_fwd(x.data_ptr<float>(), w.data_ptr<float>(), y.data_ptr<float>(), B, g, pp, cur_stream());
   check_launch("launch_conv_fwd");
 }
 
-void conv_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, const std::vector<int64_t>& geom) {
+void conv_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, const std::vector<int64_t>& geom,
+                c10::optional<torch::Tensor> part) {
   const ndp::ConvGeom g = conv_geom(geom);
   const int cls = ndp::conv_direct_class(g);
   TORCH_CHECK(cls >= 0 && ndp::conv_dgrad_direct(cls), "conv_dgrad: no direct grad-x kernel for this geometry");
@@ -466,14 +508,17 @@ void conv_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, const std::
   conv_check(dy, "dy", B, g.Co, g.OH, g.OW);
   conv_check(w, "w", g.Co, g.C, g.KH, g.KW);
   conv_check(dx, "dx", B, g.C, g.H, g.W);
-  ndp::launch_conv_dgrad(dy.data_ptr<float>(), w.data_ptr<float>(), dx.data_ptr<float>(), B, g, cur_stream());
+  float* pp = conv_part(part, ndp::conv_ksplit(cls, g, B, true), dx.numel(), "conv_dgrad");
+  ndp::launch_conv_dgrad(dy.data_ptr<float>(), w.data_ptr<float>(), dx.data_ptr<float>(), B, g, pp, cur_stream());
   check_launch("launch_conv_dgrad");
 }
 
 void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor part, torch::Tensor dw,
                 const std::vector<int64_t>& geom) {
   const ndp::ConvGeom g = conv_geom(geom);
-  const int imgs = ndp::conv_wgrad_imgs(ndp::conv_direct_class(g));
+  const int cls = ndp::conv_direct_class(g);
+  TORCH_CHECK(cls >= 0, "conv_wgrad: no direct kernel for this geometry");
+  const int imgs = ndp::conv_wgrad_imgs(cls, g, (int)x.size(0));
   const int B = conv_batch(x, g, imgs);
   conv_check(x, "x", B, g.C, g.H, g.W);
   conv_check(dy, "dy", B, g.Co, g.OH, g.OW);
@@ -584,9 +629,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("flag_wait", &flag_wait);
   m.def("toeplitz_expand", &toeplitz_expand);
   m.def("toeplitz_fold", &toeplitz_fold);
-  m.def("conv_plan", &conv_plan);
-  m.def("conv_fwd", &conv_fwd);
-  m.def("conv_dgrad", &conv_dgrad);
+  m.def("toeplitz_expand_many", &toeplitz_expand_many);
+  m.def("conv_plan", &conv_plan, py::arg("geom"), py::arg("batch"));
+  m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("geom"), py::arg("part") = py::none());
+  m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("geom"),
+        py::arg("part") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);

@@ -15,6 +15,8 @@
 
 namespace ndp {
 
+typedef float f32x4e __attribute__((ext_vector_type(4)));
+
 // Device orientation: Wt_big = W_big^T, [N = Co*OH*OW rows][K = C*H*W cols], so that both
 // kernels walk contiguous memory on both sides (a row of Wt_big reads one filter W[co]).
 // grid: (ceil(K/256), N); one thread per Wt_big element
@@ -59,6 +61,69 @@ __global__ __launch_bounds__(256) void toeplitz_fold_kernel(const float* __restr
     }
   }
   dw[idx] = acc;
+}
+
+// Every Toeplitz layer of a model in ONE launch (forward start, ToeplitzBank in
+// models/conv_gemm.py).  One workgroup per W_big^T row n = (co, oh, ow) of one layer (the
+// layer is found by scanning the <= kMaxExpand row prefix sums in the kernel arguments — no
+// table upload); thread t owns input channels ci = t, t + 256, ... and writes their H*W
+// contiguous columns (one float4 per 4 columns for the 2x2 / 4x4 maps): all index math is
+// per row or per channel, none per element.
+template <int H, int W>
+__device__ __forceinline__ void expand_row(const float* __restrict__ w, float* __restrict__ row, const ConvGeom& g,
+                                           int co, int oh, int ow) {
+  const int h0 = oh * g.stride - g.pad, w0 = ow * g.stride - g.pad;
+  for (int ci = threadIdx.x; ci < g.C; ci += 256) {
+    const float* wc = w + ((int64_t)co * g.C + ci) * g.KH * g.KW;
+    float v[H * W];
+#pragma unroll
+    for (int ih = 0; ih < H; ++ih)
+#pragma unroll
+      for (int iw = 0; iw < W; ++iw) {
+        const int kh = ih - h0, kw = iw - w0;
+        v[ih * W + iw] = (kh >= 0 && kh < g.KH && kw >= 0 && kw < g.KW) ? wc[kh * g.KW + kw] : 0.f;
+      }
+    float* d = row + (int64_t)ci * (H * W);
+    if constexpr ((H * W) % 4 == 0) {
+#pragma unroll
+      for (int j = 0; j < H * W; j += 4)
+        *reinterpret_cast<f32x4e*>(d + j) = f32x4e{v[j], v[j + 1], v[j + 2], v[j + 3]};
+    } else {
+#pragma unroll
+      for (int j = 0; j < H * W; ++j) d[j] = v[j];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void toeplitz_expand_many_kernel(ExpandBatch b) {
+  const int64_t r = blockIdx.x;
+  int e = 0;
+  while (e + 1 < b.n && r >= b.end[e]) ++e;
+  const ConvGeom& g = b.g[e];
+  const int n = (int)(r - (e ? b.end[e - 1] : 0));
+  const int OHW = g.OH * g.OW;
+  const int co = n / OHW, ohw = n - co * OHW;
+  const int oh = ohw / g.OW, ow = ohw - oh * g.OW;
+  float* row = b.wt[e] + (int64_t)n * g.C * g.H * g.W;
+  if (g.H == 1 && g.W == 1) expand_row<1, 1>(b.w[e], row, g, co, oh, ow);
+  else if (g.H == 2 && g.W == 2) expand_row<2, 2>(b.w[e], row, g, co, oh, ow);
+  else if (g.H == 4 && g.W == 4) expand_row<4, 4>(b.w[e], row, g, co, oh, ow);
+  else {
+    const int K = g.C * g.H * g.W, HW = g.H * g.W;
+    for (int kcol = threadIdx.x; kcol < K; kcol += 256) {
+      const int ci = kcol / HW, ihw = kcol - ci * HW;
+      const int ih = ihw / g.W, iw = ihw - ih * g.W;
+      const int kh = ih - oh * g.stride + g.pad, kw = iw - ow * g.stride + g.pad;
+      float v = 0.f;
+      if (kh >= 0 && kh < g.KH && kw >= 0 && kw < g.KW) v = b.w[e][((co * g.C + ci) * g.KH + kh) * g.KW + kw];
+      row[kcol] = v;
+    }
+  }
+}
+
+void launch_toeplitz_expand_many(const ExpandBatch& b, hipStream_t s) {
+  if (b.n <= 0) return;
+  hipLaunchKernelGGL(toeplitz_expand_many_kernel, dim3((unsigned)b.end[b.n - 1]), dim3(256), 0, s, b);
 }
 
 void launch_toeplitz_expand(const float* w, float* wb, const ConvGeom& g, hipStream_t s) {
@@ -139,7 +204,8 @@ struct ConvFwdCfg {
 template <int R, int S, int ST, int PD, int H, int W, int CK, int BM, int IMGS, int WM, int NBUF, int KB, bool TRANSW,
           bool VEC>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                                       float* __restrict__ y, int Cin, int Kout) {
+                                                       float* __restrict__ y, int Cin, int Kout, int cps,
+                                                       int64_t slab) {
   using G = ConvFwdCfg<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW>;
   constexpr int AE = (BM * G::KK + 3) / 4;  // float4 slots (scalar path: 4 scalars per slot)
   constexpr int A_PER_T = (AE + 255) / 256;
@@ -151,7 +217,10 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
   const int h = lane >> 5, l32 = lane & 31;
   const int m0 = blockIdx.y * BM;
   const int b0 = blockIdx.x * IMGS;
-  const int nchunks = (Cin + CK - 1) / CK;
+  // split-K: workgroup z reduces channel chunks [ch0, ch0 + nchunks) into output slab z
+  const int ch0 = blockIdx.z * cps;
+  const int nchunks = min((Cin + CK - 1) / CK - ch0, cps);
+  y += (int64_t)blockIdx.z * slab;
 
   for (int i = tid; i < NBUF * G::B_SZ; i += 256) Bs[i] = 0.f;  // zero borders (never rewritten)
 
@@ -169,7 +238,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
   f32x4c ra[A_PER_T];
   f32x4c rb[G::B_PER_T];
   auto load = [&](int ch) {
-    const int c0 = ch * CK;
+    const int c0 = (ch0 + ch) * CK;
 #pragma unroll
     for (int i = 0; i < A_PER_T; ++i) {
       const int e = tid + 256 * i;
@@ -492,14 +561,27 @@ static void set_lds(KernelT k, size_t bytes) {
   hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
+// ksplit > 1: the ksplit workgroups of an output tile each reduce 1/ksplit of the input
+// channels into their own slab of `part`; conv_slab_sum adds the slabs in split order
+// (deterministic).  Used where B / IMGS * Kout / BM alone cannot fill the 256 CUs
+// (small per-GPU batches: the strong-scaling shapes 512 / N).
 template <int R, int S, int ST, int PD, int H, int W, int CK, int BM, int IMGS, int WM, int NBUF, int KB, bool TRANSW,
           bool VEC>
-static void run_fwd(const float* x, const float* w, float* y, int B, int Cin, int Kout, hipStream_t s) {
+static void run_fwd(const float* x, const float* w, float* y, int B, int Cin, int Kout, int ksplit, float* part,
+                    hipStream_t s) {
   using G = ConvFwdCfg<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW>;
   auto k = conv_fwd_kernel<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW, VEC>;
   static bool attr = false;  // once per instantiation (> 64 KiB of LDS needs the opt-in)
   if (!attr) { set_lds(k, G::LDS_BYTES); attr = true; }
-  hipLaunchKernelGGL(k, dim3(B / IMGS, Kout / BM), dim3(256), G::LDS_BYTES, s, x, w, y, Cin, Kout);
+  const int nchunks = (Cin + CK - 1) / CK;
+  if (ksplit < 1 || part == nullptr) ksplit = 1;
+  const int cps = (nchunks + ksplit - 1) / ksplit;
+  ksplit = (nchunks + cps - 1) / cps;
+  const int64_t n = (int64_t)B * Kout * G::PQ;
+  hipLaunchKernelGGL(k, dim3(B / IMGS, Kout / BM, ksplit), dim3(256), G::LDS_BYTES, s, x, w, ksplit > 1 ? part : y,
+                     Cin, Kout, cps, n);
+  if (ksplit > 1)
+    hipLaunchKernelGGL(conv_slab_sum_kernel, dim3((unsigned)((n / 4 + 15) / 16)), dim3(256), 0, s, part, y, n, ksplit);
 }
 
 template <int R, int S, int ST, int PD, int H, int W, int CB, int BM, int NW, int NBPW, int KB>
@@ -548,32 +630,63 @@ int conv_fwd_imgs(int cls) {
   if (cls == 0) return conv_variant() == 1 ? 2 : 1;
   return cls == 3 ? 1 : 4;
 }
-int conv_wgrad_imgs(int cls) {
-  if (cls == 0) return conv_variant() == 1 ? 2 : 4;
-  return cls == 1 ? 16 : cls == 2 ? 8 : 2;
+
+static constexpr int kFillWgs = 256;  // one workgroup per CU: below this, split the reduction
+
+static int pow2_floor(int v) {
+  int p = 1;
+  while (p * 2 <= v) p *= 2;
+  return p;
+}
+
+// images per grad-W slice: the class default, lowered (power of two dividing B) until the
+// grid has >= kFillWgs workgroups.  Workgroups per slice = (Kout / 32) * ceil(Cin / CB).
+int conv_wgrad_imgs(int cls, const ConvGeom& g, int B) {
+  int def = cls == 0 ? (conv_variant() == 1 ? 2 : 4) : cls == 1 ? 16 : cls == 2 ? 8 : 2;
+  const int cb = cls == 3 ? 3 : 32;
+  const int per_slice = (g.Co / 32) * ((g.C + cb - 1) / cb);
+  while (def > 1 && (B / def) * per_slice < kFillWgs && B % (def / 2) == 0) def /= 2;
+  return def;
+}
+
+// split-K factor of the forward (dgrad = false) / grad-x (dgrad = true) kernels: a power of
+// two <= the channel chunks, so that (B / IMGS) * (outC / 64) * ksplit >= kFillWgs
+int conv_ksplit(int cls, const ConvGeom& g, int B, bool dgrad) {
+  if (cls == 3 || (dgrad && !conv_dgrad_direct(cls))) return 1;
+  const int inC = dgrad ? g.Co : g.C, outC = dgrad ? g.C : g.Co;
+  const int base = (B / conv_fwd_imgs(cls)) * (outC / 64);
+  const int nchunks = inC / 8;
+  int ks = 1;
+  while (ks * 2 <= nchunks && base * ks < kFillWgs) ks *= 2;
+  return pow2_floor(ks);
 }
 bool conv_dgrad_direct(int cls) { return cls == 0 || cls == 1; }
-void launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, hipStream_t s) {
-  switch (conv_direct_class(g)) {
+void launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s) {
+  const int cls = conv_direct_class(g);
+  const int ks = conv_ksplit(cls, g, B, false);
+  switch (cls) {
     case 0:
-      if (conv_variant() == 1) run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 2, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, s);
-      else run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, s);
+      if (conv_variant() == 1) run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 2, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s);
+      else run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s);
       break;
-    case 1: run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, s); break;
-    case 2: run_fwd<3, 3, 2, 1, 8, 8, 8, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, s); break;
-    case 3: run_fwd<7, 7, 2, 3, 32, 32, 4, 64, 1, 2, 1, 7, false, false>(x, w, y, B, g.C, g.Co, s); break;
+    case 1: run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s); break;
+    case 2: run_fwd<3, 3, 2, 1, 8, 8, 8, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s); break;
+    case 3: run_fwd<7, 7, 2, 3, 32, 32, 4, 64, 1, 2, 1, 7, false, false>(x, w, y, B, g.C, g.Co, 1, nullptr, s); break;
     default: break;
   }
 }
 
 // dx[B, C, H, W] from dy[B, Co, OH, OW] (stride-1 classes only)
-void launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, hipStream_t s) {
-  switch (conv_direct_class(g)) {
+void launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, float* part,
+                       hipStream_t s) {
+  const int cls = conv_direct_class(g);
+  const int ks = conv_ksplit(cls, g, B, true);
+  switch (cls) {
     case 0:
-      if (conv_variant() == 1) run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 2, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, s);
-      else run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, s);
+      if (conv_variant() == 1) run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 2, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s);
+      else run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s);
       break;
-    case 1: run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, s); break;
+    case 1: run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s); break;
     default: break;
   }
 }
@@ -582,7 +695,7 @@ void launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const 
 void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, int B, const ConvGeom& g,
                        hipStream_t s) {
   const int cls = conv_direct_class(g);
-  const int imgs = conv_wgrad_imgs(cls);
+  const int imgs = conv_wgrad_imgs(cls, g, B);
   switch (cls) {
     case 0: run_wgrad<3, 3, 1, 1, 8, 8, 32, 32, 3, 3, 4>(x, dy, part, dw, B, g.C, g.Co, imgs, s); break;
     case 1: run_wgrad<3, 3, 1, 1, 4, 4, 32, 32, 3, 3, 4>(x, dy, part, dw, B, g.C, g.Co, imgs, s); break;

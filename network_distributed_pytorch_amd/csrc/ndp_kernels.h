@@ -134,16 +134,30 @@ struct ConvGeom {
 };
 // Wt_big [Co*OH*OW, C*H*W] <- W [Co, C, KH, KW]  (transposed Toeplitz form of a small-spatial conv)
 void launch_toeplitz_expand(const float* w, float* wb, const ConvGeom& g, hipStream_t s);
+// several layers' W_big^T in one launch (by-value kernel arguments)
+constexpr int kMaxExpand = 24;
+struct ExpandBatch {
+  const float* w[kMaxExpand];
+  float* wt[kMaxExpand];
+  ConvGeom g[kMaxExpand];
+  int64_t end[kMaxExpand];  // inclusive prefix sums of the W_big^T row counts N = Co*OH*OW
+  int n;
+};
+void launch_toeplitz_expand_many(const ExpandBatch& b, hipStream_t s);
 // dW [Co, C, KH, KW] <- fold of dWt_big [Co*OH*OW, C*H*W]  (fixed-order sum, deterministic)
 void launch_toeplitz_fold(const float* dwb, float* dw, const ConvGeom& g, hipStream_t s);
 // direct fp32-MFMA convolutions: shape class (-1 = none), images per workgroup / slice
 int conv_direct_class(const ConvGeom& g);
 int conv_fwd_imgs(int cls);
-int conv_wgrad_imgs(int cls);
+int conv_wgrad_imgs(int cls, const ConvGeom& g, int B);
 bool conv_dgrad_direct(int cls);
-void launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, hipStream_t s);
-void launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, hipStream_t s);
-// part: (B / conv_wgrad_imgs(cls)) * Co*C*KH*KW floats of scratch
+// split-K factor (1 = none) of the forward / grad-x kernel for batch B; with ksplit > 1 the
+// launchers need `part` scratch of ksplit * numel(output) floats
+int conv_ksplit(int cls, const ConvGeom& g, int B, bool dgrad);
+void launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s);
+void launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, float* part,
+                       hipStream_t s);
+// part: (B / conv_wgrad_imgs(cls, g, B)) * Co*C*KH*KW floats of scratch
 void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, int B, const ConvGeom& g,
                        hipStream_t s);
 }  // namespace ndp

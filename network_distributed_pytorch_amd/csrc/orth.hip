@@ -16,8 +16,12 @@
 //    poller: relaxed loads, ONE acquire fence).  Every workgroup of a matrix, and every
 //    rank (same plan), computes the bitwise-identical result: replicas stay consistent.
 //  * Partial slabs are double-buffered by barrier parity (a fast workgroup can be at most
-//    one barrier ahead); counters are zeroed by a memset node before each launch; spins are
-//    bounded and report through an error word instead of hanging the GPU.
+//    one barrier ahead).  Counters are never reset (no memset node per launch): every
+//    workgroup increments its matrix counter exactly once per barrier, so a launch moves it
+//    by period = (2r - 1) * nwg and each launch starts on a multiple of the period; a
+//    workgroup reads its base on entry (before barrier 0 can complete, so the counter is
+//    then in [base, base + nwg)).  Spins are bounded and report through an error word
+//    instead of hanging the GPU.
 //  * Residency: workgroups are dispatched in grid order, so the barrier can only
 //    deadlock if ONE matrix needs more workgroups than the device holds at once.  The
 //    plan checks every matrix's workgroup count against orth_coresident_cap() =
@@ -63,7 +67,7 @@ struct OrthCtx {
 // Sum v[] over all workgroups of the matrix (deterministic, identical everywhere).
 template <int K>
 __device__ __forceinline__ void group_sum(float (&v)[K], float* red, const OrthItem& it, const OrthCtx& cx,
-                                          int& bar, int* bad) {
+                                          int& bar, unsigned base, int* bad) {
   block_sum_o<K>(v, red);
   if (it.nwg == 1) return;
   float* slab = cx.partial + ((size_t)(bar & 1) * cx.n_items + it.slab0) * kMaxRank;
@@ -78,9 +82,9 @@ __device__ __forceinline__ void group_sum(float (&v)[K], float* red, const OrthI
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_fetch_add(cx.ctr + it.mat, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned target = (unsigned)(bar + 1) * (unsigned)it.nwg;
+    const unsigned target = base + (unsigned)(bar + 1) * (unsigned)it.nwg;
     unsigned spins = 0;
-    while (__hip_atomic_load(cx.ctr + it.mat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    while ((int)(__hip_atomic_load(cx.ctr + it.mat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
       __builtin_amdgcn_s_sleep(2);
       if (++spins > cx.max_spins) {  // report (and poison, below) instead of hanging
         __hip_atomic_fetch_or(cx.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -114,6 +118,14 @@ __global__ __launch_bounds__(256) void psgd_orth_mw_kernel(const MatGeom* __rest
   const int r = g.r;
   float* P = p + g.p_off;
   const int tid = threadIdx.x;
+  __shared__ unsigned base_s;
+  if (tid == 0 && it.nwg > 1) {
+    const unsigned period = (unsigned)(2 * r - 1) * (unsigned)it.nwg;
+    const unsigned c0 = __hip_atomic_load(cx.ctr + it.mat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    base_s = c0 - c0 % period;
+  }
+  __syncthreads();
+  const unsigned base = it.nwg > 1 ? base_s : 0u;
 
   float v[RPT][RMAX];
 #pragma unroll
@@ -132,7 +144,7 @@ __global__ __launch_bounds__(256) void psgd_orth_mw_kernel(const MatGeom* __rest
 #pragma unroll
       for (int c = 0; c < RMAX; ++c)
         if (c == i) s[0] += v[k][c] * v[k][c];
-    group_sum<1>(s, red, it, cx, bar, &bad);
+    group_sum<1>(s, red, it, cx, bar, base, &bad);
     const float nrm = sqrtf(s[0]) + eps;
     float vi[RPT];
 #pragma unroll
@@ -154,7 +166,7 @@ __global__ __launch_bounds__(256) void psgd_orth_mw_kernel(const MatGeom* __rest
       for (int k = 0; k < RPT; ++k)
         if (j > i) d[j] += vi[k] * v[k][j];
     }
-    group_sum<RMAX>(d, red, it, cx, bar, &bad);
+    group_sum<RMAX>(d, red, it, cx, bar, base, &bad);
 #pragma unroll
     for (int k = 0; k < RPT; ++k)
 #pragma unroll
@@ -186,7 +198,6 @@ void launch_psgd_orth(const MatGeom* geom, const OrthItem* items, int n_items, i
                       float p_div, float eps, int max_rank, float* partial, unsigned* counters,
                       unsigned* err, int n_items_total, unsigned max_spins, hipStream_t s) {
   if (n_items <= 0) return;
-  (void)hipMemsetAsync(counters, 0, sizeof(unsigned) * (size_t)n_mats, s);
   OrthCtx cx{partial, counters, err, n_items_total, max_spins};
   if (max_rank <= 4)
     hipLaunchKernelGGL((psgd_orth_mw_kernel<4, 8>), dim3(n_items), dim3(256), 0, s, geom, items, p, p_div, eps, cx);

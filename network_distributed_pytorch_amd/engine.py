@@ -189,6 +189,8 @@ def run_task(config) -> Dict[str, Any]:
                  "overlap": config.get("overlap"), "groups": config.get("psgd_groups")}
         if not extra["reuse_query"]:
             graph_mode = "none"  # the per-step query re-draw is host-side (not capturable)
+    elif config["grad_sync"] == "dense":
+        extra = {"overlap": config.get("overlap")}
     sync = build_grad_sync(config["grad_sync"], model, comm, lr=config["learning_rate"],
                            momentum=config["momentum"], rank=config["reducer_rank"],
                            bucket_mb=config.get("bucket_mb"), seed=config["seed"], **extra)

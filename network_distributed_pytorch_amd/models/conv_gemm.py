@@ -11,7 +11,8 @@ where W_big[(ci,ih,iw), (co,oh,ow)] = W[co, ci, ih - oh*s + p, iw - ow*s + p] (0
 the kernel).  Both views are plain NCHW, so forward, grad-input and grad-weight are three
 hipBLASLt GEMMs; W_big is built from W and grad-W is folded back from grad-W_big by two
 gfx950 kernels (csrc/conv.hip) with a fixed-order sum (deterministic, no atomics).  Only the taps that can ever touch real
-pixels cost FLOPs.  1x1 strided convs subsample the input first.
+pixels cost FLOPs.  On device the stride of a 1x1 strided conv stays inside W_big; on CPU
+the input is subsampled first.
 
 ``GemmConv2d`` is a drop-in ``nn.Conv2d`` (same parameters / state_dict) that picks, per
 input geometry, the fastest native path:
@@ -32,7 +33,7 @@ from ..ops._ext import ext
 from ..ops import conv as _conv
 from ..ops.conv import DirectConvFn, direct_plan, side_stream
 
-__all__ = ["GemmConv2d", "toeplitz_maps", "eligible"]
+__all__ = ["GemmConv2d", "ToeplitzBank", "toeplitz_maps", "eligible"]
 
 
 def eligible(h: int, w: int, oh: int, ow: int) -> bool:
@@ -63,19 +64,57 @@ def toeplitz_maps(C: int, H: int, W: int, Co: int, KH: int, KW: int, s: int, p: 
     return src.view(K, N), dst, (OH, OW)
 
 
+class ToeplitzBank:
+    """Persistent W_big^T buffers of every Toeplitz layer of one model, (re)built by ONE
+    launch per forward pass (csrc/conv.hip toeplitz_expand_many) instead of one expand
+    kernel per layer.
+
+    Layers join the bank on their first device forward (eager: warm-up, never inside a
+    capture) and are expanded on their own that time.  Afterwards the first member to run
+    in a pass — forward order is fixed — expands every member; the others reuse their
+    buffer.  Valid because weights only change between passes (optimizer step); a
+    ``w_big`` saved for backward is rebuilt by the NEXT forward, i.e. after that backward.
+    """
+
+    def __init__(self):
+        self.members: list = []  # [(layer, geom, w_big)]
+        self._index: dict = {}
+
+    def get(self, layer, weight: torch.Tensor, geom: tuple, n: int, k: int) -> torch.Tensor:
+        key = id(layer)
+        i = self._index.get(key)
+        if i is None or self.members[i][1] != geom or self.members[i][2].device != weight.device:
+            assert not torch.cuda.is_current_stream_capturing(), "Toeplitz bank grows during capture"
+            w_big = torch.empty(n, k, device=weight.device, dtype=torch.float32)
+            ext().toeplitz_expand(weight.contiguous(), w_big, list(geom))
+            if i is None:
+                self._index[key] = len(self.members)
+                self.members.append((layer, geom, w_big))
+            else:
+                self.members[i] = (layer, geom, w_big)
+            return w_big
+        if i == 0:
+            ext().toeplitz_expand_many([(m.weight, wb, list(g)) for m, g, wb in self.members])
+        return self.members[i][2]
+
+
 class _ToeplitzConv(torch.autograd.Function):
     """Device tensors: W_big built / grad-W folded by csrc/conv.hip (index arithmetic, one
-    launch each); CPU tensors (fp64 tests): the same maps as index tensors."""
+    launch each, or one expand launch for a whole :class:`ToeplitzBank`); CPU tensors (fp64
+    tests): the same maps as index tensors."""
 
     @staticmethod
-    def forward(ctx, x, weight, src, dst, oh, ow, geom=None):
+    def forward(ctx, x, weight, src, dst, oh, ow, geom=None, bank=None, layer=None):
         B = x.shape[0]
         co = weight.shape[0]
         X = x.reshape(B, -1)
         if x.is_cuda and geom is not None:  # device: W_big^T [N, K], built by one kernel
             C, H, W = x.shape[1:]
-            w_big = torch.empty(co * oh * ow, C * H * W, device=x.device, dtype=x.dtype)
-            ext().toeplitz_expand(weight.contiguous(), w_big, list(geom))
+            if bank is not None:
+                w_big = bank.get(layer, weight, tuple(geom), co * oh * ow, C * H * W)
+            else:
+                w_big = torch.empty(co * oh * ow, C * H * W, device=x.device, dtype=x.dtype)
+                ext().toeplitz_expand(weight.contiguous(), w_big, list(geom))
             out = X @ w_big.t()
         else:
             w_ext = torch.cat([weight.reshape(-1), weight.new_zeros(1)])
@@ -108,14 +147,14 @@ class _ToeplitzConv(torch.autograd.Function):
                 dx = (G @ w_big).view(ctx.x_shape)
             if fork:
                 main.wait_stream(side)
-            return dx, dw, None, None, None, None, None
+            return dx, dw, None, None, None, None, None, None, None
         if ctx.needs_input_grad[0]:
             dx = (G @ w_big.t()).view(ctx.x_shape)
         if ctx.needs_input_grad[1]:
             dw_big = X.t() @ G                                    # [K, N]
             ext_ = torch.cat([dw_big.reshape(-1), dw_big.new_zeros(1)])
             dw = ext_[dst].sum(-1).view(ctx.w_shape)              # fixed-order, deterministic
-        return dx, dw, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None, None
 
 
 class GemmConv2d(nn.Conv2d):
@@ -126,13 +165,17 @@ class GemmConv2d(nn.Conv2d):
         self.gemm = gemm
         self.direct = direct
         self._maps: Dict[Tuple, tuple] = {}
+        self.bank: "ToeplitzBank | None" = None  # set by the owning model (one expand launch per pass)
 
     def _plan(self, x):
         C, H, W = x.shape[1:]
         kh, kw = self.kernel_size
         s, p = self.stride[0], self.padding[0]
         sub = 1
-        if kh == 1 and kw == 1 and p == 0 and s > 1:  # 1x1 strided: subsample, then stride 1
+        # 1x1 strided on CPU: subsample, then stride 1.  On device the stride stays inside
+        # W_big (the expand kernel handles it): no slice + contiguous forward, no
+        # zero-fill + strided-copy pairs in backward (4 ATen launches per downsample).
+        if kh == 1 and kw == 1 and p == 0 and s > 1 and not x.is_cuda:
             sub, s = s, 1
             H, W = (H + sub - 1) // sub, (W + sub - 1) // sub
         key = (C, H, W, x.device, sub)
@@ -166,4 +209,4 @@ class GemmConv2d(nn.Conv2d):
         src, dst, oh2, ow2, sub, geom = self._plan(x)
         if sub > 1:
             x = x[:, :, ::sub, ::sub]
-        return _ToeplitzConv.apply(x.contiguous(), self.weight, src, dst, oh2, ow2, geom)
+        return _ToeplitzConv.apply(x.contiguous(), self.weight, src, dst, oh2, ow2, geom, self.bank, self)

@@ -27,7 +27,7 @@ import torch.nn as nn
 
 from ..ops.batchnorm import BatchNormAct2d
 from ..ops.pool import MaxPool2d
-from .conv_gemm import GemmConv2d
+from .conv_gemm import GemmConv2d, ToeplitzBank
 
 __all__ = ["ResNet", "BasicBlock", "Bottleneck", "resnet18", "resnet34", "resnet50", "resnet101",
            "resnet152", "build_resnet"]
@@ -114,10 +114,12 @@ class ResNet(nn.Module):
         self.layer4 = self._make_layer(block, 512, layers[3], stride=2)
         self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
         self.fc = nn.Linear(512 * block.expansion, num_classes)
+        bank = ToeplitzBank()  # every Toeplitz layer's W_big in one launch per forward
         for m in self.modules():
             if isinstance(m, GemmConv2d):
                 m.gemm = gemm_convs
                 m.direct = gemm_convs
+                m.bank = bank
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
             elif isinstance(m, nn.BatchNorm2d):  # includes BatchNormAct2d

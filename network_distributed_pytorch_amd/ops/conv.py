@@ -42,7 +42,9 @@ def side_stream(device: torch.device) -> torch.cuda.Stream:
 
 
 def direct_plan(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int) -> Optional[Tuple]:
-    """(geom, fwd_imgs, wgrad_imgs, dgrad_direct) if a direct kernel covers this conv."""
+    """(geom, fwd_imgs, wgrad_imgs, dgrad_direct, fwd_ksplit, dgrad_ksplit) if a direct kernel
+    covers this conv at this batch size (the split-K factors and grad-W slice size adapt to
+    the batch so that small per-GPU batches still fill the 256 CUs)."""
     if not (x.is_cuda and x.dtype == torch.float32 and weight.dtype == torch.float32 and x.dim() == 4):
         return None
     B, C, H, W = x.shape
@@ -50,10 +52,11 @@ def direct_plan(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int
     if Ci != C:
         return None
     geom = (C, H, W, Co, KH, KW, int(stride), int(padding))
-    if geom not in _PLANS:
-        cls, fi, wi, dd = ext().conv_plan(list(geom))
-        _PLANS[geom] = None if cls < 0 else (geom, int(fi), int(wi), bool(dd))
-    plan = _PLANS[geom]
+    key = (geom, int(B))
+    if key not in _PLANS:
+        cls, fi, wi, dd, ksf, ksd = ext().conv_plan(list(geom), int(B))
+        _PLANS[key] = None if cls < 0 else (geom, int(fi), int(wi), bool(dd), int(ksf), int(ksd))
+    plan = _PLANS[key]
     if plan is None or B % plan[1] or B % plan[2]:
         return None
     return plan
@@ -62,7 +65,7 @@ def direct_plan(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int
 class DirectConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, plan):
-        geom, _, wgrad_imgs, dgrad_direct = plan
+        geom, _, wgrad_imgs, dgrad_direct, ks_fwd, _ = plan
         C, H, W, Co, KH, KW, s, p = geom
         x = x.contiguous()
         weight = weight.contiguous()
@@ -70,7 +73,8 @@ class DirectConvFn(torch.autograd.Function):
         OH = (H + 2 * p - KH) // s + 1
         OW = (W + 2 * p - KW) // s + 1
         y = torch.empty(B, Co, OH, OW, device=x.device, dtype=x.dtype)
-        ext().conv_fwd(x, weight, y, list(geom))
+        part = torch.empty(ks_fwd * y.numel(), device=x.device, dtype=x.dtype) if ks_fwd > 1 else None
+        ext().conv_fwd(x, weight, y, list(geom), part)
         ctx.save_for_backward(x, weight)
         ctx.plan = plan
         return y
@@ -78,7 +82,7 @@ class DirectConvFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, weight = ctx.saved_tensors
-        geom, _, wgrad_imgs, dgrad_direct = ctx.plan
+        geom, _, wgrad_imgs, dgrad_direct, _, ks_dgrad = ctx.plan
         s, p = geom[6], geom[7]
         dy = dy.contiguous()
         dx = dw = None
@@ -95,7 +99,8 @@ class DirectConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if dgrad_direct:
                 dx = torch.empty_like(x)
-                ext().conv_dgrad(dy, weight, dx, list(geom))
+                part = torch.empty(ks_dgrad * dx.numel(), device=x.device, dtype=x.dtype) if ks_dgrad > 1 else None
+                ext().conv_dgrad(dy, weight, dx, list(geom), part)
             else:
                 dx = torch.ops.aten.convolution_backward(dy, x, weight, None, [s, s], [p, p], [1, 1], False, [0, 0],
                                                          1, [True, False, False])[0]

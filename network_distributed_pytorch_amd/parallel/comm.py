@@ -253,6 +253,13 @@ class Communicator:
         return os.environ.get("NDP_FORCE_COLLECTIVES") == "1" and dist.is_available() and dist.is_initialized()
 
     @property
+    def has_traffic(self) -> bool:
+        """Whether a step spends time on the wire: real collectives, or link-model pacing of an
+        emulated world.  Overlapping the gradient sync with backward only pays when True (at
+        one rank the side stream would only add a resident wait kernel)."""
+        return self.active or (self.link is not None and self.paced_world > 1)
+
+    @property
     def backend(self) -> str:
         if self._native is not None:
             return "rccl-native"

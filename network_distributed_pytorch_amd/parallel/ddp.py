@@ -58,7 +58,7 @@ def average_gradients(model: torch.nn.Module, comm: Optional[Communicator] = Non
 class BucketedDataParallel:
     def __init__(self, model: torch.nn.Module, comm: Optional[Communicator] = None, lr: float = 1e-3,
                  momentum: float = 0.9, bucket_mb: Optional[float] = None, broadcast_params: bool = True,
-                 overlap: bool = True):
+                 overlap: Optional[bool] = None):
         bucket_mb = DEFAULT_BUCKET_MB if bucket_mb is None else float(bucket_mb)
         self.model = model
         self.comm = comm if comm is not None else Communicator()
@@ -109,6 +109,8 @@ class BucketedDataParallel:
         self._next = 0
         # stream mode: flatten + collective on the side stream (native RCCL / world 1, device)
         self.stream_mode = self.device.type == "cuda" and self.comm.stream_ordered
+        if overlap is None:  # default: overlap only when a step has wire time to hide
+            overlap = self.comm.has_traffic
         self.overlap = overlap and (self.comm.active or self.stream_mode)
         self._hooks = []
         if overlap:

@@ -488,7 +488,9 @@ class PowerSGDOptimizer:
         self._grad_key = None
         self._r1_key = None
 
-        want = overlap if overlap is not None else os.environ.get("NDP_PSGD_OVERLAP", "1") != "0"
+        # default: overlap when a step has wire time to hide (N > 1 or link emulation)
+        want = overlap if overlap is not None else (os.environ.get("NDP_PSGD_OVERLAP", "1") != "0"
+                                                    and self.comm.has_traffic)
         self.overlap = bool(want) and self.native and self.comm.stream_ordered and bool(hi)
         if overlap and not self.overlap:
             raise ValueError("overlap=True needs device tensors, the native extension and a stream-ordered "

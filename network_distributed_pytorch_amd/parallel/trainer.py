@@ -144,8 +144,8 @@ class ReferenceDenseLoop:
 
 
 class _DenseSync:
-    def __init__(self, model, comm, lr, momentum, bucket_mb):
-        self.ddp = BucketedDataParallel(model, comm, lr=lr, momentum=momentum, bucket_mb=bucket_mb)
+    def __init__(self, model, comm, lr, momentum, bucket_mb, overlap=None):
+        self.ddp = BucketedDataParallel(model, comm, lr=lr, momentum=momentum, bucket_mb=bucket_mb, overlap=overlap)
         self.bytes_per_step = self.ddp.bytes_per_step
 
     @property
@@ -198,7 +198,7 @@ def build_grad_sync(kind: str, model: torch.nn.Module, comm: Optional[Communicat
     if kind == "powersgd-api":
         return ReferencePowerSGDLoop(model, comm, lr, momentum, rank, seed=seed, native_reducer=True)
     if kind == "dense":
-        return _DenseSync(model, comm, lr, momentum, bucket_mb)
+        return _DenseSync(model, comm, lr, momentum, bucket_mb, overlap=kw.get("overlap"))
     if kind == "dense-ref":
         return ReferenceDenseLoop(model, comm, lr, momentum)
     if kind in ("local-sgd-nesterov", "local-adamw"):

@@ -233,13 +233,18 @@ class StepRunner:
         # an eager step since capture may have re-bound a table the graph reads
         self._upload_gen = _UPLOADS.ensure(self._uploads, self._upload_gen)
         if self.side_graphs:
+            # comm graph FIRST: the command processor serves the queues roughly in doorbell
+            # order, so a comm graph submitted after the compute graph is dispatched only
+            # when the compute queue's kernel train has (nearly) drained — measured with
+            # tools/probe_queue.py (profiles/r2/queue_probe.md).  Submitted first, its
+            # flag-wait kernel is resident before the compute graph starts.
             t0 = time.perf_counter()
-            self.graphs[0].replay()          # waits (device flag) for the previous comm graph
-            t1 = time.perf_counter()
             with self._comm.on_side():
                 self.side_graphs[0].replay()  # each piece waits for its compute-graph signal
-            self.host_launch_s[0] += t1 - t0
-            self.host_launch_s[1] += time.perf_counter() - t1
+            t1 = time.perf_counter()
+            self.graphs[0].replay()          # waits (device flag) for the previous comm graph
+            self.host_launch_s[1] += t1 - t0
+            self.host_launch_s[0] += time.perf_counter() - t1
             self._joined = False
         else:
             t0 = time.perf_counter()

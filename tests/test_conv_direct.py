@@ -4,8 +4,10 @@ import torch
 import torch.nn.functional as F
 
 # (cin, cout, k, stride, pad, hw, batch) — the ResNet CIFAR-shape classes
+# small batches run split-K forward / grad-x (+ slab sum) and 1-image grad-W slices
 CASES = [(64, 64, 3, 1, 1, 8, 8), (128, 128, 3, 1, 1, 4, 16), (64, 128, 3, 2, 1, 8, 8), (3, 64, 7, 2, 3, 32, 4),
-         (128, 64, 3, 1, 1, 8, 4), (64, 192, 3, 1, 1, 4, 16)]
+         (128, 64, 3, 1, 1, 8, 4), (64, 192, 3, 1, 1, 4, 16), (64, 64, 3, 1, 1, 8, 64), (128, 128, 3, 1, 1, 4, 64),
+         (64, 64, 3, 1, 1, 8, 6)]
 
 
 @pytest.mark.gpu
@@ -39,7 +41,7 @@ def test_direct_conv_deterministic(device):
     from network_distributed_pytorch_amd.ops.conv import conv2d_direct
 
     torch.manual_seed(1)
-    x = torch.randn(64, 64, 8, 8, device=device, requires_grad=True)
+    x = torch.randn(64, 64, 8, 8, device=device, requires_grad=True)  # split-K at batch 64
     w = torch.randn(64, 64, 3, 3, device=device, requires_grad=True)
     outs = []
     for _ in range(2):
@@ -58,5 +60,17 @@ def test_direct_plan_rejects_other_shapes(device):
     x = torch.randn(8, 64, 16, 16, device=device)
     w = torch.randn(64, 64, 3, 3, device=device)
     assert direct_plan(x, w, 1, 1) is None
-    x = torch.randn(6, 64, 8, 8, device=device)   # batch not a multiple of the wgrad slice
-    assert direct_plan(x, w, 1, 1) is None
+    x = torch.randn(6, 128, 4, 4, device=device)  # batch not a multiple of the 4-image fwd tile
+    assert direct_plan(x, torch.randn(128, 128, 3, 3, device=device), 1, 1) is None
+
+
+@pytest.mark.gpu
+def test_direct_plan_adapts_to_batch(device):
+    """Strong-scaling shapes: split-K + finer grad-W slices at small batch, none at 512."""
+    from network_distributed_pytorch_amd.ops.conv import direct_plan
+
+    w = torch.randn(128, 128, 3, 3, device=device)
+    small = direct_plan(torch.randn(64, 128, 4, 4, device=device), w, 1, 1)
+    big = direct_plan(torch.randn(512, 128, 4, 4, device=device), w, 1, 1)
+    assert small[4] > 1 and small[5] > 1 and small[2] < big[2]
+    assert big[4] == 1 and big[5] == 1

@@ -86,3 +86,53 @@ def test_resnet18_native_convs_vs_fp64(device, mode):
             # one flipped ReLU in a batch-32 layer4 BN moved a single weight-grad row by
             # 0.15 of the max (cos 0.9998) on MI355X: bound the L2 error, keep a gross cap
             assert cos > 0.999 and rel2 < 0.05 and rel < 0.3, (which, n, float(cos), float(rel2), float(rel))
+
+
+@pytest.mark.gpu
+def test_toeplitz_expand_many_matches_single(device):
+    """One-launch W_big build of a whole ResNet's Toeplitz layers == per-layer builds."""
+    from network_distributed_pytorch_amd.ops._ext import ext
+
+    X = ext()
+    geoms = [(128, 4, 4, 256, 3, 3, 2, 1), (256, 2, 2, 256, 3, 3, 1, 1), (128, 4, 4, 256, 1, 1, 2, 0),
+             (256, 2, 2, 512, 3, 3, 2, 1), (512, 1, 1, 512, 3, 3, 1, 1), (256, 2, 2, 512, 1, 1, 2, 0),
+             (8, 3, 3, 16, 3, 3, 1, 1)]  # last: generic (non 1/2/4) map
+    torch.manual_seed(0)
+    entries, refs = [], []
+    for C, H, W, Co, kh, kw, s, p in geoms:
+        oh, ow = (H + 2 * p - kh) // s + 1, (W + 2 * p - kw) // s + 1
+        w = torch.randn(Co, C, kh, kw, device=device)
+        ref = torch.empty(Co * oh * ow, C * H * W, device=device)
+        X.toeplitz_expand(w, ref, [C, H, W, Co, kh, kw, s, p])
+        entries.append((w, torch.full_like(ref, float("nan")), [C, H, W, Co, kh, kw, s, p]))
+        refs.append(ref)
+    X.toeplitz_expand_many(entries)
+    for (_, got, g), ref in zip(entries, refs):
+        assert torch.equal(got, ref), g
+
+
+@pytest.mark.gpu
+def test_resnet_toeplitz_bank_one_launch_equals_per_layer(device):
+    """ResNet-18 forward+backward with the model-wide Toeplitz bank == without it."""
+    from network_distributed_pytorch_amd.models import build_resnet
+    from network_distributed_pytorch_amd.models.conv_gemm import GemmConv2d
+
+    torch.manual_seed(0)
+    outs = []
+    det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True  # MIOpen (layer2 downsample): no split-K atomics
+    for banked in (True, False):
+        torch.manual_seed(3)
+        m = build_resnet(18, 10).to(device)
+        if not banked:
+            for mod in m.modules():
+                if isinstance(mod, GemmConv2d):
+                    mod.bank = None
+        x = torch.randn(16, 3, 32, 32, device=device, generator=torch.Generator(device=device).manual_seed(1))
+        for _ in range(2):  # second pass: the bank's batched expand
+            m.zero_grad()
+            m(x).square().mean().backward()
+        outs.append([p.grad.clone() for p in m.parameters()])
+    torch.backends.cudnn.deterministic = det
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

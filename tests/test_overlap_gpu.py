@@ -146,7 +146,7 @@ def _train(device, kind, sync_kind, mode, overlap, steps=3, rank=4, groups=3):
     torch.manual_seed(5)
     model = _resnet(device) if kind == "resnet" else _EmbedNet().to(device)
     comm = Communicator(device=device)
-    kw = {"overlap": overlap, "groups": groups} if sync_kind == "powersgd" else {}
+    kw = {"overlap": overlap, "groups": groups} if sync_kind == "powersgd" else {"overlap": overlap}
     sync = build_grad_sync(sync_kind, model, comm, lr=1e-2, momentum=0.9, rank=rank, **kw)
     if sync_kind == "dense" and not overlap:
         sync.ddp.overlap = False

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Direct fp32-MFMA conv kernels vs MIOpen on ResNet-18's CIFAR shapes (batch 512).
+"""Direct fp32-MFMA conv kernels vs MIOpen on ResNet-18's CIFAR shapes (batch argv[1], default 512).
 
 Per shape: forward, grad-input and grad-weight time of the csrc/conv.hip kernels and of
 MIOpen (F.conv2d / aten.convolution_backward), each timed as 20 calls in one hipGraph.
@@ -52,13 +52,15 @@ for name, cin, cout, k, s, p, hw, cnt in SHAPES:
     x = torch.randn(B, cin, hw, hw, device=dev)
     w = torch.randn(cout, cin, k, k, device=dev) * 0.05
     plan = direct_plan(x, w, s, p)
-    geom, _, wi, dd = plan
+    geom, _, wi, dd, ksf, ksd = plan
     y = F.conv2d(x, w, stride=s, padding=p)
     g = torch.randn_like(y)
     yd = torch.empty_like(y)
     dx = torch.empty_like(x)
     dw = torch.empty_like(w)
     part = torch.empty((B // wi) * w.numel(), device=dev)
+    pf = torch.empty(ksf * y.numel(), device=dev) if ksf > 1 else None
+    pd = torch.empty(ksd * x.numel(), device=dev) if ksd > 1 else None
     oh = y.shape[2]
     fl = 2.0 * B * oh * oh * cout * cin * k * k
     t_mf = timeit(lambda: F.conv2d(x, w, stride=s, padding=p))
@@ -66,15 +68,15 @@ for name, cin, cout, k, s, p, hw, cnt in SHAPES:
                                                               [True, False, False]))
     t_mw = timeit(lambda: torch.ops.aten.convolution_backward(g, x, w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
                                                               [False, True, False]))
-    t_df = timeit(lambda: X.conv_fwd(x, w, yd, list(geom)))
-    t_dd = timeit(lambda: X.conv_dgrad(g, w, dx, list(geom))) if dd else float("nan")
+    t_df = timeit(lambda: X.conv_fwd(x, w, yd, list(geom), pf))
+    t_dd = timeit(lambda: X.conv_dgrad(g, w, dx, list(geom), pd)) if dd else float("nan")
     t_dw = timeit(lambda: X.conv_wgrad(x, g, part, dw, list(geom)))
-    X.conv_fwd(x, w, yd, list(geom))
+    X.conv_fwd(x, w, yd, list(geom), pf)
     err = (yd - y).abs().max().item() / y.abs().max().item()
     need_dx = name != "stem7x7s2"
     tot["mi"] += cnt * (t_mf + (t_md if need_dx else 0) + t_mw)
     tot["di"] += cnt * (t_df + ((t_dd if dd else t_md) if need_dx else 0) + t_dw)
     print(f"| {name} | {cnt} | {fl / 1e9:.2f} | {t_mf:.1f} | {t_df:.1f} | {t_md:.1f} | {t_dd:.1f} | {t_mw:.1f} | "
-          f"{t_dw:.1f} | {fl / t_df / 1e6:.1f} | {fl / t_dw / 1e6:.1f} |  (rel err fwd {err:.1e})")
+          f"{t_dw:.1f} | {fl / t_df / 1e6:.1f} | {fl / t_dw / 1e6:.1f} |  (rel err fwd {err:.1e}, ksplit {ksf}/{ksd}, wgrad imgs {wi})")
 print(f"\nper ResNet-18 step (these shapes, x count, grad-x only where needed): MIOpen {tot['mi']:.0f} us, "
       f"direct {tot['di']:.0f} us")
