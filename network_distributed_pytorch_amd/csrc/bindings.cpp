@@ -465,11 +465,11 @@ py::tuple conv_plan(const std::vector<int64_t>& geom, int64_t B) {
                         ndp::conv_ksplit(cls, g, (int)B, true));
 }
 
-float* conv_part(const c10::optional<torch::Tensor>& part, int ks, int64_t out_numel, const char* who) {
+float* conv_part(const c10::optional<torch::Tensor>& part, int ks, int64_t slab, const char* who) {
   if (ks <= 1) return nullptr;
   TORCH_CHECK(part.has_value(), who, ": split-K needs a part scratch tensor");
   check_f32(*part, "part");
-  TORCH_CHECK(part->numel() >= ks * out_numel, who, ": part scratch too small");
+  TORCH_CHECK(part->numel() >= ks * slab, who, ": part scratch too small");
   return part->data_ptr<float>();
 }
 
@@ -494,7 +494,8 @@ void conv_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, const std::vect
   conv_check(x, "x", B, g.C, g.H, g.W);
   conv_check(w, "w", g.Co, g.C, g.KH, g.KW);
   conv_check(y, "y", B, g.Co, g.OH, g.OW);
-  float* pp = conv_part(part, ndp::conv_ksplit(cls, g, B, false), y.numel(), "conv_fwd");
+  const int ks = ndp::conv_ksplit(cls, g, B, false);
+  float* pp = conv_part(part, ks, y.numel(), "conv_fwd");
   ndp::launch_conv_fwd(x.data_ptr<float>(), w.data_ptr<float>(), y.data_ptr<float>(), B, g, pp, cur_stream());
   check_launch("launch_conv_fwd");
 }
@@ -508,7 +509,11 @@ void conv_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, const std::
   conv_check(dy, "dy", B, g.Co, g.OH, g.OW);
   conv_check(w, "w", g.Co, g.C, g.KH, g.KW);
   conv_check(dx, "dx", B, g.C, g.H, g.W);
-  float* pp = conv_part(part, ndp::conv_ksplit(cls, g, B, true), dx.numel(), "conv_dgrad");
+  const int ks = ndp::conv_ksplit(cls, g, B, true);
+  // partial slabs are compact [B][C][OH*OW]-pixel tiles of the transposed product (for the
+  // stride-2 1x1 class the 4x4 map, before the even-pixel scatter)
+  const int64_t slab = (int64_t)B * g.C * (cls == 4 ? g.OH * g.OW : g.H * g.W);
+  float* pp = conv_part(part, ks, slab, "conv_dgrad");
   ndp::launch_conv_dgrad(dy.data_ptr<float>(), w.data_ptr<float>(), dx.data_ptr<float>(), B, g, pp, cur_stream());
   check_launch("launch_conv_dgrad");
 }

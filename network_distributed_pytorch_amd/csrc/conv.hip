@@ -202,10 +202,10 @@ struct ConvFwdCfg {
 // written transposed into the [kk][m] LDS image.  VEC=1 needs Cin % CK == 0 (float4 over
 // whole channels); the stem (Cin = 3 < CK) stages scalars.
 template <int R, int S, int ST, int PD, int H, int W, int CK, int BM, int IMGS, int WM, int NBUF, int KB, bool TRANSW,
-          bool VEC>
+          bool VEC, int UPS = 1>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                                       float* __restrict__ y, int Cin, int Kout, int cps,
-                                                       int64_t slab) {
+                                                       float* __restrict__ y, float* __restrict__ part, int Cin,
+                                                       int Kout, int cps, int64_t slab) {
   using G = ConvFwdCfg<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW>;
   constexpr int AE = (BM * G::KK + 3) / 4;  // float4 slots (scalar path: 4 scalars per slot)
   constexpr int A_PER_T = (AE + 255) / 256;
@@ -220,7 +220,6 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
   // split-K: workgroup z reduces channel chunks [ch0, ch0 + nchunks) into output slab z
   const int ch0 = blockIdx.z * cps;
   const int nchunks = min((Cin + CK - 1) / CK - ch0, cps);
-  y += (int64_t)blockIdx.z * slab;
 
   for (int i = tid; i < NBUF * G::B_SZ; i += 256) Bs[i] = 0.f;  // zero borders (never rewritten)
 
@@ -372,17 +371,50 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
     __syncthreads();
   }
 
+  // split-K (gridDim.z > 1): every workgroup stores its partial tile to its slab of `part`
+  // (compact [B][Kout][PQ] layout); conv_slab_sum(_ups) adds the slabs in z order
+  // (deterministic).  A last-arrival fixup inside this kernel was measured 4x slower: the
+  // agent-scope release fence writes the XCD's L2 back and the fixing workgroup re-reads
+  // the other XCDs' slabs from HBM on a serial dependency chain.
+  if (gridDim.z > 1) {
+    float* pz = part + (int64_t)blockIdx.z * slab;
+#pragma unroll
+    for (int tm = 0; tm < G::TM; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < G::TN; ++tn) {
+        const int n = (wn * G::TN + tn) * 32 + l32;
+        const int img = n / G::PQ, pq = n - img * G::PQ;
+        float* pb = pz + (int64_t)(b0 + img) * Kout * G::PQ + pq;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + (wm * G::TM + tm) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          pb[(int64_t)m * G::PQ] = acc[tm][tn][r];
+        }
+      }
+    return;
+  }
+
+  // UPS = 2 (grad-x of a 1x1 stride-2 conv): the result lands on the even pixels of a
+  // (2P) x (2Q) plane and the three odd neighbours of each are written as zeros
+  constexpr int OPQ = G::PQ * UPS * UPS;
 #pragma unroll
   for (int tm = 0; tm < G::TM; ++tm)
 #pragma unroll
     for (int tn = 0; tn < G::TN; ++tn) {
       const int n = (wn * G::TN + tn) * 32 + l32;
       const int img = n / G::PQ, pq = n - img * G::PQ;
-      float* yb = y + (int64_t)(b0 + img) * Kout * G::PQ + pq;
+      const int opix = UPS == 1 ? pq : (pq / G::Q) * UPS * (UPS * G::Q) + (pq % G::Q) * UPS;
+      float* yb = y + (int64_t)(b0 + img) * Kout * OPQ + opix;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + (wm * G::TM + tm) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        yb[(int64_t)m * G::PQ] = acc[tm][tn][r];
+        float* d = yb + (int64_t)m * OPQ;
+        d[0] = acc[tm][tn][r];
+        if constexpr (UPS == 2) {
+          d[1] = 0.f;
+          d[2 * G::Q] = 0.f;
+          d[2 * G::Q + 1] = 0.f;
+        }
       }
     }
 }
@@ -555,6 +587,30 @@ __global__ __launch_bounds__(256) void conv_slab_sum_kernel(const float* __restr
   }
 }
 
+// split-K sum for the stride-2 1x1 grad-x: dx[b, c, 2p + i, 2q + j] = (i == j == 0) ?
+// sum_z part[z][b][c][p][q] : 0; one thread per float4 of dx (two output rows of 8 columns
+// = 4 float4; PQ = 16 compact pixels per plane)
+__global__ __launch_bounds__(256) void conv_slab_sum_ups_kernel(const float* __restrict__ part, float* __restrict__ dx,
+                                                                int64_t slab, int n_slices) {
+  const int64_t i4 = (int64_t)blockIdx.x * 256 + threadIdx.x;  // float4 index into dx
+  if (i4 * 4 >= slab * 4) return;                              // dx has 4x the compact elements
+  const int64_t plane = i4 / 16, r4 = i4 - plane * 16;         // 16 float4 per 8x8 plane
+  const int row = (int)(r4 >> 1), half = (int)(r4 & 1);        // 2 float4 per 8-wide row
+  f32x4c v = {0.f, 0.f, 0.f, 0.f};
+  if ((row & 1) == 0) {
+    const int p = row >> 1, q0 = half * 2;                    // this float4 covers q = q0, q0 + 1
+    const float* src = part + plane * 16 + p * 4 + q0;
+    float a = 0.f, b = 0.f;
+    for (int z = 0; z < n_slices; ++z) {
+      a += src[z * slab];
+      b += src[z * slab + 1];
+    }
+    v.x = a;
+    v.z = b;
+  }
+  *reinterpret_cast<f32x4c*>(dx + i4 * 4) = v;
+}
+
 // ---- dispatch -----------------------------------------------------------------------------
 template <typename KernelT>
 static void set_lds(KernelT k, size_t bytes) {
@@ -562,26 +618,32 @@ static void set_lds(KernelT k, size_t bytes) {
 }
 
 // ksplit > 1: the ksplit workgroups of an output tile each reduce 1/ksplit of the input
-// channels into their own slab of `part`; conv_slab_sum adds the slabs in split order
+// channels into their own slab of `part`; conv_slab_sum(_ups) adds the slabs in split order
 // (deterministic).  Used where B / IMGS * Kout / BM alone cannot fill the 256 CUs
 // (small per-GPU batches: the strong-scaling shapes 512 / N).
 template <int R, int S, int ST, int PD, int H, int W, int CK, int BM, int IMGS, int WM, int NBUF, int KB, bool TRANSW,
-          bool VEC>
+          bool VEC, int UPS = 1>
 static void run_fwd(const float* x, const float* w, float* y, int B, int Cin, int Kout, int ksplit, float* part,
                     hipStream_t s) {
   using G = ConvFwdCfg<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW>;
-  auto k = conv_fwd_kernel<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW, VEC>;
+  auto k = conv_fwd_kernel<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW, VEC, UPS>;
   static bool attr = false;  // once per instantiation (> 64 KiB of LDS needs the opt-in)
   if (!attr) { set_lds(k, G::LDS_BYTES); attr = true; }
   const int nchunks = (Cin + CK - 1) / CK;
   if (ksplit < 1 || part == nullptr) ksplit = 1;
   const int cps = (nchunks + ksplit - 1) / ksplit;
   ksplit = (nchunks + cps - 1) / cps;
-  const int64_t n = (int64_t)B * Kout * G::PQ;
-  hipLaunchKernelGGL(k, dim3(B / IMGS, Kout / BM, ksplit), dim3(256), G::LDS_BYTES, s, x, w, ksplit > 1 ? part : y,
-                     Cin, Kout, cps, n);
-  if (ksplit > 1)
-    hipLaunchKernelGGL(conv_slab_sum_kernel, dim3((unsigned)((n / 4 + 15) / 16)), dim3(256), 0, s, part, y, n, ksplit);
+  const int64_t slab = (int64_t)B * Kout * G::PQ;  // compact partial tile layout
+  hipLaunchKernelGGL(k, dim3(B / IMGS, Kout / BM, ksplit), dim3(256), G::LDS_BYTES, s, x, w, y, part, Cin, Kout, cps,
+                     slab);
+  if (ksplit > 1) {
+    if constexpr (UPS == 1)
+      hipLaunchKernelGGL(conv_slab_sum_kernel, dim3((unsigned)((slab / 4 + 15) / 16)), dim3(256), 0, s, part, y, slab,
+                         ksplit);
+    else
+      hipLaunchKernelGGL(conv_slab_sum_ups_kernel, dim3((unsigned)((slab + 255) / 256)), dim3(256), 0, s, part, y, slab,
+                         ksplit);
+  }
 }
 
 template <int R, int S, int ST, int PD, int H, int W, int CB, int BM, int NW, int NBPW, int KB>
@@ -603,6 +665,9 @@ static void run_wgrad(const float* x, const float* dy, float* part, float* dw, i
 //   id 1: 3x3 s1 p1 on 4x4   (ResNet layer2)           C, K % 64 == 0
 //   id 2: 3x3 s2 p1 8x8->4x4 (layer2 first conv)       C % 32 == 0, K % 64 == 0
 //   id 3: 7x7 s2 p3 32x32->16x16, C = 3 (stem)         K % 64 == 0
+//   id 4: 1x1 s2 p0 8x8->4x4 (layer2 downsample)        C % 32 == 0, K % 64 == 0;
+//         grad-x = the 1x1 transposed product on the 4x4 map, written to the even pixels
+//         of the 8x8 plane (UPS = 2 epilogue, odd pixels zero)
 int conv_direct_class(const ConvGeom& g) {
   if (g.KH == 3 && g.KW == 3 && g.pad == 1 && g.stride == 1 && g.H == 8 && g.W == 8 && g.C % 64 == 0 && g.Co % 64 == 0)
     return 0;
@@ -612,6 +677,8 @@ int conv_direct_class(const ConvGeom& g) {
     return 2;
   if (g.KH == 7 && g.KW == 7 && g.pad == 3 && g.stride == 2 && g.H == 32 && g.W == 32 && g.C == 3 && g.Co % 64 == 0)
     return 3;
+  if (g.KH == 1 && g.KW == 1 && g.pad == 0 && g.stride == 2 && g.H == 8 && g.W == 8 && g.C % 64 == 0 && g.Co % 64 == 0)
+    return 4;
   return -1;
 }
 
@@ -642,7 +709,7 @@ static int pow2_floor(int v) {
 // images per grad-W slice: the class default, lowered (power of two dividing B) until the
 // grid has >= kFillWgs workgroups.  Workgroups per slice = (Kout / 32) * ceil(Cin / CB).
 int conv_wgrad_imgs(int cls, const ConvGeom& g, int B) {
-  int def = cls == 0 ? (conv_variant() == 1 ? 2 : 4) : cls == 1 ? 16 : cls == 2 ? 8 : 2;
+  int def = cls == 0 ? (conv_variant() == 1 ? 2 : 4) : cls == 1 ? 16 : cls == 2 ? 8 : cls == 4 ? 8 : 2;
   const int cb = cls == 3 ? 3 : 32;
   const int per_slice = (g.Co / 32) * ((g.C + cb - 1) / cb);
   while (def > 1 && (B / def) * per_slice < kFillWgs && B % (def / 2) == 0) def /= 2;
@@ -660,7 +727,7 @@ int conv_ksplit(int cls, const ConvGeom& g, int B, bool dgrad) {
   while (ks * 2 <= nchunks && base * ks < kFillWgs) ks *= 2;
   return pow2_floor(ks);
 }
-bool conv_dgrad_direct(int cls) { return cls == 0 || cls == 1; }
+bool conv_dgrad_direct(int cls) { return cls == 0 || cls == 1 || cls == 4; }
 void launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s) {
   const int cls = conv_direct_class(g);
   const int ks = conv_ksplit(cls, g, B, false);
@@ -672,6 +739,7 @@ void launch_conv_fwd(const float* x, const float* w, float* y, int B, const Conv
     case 1: run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s); break;
     case 2: run_fwd<3, 3, 2, 1, 8, 8, 8, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s); break;
     case 3: run_fwd<7, 7, 2, 3, 32, 32, 4, 64, 1, 2, 1, 7, false, false>(x, w, y, B, g.C, g.Co, 1, nullptr, s); break;
+    case 4: run_fwd<1, 1, 2, 0, 8, 8, 8, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s); break;
     default: break;
   }
 }
@@ -687,6 +755,7 @@ void launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const 
       else run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s);
       break;
     case 1: run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s); break;
+    case 4: run_fwd<1, 1, 1, 0, 4, 4, 8, 64, 4, 2, 2, 4, true, true, 2>(dy, w, dx, B, g.Co, g.C, ks, part, s); break;
     default: break;
   }
 }
@@ -701,6 +770,7 @@ void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, 
     case 1: run_wgrad<3, 3, 1, 1, 4, 4, 32, 32, 3, 3, 4>(x, dy, part, dw, B, g.C, g.Co, imgs, s); break;
     case 2: run_wgrad<3, 3, 2, 1, 8, 8, 32, 32, 3, 3, 4>(x, dy, part, dw, B, g.C, g.Co, imgs, s); break;
     case 3: run_wgrad<7, 7, 2, 3, 32, 32, 3, 32, 5, 1, 4>(x, dy, part, dw, B, g.C, g.Co, imgs, s); break;
+    case 4: run_wgrad<1, 1, 2, 0, 8, 8, 32, 32, 1, 1, 4>(x, dy, part, dw, B, g.C, g.Co, imgs, s); break;
     default: break;
   }
 }

@@ -152,7 +152,8 @@ int conv_fwd_imgs(int cls);
 int conv_wgrad_imgs(int cls, const ConvGeom& g, int B);
 bool conv_dgrad_direct(int cls);
 // split-K factor (1 = none) of the forward / grad-x kernel for batch B; with ksplit > 1 the
-// launchers need `part` scratch of ksplit * numel(output) floats
+// launchers need `part` scratch of ksplit * (compact output) floats: B * outC * OH * OW
+// (the stride-2 1x1 grad-x: B * C * 4 * 4 before its even-pixel scatter)
 int conv_ksplit(int cls, const ConvGeom& g, int B, bool dgrad);
 void launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s);
 void launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, float* part,

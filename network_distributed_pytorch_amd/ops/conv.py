@@ -2,9 +2,11 @@
 
 ``conv2d_direct(x, weight, stride, padding)`` runs forward, grad-input and grad-weight on
 hand-written gfx950 kernels for the shape classes the extension reports through
-``conv_plan`` (ResNet stem 7x7/2 on 32x32, layer1 3x3 on 8x8, layer2 3x3 on 4x4 and its
-strided 8x8->4x4 entry conv).  Grad-input of the strided classes goes to MIOpen
-(``aten.convolution_backward``); the stem's input never needs a gradient.
+``conv_plan`` (ResNet stem 7x7/2 on 32x32, layer1 3x3 on 8x8, layer2 3x3 on 4x4, its
+strided 8x8->4x4 entry conv and its 1x1/2 downsample).  Grad-input of the strided 3x3 class
+goes to MIOpen (``aten.convolution_backward``); the 1x1/2 downsample's grad-input is the
+transposed 1x1 product written to the even pixels (native); the stem's input never needs a
+gradient.
 :func:`direct_plan` returns None for every other geometry, so callers keep their MIOpen /
 Toeplitz paths there.
 """
@@ -21,6 +23,7 @@ __all__ = ["direct_plan", "conv2d_direct", "DirectConvFn", "side_stream"]
 
 _PLANS: dict = {}
 _SIDE: dict = {}
+
 # grad-W on a side stream measured SLOWER on ResNet-18 (2.47 vs 2.37 ms/step: the two
 # halves contend for CUs / L2 instead of filling gaps), so it is opt-in.
 FORK_WGRAD = os.environ.get("NDP_CONV_FORK", "0") == "1"
@@ -99,7 +102,9 @@ class DirectConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if dgrad_direct:
                 dx = torch.empty_like(x)
-                part = torch.empty(ks_dgrad * dx.numel(), device=x.device, dtype=x.dtype) if ks_dgrad > 1 else None
+                part = None
+                if ks_dgrad > 1:  # compact partials: numel(dy) * C / Co floats per split
+                    part = torch.empty(ks_dgrad * (dy.numel() // geom[3]) * geom[0], device=x.device, dtype=x.dtype)
                 ext().conv_dgrad(dy, weight, dx, list(geom), part)
             else:
                 dx = torch.ops.aten.convolution_backward(dy, x, weight, None, [s, s], [p, p], [1, 1], False, [0, 0],

@@ -7,7 +7,7 @@ import torch.nn.functional as F
 # small batches run split-K forward / grad-x (+ slab sum) and 1-image grad-W slices
 CASES = [(64, 64, 3, 1, 1, 8, 8), (128, 128, 3, 1, 1, 4, 16), (64, 128, 3, 2, 1, 8, 8), (3, 64, 7, 2, 3, 32, 4),
          (128, 64, 3, 1, 1, 8, 4), (64, 192, 3, 1, 1, 4, 16), (64, 64, 3, 1, 1, 8, 64), (128, 128, 3, 1, 1, 4, 64),
-         (64, 64, 3, 1, 1, 8, 6)]
+         (64, 64, 3, 1, 1, 8, 6), (64, 128, 1, 2, 0, 8, 8), (64, 128, 1, 2, 0, 8, 64), (256, 512, 1, 2, 0, 8, 16)]
 
 
 @pytest.mark.gpu
