@@ -146,7 +146,7 @@ class BucketedDataParallel:
 
     def _allreduce(self, b: int):
         s, e, _ = self.buckets[b]
-        if self.comm.active:
+        if self.comm.has_traffic:  # N > 1, or a 1-GPU link emulation (pacing only, no data)
             self._works[b] = self.comm.all_reduce(self.g[s:e], async_op=True)
 
     def _launch(self, b: int):
