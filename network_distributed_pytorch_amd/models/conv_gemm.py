@@ -76,6 +76,8 @@ class ToeplitzBank:
     ``w_big`` saved for backward is rebuilt by the NEXT forward, i.e. after that backward.
     """
 
+    MAX_EXPAND = 24  # csrc/ndp_kernels.h kMaxExpand
+
     def __init__(self):
         self.members: list = []  # [(layer, geom, w_big)]
         self._index: dict = {}
@@ -93,8 +95,10 @@ class ToeplitzBank:
             else:
                 self.members[i] = (layer, geom, w_big)
             return w_big
-        if i == 0:
-            ext().toeplitz_expand_many([(m.weight, wb, list(g)) for m, g, wb in self.members])
+        if i == 0:  # <= MAX_EXPAND layers per launch (kernel-argument table)
+            batch = [(m.weight, wb, list(g)) for m, g, wb in self.members]
+            for j in range(0, len(batch), self.MAX_EXPAND):
+                ext().toeplitz_expand_many(batch[j: j + self.MAX_EXPAND])
         return self.members[i][2]
 
 
