@@ -535,6 +535,26 @@ void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor part, torch::Te
   check_launch("launch_conv_wgrad");
 }
 
+void embedding_backward(torch::Tensor ids, torch::Tensor gout, torch::Tensor gw, int64_t pad, torch::Tensor perm,
+                        torch::Tensor row_start, torch::Tensor row_cnt) {
+  check_dev(ids, "ids"); check_f32(gout, "grad_out"); check_f32(gw, "grad_weight");
+  check_dev(perm, "perm"); check_dev(row_start, "row_start"); check_dev(row_cnt, "row_cnt");
+  TORCH_CHECK(ids.scalar_type() == torch::kInt64 && ids.is_contiguous(), "embedding_backward: ids must be contiguous int64");
+  TORCH_CHECK(gw.dim() == 2 && gw.size(1) % 4 == 0, "embedding_backward: grad_weight [V, D] with D % 4 == 0");
+  const int64_t T = ids.numel(), V = gw.size(0), D = gw.size(1);
+  TORCH_CHECK(gout.numel() == T * D, "embedding_backward: grad_out must be [T, D]");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(gout.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(gw.data_ptr()) & 15) == 0,
+              "embedding_backward: 16-B aligned grad tensors");
+  for (auto* t : {&perm, &row_start, &row_cnt})
+    TORCH_CHECK(t->scalar_type() == torch::kInt32 && t->is_contiguous(), "embedding_backward: int32 scratch");
+  TORCH_CHECK(perm.numel() >= T && row_start.numel() >= V && row_cnt.numel() >= V, "embedding_backward: scratch too small");
+  TORCH_CHECK(T < (1LL << 29) && V < (1LL << 31), "embedding_backward: too many tokens / rows");
+  ndp::launch_embedding_backward(ids.data_ptr<int64_t>(), (int)T, gout.data_ptr<float>(), (int)V, (int)D, (int)pad,
+                                 perm.data_ptr<int32_t>(), row_start.data_ptr<int32_t>(), row_cnt.data_ptr<int32_t>(),
+                                 gw.data_ptr<float>(), cur_stream());
+  check_launch("launch_embedding_backward");
+}
+
 // q/k/v/o: [B, S, H, 64] fp32 contiguous (== the [B, S, H*64] projections); mask [B, S] int32 or None
 void attn_check(const torch::Tensor& t, const char* n, const torch::Tensor& q) {
   check_f32(t, n);
@@ -640,6 +660,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("geom"),
         py::arg("part") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
+  m.def("embedding_backward", &embedding_backward);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   register_comm(m);

@@ -124,6 +124,15 @@ void launch_bn_bwd(const float* dy, const float* y, const float* x, const float*
                    int N, int C, int HW, int S, int relu, int single, hipStream_t s);
 }  // namespace ndp
 
+// ---- embedding backward (embedding.hip) -------------------------------------------------
+// grad_W [V, D] (dense, zeros for unreferenced rows and `pad`) from ids [T] int64 and
+// grad_out [T, D]; perm [T], row_start [V] int32 scratch, row_cnt [V] int32 zeroed once
+// at allocation (the kernels re-arm it).  Deterministic (fixed summation order).
+namespace ndp {
+void launch_embedding_backward(const int64_t* ids, int T, const float* gout, int V, int D, int pad, int* perm,
+                               int* row_start, int* row_cnt, float* gw, hipStream_t s);
+}  // namespace ndp
+
 // ---- convolutions, NCHW fp32 (conv.hip) -------------------------------------------------
 namespace ndp {
 struct ConvGeom {

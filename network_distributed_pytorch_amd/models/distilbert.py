@@ -24,6 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.attention import attention, fused_ok
+from ..ops.embedding import Embedding
 
 __all__ = ["DistilBertConfig", "DistilBertForSequenceClassification", "distilbert_base"]
 
@@ -49,7 +50,8 @@ class DistilBertConfig:
 class Embeddings(nn.Module):
     def __init__(self, c: DistilBertConfig):
         super().__init__()
-        self.word_embeddings = nn.Embedding(c.vocab_size, c.dim, padding_idx=c.pad_token_id)
+        # native deterministic backward (graph-replayable; ops/embedding.py)
+        self.word_embeddings = Embedding(c.vocab_size, c.dim, padding_idx=c.pad_token_id)
         self.position_embeddings = nn.Embedding(c.max_position_embeddings, c.dim)
         self.LayerNorm = nn.LayerNorm(c.dim, eps=c.layer_norm_eps)
         self.dropout = nn.Dropout(c.dropout)
