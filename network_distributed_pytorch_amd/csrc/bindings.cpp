@@ -535,6 +535,18 @@ void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor part, torch::Te
   check_launch("launch_conv_wgrad");
 }
 
+// db = g.sum(0) for g [M, N] contiguous fp32, N % 4 == 0 (deterministic, graph-safe)
+void colsum(torch::Tensor g, torch::Tensor out) {
+  check_f32(g, "g"); check_f32(out, "out");
+  TORCH_CHECK(g.dim() == 2 && g.size(1) % 4 == 0 && out.numel() == g.size(1), "colsum: g [M, N] with N % 4 == 0");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(g.data_ptr()) & 15) == 0, "colsum: 16-B aligned input");
+  const int64_t M = g.size(0);
+  const int N = (int)g.size(1);
+  auto part = torch::empty({(int64_t)ndp::colsum_chunks(M, N) * N}, g.options());
+  ndp::launch_colsum(g.data_ptr<float>(), M, N, part.data_ptr<float>(), out.data_ptr<float>(), cur_stream());
+  check_launch("launch_colsum");
+}
+
 void embedding_backward(torch::Tensor ids, torch::Tensor gout, torch::Tensor gw, int64_t pad, torch::Tensor perm,
                         torch::Tensor row_start, torch::Tensor row_cnt) {
   check_dev(ids, "ids"); check_f32(gout, "grad_out"); check_f32(gw, "grad_weight");
@@ -661,6 +673,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("part") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
   m.def("embedding_backward", &embedding_backward);
+  m.def("colsum", &colsum);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   register_comm(m);

@@ -180,7 +180,38 @@ __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
 template <int R, int S, int ST, int PD, int H, int W, int CK, int BM, int IMGS, int WM, int NBUF, int KB, bool TRANSW>
 struct ConvFwdCfg {
   static constexpr int P = (H + 2 * PD - R) / ST + 1, Q = (W + 2 * PD - S) / ST + 1, PQ = P * Q;
-  static constexpr int Hp = H + 2 * PD, Wp = W + 2 * PD, HWp = Hp * Wp, HW = H * W;
+  // Bank-conflict-free LDS image (ds_read_b32: bank = dword % 32, one 32-lane half-wave per
+  // LDS cycle; the B read of a half-wave is 32 output pixels at pixel_base + tap):
+  //  * 8x8 stride 1, one image per tile: lanes cover 8 rows x 4 columns (MAP 1) of a
+  //    12-wide row stride -> row offsets 12p mod 32 = {0,12,24,4,16,28,8,20}: 32 banks;
+  //  * 4x4 stride 1, 2 images per half-wave: row stride 8 (4 rows x 4 columns = banks
+  //    {0-3, 8-11, 16-19, 24-27}) and an image stride = 4 (mod 32) for the second image;
+  //  * 8x8 stride 2, 2 images per half-wave: row stride 12 (rows 24p = {0,24,16,8} mod 32,
+  //    even columns -> the 16 even banks) and an image stride = 1 (mod 32): odd banks.
+  // (Measured before: 34-54 % of LDS cycles were conflict cycles, profiles/r2/pmc_counters.md.)
+  static constexpr int LAYOUT = (ST == 1 && H == 8 && W == 8 && PD == 1 && IMGS == 1) ? 1
+                                : (ST == 1 && H == 4 && W == 4 && IMGS % 2 == 0)      ? 2
+                                : (ST == 2 && H == 8 && W == 8 && IMGS % 2 == 0)      ? 3
+                                                                                       : 0;
+  static constexpr int Hp = H + 2 * PD;
+  static constexpr int Wp = LAYOUT == 1 ? 12 : LAYOUT == 2 ? 8 : LAYOUT == 3 ? 12 : W + 2 * PD;
+  static constexpr int HWp = Hp * Wp, HW = H * W;
+  static constexpr int IPAD0 = LAYOUT == 2 ? 4 : LAYOUT == 3 ? 1 : 0;  // target image stride mod 32
+  static constexpr int IMGSTR = LAYOUT >= 2 ? (CK * HWp + 31) / 32 * 32 + IPAD0 : CK * HWp;
+  static_assert(Wp >= W + 2 * PD, "row stride holds the zero border");
+  // output pixel n of the tile -> (image, row, column)
+  __device__ static __forceinline__ void pix(int n, int& img, int& p, int& q) {
+    if constexpr (LAYOUT == 1) {
+      img = 0;
+      p = (n & 31) >> 2;
+      q = (n & 3) + 4 * (n >> 5);
+    } else {
+      img = n / PQ;
+      const int pq = n - img * PQ;
+      p = pq / Q;
+      q = pq - p * Q;
+    }
+  }
   static constexpr int RS = R * S, KK = CK * RS;
   static constexpr int NSTEP = (CK / 2) * RS, NBLK = NSTEP / KB;
   static constexpr int BN = IMGS * PQ;
@@ -188,7 +219,7 @@ struct ConvFwdCfg {
   static constexpr int TM = BM / 32 / WM, TN = BN / 32 / WN;
   static constexpr int LDA = BM + 1;    // [kk][m], odd stride: conflict-free transposing writes
   static constexpr int A_SZ = KK * LDA;
-  static constexpr int B_SZ = IMGS * CK * HWp;
+  static constexpr int B_SZ = IMGS * IMGSTR;
   // A staging: float4 rows when every chunk is whole channels and rows are 16-B aligned
   static constexpr int B4 = IMGS * CK * HW / 4, B_PER_T = (B4 + 255) / 256;
   static constexpr size_t LDS_BYTES = (size_t)NBUF * (A_SZ + B_SZ) * sizeof(float);
@@ -229,9 +260,9 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
 #pragma unroll
   for (int tn = 0; tn < G::TN; ++tn) {
     const int n = (wn * G::TN + tn) * 32 + l32;
-    const int img = n / G::PQ, pq = n - img * G::PQ;
-    const int p = pq / G::Q, q = pq - p * G::Q;
-    b_base[tn] = img * CK * G::HWp + h * (CK / 2) * G::HWp + p * ST * G::Wp + q * ST;
+    int img, p, q;
+    G::pix(n, img, p, q);
+    b_base[tn] = img * G::IMGSTR + h * (CK / 2) * G::HWp + p * ST * G::Wp + q * ST;
   }
 
   f32x4c ra[A_PER_T];
@@ -310,7 +341,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
         const int img = e / (CK * G::HW / 4), rem = 4 * (e - img * (CK * G::HW / 4));
         const int c = rem / G::HW, hw = rem - c * G::HW;
         const int hh = hw / W, ww = hw - hh * W;
-        float* d = B + img * CK * G::HWp + c * G::HWp + (hh + PD) * G::Wp + ww + PD;
+        float* d = B + img * G::IMGSTR + c * G::HWp + (hh + PD) * G::Wp + ww + PD;
         d[0] = rb[i].x; d[1] = rb[i].y; d[2] = rb[i].z; d[3] = rb[i].w;
       }
     }
@@ -383,8 +414,9 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
 #pragma unroll
       for (int tn = 0; tn < G::TN; ++tn) {
         const int n = (wn * G::TN + tn) * 32 + l32;
-        const int img = n / G::PQ, pq = n - img * G::PQ;
-        float* pb = pz + (int64_t)(b0 + img) * Kout * G::PQ + pq;
+        int img, p, q;
+        G::pix(n, img, p, q);
+        float* pb = pz + (int64_t)(b0 + img) * Kout * G::PQ + p * G::Q + q;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int m = m0 + (wm * G::TM + tm) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -402,8 +434,9 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
 #pragma unroll
     for (int tn = 0; tn < G::TN; ++tn) {
       const int n = (wn * G::TN + tn) * 32 + l32;
-      const int img = n / G::PQ, pq = n - img * G::PQ;
-      const int opix = UPS == 1 ? pq : (pq / G::Q) * UPS * (UPS * G::Q) + (pq % G::Q) * UPS;
+      int img, pp, qq;
+      G::pix(n, img, pp, qq);
+      const int opix = UPS == 1 ? pp * G::Q + qq : pp * UPS * (UPS * G::Q) + qq * UPS;
       float* yb = y + (int64_t)(b0 + img) * Kout * OPQ + opix;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {

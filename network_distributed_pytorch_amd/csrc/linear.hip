@@ -1,0 +1,67 @@
+// Linear-layer bias gradient: db[n] = sum_m g[m, n] — deterministic and hipGraph-safe.
+//
+// PyTorch-ROCm computes it with at::native::reduce_kernel; for the DistilBERT shapes
+// (8192 x 768 / 3072 rows x columns) that reduction is multi-block with a global staging
+// buffer and, replayed inside a captured hipGraph, returned garbage for some layers
+// (k_lin / lin1 bias grads off by 5e-2 while eager was exact — tools/
+// diag_bert_graph_vs_eager.py), besides costing 18 µs a call.  Here:
+//   pass 1: workgroup (column strip of 256 columns, row chunk) — 64 lanes own 4 columns
+//           each (float4 loads, whole rows coalesced), 4 lane groups stride the chunk's
+//           rows; the 4 group sums are added in LDS in fixed order -> part[chunk][n];
+//   pass 2: db[n] = sum over chunks in order.
+// Fixed summation order everywhere: bitwise reproducible, no atomics, no semaphores.
+#include <hip/hip_runtime.h>
+#include "ndp_kernels.h"
+
+namespace ndp {
+
+typedef float f4l __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ g, int64_t M, int N,
+                                                             int rows_per_chunk, float* __restrict__ part) {
+  __shared__ f4l red[4][64];
+  const int c4 = blockIdx.x * 64 + (threadIdx.x & 63);  // float4 column index
+  const int grp = threadIdx.x >> 6;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
+  const int64_t r1 = min(M, r0 + rows_per_chunk);
+  f4l acc = {0.f, 0.f, 0.f, 0.f};
+  if (4 * c4 < N) {
+    const f4l* src = reinterpret_cast<const f4l*>(g) + c4;
+    const int64_t n4 = N / 4;
+    for (int64_t r = r0 + grp; r < r1; r += 4) acc += src[r * n4];
+  }
+  red[grp][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (grp == 0 && 4 * c4 < N) {
+    const int l = threadIdx.x;
+    const f4l s = ((red[0][l] + red[1][l]) + red[2][l]) + red[3][l];
+    reinterpret_cast<f4l*>(part + (int64_t)blockIdx.y * N)[c4] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int chunks, int N,
+                                                           float* __restrict__ out) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int c = 0; c < chunks; ++c) s += part[(int64_t)c * N + n];
+  out[n] = s;
+}
+
+int colsum_chunks(int64_t M, int N) {
+  const int strips = (N / 4 + 63) / 64;
+  int chunks = (256 + strips - 1) / strips;          // ~256 workgroups in pass 1
+  const int64_t max_chunks = (M + 31) / 32;          // >= 32 rows per chunk
+  if (chunks > max_chunks) chunks = (int)max_chunks;
+  return chunks < 1 ? 1 : chunks;
+}
+
+void launch_colsum(const float* g, int64_t M, int N, float* part, float* out, hipStream_t s) {
+  const int chunks = colsum_chunks(M, N);
+  const int rpc = (int)((M + chunks - 1) / chunks);
+  const int strips = (N / 4 + 63) / 64;
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3(strips, chunks), dim3(256), 0, s, g, M, N, rpc, part);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((N + 255) / 256), dim3(256), 0, s, part, chunks, N, out);
+}
+
+}  // namespace ndp

@@ -129,6 +129,10 @@ void launch_bn_bwd(const float* dy, const float* y, const float* x, const float*
 // grad_out [T, D]; perm [T], row_start [V] int32 scratch, row_cnt [V] int32 zeroed once
 // at allocation (the kernels re-arm it).  Deterministic (fixed summation order).
 namespace ndp {
+// column sums of a row-major [M, N] fp32 matrix (N % 4 == 0): Linear bias gradient
+// (linear.hip); part: colsum_chunks(M, N) * N floats of scratch
+int colsum_chunks(int64_t M, int N);
+void launch_colsum(const float* g, int64_t M, int N, float* part, float* out, hipStream_t s);
 void launch_embedding_backward(const int64_t* ids, int T, const float* gout, int V, int D, int pad, int* perm,
                                int* row_start, int* row_cnt, float* gw, hipStream_t s);
 }  // namespace ndp

@@ -25,6 +25,7 @@ import torch.nn.functional as F
 
 from ..ops.attention import attention, fused_ok
 from ..ops.embedding import Embedding
+from ..ops.linear import Linear
 
 __all__ = ["DistilBertConfig", "DistilBertForSequenceClassification", "distilbert_base"]
 
@@ -68,10 +69,10 @@ class MultiHeadSelfAttention(nn.Module):
         super().__init__()
         self.n_heads = c.n_heads
         self.dim = c.dim
-        self.q_lin = nn.Linear(c.dim, c.dim)
-        self.k_lin = nn.Linear(c.dim, c.dim)
-        self.v_lin = nn.Linear(c.dim, c.dim)
-        self.out_lin = nn.Linear(c.dim, c.dim)
+        self.q_lin = Linear(c.dim, c.dim)
+        self.k_lin = Linear(c.dim, c.dim)
+        self.v_lin = Linear(c.dim, c.dim)
+        self.out_lin = Linear(c.dim, c.dim)
         self.dropout = nn.Dropout(c.attention_dropout)
         self.fused = c.fused_attention
 
@@ -102,8 +103,8 @@ class MultiHeadSelfAttention(nn.Module):
 class FFN(nn.Module):
     def __init__(self, c: DistilBertConfig):
         super().__init__()
-        self.lin1 = nn.Linear(c.dim, c.hidden_dim)
-        self.lin2 = nn.Linear(c.hidden_dim, c.dim)
+        self.lin1 = Linear(c.dim, c.hidden_dim)
+        self.lin2 = Linear(c.hidden_dim, c.dim)
         self.dropout = nn.Dropout(c.dropout)
 
     def forward(self, x):
@@ -164,8 +165,8 @@ class DistilBertForSequenceClassification(nn.Module):
         c = config or DistilBertConfig()
         self.config = c
         self.distilbert = DistilBertModel(c)
-        self.pre_classifier = nn.Linear(c.dim, c.dim)
-        self.classifier = nn.Linear(c.dim, c.num_labels)
+        self.pre_classifier = Linear(c.dim, c.dim)
+        self.classifier = Linear(c.dim, c.num_labels)
         self.dropout = nn.Dropout(c.seq_classif_dropout)
         self.apply(self._init)
 

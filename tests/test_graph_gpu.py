@@ -145,3 +145,34 @@ def test_resnet18_graph_matches_eager(device):
     print(f"eager-vs-eager {noise:.3e}  graph-vs-eager {diff:.3e}")
     assert noise == 0.0, noise
     assert diff == 0.0, diff
+
+
+def test_distilbert_graph_replays_match_eager(device):
+    """DistilBERT (2 layers, dropout 0) + PowerSGD r=4: 10 hipGraph replays over 4 rotating
+    batches == eager.  Regression test for the rocPRIM-sort embedding backward that faulted
+    on the 2nd replay (now the native ops/embedding.py backward)."""
+    from network_distributed_pytorch_amd.models import distilbert_base
+    from network_distributed_pytorch_amd.utils.data import SyntheticIMDb
+
+    ds = SyntheticIMDb(n=4 * 8, seq_len=128, seed=5, device=device)
+    pool = [{k: v[i * 8:(i + 1) * 8].contiguous() for k, v in ds.columns.items()} for i in range(4)]
+    results = []
+    for graphed in (False, True):
+        torch.manual_seed(7)
+        model = distilbert_base(n_layers=2, dropout=0.0, attention_dropout=0.0, seq_classif_dropout=0.0).to(device)
+        sync = build_grad_sync("powersgd", model, lr=1e-3, momentum=0.9, rank=4)
+        static = {k: v.clone() for k, v in pool[0].items()}
+
+        def pre():
+            sync.zero_grad()
+            model(static["input_ids"], attention_mask=static["attention_mask"], labels=static["labels"])[0].backward()
+
+        runner = StepRunner(pre, sync, mode="full" if graphed else "none", warmup=2)
+        for i in range(10):
+            for k, v in pool[i % 4].items():
+                static[k].copy_(v)
+            runner()
+        torch.cuda.synchronize()
+        results.append(torch.cat([p.detach().reshape(-1) for p in model.parameters()]).clone())
+    assert torch.isfinite(results[1]).all()
+    torch.testing.assert_close(results[1], results[0], rtol=1e-5, atol=1e-6)

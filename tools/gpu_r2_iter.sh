@@ -12,4 +12,4 @@ for b in 512 64; do
   timeout -k 10 200 python bench.py --global-batch $b --steps 50 --warmup 10 > gpurun_out/it_b$b.json 2> gpurun_out/it_b$b.err || { tail -5 gpurun_out/it_b$b.err; exit 1; }
   echo "b$b $(python3 tools/jline.py gpurun_out/it_b$b.json)"
 done
-bash tools/gpu_r2_prof.sh b64 "--global-batch 64" ${PROF_EXTRA:-}
+[ "${SKIP_PROF:-0}" = "1" ] || bash tools/gpu_r2_prof.sh b64 "--global-batch 64" ${PROF_EXTRA:-}
