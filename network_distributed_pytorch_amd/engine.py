@@ -32,6 +32,7 @@ from .models import build_model
 from .parallel.comm import LINK_PRESETS, Communicator
 from .parallel.trainer import build_grad_sync
 from .utils.checkpoint import load_checkpoint, save_checkpoint
+from .utils.config import validate_config
 from .utils.data import DeviceLoader, SyntheticCIFAR10, SyntheticIMDb, train_val_split
 from .utils.divergence import ReplicaChecker
 from .utils.metrics import JsonlLogger, PhaseTimer, print_epoch
@@ -166,6 +167,9 @@ def _loss_fn(config, model, crit):
 
 def run_task(config) -> Dict[str, Any]:
     """The reference's training loop for the configured task (returns a summary)."""
+    validate_config(config, strict=False)  # typed schema: types, choices, cross-field rules
+    if config.get("_unknown_keys"):
+        _log(config, f"[config] ignoring unknown keys {config['_unknown_keys']}")
     _log(config, "==============================")
     _log(config, ">>>>> Run Designated Task <<<<<")
     device = device_for(config)

@@ -14,8 +14,8 @@ while [ $# -ge 2 ]; do
   timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/tr_$name -o run -- \
     python3 bench.py --steps 25 --warmup 5 $args > gpurun_out/tr_$name.out 2>&1 || { tail -5 gpurun_out/tr_$name.out; exit 1; }
   f=$(find gpurun_out/tr_$name -name '*kernel_trace.csv' | sort | head -n 1)
-  python3 tools/prof_timeline.py "$f" --steps 20 --dump gpurun_out/tr_$name.last.txt > gpurun_out/tr_$name.timeline.md &&
-  python3 tools/prof_summary.py "$f" --steps 20 --marker "${MARKER:-conv_fwd_kernel<7, 7}" --top 80 > gpurun_out/tr_$name.kernels.md || exit 1
+  python3 tools/prof_timeline.py "$f" --steps ${PSTEPS:-20} --marker "${MARKER:-conv_fwd_kernel<7, 7}" --dump gpurun_out/tr_$name.last.txt > gpurun_out/tr_$name.timeline.md &&
+  python3 tools/prof_summary.py "$f" --steps ${PSTEPS:-20} --marker "${MARKER:-conv_fwd_kernel<7, 7}" --top 80 > gpurun_out/tr_$name.kernels.md || exit 1
   echo "== $name: $(python3 tools/jline.py gpurun_out/tr_$name.out)"
   sed -n 5,8p gpurun_out/tr_$name.timeline.md
   rm -rf gpurun_out/tr_$name
