@@ -18,8 +18,9 @@ def test_plan_builder_under_asan_ubsan(tmp_path):
            "-fno-omit-frame-pointer", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", "-I" + csrc,
            os.path.join(ROOT, "tools", "asan", "plan_fuzz.cpp"), os.path.join(csrc, "plan.cpp"), "-o", str(exe)]
     subprocess.run(cmd, check=True, capture_output=True, timeout=300)
-    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1")
-    env.pop("LD_PRELOAD", None)
+    # verify_asan_link_order=0: the environment may preload other libraries ahead of ASan
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1:verify_asan_link_order=0",
+               UBSAN_OPTIONS="print_stacktrace=1")
     out = subprocess.run([str(exe), "150"], capture_output=True, text=True, timeout=300, env=env)
     assert out.returncode == 0, out.stderr[-3000:]
     assert "plan_fuzz ok" in out.stdout
