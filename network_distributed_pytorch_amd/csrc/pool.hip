@@ -120,6 +120,100 @@ __global__ __launch_bounds__(kPoolThreads) void maxpool_bwd_kernel(const float* 
   dx[e] = acc;
 }
 
+// ---- ResNet stem window (3, 2, 1) on even maps with W % 4 == 0: vectorised fast paths ----
+// fwd: one thread per PAIR of outputs (oh, 2j), (oh, 2j + 1): the three input rows'
+//      columns 4j .. 4j+3 come as one float4 each, column 4j - 1 from the left lane (the
+//      W/4 lanes of a row are adjacent in the wave, W/4 | 64), 2 outputs + 2 index bytes
+//      stored together.  Same scan order / NaN rule as the generic kernel.
+// bwd: one thread per output position (i, j) writes the 2x2 input block it owns,
+//      [2i, 2i+1] x [2j, 2j+1], gathering the (<= 4) windows that can pick each pixel in
+//      the generic kernel's (oh, ow) order: float2 stores, no zero-fill, no atomics.
+__global__ __launch_bounds__(kPoolThreads) void maxpool_fwd_s2_kernel(const float* __restrict__ x,
+                                                                      float* __restrict__ y,
+                                                                      uint8_t* __restrict__ idx, PoolArgs a) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const uint32_t e = blockIdx.x * kPoolThreads + threadIdx.x;  // pair index
+  const int H = a.g.H, W = a.g.W, OW = a.g.OW, W4 = W >> 2;
+  const uint32_t pairs_per_plane = (uint32_t)(a.g.OH * W4);
+  const bool live = e < a.total;
+  const uint32_t plane = live ? e / pairs_per_plane : 0;
+  const uint32_t r = live ? e - plane * pairs_per_plane : 0;
+  const int oh = (int)(r / (uint32_t)W4), j = (int)(r - (uint32_t)oh * W4);
+  const float* xp = x + (size_t)plane * a.in_plane.d;
+  float v[3][5];  // rows 2oh-1 .. 2oh+1, columns 4j-1 .. 4j+3
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh) {
+    const int h = 2 * oh - 1 + kh;
+    f4 q = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    if (live && h >= 0 && h < H) q = *reinterpret_cast<const f4*>(xp + h * W + 4 * j);
+    const float left = __shfl_up(q.w, 1, 64);
+    v[kh][0] = (j > 0) ? left : -INFINITY;
+    v[kh][1] = q.x; v[kh][2] = q.y; v[kh][3] = q.z; v[kh][4] = q.w;
+  }
+  if (!live) return;
+  float out[2];
+  uint8_t arg[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {  // output column ow = 2j + t: taps at columns 4j - 1 + 2t + kw
+    const int ow = 2 * j + t;
+    const int kh0 = oh == 0 ? 1 : 0, kw0 = ow == 0 ? 1 : 0;
+    float best = -INFINITY;
+    int a0 = kh0 * 3 + kw0;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      if (kh < kh0 || 2 * oh - 1 + kh >= H) continue;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        if (kw < kw0 || 2 * ow - 1 + kw >= W) continue;
+        const float val = v[kh][2 * t + kw];
+        if (val > best || isnan(val)) {
+          best = val;
+          a0 = kh * 3 + kw;
+        }
+      }
+    }
+    out[t] = best;
+    arg[t] = (uint8_t)a0;
+  }
+  const size_t o = (size_t)plane * a.out_plane.d + (size_t)oh * OW + 2 * j;
+  *reinterpret_cast<float2*>(y + o) = make_float2(out[0], out[1]);
+  idx[o] = arg[0];
+  idx[o + 1] = arg[1];
+}
+
+__global__ __launch_bounds__(kPoolThreads) void maxpool_bwd_s2_kernel(const float* __restrict__ dy,
+                                                                      const uint8_t* __restrict__ idx,
+                                                                      float* __restrict__ dx, PoolArgs a) {
+  const uint32_t e = blockIdx.x * kPoolThreads + threadIdx.x;  // output position
+  if (e >= a.total) return;
+  const int OH = a.g.OH, OW = a.g.OW, W = a.g.W;
+  const uint32_t plane = fdiv(e, a.out_plane);
+  const uint32_t o = e - plane * a.out_plane.d;
+  const int i = (int)fdiv(o, a.ow), j = (int)(o - (uint32_t)i * a.ow.d);
+  const float* dyp = dy + (size_t)plane * a.out_plane.d;
+  const uint8_t* ip = idx + (size_t)plane * a.out_plane.d;
+  const bool right = j + 1 < OW, down = i + 1 < OH;
+  const int c = i * OW + j;
+  const float g00 = dyp[c], g01 = right ? dyp[c + 1] : 0.f, g10 = down ? dyp[c + OW] : 0.f,
+              g11 = (right && down) ? dyp[c + OW + 1] : 0.f;
+  const int a00 = ip[c], a01 = right ? ip[c + 1] : -1, a10 = down ? ip[c + OW] : -1,
+            a11 = (right && down) ? ip[c + OW + 1] : -1;
+  // window (oh, ow) covers input rows 2oh-1 .. 2oh+1: tap kh = h - 2oh + 1
+  float d00 = 0.f, d01 = 0.f, d10 = 0.f, d11 = 0.f;
+  if (a00 == 4) d00 += g00;                     // (2i, 2j)     <- (i, j) tap (1,1)
+  if (a00 == 5) d01 += g00;                     // (2i, 2j+1)   <- (i, j) tap (1,2)
+  if (a01 == 3) d01 += g01;                     //              <- (i, j+1) tap (1,0)
+  if (a00 == 7) d10 += g00;                     // (2i+1, 2j)   <- (i, j) tap (2,1)
+  if (a10 == 1) d10 += g10;                     //              <- (i+1, j) tap (0,1)
+  if (a00 == 8) d11 += g00;                     // (2i+1, 2j+1) <- (i, j) tap (2,2)
+  if (a01 == 6) d11 += g01;                     //              <- (i, j+1) tap (2,0)
+  if (a10 == 2) d11 += g10;                     //              <- (i+1, j) tap (0,2)
+  if (a11 == 0) d11 += g11;                     //              <- (i+1, j+1) tap (0,0)
+  float* dxp = dx + (size_t)plane * a.in_plane.d + (size_t)(2 * i) * W + 2 * j;
+  *reinterpret_cast<float2*>(dxp) = make_float2(d00, d01);
+  *reinterpret_cast<float2*>(dxp + W) = make_float2(d10, d11);
+}
+
 PoolArgs pool_args(const PoolGeom& g, int64_t total) {
   PoolArgs a;
   a.g = g;
@@ -133,11 +227,23 @@ PoolArgs pool_args(const PoolGeom& g, int64_t total) {
 
 bool resnet_window(const PoolGeom& g) { return g.KH == 3 && g.KW == 3 && g.stride == 2 && g.pad == 1; }
 
+// the vectorised paths: even maps, whole float4 rows, W/4 lanes per row inside one wave
+bool s2_fast(const PoolGeom& g) {
+  return resnet_window(g) && g.H == 2 * g.OH && g.W == 2 * g.OW && g.W % 4 == 0 && 64 % (g.W / 4) == 0;
+}
+
 }  // namespace
 
 void launch_maxpool_fwd(const float* x, float* y, uint8_t* idx, int planes, const PoolGeom& g, hipStream_t s) {
   const int64_t total = (int64_t)planes * g.OH * g.OW;
   if (total <= 0) return;
+  if (s2_fast(g)) {
+    const int64_t pairs = (int64_t)planes * g.OH * (g.W / 4);
+    const PoolArgs a = pool_args(g, pairs);
+    hipLaunchKernelGGL(maxpool_fwd_s2_kernel, dim3((unsigned)((pairs + kPoolThreads - 1) / kPoolThreads)),
+                       dim3(kPoolThreads), 0, s, x, y, idx, a);
+    return;
+  }
   const PoolArgs a = pool_args(g, total);
   const dim3 grid((unsigned)((total + kPoolThreads - 1) / kPoolThreads));
   if (resnet_window(g))
@@ -150,6 +256,13 @@ void launch_maxpool_bwd(const float* dy, const uint8_t* idx, float* dx, int plan
                         hipStream_t s) {
   const int64_t total = (int64_t)planes * g.H * g.W;
   if (total <= 0) return;
+  if (s2_fast(g)) {
+    const int64_t outs = (int64_t)planes * g.OH * g.OW;
+    const PoolArgs a = pool_args(g, outs);
+    hipLaunchKernelGGL(maxpool_bwd_s2_kernel, dim3((unsigned)((outs + kPoolThreads - 1) / kPoolThreads)),
+                       dim3(kPoolThreads), 0, s, dy, idx, dx, a);
+    return;
+  }
   const PoolArgs a = pool_args(g, total);
   const dim3 grid((unsigned)((total + kPoolThreads - 1) / kPoolThreads));
   if (resnet_window(g))

@@ -19,7 +19,9 @@ def test_maxpool_module_cpu_matches_torch():
 @pytest.mark.gpu
 @pytest.mark.parametrize("shape,k,s,p", [((512, 64, 16, 16), 3, 2, 1), ((4, 8, 15, 13), 3, 2, 1),
                                          ((3, 5, 7, 7), 2, 2, 0), ((2, 3, 11, 9), 5, 3, 2),
-                                         ((1, 1, 1, 1), 1, 1, 0), ((6, 4, 8, 8), 3, 1, 1)])
+                                         ((1, 1, 1, 1), 1, 1, 0), ((6, 4, 8, 8), 3, 1, 1),
+                                         # vectorised stem paths (even maps, W % 4 == 0)
+                                         ((3, 4, 8, 8), 3, 2, 1), ((2, 3, 32, 32), 3, 2, 1), ((64, 64, 16, 16), 3, 2, 1)])
 def test_maxpool_fwd_bwd(device, shape, k, s, p):
     assert ops.native_available()
     torch.manual_seed(0)
@@ -36,8 +38,9 @@ def test_maxpool_fwd_bwd(device, shape, k, s, p):
 
 
 @pytest.mark.gpu
-def test_maxpool_ties_pick_first_and_deterministic(device):
-    x = torch.zeros(2, 3, 6, 6, device=device, requires_grad=True)  # every window is a tie
+@pytest.mark.parametrize("hw", [6, 16])  # generic kernel / vectorised stem path
+def test_maxpool_ties_pick_first_and_deterministic(device, hw):
+    x = torch.zeros(2, 3, hw, hw, device=device, requires_grad=True)  # every window is a tie
     x2 = x.detach().clone().requires_grad_(True)
     y = MaxPool2d(3, 2, 1)(x)
     ref = F.max_pool2d(x2, 3, 2, 1)
