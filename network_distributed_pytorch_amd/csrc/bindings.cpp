@@ -444,11 +444,65 @@ void toeplitz_expand_many(const std::vector<std::tuple<torch::Tensor, torch::Ten
   check_launch("launch_toeplitz_expand_many");
 }
 
+// entries: [(dw_big, dw, geom)] -> every fold in one launch
+void toeplitz_fold_many(const std::vector<std::tuple<torch::Tensor, torch::Tensor, std::vector<int64_t>>>& entries) {
+  TORCH_CHECK(!entries.empty() && (int)entries.size() <= ndp::kMaxExpand, "toeplitz_fold_many: 1..",
+              ndp::kMaxExpand, " layers");
+  ndp::FoldBatch b{};
+  int64_t acc = 0;
+  for (const auto& en : entries) {
+    const torch::Tensor& dwb = std::get<0>(en);
+    const torch::Tensor& dw = std::get<1>(en);
+    check_f32(dwb, "dw_big"); check_f32(dw, "dw");
+    const ndp::ConvGeom g = conv_geom(std::get<2>(en));
+    const int64_t nw = (int64_t)g.Co * g.C * g.KH * g.KW;
+    TORCH_CHECK(dw.numel() == nw, "toeplitz_fold_many: weight size");
+    TORCH_CHECK(dwb.numel() == (int64_t)g.C * g.H * g.W * g.Co * g.OH * g.OW, "toeplitz_fold_many: dw_big size");
+    b.dwt[b.n] = dwb.data_ptr<float>();
+    b.dw[b.n] = dw.data_ptr<float>();
+    TORCH_CHECK(g.KH * g.KW <= 9 && g.H * g.W <= 64, "toeplitz_fold_many: kernel / map too large");
+    b.g[b.n] = g;
+    acc += (int64_t)g.Co * g.C;
+    b.end[b.n] = acc;
+    ++b.n;
+  }
+  ndp::launch_toeplitz_fold_many(b, cur_stream());
+  check_launch("launch_toeplitz_fold_many");
+}
+
+// entries: [(part, dw, slices)] -> dw = sum_s part[s * numel(dw) :], every entry in one launch
+void slab_sum_many(const std::vector<std::tuple<torch::Tensor, torch::Tensor, int64_t>>& entries) {
+  TORCH_CHECK(!entries.empty() && (int)entries.size() <= ndp::kMaxExpand, "slab_sum_many: 1..", ndp::kMaxExpand,
+              " entries");
+  ndp::SlabBatch b{};
+  int64_t blocks = 0;
+  for (const auto& en : entries) {
+    const torch::Tensor& part = std::get<0>(en);
+    const torch::Tensor& dw = std::get<1>(en);
+    const int64_t slices = std::get<2>(en);
+    check_f32(part, "part"); check_f32(dw, "dw");
+    const int64_t n = dw.numel();
+    TORCH_CHECK(n % 4 == 0 && slices >= 1 && part.numel() >= slices * n, "slab_sum_many: bad entry");
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(part.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(dw.data_ptr()) & 15) == 0,
+                "slab_sum_many: 16-B aligned tensors");
+    b.part[b.n] = part.data_ptr<float>();
+    b.dw[b.n] = dw.data_ptr<float>();
+    b.numel[b.n] = n;
+    b.slices[b.n] = (int)slices;
+    blocks += (n / 4 + 15) / 16;
+    b.end[b.n] = blocks;
+    ++b.n;
+  }
+  ndp::launch_slab_sum_many(b, cur_stream());
+  check_launch("launch_slab_sum_many");
+}
+
 void toeplitz_fold(torch::Tensor dwb, torch::Tensor dw, const std::vector<int64_t>& geom) {
   check_f32(dwb, "dw_big"); check_f32(dw, "dw");
   const ndp::ConvGeom g = conv_geom(geom);
   TORCH_CHECK(dw.numel() == (int64_t)g.Co * g.C * g.KH * g.KW, "toeplitz_fold: weight size");
   TORCH_CHECK(dwb.numel() == (int64_t)g.C * g.H * g.W * g.Co * g.OH * g.OW, "toeplitz_fold: dw_big size");
+  TORCH_CHECK(g.KH * g.KW <= 9, "toeplitz_fold: kernel too large");
   ndp::launch_toeplitz_fold(dwb.data_ptr<float>(), dw.data_ptr<float>(), g, cur_stream());
   check_launch("launch_toeplitz_fold");
 }
@@ -501,7 +555,7 @@ void conv_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, const std::vect
 }
 
 void conv_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, const std::vector<int64_t>& geom,
-                c10::optional<torch::Tensor> part) {
+                c10::optional<torch::Tensor> part, c10::optional<torch::Tensor> addend) {
   const ndp::ConvGeom g = conv_geom(geom);
   const int cls = ndp::conv_direct_class(g);
   TORCH_CHECK(cls >= 0 && ndp::conv_dgrad_direct(cls), "conv_dgrad: no direct grad-x kernel for this geometry");
@@ -514,11 +568,19 @@ void conv_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, const std::
   // stride-2 1x1 class the 4x4 map, before the even-pixel scatter)
   const int64_t slab = (int64_t)B * g.C * (cls == 4 ? g.OH * g.OW : g.H * g.W);
   float* pp = conv_part(part, ks, slab, "conv_dgrad");
-  ndp::launch_conv_dgrad(dy.data_ptr<float>(), w.data_ptr<float>(), dx.data_ptr<float>(), B, g, pp, cur_stream());
+  const float* ap = nullptr;
+  if (addend.has_value()) {
+    TORCH_CHECK(cls != 4, "conv_dgrad: no addend for the stride-2 1x1 class");
+    conv_check(*addend, "addend", B, g.C, g.H, g.W);
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(addend->data_ptr()) & 15) == 0, "conv_dgrad: 16-B aligned addend");
+    ap = addend->data_ptr<float>();
+  }
+  ndp::launch_conv_dgrad(dy.data_ptr<float>(), w.data_ptr<float>(), dx.data_ptr<float>(), B, g, pp, cur_stream(), ap);
   check_launch("launch_conv_dgrad");
 }
 
-void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor part, torch::Tensor dw,
+// dw None: write the per-slice partial slabs only (the caller sums them, batched)
+void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor part, c10::optional<torch::Tensor> dw_opt,
                 const std::vector<int64_t>& geom) {
   const ndp::ConvGeom g = conv_geom(geom);
   const int cls = ndp::conv_direct_class(g);
@@ -527,11 +589,14 @@ void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor part, torch::Te
   const int B = conv_batch(x, g, imgs);
   conv_check(x, "x", B, g.C, g.H, g.W);
   conv_check(dy, "dy", B, g.Co, g.OH, g.OW);
-  conv_check(dw, "dw", g.Co, g.C, g.KH, g.KW);
+  float* dwp = nullptr;
+  if (dw_opt.has_value()) {
+    conv_check(*dw_opt, "dw", g.Co, g.C, g.KH, g.KW);
+    dwp = dw_opt->data_ptr<float>();
+  }
   check_f32(part, "part");
-  TORCH_CHECK(part.numel() >= (int64_t)(B / imgs) * dw.numel(), "conv_wgrad: partial scratch too small");
-  ndp::launch_conv_wgrad(x.data_ptr<float>(), dy.data_ptr<float>(), part.data_ptr<float>(), dw.data_ptr<float>(), B,
-                         g, cur_stream());
+  TORCH_CHECK(part.numel() >= (int64_t)(B / imgs) * g.Co * g.C * g.KH * g.KW, "conv_wgrad: partial scratch too small");
+  ndp::launch_conv_wgrad(x.data_ptr<float>(), dy.data_ptr<float>(), part.data_ptr<float>(), dwp, B, g, cur_stream());
   check_launch("launch_conv_wgrad");
 }
 
@@ -667,11 +732,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("toeplitz_expand", &toeplitz_expand);
   m.def("toeplitz_fold", &toeplitz_fold);
   m.def("toeplitz_expand_many", &toeplitz_expand_many);
+  m.def("toeplitz_fold_many", &toeplitz_fold_many);
+  m.def("slab_sum_many", &slab_sum_many);
   m.def("conv_plan", &conv_plan, py::arg("geom"), py::arg("batch"));
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("geom"), py::arg("part") = py::none());
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("geom"),
-        py::arg("part") = py::none());
-  m.def("conv_wgrad", &conv_wgrad);
+        py::arg("part") = py::none(), py::arg("addend") = py::none());
+  m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("part"), py::arg("dw"), py::arg("geom"));
   m.def("embedding_backward", &embedding_backward);
   m.def("colsum", &colsum);
   m.def("attn_fwd", &attn_fwd);

@@ -38,31 +38,6 @@ __global__ __launch_bounds__(256) void toeplitz_expand_kernel(const float* __res
   wt[(int64_t)n * K + kcol] = v;
 }
 
-// one thread per weight element: dW[co,ci,kh,kw] = sum_{oh,ow valid} dWt[(co,oh,ow),(ci,ih,iw)]
-__global__ __launch_bounds__(256) void toeplitz_fold_kernel(const float* __restrict__ dwt, float* __restrict__ dw,
-                                                            ConvGeom g) {
-  const int nw = g.Co * g.C * g.KH * g.KW;
-  const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx >= nw) return;
-  const int kw = idx % g.KW;
-  const int kh = (idx / g.KW) % g.KH;
-  const int ci = (idx / (g.KW * g.KH)) % g.C;
-  const int co = idx / (g.KW * g.KH * g.C);
-  const int K = g.C * g.H * g.W;
-  float acc = 0.f;
-  for (int oh = 0; oh < g.OH; ++oh) {
-    const int ih = oh * g.stride - g.pad + kh;
-    if (ih < 0 || ih >= g.H) continue;
-    for (int ow = 0; ow < g.OW; ++ow) {
-      const int iw = ow * g.stride - g.pad + kw;
-      if (iw < 0 || iw >= g.W) continue;
-      const int n = (co * g.OH + oh) * g.OW + ow;
-      acc += dwt[(int64_t)n * K + (ci * g.H + ih) * g.W + iw];
-    }
-  }
-  dw[idx] = acc;
-}
-
 // Every Toeplitz layer of a model in ONE launch (forward start, ToeplitzBank in
 // models/conv_gemm.py).  One workgroup per W_big^T row n = (co, oh, ow) of one layer (the
 // layer is found by scanning the <= kMaxExpand row prefix sums in the kernel arguments — no
@@ -126,14 +101,96 @@ void launch_toeplitz_expand_many(const ExpandBatch& b, hipStream_t s) {
   hipLaunchKernelGGL(toeplitz_expand_many_kernel, dim3((unsigned)b.end[b.n - 1]), dim3(256), 0, s, b);
 }
 
+// One thread per (co, ci) weight PAIR: it reads, for every output position (oh, ow), the
+// H*W contiguous dWt_big columns of input channel ci (row n = (co, oh, ow)) — lanes with
+// consecutive ci read consecutive segments, fully coalesced — and accumulates them into
+// its KH*KW taps in registers (the same (oh, ow)-ascending order per tap as the one-thread-
+// per-weight fold, so results are bitwise identical); then writes its KH*KW contiguous
+// weights.  Toeplitz layers have KH, KW <= 3 and H*W <= 16.
+constexpr int kFoldMaxTaps = 9;
+__device__ __forceinline__ void fold_pair(const float* __restrict__ dwt, const ConvGeom& g, int pair,
+                                          float (&acc)[kFoldMaxTaps]) {
+  const int co = pair / g.C, ci = pair - co * g.C;
+  const int K = g.C * g.H * g.W, HW = g.H * g.W;
+#pragma unroll
+  for (int t = 0; t < kFoldMaxTaps; ++t) acc[t] = 0.f;
+  for (int oh = 0; oh < g.OH; ++oh)
+    for (int ow = 0; ow < g.OW; ++ow) {
+      const float* row = dwt + (int64_t)((co * g.OH + oh) * g.OW + ow) * K + ci * HW;
+      for (int ih = 0; ih < g.H; ++ih) {
+        const int kh = ih - oh * g.stride + g.pad;
+        if (kh < 0 || kh >= g.KH) continue;
+        for (int iw = 0; iw < g.W; ++iw) {
+          const int kw = iw - ow * g.stride + g.pad;
+          if (kw < 0 || kw >= g.KW) continue;
+          const float v = row[ih * g.W + iw];
+#pragma unroll
+          for (int t = 0; t < kFoldMaxTaps; ++t)
+            if (t == kh * g.KW + kw) acc[t] += v;
+        }
+      }
+    }
+}
+
+// Every deferred grad-W fold of a backward pass in ONE launch (ops/gradfinish.py): flat
+// grid over all layers' (co, ci) pairs, the layer found from the <= kMaxExpand prefix sums
+// in the kernel arguments.  A workgroup's 256 pairs own one contiguous run of 256 * KH*KW
+// weights, so the taps go through LDS and leave as coalesced float stores (a lane writing
+// its own 9 weights would stride the wave's stores by 36 B).
+__global__ __launch_bounds__(256) void toeplitz_fold_many_kernel(FoldBatch b) {
+  __shared__ float stage[256 * kFoldMaxTaps];
+  const int64_t base = (int64_t)blockIdx.x * 256;
+  const int64_t i = base + threadIdx.x;
+  const int64_t total = b.end[b.n - 1];
+  int e = 0;
+  while (e + 1 < b.n && base >= b.end[e]) ++e;  // the workgroup's first entry
+  const int64_t e_lo = e ? b.end[e - 1] : 0;
+  const bool one_entry = base + 256 <= b.end[e];  // whole workgroup inside entry e
+  if (one_entry) {
+    const ConvGeom& g = b.g[e];
+    const int T = g.KH * g.KW;
+    float acc[kFoldMaxTaps];
+    fold_pair(b.dwt[e], g, (int)(i - e_lo), acc);
+#pragma unroll
+    for (int t = 0; t < kFoldMaxTaps; ++t)
+      if (t < T) stage[threadIdx.x * T + t] = acc[t];
+    __syncthreads();
+    float* out = b.dw[e] + (base - e_lo) * T;
+    for (int k = threadIdx.x; k < 256 * T; k += 256) out[k] = stage[k];
+    return;
+  }
+  if (i >= total) return;  // straddling workgroup: direct per-lane writes
+  while (e + 1 < b.n && i >= b.end[e]) ++e;
+  const ConvGeom& g = b.g[e];
+  const int T = g.KH * g.KW;
+  const int pair = (int)(i - (e ? b.end[e - 1] : 0));
+  float acc[kFoldMaxTaps];
+  fold_pair(b.dwt[e], g, pair, acc);
+  float* out = b.dw[e] + (int64_t)pair * T;
+#pragma unroll
+  for (int t = 0; t < kFoldMaxTaps; ++t)
+    if (t < T) out[t] = acc[t];
+}
+
+void launch_toeplitz_fold_many(const FoldBatch& b, hipStream_t s) {
+  if (b.n <= 0) return;
+  const int64_t total = b.end[b.n - 1];  // (co, ci) pairs
+  hipLaunchKernelGGL(toeplitz_fold_many_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, b);
+}
+
 void launch_toeplitz_expand(const float* w, float* wb, const ConvGeom& g, hipStream_t s) {
   const int N = g.Co * g.OH * g.OW, K = g.C * g.H * g.W;
   hipLaunchKernelGGL(toeplitz_expand_kernel, dim3((K + 255) / 256, N), dim3(256), 0, s, w, wb, g);
 }
 
 void launch_toeplitz_fold(const float* dwb, float* dw, const ConvGeom& g, hipStream_t s) {
-  const int nw = g.Co * g.C * g.KH * g.KW;
-  hipLaunchKernelGGL(toeplitz_fold_kernel, dim3((nw + 255) / 256), dim3(256), 0, s, dwb, dw, g);
+  FoldBatch b{};
+  b.dwt[0] = dwb;
+  b.dw[0] = dw;
+  b.g[0] = g;
+  b.end[0] = (int64_t)g.Co * g.C;
+  b.n = 1;
+  launch_toeplitz_fold_many(b, s);
 }
 
 
@@ -236,7 +293,8 @@ template <int R, int S, int ST, int PD, int H, int W, int CK, int BM, int IMGS, 
           bool VEC, int UPS = 1>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                        float* __restrict__ y, float* __restrict__ part, int Cin,
-                                                       int Kout, int cps, int64_t slab) {
+                                                       int Kout, int cps, int64_t slab,
+                                                       const float* __restrict__ addend) {
   using G = ConvFwdCfg<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW>;
   constexpr int AE = (BM * G::KK + 3) / 4;  // float4 slots (scalar path: 4 scalars per slot)
   constexpr int A_PER_T = (AE + 255) / 256;
@@ -437,12 +495,15 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
       int img, pp, qq;
       G::pix(n, img, pp, qq);
       const int opix = UPS == 1 ? pp * G::Q + qq : pp * UPS * (UPS * G::Q) + qq * UPS;
-      float* yb = y + (int64_t)(b0 + img) * Kout * OPQ + opix;
+      const int64_t yoff = (int64_t)(b0 + img) * Kout * OPQ + opix;
+      float* yb = y + yoff;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + (wm * G::TM + tm) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         float* d = yb + (int64_t)m * OPQ;
-        d[0] = acc[tm][tn][r];
+        // addend (UPS == 1 only): y += addend, e.g. the identity-branch gradient of a
+        // residual block added into conv1's grad-x (no separate add launch)
+        d[0] = addend ? acc[tm][tn][r] + addend[yoff + (int64_t)m * OPQ] : acc[tm][tn][r];
         if constexpr (UPS == 2) {
           d[1] = 0.f;
           d[2 * G::Q] = 0.f;
@@ -601,7 +662,8 @@ __global__ __launch_bounds__(64 * NW) void conv_wgrad_kernel(const float* __rest
 // group 0 adds the 16 group sums in order — a fixed summation tree (deterministic) with
 // 16x the memory-level parallelism of a one-thread-per-column sum.
 __global__ __launch_bounds__(256) void conv_slab_sum_kernel(const float* __restrict__ part, float* __restrict__ dw,
-                                                            int64_t n, int n_slices) {
+                                                            int64_t n, int n_slices,
+                                                            const float* __restrict__ addend = nullptr) {
   __shared__ f32x4c red[16][16];
   const int col = threadIdx.x & 15, g = threadIdx.x >> 4;
   const int64_t i4 = ((int64_t)blockIdx.x * 16 + col) * 4;
@@ -616,8 +678,43 @@ __global__ __launch_bounds__(256) void conv_slab_sum_kernel(const float* __restr
     f32x4c t = red[0][col];
 #pragma unroll
     for (int k = 1; k < 16; ++k) t += red[k][col];
+    if (addend) t += *reinterpret_cast<const f32x4c*>(addend + i4);  // fused residual-branch gradient
     *reinterpret_cast<f32x4c*>(dw + i4) = t;
   }
+}
+
+// Every deferred grad-W slab sum of a backward pass in ONE launch (ops/gradfinish.py):
+// entry e owns blocks [end[e-1], end[e]); inside an entry the same 16-group fixed-order
+// tree as conv_slab_sum_kernel (bitwise identical results).
+__global__ __launch_bounds__(256) void conv_slab_sum_many_kernel(SlabBatch b) {
+  __shared__ f32x4c red[16][16];
+  const int64_t blk = blockIdx.x;
+  int e = 0;
+  while (e + 1 < b.n && blk >= b.end[e]) ++e;
+  const int64_t lb = blk - (e ? b.end[e - 1] : 0);
+  const float* part = b.part[e];
+  const int64_t n = b.numel[e];
+  const int n_slices = b.slices[e];
+  const int col = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int64_t i4 = (lb * 16 + col) * 4;
+  f32x4c acc = {0.f, 0.f, 0.f, 0.f};
+  if (i4 < n) {
+#pragma unroll 4
+    for (int sl = g; sl < n_slices; sl += 16) acc += *reinterpret_cast<const f32x4c*>(part + (int64_t)sl * n + i4);
+  }
+  red[g][col] = acc;
+  __syncthreads();
+  if (g == 0 && i4 < n) {
+    f32x4c t = red[0][col];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) t += red[k][col];
+    *reinterpret_cast<f32x4c*>(b.dw[e] + i4) = t;
+  }
+}
+
+void launch_slab_sum_many(const SlabBatch& b, hipStream_t s) {
+  if (b.n <= 0) return;
+  hipLaunchKernelGGL(conv_slab_sum_many_kernel, dim3((unsigned)b.end[b.n - 1]), dim3(256), 0, s, b);
 }
 
 // split-K sum for the stride-2 1x1 grad-x: dx[b, c, 2p + i, 2q + j] = (i == j == 0) ?
@@ -657,7 +754,7 @@ static void set_lds(KernelT k, size_t bytes) {
 template <int R, int S, int ST, int PD, int H, int W, int CK, int BM, int IMGS, int WM, int NBUF, int KB, bool TRANSW,
           bool VEC, int UPS = 1>
 static void run_fwd(const float* x, const float* w, float* y, int B, int Cin, int Kout, int ksplit, float* part,
-                    hipStream_t s) {
+                    hipStream_t s, const float* addend = nullptr) {
   using G = ConvFwdCfg<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW>;
   auto k = conv_fwd_kernel<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW, VEC, UPS>;
   static bool attr = false;  // once per instantiation (> 64 KiB of LDS needs the opt-in)
@@ -668,11 +765,11 @@ static void run_fwd(const float* x, const float* w, float* y, int B, int Cin, in
   ksplit = (nchunks + cps - 1) / cps;
   const int64_t slab = (int64_t)B * Kout * G::PQ;  // compact partial tile layout
   hipLaunchKernelGGL(k, dim3(B / IMGS, Kout / BM, ksplit), dim3(256), G::LDS_BYTES, s, x, w, y, part, Cin, Kout, cps,
-                     slab);
+                     slab, ksplit > 1 ? nullptr : addend);
   if (ksplit > 1) {
     if constexpr (UPS == 1)
       hipLaunchKernelGGL(conv_slab_sum_kernel, dim3((unsigned)((slab / 4 + 15) / 16)), dim3(256), 0, s, part, y, slab,
-                         ksplit);
+                         ksplit, addend);
     else
       hipLaunchKernelGGL(conv_slab_sum_ups_kernel, dim3((unsigned)((slab + 255) / 256)), dim3(256), 0, s, part, y, slab,
                          ksplit);
@@ -689,6 +786,7 @@ static void run_wgrad(const float* x, const float* dy, float* part, float* dw, i
   const int slices = B / imgs;
   hipLaunchKernelGGL(k, dim3(slices, Kout / BM, (Cin + CB - 1) / CB), dim3(G::NT), G::LDS_BYTES, s, x, dy, part, Cin,
                      Kout, imgs);
+  if (dw == nullptr) return;  // partials only: the caller sums the slabs (batched, ops/gradfinish.py)
   const int64_t n = (int64_t)Kout * Cin * G::RS;  // multiple of 4 for every class
   hipLaunchKernelGGL(conv_slab_sum_kernel, dim3((unsigned)((n / 4 + 15) / 16)), dim3(256), 0, s, part, dw, n, slices);
 }
@@ -779,15 +877,16 @@ void launch_conv_fwd(const float* x, const float* w, float* y, int B, const Conv
 
 // dx[B, C, H, W] from dy[B, Co, OH, OW] (stride-1 classes only)
 void launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, float* part,
-                       hipStream_t s) {
+                       hipStream_t s, const float* addend) {
   const int cls = conv_direct_class(g);
   const int ks = conv_ksplit(cls, g, B, true);
   switch (cls) {
     case 0:
-      if (conv_variant() == 1) run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 2, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s);
-      else run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s);
+      if (conv_variant() == 1)
+        run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 2, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s, addend);
+      else run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s, addend);
       break;
-    case 1: run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s); break;
+    case 1: run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s, addend); break;
     case 4: run_fwd<1, 1, 1, 0, 4, 4, 8, 64, 4, 2, 2, 4, true, true, 2>(dy, w, dx, B, g.Co, g.C, ks, part, s); break;
     default: break;
   }

@@ -157,6 +157,25 @@ struct ExpandBatch {
   int n;
 };
 void launch_toeplitz_expand_many(const ExpandBatch& b, hipStream_t s);
+// several layers' grad-W folds in one launch
+struct FoldBatch {
+  const float* dwt[kMaxExpand];
+  float* dw[kMaxExpand];
+  ConvGeom g[kMaxExpand];
+  int64_t end[kMaxExpand];  // inclusive prefix sums of the (co, ci) pair counts Co*C
+  int n;
+};
+void launch_toeplitz_fold_many(const FoldBatch& b, hipStream_t s);
+// several grad-W slab sums in one launch: dw_e = sum over slices of part_e (numel % 4 == 0)
+struct SlabBatch {
+  const float* part[kMaxExpand];
+  float* dw[kMaxExpand];
+  int64_t numel[kMaxExpand];
+  int slices[kMaxExpand];
+  int64_t end[kMaxExpand];  // inclusive prefix sums of blocks (64 floats per block)
+  int n;
+};
+void launch_slab_sum_many(const SlabBatch& b, hipStream_t s);
 // dW [Co, C, KH, KW] <- fold of dWt_big [Co*OH*OW, C*H*W]  (fixed-order sum, deterministic)
 void launch_toeplitz_fold(const float* dwb, float* dw, const ConvGeom& g, hipStream_t s);
 // direct fp32-MFMA convolutions: shape class (-1 = none), images per workgroup / slice
@@ -169,8 +188,9 @@ bool conv_dgrad_direct(int cls);
 // (the stride-2 1x1 grad-x: B * C * 4 * 4 before its even-pixel scatter)
 int conv_ksplit(int cls, const ConvGeom& g, int B, bool dgrad);
 void launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s);
+// addend (nullable, stride-1 classes): dx += addend in the epilogue / split-K sum
 void launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, float* part,
-                       hipStream_t s);
+                       hipStream_t s, const float* addend = nullptr);
 // part: (B / conv_wgrad_imgs(cls, g, B)) * Co*C*KH*KW floats of scratch
 void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, int B, const ConvGeom& g,
                        hipStream_t s);

@@ -29,9 +29,11 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops import gradfinish
 from ..ops._ext import ext
 from ..ops import conv as _conv
 from ..ops.conv import DirectConvFn, direct_plan, side_stream
+from ..ops.gradlink import InjectGrad
 
 __all__ = ["GemmConv2d", "ToeplitzBank", "toeplitz_maps", "eligible"]
 
@@ -108,7 +110,7 @@ class _ToeplitzConv(torch.autograd.Function):
     tests): the same maps as index tensors."""
 
     @staticmethod
-    def forward(ctx, x, weight, src, dst, oh, ow, geom=None, bank=None, layer=None):
+    def forward(ctx, x, weight, src, dst, oh, ow, geom=None, bank=None, layer=None, link=None):
         B = x.shape[0]
         co = weight.shape[0]
         X = x.reshape(B, -1)
@@ -126,6 +128,8 @@ class _ToeplitzConv(torch.autograd.Function):
             out = X @ w_big
         ctx.save_for_backward(X, w_big, dst)
         ctx.geom = geom
+        ctx.weight = weight  # the Parameter: a deferred fold writes its adopted .grad
+        ctx.link = link      # ops/gradlink.py: residual-branch gradient, folded in by addmm
         ctx.x_shape = x.shape
         ctx.w_shape = weight.shape
         return out.view(B, co, oh, ow)
@@ -146,19 +150,26 @@ class _ToeplitzConv(torch.autograd.Function):
                 side.wait_stream(main)
                 with torch.cuda.stream(side):
                     torch.mm(G.t(), X, out=dwt)                   # [N, K]
-                    ext().toeplitz_fold(dwt, dw, list(ctx.geom))
+                    if not fork and gradfinish.can_defer(ctx.weight):  # one batched fold launch later
+                        gradfinish.defer_fold(dwt, dw, ctx.geom)
+                    else:
+                        ext().toeplitz_fold(dwt, dw, list(ctx.geom))
             if ctx.needs_input_grad[0]:
-                dx = (G @ w_big).view(ctx.x_shape)
+                addend = ctx.link.take() if ctx.link is not None else None
+                if addend is not None:  # dx = addend + G @ W_big in one GEMM (beta = 1)
+                    dx = torch.addmm(addend.reshape(G.shape[0], -1), G, w_big).view(ctx.x_shape)
+                else:
+                    dx = (G @ w_big).view(ctx.x_shape)
             if fork:
                 main.wait_stream(side)
-            return dx, dw, None, None, None, None, None, None, None
+            return dx, dw, None, None, None, None, None, None, None, None
         if ctx.needs_input_grad[0]:
             dx = (G @ w_big.t()).view(ctx.x_shape)
         if ctx.needs_input_grad[1]:
             dw_big = X.t() @ G                                    # [K, N]
             ext_ = torch.cat([dw_big.reshape(-1), dw_big.new_zeros(1)])
             dw = ext_[dst].sum(-1).view(ctx.w_shape)              # fixed-order, deterministic
-        return dx, dw, None, None, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None, None, None
 
 
 class GemmConv2d(nn.Conv2d):
@@ -194,23 +205,27 @@ class GemmConv2d(nn.Conv2d):
                 self._maps[key] = (src, dst, oh, ow, sub, None)
         return self._maps[key]
 
-    def forward(self, x):
+    def forward(self, x, link=None):
+        """``link`` (ops/gradlink.GradLink): a residual-branch gradient to add into this
+        conv's grad-x (fused into the kernel / GEMM where the path allows)."""
         if not (self.gemm and x.is_cuda and self.groups == 1 and self.dilation == (1, 1) and self.bias is None
                 and self.stride[0] == self.stride[1] and self.padding[0] == self.padding[1]
                 and self.padding_mode == "zeros" and x.dtype == torch.float32):
-            return super().forward(x)
+            return super().forward(InjectGrad.apply(x, link) if link is not None else x)
         H, W = x.shape[2:]
         kh, kw = self.kernel_size
         s, p = self.stride[0], self.padding[0]
         if self.direct:
             plan = direct_plan(x, self.weight, s, p)
             if plan is not None:
-                return DirectConvFn.apply(x, self.weight, plan)
+                return DirectConvFn.apply(x, self.weight, plan, link)
         oh = (H + 2 * p - kh) // s + 1
         ow = (W + 2 * p - kw) // s + 1
         if not eligible(H, W, oh, ow):
-            return super().forward(x)
+            return super().forward(InjectGrad.apply(x, link) if link is not None else x)
         src, dst, oh2, ow2, sub, geom = self._plan(x)
         if sub > 1:
             x = x[:, :, ::sub, ::sub]
-        return _ToeplitzConv.apply(x.contiguous(), self.weight, src, dst, oh2, ow2, geom, self.bank, self)
+        if link is not None and geom is None:  # CPU index-map path: plain add in backward
+            x, link = InjectGrad.apply(x, link), None
+        return _ToeplitzConv.apply(x.contiguous(), self.weight, src, dst, oh2, ow2, geom, self.bank, self, link)

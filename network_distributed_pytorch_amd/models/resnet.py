@@ -26,6 +26,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.batchnorm import BatchNormAct2d
+from ..ops.gradlink import GradLink
 from ..ops.pool import MaxPool2d
 from .conv_gemm import GemmConv2d, ToeplitzBank
 
@@ -60,8 +61,12 @@ class BasicBlock(nn.Module):
     def forward(self, x):
         identity = x if self.downsample is None else self.downsample(x)
         if self.fused:  # conv -> BN+ReLU ; conv -> BN + identity + ReLU (fused kernels)
-            out = self.bn1(self.conv1(x), relu=True)
-            return self.bn2(self.conv2(out), residual=identity, relu=True)
+            # identity block: BN2's residual gradient is folded into conv1's grad-x
+            # (ops/gradlink.py) instead of an autograd add of the two branches
+            link = (GradLink() if self.downsample is None and x.is_cuda and torch.is_grad_enabled()
+                    and x.requires_grad and self.training else None)
+            out = self.bn1(self.conv1(x, link=link) if link is not None else self.conv1(x), relu=True)
+            return self.bn2(self.conv2(out), residual=identity, relu=True, link=link)
         out = self.relu(self.bn1(self.conv1(x)))
         out = self.bn2(self.conv2(out))
         return self.relu(out + identity)

@@ -26,7 +26,8 @@ __all__ = ["BatchNormAct2d", "bn_act"]
 
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, res, weight, bias, running_mean, running_var, nbt, part, eps, momentum, relu, single=False):
+    def forward(ctx, x, res, weight, bias, running_mean, running_var, nbt, part, eps, momentum, relu, single=False,
+                link=None):
         X = ext()
         x = x.contiguous()
         if res is not None:
@@ -40,6 +41,7 @@ class _BNActFn(torch.autograd.Function):
         ctx.relu = bool(relu)
         ctx.single = bool(single)
         ctx.has_res = res is not None
+        ctx.link = link  # ops/gradlink.py: the residual gradient goes here, not to `res`
         ctx.has_w = weight is not None
         ctx.save_for_backward(x, y if relu else None, weight, save_mean, save_invstd, part)
         ctx.mark_non_differentiable(save_mean, save_invstd)
@@ -54,11 +56,14 @@ class _BNActFn(torch.autograd.Function):
         dgamma = torch.empty_like(weight) if ctx.has_w else None
         dbeta = torch.empty_like(weight) if ctx.has_w else None
         ext().bn_bwd(dy, y, x, weight, save_mean, save_invstd, dx, dres, dgamma, dbeta, part, ctx.relu, ctx.single)
-        return dx, dres, dgamma, dbeta, None, None, None, None, None, None, None, None
+        if ctx.link is not None and dres is not None:
+            ctx.link.put(dres)
+            dres = None
+        return dx, dres, dgamma, dbeta, None, None, None, None, None, None, None, None, None
 
 
 def bn_act(x, weight, bias, running_mean, running_var, nbt, part, training, momentum, eps,
-           residual=None, relu=False, single=False):
+           residual=None, relu=False, single=False, link=None):
     needs_grad = torch.is_grad_enabled() and (x.requires_grad or (weight is not None and weight.requires_grad)
                                               or (residual is not None and residual.requires_grad))
     if x.is_cuda and (training or not needs_grad):  # eval + autograd: differentiable torch path below
@@ -66,8 +71,10 @@ def bn_act(x, weight, bias, running_mean, running_var, nbt, part, training, mome
             x = x.float()
             residual = residual.float() if residual is not None else None
         if training:
+            if link is not None and residual is not None:
+                residual = residual.detach()  # its gradient travels through `link`
             return _BNActFn.apply(x, residual, weight, bias, running_mean, running_var, nbt, part, eps,
-                                  momentum, relu, single)
+                                  momentum, relu, single, link)
         y = torch.empty_like(x := x.contiguous())
         C = x.shape[1]
         sm = torch.empty(C, device=x.device)
@@ -104,7 +111,9 @@ class BatchNormAct2d(nn.BatchNorm2d):
                 self._part = torch.zeros(need, dtype=torch.float64, device=x.device)
             self._part_key = key
 
-    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, relu: bool = False):
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, relu: bool = False, link=None):
+        """``link`` (ops/gradlink.GradLink, training on device only): deposit the residual's
+        gradient there instead of returning it (the caller's conv absorbs it)."""
         if self.momentum is None or not self.track_running_stats:
             y = super().forward(x)
             if residual is not None:
@@ -115,4 +124,4 @@ class BatchNormAct2d(nn.BatchNorm2d):
             self._ensure_part(x)
         return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var,
                       self.num_batches_tracked if training else None, self._part, training, self.momentum,
-                      self.eps, residual, relu, x.is_cuda and self.fused_small)
+                      self.eps, residual, relu, x.is_cuda and self.fused_small, link)

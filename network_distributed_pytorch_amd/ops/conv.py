@@ -17,6 +17,7 @@ from typing import Optional, Tuple
 
 import torch
 
+from . import gradfinish
 from ._ext import ext
 
 __all__ = ["direct_plan", "conv2d_direct", "DirectConvFn", "side_stream"]
@@ -67,7 +68,9 @@ def direct_plan(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int
 
 class DirectConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, plan):
+    def forward(ctx, x, weight, plan, link=None):
+        wparam = weight
+        ctx.link = link  # ops/gradlink.py: residual-branch gradient folded into grad-x
         geom, _, wgrad_imgs, dgrad_direct, ks_fwd, _ = plan
         C, H, W, Co, KH, KW, s, p = geom
         x = x.contiguous()
@@ -80,6 +83,7 @@ class DirectConvFn(torch.autograd.Function):
         ext().conv_fwd(x, weight, y, list(geom), part)
         ctx.save_for_backward(x, weight)
         ctx.plan = plan
+        ctx.weight = wparam  # the Parameter itself: its .grad is where a deferred sum lands
         return y
 
     @staticmethod
@@ -98,23 +102,34 @@ class DirectConvFn(torch.autograd.Function):
             side = side_stream(x.device) if fork else main
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                ext().conv_wgrad(x, dy, part, dw, list(geom))
+                if not fork and gradfinish.can_defer(ctx.weight):  # slabs now, one batched sum later
+                    ext().conv_wgrad(x, dy, part, None, list(geom))
+                    gradfinish.defer_slab(part, dw, B // wgrad_imgs)
+                else:
+                    ext().conv_wgrad(x, dy, part, dw, list(geom))
+        addend = ctx.link.take() if ctx.link is not None else None
         if ctx.needs_input_grad[0]:
             if dgrad_direct:
                 dx = torch.empty_like(x)
                 part = None
                 if ks_dgrad > 1:  # compact partials: numel(dy) * C / Co floats per split
                     part = torch.empty(ks_dgrad * (dy.numel() // geom[3]) * geom[0], device=x.device, dtype=x.dtype)
-                ext().conv_dgrad(dy, weight, dx, list(geom), part)
+                fuse = addend is not None and geom[6] == 1  # stride-1 classes take the addend in-kernel
+                ext().conv_dgrad(dy, weight, dx, list(geom), part, addend.contiguous() if fuse else None)
+                if fuse:
+                    addend = None
             else:
                 dx = torch.ops.aten.convolution_backward(dy, x, weight, None, [s, s], [p, p], [1, 1], False, [0, 0],
                                                          1, [True, False, False])[0]
+            if addend is not None:
+                dx = dx + addend
         if fork:
             main.wait_stream(side)
-        return dx, dw, None
+        return dx, dw, None, None
 
 
-def conv2d_direct(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int, plan=None) -> torch.Tensor:
+def conv2d_direct(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int, plan=None,
+                  link=None) -> torch.Tensor:
     plan = plan if plan is not None else direct_plan(x, weight, stride, padding)
     assert plan is not None, "no direct kernel for this convolution"
-    return DirectConvFn.apply(x, weight, plan)
+    return DirectConvFn.apply(x, weight, plan, link)

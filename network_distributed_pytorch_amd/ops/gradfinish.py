@@ -1,0 +1,93 @@
+"""Deferred, batched weight-gradient finishing for the native convolutions.
+
+Each direct-conv grad-W ends with a split-slab sum and each Toeplitz conv grad-W with a
+fold of grad-W_big into the weight shape: ~20 small launches per ResNet-18 backward that
+are latency-bound (4-7 µs each).  Instead, the conv backward functions record them here
+and ONE ``slab_sum_many`` + ONE ``toeplitz_fold_many`` launch (csrc/conv.hip) finish them
+all when autograd's backward pass ends (``queue_callback`` on the execution engine: the
+gradients are complete when ``backward()`` returns, exactly as without deferral), or
+earlier when a consumer needs them mid-backward (:func:`flush`: the overlapped gradient
+sync calls it before handing a group's gradients to the side stream).  Same summation
+order per element as the per-layer kernels: results are bitwise identical.
+
+Capture-safe (kernel arguments only, no table uploads).  ``NDP_DEFER_GRADW=0`` restores
+per-layer launches.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from ._ext import ext
+
+__all__ = ["enabled", "can_defer", "defer_slab", "defer_fold", "flush", "pending"]
+
+_MAX = 24  # csrc/ndp_kernels.h kMaxExpand
+_ENABLED = os.environ.get("NDP_DEFER_GRADW", "1") != "0"
+_slabs: list = []
+_folds: list = []
+_queued = [False]
+
+
+def enabled() -> bool:
+    return _ENABLED
+
+
+def pending() -> int:
+    return len(_slabs) + len(_folds)
+
+
+def _queue():
+    if not _queued[0]:
+        try:
+            torch.autograd.Variable._execution_engine.queue_callback(_end_of_backward)
+            _queued[0] = True
+        except RuntimeError:  # not inside a backward pass: finish right away
+            flush()
+
+
+def _end_of_backward():
+    _queued[0] = False
+    flush()
+
+
+def can_defer(param: torch.Tensor) -> bool:
+    """Deferral needs the returned buffer to BE the final gradient: ``param.grad is None``
+    (AccumulateGrad adopts the buffer, or ``autograd.grad`` returns it) and no
+    double-backward graph."""
+    return _ENABLED and param.grad is None and not torch.is_grad_enabled()
+
+
+def _alias(t: torch.Tensor) -> torch.Tensor:
+    """A tensor on ``t``'s storage that is NOT a reference to ``t``'s TensorImpl: holding it
+    keeps the memory alive without raising ``t``'s use count (with a second reference
+    AccumulateGrad would copy the still-unfinished buffer instead of adopting it)."""
+    return torch.empty(0, dtype=t.dtype, device=t.device).set_(t.untyped_storage(), t.storage_offset(), t.shape,
+                                                               t.stride())
+
+
+def defer_slab(part: torch.Tensor, dw: torch.Tensor, slices: int) -> None:
+    """``dw`` (the buffer the backward returns) = sum over ``slices`` slabs of ``part``, later."""
+    _slabs.append((part, _alias(dw), int(slices)))
+    _queue()
+
+
+def defer_fold(dwt: torch.Tensor, dw: torch.Tensor, geom) -> None:
+    """``dw`` = fold(dw_big) (csrc/conv.hip toeplitz_fold), later."""
+    _folds.append((dwt, _alias(dw), list(geom)))
+    _queue()
+
+
+def flush() -> None:
+    """Finish every pending weight gradient (one launch per kind, per 24 entries)."""
+    if not _slabs and not _folds:
+        return
+    X = ext()
+    slabs, folds = list(_slabs), list(_folds)
+    _slabs.clear()
+    _folds.clear()
+    for i in range(0, len(slabs), _MAX):
+        X.slab_sum_many(slabs[i: i + _MAX])
+    for i in range(0, len(folds), _MAX):
+        X.toeplitz_fold_many(folds[i: i + _MAX])

@@ -31,7 +31,7 @@ from typing import List, Optional
 
 import torch
 
-from ..ops import SegPlan, capturing, sgd_momentum_
+from ..ops import SegPlan, capturing, gradfinish, sgd_momentum_
 from .comm import Communicator, all_reduce, world_size
 
 __all__ = ["average_gradients", "BucketedDataParallel", "DEFAULT_BUCKET_MB"]
@@ -150,6 +150,7 @@ class BucketedDataParallel:
             self._works[b] = self.comm.all_reduce(self.g[s:e], async_op=True)
 
     def _launch(self, b: int):
+        gradfinish.flush()  # deferred conv grad-W sums / folds (launches on the compute stream)
         if self.stream_mode:
             self._bind(b)              # table upload on the compute stream, before the fork
 

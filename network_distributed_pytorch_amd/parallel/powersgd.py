@@ -37,7 +37,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from ..ops import SegPlan, capturing, ext, upload, upload_epoch
+from ..ops import SegPlan, capturing, ext, gradfinish, upload, upload_epoch
 from .comm import Communicator, n_bits
 
 __all__ = [
@@ -564,6 +564,7 @@ class PowerSGDOptimizer:
 
     @torch.no_grad()
     def _launch_group(self, g: _Group):
+        gradfinish.flush()  # deferred conv grad-W sums / folds of the layers done so far
         B = self.buf
         X = ext()
         N = self.comm.world_size

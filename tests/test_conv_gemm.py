@@ -136,3 +136,30 @@ def test_resnet_toeplitz_bank_one_launch_equals_per_layer(device):
     torch.backends.cudnn.deterministic = det
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [64, 16])
+def test_deferred_gradw_finishing_is_bitwise(device, batch):
+    """Batched end-of-backward slab sums / Toeplitz folds (ops/gradfinish.py) == per-layer
+    launches, bitwise; nothing is left pending once backward() returns."""
+    from network_distributed_pytorch_amd.models import build_resnet
+    from network_distributed_pytorch_amd.ops import gradfinish
+
+    det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
+    outs = []
+    try:
+        for defer in (False, True):
+            gradfinish._ENABLED = defer
+            torch.manual_seed(3)
+            m = build_resnet(18, 10).to(device)
+            x = torch.randn(batch, 3, 32, 32, device=device, generator=torch.Generator(device=device).manual_seed(1))
+            m(x).square().mean().backward()
+            assert gradfinish.pending() == 0
+            outs.append([p.grad.clone() for p in m.parameters()])
+    finally:
+        gradfinish._ENABLED = True
+        torch.backends.cudnn.deterministic = det
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
