@@ -115,6 +115,9 @@ class Workload:
 
         self.args, self.device, self.world, self.rank = args, device, world, rank
         self.is_bert = args.model.startswith("distilbert")
+        from network_distributed_pytorch_amd.ops import gemm_tuning
+
+        self.tuned_gemms = gemm_tuning.enable()  # measured hipBLASLt/rocBLAS solutions (ops/gemm_tuning.py)
         self.model = build_model(args.model, args.num_classes, fused_bn=not args.no_fused_bn,
                                  gemm_convs=not args.no_gemm_convs,
                                  fused_attention=not args.no_fused_attn).to(device)
@@ -307,6 +310,7 @@ def main(argv=None):
                 "channels_last": args.channels_last,
                 "stock_model_ops": bool(args.no_fused_bn and args.no_gemm_convs),
                 "hip_graph": graph_mode,
+                "tuned_gemms": wl.tuned_gemms,
                 "fused_attention": (not args.no_fused_attn) if is_bert else None,
             },
             "comm_stats_timed": comm_stats,

@@ -28,6 +28,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from .ops import gemm_tuning
 from .models import build_model
 from .parallel.comm import LINK_PRESETS, Communicator
 from .parallel.trainer import build_grad_sync
@@ -178,6 +179,8 @@ def run_task(config) -> Dict[str, Any]:
     graph_mode = config.get("graph_mode", "auto")
     if device.type != "cuda":
         graph_mode = "none"
+    else:
+        gemm_tuning.enable()  # measured GEMM solutions for the library GEMMs (ops/gemm_tuning.py)
 
     model_name = config["model"] if config["task"] != "imdb" else "distilbert"
     if config["task"] == "mlp":

@@ -12,7 +12,8 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("shape", [(512, 64, 8, 8), (64, 128, 4, 4), (32, 512, 1, 1), (16, 24, 7, 7),
                                    (8, 64, 16, 16), (3, 5, 2, 3), (512, 256, 2, 2), (40, 96, 2, 1),
-                                   (7, 40, 2, 4), (8192, 64, 1, 1), (33, 300, 1, 1), (17, 70, 2, 2)])
+                                   (7, 40, 2, 4), (8192, 64, 1, 1), (33, 300, 1, 1), (17, 70, 2, 2),
+                                   (64, 64, 8, 8), (128, 64, 8, 8), (100, 32, 8, 8)])
 @pytest.mark.parametrize("res,relu", [(False, False), (False, True), (True, True)])
 def test_bn_act_train_fwd_bwd(device, shape, res, relu):
     assert ops.native_available()
@@ -83,7 +84,8 @@ def test_resnet18_fused_matches_unfused(device):
 
 
 @pytest.mark.parametrize("shape", [(512, 512, 1, 1), (512, 256, 2, 2), (40, 96, 2, 1), (3, 20, 1, 1),
-                                   (512, 128, 4, 4), (100, 64, 4, 2)])
+                                   (512, 128, 4, 4), (100, 64, 4, 2), (64, 64, 8, 8), (128, 64, 8, 8),
+                                   (7, 16, 8, 8)])
 def test_bn_single_launch_small_path(device, shape):
     """Single-launch register-resident small-map BN: matches the 3-kernel path and is
     deterministic (run twice, bitwise equal)."""
