@@ -133,7 +133,10 @@ class Workload:
                 kw["groups"] = args.psgd_groups
         self.sync = build_grad_sync(args.reducer, self.model, self.comm, lr=args.lr, momentum=0.9,
                                     rank=args.rank, bucket_mb=args.bucket_mb, **kw)
-        self.crit = torch.nn.CrossEntropyLoss()
+        from network_distributed_pytorch_amd.ops.loss import CrossEntropyLoss
+
+        # fused gfx950 softmax cross-entropy (ops/loss.py); --stock keeps PyTorch-ROCm's
+        self.crit = torch.nn.CrossEntropyLoss() if args.stock else CrossEntropyLoss()
         self.loss_acc = torch.zeros((), device=device)
         self.graph_mode = None
 

@@ -432,15 +432,23 @@ __global__ __launch_bounds__(256) void bn_small_apply_kernel(
 constexpr int kFusedThreads = 512;
 constexpr int kFusedMaxN = 512;
 
-template <int HW, int BWD, int CW>
+//
+// src (nullable): the kernel's main input — x in forward, dy in backward — is the sum of
+// `nslab` split-K slabs (slab stride = numel) of the producing convolution (a deferred
+// conv_slab_sum, ops/slablink.py), added in slab order exactly like conv_slab_sum_kernel
+// (bitwise-equal values); the forward also stores the sum to x (BN's saved input).
+// MAXN: largest batch the register arrays hold (512 for HW <= 16; 128 for the 8x8 maps of
+// layer1 at the strong-scaling per-GPU batches 64 / 128, CW = HW = 64).
+template <int HW, int BWD, int CW, int MAXN = kFusedMaxN>
 __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
     const float* __restrict__ x, const float* __restrict__ res, const float* __restrict__ dy,
     const float* __restrict__ yin, const float* __restrict__ gamma, const float* __restrict__ beta,
     float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt, float* __restrict__ save_mean,
     float* __restrict__ save_invstd, float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ out,
-    float* __restrict__ dres, int N, int C, float eps, float momentum, int relu) {
+    float* __restrict__ dres, int N, int C, float eps, float momentum, int relu, const float* __restrict__ src,
+    int nslab) {
   constexpr int RG = kFusedThreads / CW;
-  constexpr int NP = kFusedMaxN / RG;
+  constexpr int NP = MAXN / RG;
   constexpr int NW = kFusedThreads / 64;
   static_assert(CW % HW == 0 && 64 % CW == 0, "bad column block");
   __shared__ double red[2][NW][CW];
@@ -460,12 +468,26 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
     const int n = g + k * RG;
     const bool ok = ok_col && n < N;
     const int64_t o = (int64_t)n * CHW + j;
-    v[k] = ok ? x[o] : 0.f;
-    if (BWD) {
-      d[k] = ok ? dy[o] : 0.f;
-      m[k] = (ok && relu) ? yin[o] : 1.f;
-    } else {
+    float sum = 0.f;
+    if (src != nullptr && ok) {  // deferred split-K sum, slab order
+      const int64_t slab = (int64_t)N * CHW;
+      sum = src[o];
+      for (int z = 1; z < nslab; ++z) sum += src[z * slab + o];
+    }
+    if (!BWD) {
+      v[k] = ok ? (src ? sum : x[o]) : 0.f;
       d[k] = (ok && res) ? res[o] : 0.f;
+    } else {
+      v[k] = ok ? x[o] : 0.f;
+      d[k] = ok ? (src ? sum : dy[o]) : 0.f;
+      m[k] = (ok && relu) ? yin[o] : 1.f;
+    }
+  }
+  if (!BWD && src != nullptr) {  // BN's saved input = the conv output
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const int n = g + k * RG;
+      if (ok_col && n < N) const_cast<float*>(x)[(int64_t)n * CHW + j] = v[k];
     }
   }
   double a = 0.0, b = 0.0;
@@ -563,7 +585,22 @@ static int bn_single_max() {
   return v;
 }
 
+// 8x8 maps (ResNet layer1) at per-GPU batch <= kFused64MaxN: one launch per direction, one
+// workgroup per channel.  OFF by default (NDP_BN_SINGLE64=1 to A/B): measured on 1x MI355X
+// (ResNet-18 step, graph) 1.0797 vs 1.0772 ms at batch 64 and 1.2322 vs 1.2122 at 128 — 64
+// workgroups cannot stream the 8x8 maps (or the split-K slabs they would sum) fast enough.
+constexpr int kFused64MaxN = 128;
+static bool bn_single64() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("NDP_BN_SINGLE64");
+    v = e ? atoi(e) : 0;
+  }
+  return v != 0;
+}
+
 static bool bn_fused_ok(int N, int C, int HW) {
+  if (HW == 64) return bn_single64() && N >= 1 && N <= kFused64MaxN;
   return (HW == 1 || HW == 2 || HW == 4 || HW == 8 || HW == 16) && HW <= bn_single_max() && N >= 1 &&
          N <= kFusedMaxN && (int64_t)N * C * HW < (1LL << 30);
 }
@@ -583,12 +620,13 @@ template <int BWD, int CW>
 static void launch_small_fused_cw(int HW, const float* x, const float* res, const float* dy, const float* yin,
                                   const float* gamma, const float* beta, float* rmean, float* rvar, int64_t* nbt,
                                   float* sm, float* si, float* dgamma, float* dbeta, float* out, float* dres, int N,
-                                  int C, float eps, float momentum, int relu, hipStream_t s) {
+                                  int C, float eps, float momentum, int relu, hipStream_t s, const float* src,
+                                  int nslab) {
   const dim3 grid((unsigned)(((int64_t)C * HW + CW - 1) / CW));
 #define NDP_BN_FUSED(HWV)                                                                                            \
   if constexpr (CW % HWV == 0)                                                                                       \
     hipLaunchKernelGGL((bn_small_fused_kernel<HWV, BWD, CW>), grid, dim3(kFusedThreads), 0, s, x, res, dy, yin, gamma, \
-                       beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out, dres, N, C, eps, momentum, relu)
+                       beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out, dres, N, C, eps, momentum, relu, src, nslab)
   switch (HW) {  // the caller picks CW >= HW
     case 1: NDP_BN_FUSED(1); break;
     case 2: NDP_BN_FUSED(2); break;
@@ -603,19 +641,26 @@ template <int BWD>
 static void launch_small_fused(int HW, const float* x, const float* res, const float* dy, const float* yin,
                                const float* gamma, const float* beta, float* rmean, float* rvar, int64_t* nbt,
                                float* sm, float* si, float* dgamma, float* dbeta, float* out, float* dres, int N,
-                               int C, float eps, float momentum, int relu, hipStream_t s) {
+                               int C, float eps, float momentum, int relu, hipStream_t s, const float* src,
+                               int nslab) {
+  if (HW == 64) {  // one workgroup per channel: 64 lanes x 8 row groups, <= 128 images
+    hipLaunchKernelGGL((bn_small_fused_kernel<64, BWD, 64, kFused64MaxN>), dim3((unsigned)C), dim3(kFusedThreads), 0,
+                       s, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out, dres, N, C, eps,
+                       momentum, relu, src, nslab);
+    return;
+  }
   switch (bn_colw() > HW ? bn_colw() : HW) {
     case 16:
       launch_small_fused_cw<BWD, 16>(HW, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out,
-                                     dres, N, C, eps, momentum, relu, s);
+                                     dres, N, C, eps, momentum, relu, s, src, nslab);
       break;
     default:
       launch_small_fused_cw<BWD, 8>(HW, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out,
-                                    dres, N, C, eps, momentum, relu, s);
+                                    dres, N, C, eps, momentum, relu, s, src, nslab);
       break;
     case 4:
       launch_small_fused_cw<BWD, 4>(HW, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out,
-                                    dres, N, C, eps, momentum, relu, s);
+                                    dres, N, C, eps, momentum, relu, s, src, nslab);
   }
 }
 
@@ -672,12 +717,15 @@ int bn_slices(int N, int C, int HW) {
 void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamma, const float* beta,
                    float* rmean, float* rvar, int64_t* nbt, float* save_mean, float* save_invstd,
                    double* part, int N, int C, int HW, int S, float eps, float momentum, int relu,
-                   int training, int single, hipStream_t s) {
+                   int training, int single, hipStream_t s, const float* xpart, int nslab) {
+  if (xpart != nullptr && nslab < 2) xpart = nullptr;
   if (training && single && bn_fused_ok(N, C, HW)) {
     launch_small_fused<0>(HW, x, res, nullptr, nullptr, gamma, beta, rmean, rvar, nbt, save_mean, save_invstd,
-                          nullptr, nullptr, y, nullptr, N, C, eps, momentum, relu, s);
+                          nullptr, nullptr, y, nullptr, N, C, eps, momentum, relu, s, xpart, nslab);
     return;
   }
+  if (xpart != nullptr)  // no fused consumer for this shape: finish the conv's split-K sum here
+    launch_slab_sum(xpart, const_cast<float*>(x), (int64_t)N * C * HW, nslab, s);
   if (training && bn_small_path(N, C, HW)) {
     const int Ss = bn_small_slices(N, C, HW);
     double* coef = part + (int64_t)C * Ss * 2;
@@ -706,13 +754,17 @@ void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamm
 
 void launch_bn_bwd(const float* dy, const float* y, const float* x, const float* gamma, const float* save_mean,
                    const float* save_invstd, float* dx, float* dres, float* dgamma, float* dbeta, double* part,
-                   int N, int C, int HW, int S, int relu, int single, hipStream_t s) {
+                   int N, int C, int HW, int S, int relu, int single, hipStream_t s, const float* dypart,
+                   int nslab) {
+  if (dypart != nullptr && nslab < 2) dypart = nullptr;
   if (single && bn_fused_ok(N, C, HW)) {
     launch_small_fused<1>(HW, x, nullptr, dy, y, gamma, nullptr, nullptr, nullptr, nullptr,
                           const_cast<float*>(save_mean), const_cast<float*>(save_invstd), dgamma, dbeta, dx, dres, N, C,
-                          0.f, 0.f, relu, s);
+                          0.f, 0.f, relu, s, dypart, nslab);
     return;
   }
+  if (dypart != nullptr)  // no fused consumer: finish the conv's split-K grad-x sum into dy
+    launch_slab_sum(dypart, const_cast<float*>(dy), (int64_t)N * C * HW, nslab, s);
   if (bn_small_path(N, C, HW)) {
     const int Ss = bn_small_slices(N, C, HW);
     double* coef = part + (int64_t)C * Ss * 2;

@@ -273,13 +273,31 @@ const float* opt_f32(const c10::optional<torch::Tensor>& t, const char* name) {
   return t->data_ptr<float>();
 }
 
+// deferred split-K slabs of a conv output (ops/slablink.py): nslab slabs of `numel` floats
+const float* slab_input(const c10::optional<torch::Tensor>& part, int64_t nslab, int64_t numel, const char* who) {
+  if (!part.has_value() || nslab < 2) return nullptr;
+  check_f32(*part, "slab part");
+  TORCH_CHECK(numel % 4 == 0 && part->numel() >= nslab * numel, who, ": slab scratch too small");
+  return part->data_ptr<float>();
+}
+
+// out = sum of nslab split-K slabs (a deferred conv sum that found no fused consumer)
+void slab_sum(torch::Tensor part, torch::Tensor out, int64_t nslab) {
+  check_f32(out, "out");
+  TORCH_CHECK(out.is_contiguous(), "slab_sum: contiguous output");
+  const float* p = slab_input(part, nslab, out.numel(), "slab_sum");
+  TORCH_CHECK(p != nullptr, "slab_sum: needs >= 2 slabs");
+  ndp::launch_slab_sum(p, out.data_ptr<float>(), out.numel(), (int)nslab, cur_stream());
+  check_launch("launch_slab_sum");
+}
+
 // fused BN(+res)(+relu) forward; returns nothing, writes y / save_mean / save_invstd
 void bn_fwd(torch::Tensor x, c10::optional<torch::Tensor> res, torch::Tensor y,
             c10::optional<torch::Tensor> gamma, c10::optional<torch::Tensor> beta,
             c10::optional<torch::Tensor> rmean, c10::optional<torch::Tensor> rvar,
             c10::optional<torch::Tensor> nbt, torch::Tensor save_mean, torch::Tensor save_invstd,
             torch::Tensor part, double eps, double momentum, bool relu, bool training,
-            bool single) {
+            bool single, c10::optional<torch::Tensor> xpart, int64_t nslab) {
   check_f32(x, "x"); check_f32(y, "y"); check_f32(save_mean, "save_mean"); check_f32(save_invstd, "save_invstd");
   check_dev(part, "part");
   TORCH_CHECK(x.dim() >= 2 && x.sizes() == y.sizes(), "bn_fwd: bad shapes");
@@ -296,18 +314,20 @@ void bn_fwd(torch::Tensor x, c10::optional<torch::Tensor> res, torch::Tensor y,
     TORCH_CHECK(nbt->scalar_type() == torch::kInt64, "num_batches_tracked must be int64");
     nb = nbt->data_ptr<int64_t>();
   }
+  const float* xp = slab_input(xpart, nslab, x.numel(), "bn_fwd");
+  TORCH_CHECK(xp == nullptr || training, "bn_fwd: deferred conv slabs need training mode");
   ndp::launch_bn_fwd(x.data_ptr<float>(), opt_f32(res, "res"), y.data_ptr<float>(), opt_f32(gamma, "gamma"),
                      opt_f32(beta, "beta"), const_cast<float*>(opt_f32(rmean, "running_mean")),
                      const_cast<float*>(opt_f32(rvar, "running_var")), nb, save_mean.data_ptr<float>(),
                      save_invstd.data_ptr<float>(), part.data_ptr<double>(), N, C, HW, S, (float)eps,
-                     (float)momentum, relu ? 1 : 0, training ? 1 : 0, single ? 1 : 0, cur_stream());
+                     (float)momentum, relu ? 1 : 0, training ? 1 : 0, single ? 1 : 0, cur_stream(), xp, (int)nslab);
   check_launch("launch_bn_fwd");
 }
 
 void bn_bwd(torch::Tensor dy, c10::optional<torch::Tensor> y, torch::Tensor x, c10::optional<torch::Tensor> gamma,
             torch::Tensor save_mean, torch::Tensor save_invstd, torch::Tensor dx, c10::optional<torch::Tensor> dres,
             c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta, torch::Tensor part,
-            bool relu, bool single) {
+            bool relu, bool single, c10::optional<torch::Tensor> dypart, int64_t nslab) {
   check_f32(dy, "dy"); check_f32(x, "x"); check_f32(dx, "dx"); check_dev(part, "part");
   TORCH_CHECK(dy.sizes() == x.sizes() && dx.sizes() == x.sizes(), "bn_bwd: bad shapes");
   TORCH_CHECK(!relu || y.has_value(), "bn_bwd: relu needs y");
@@ -320,7 +340,8 @@ void bn_bwd(torch::Tensor dy, c10::optional<torch::Tensor> y, torch::Tensor x, c
                      save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(), dx.data_ptr<float>(),
                      const_cast<float*>(opt_f32(dres, "dres")), const_cast<float*>(opt_f32(dgamma, "dgamma")),
                      const_cast<float*>(opt_f32(dbeta, "dbeta")), part.data_ptr<double>(), N, C, HW, S,
-                     relu ? 1 : 0, single ? 1 : 0, cur_stream());
+                     relu ? 1 : 0, single ? 1 : 0, cur_stream(), slab_input(dypart, nslab, dy.numel(), "bn_bwd"),
+                     (int)nslab);
   check_launch("launch_bn_bwd");
 }
 
@@ -540,8 +561,9 @@ int conv_batch(const torch::Tensor& t, const ndp::ConvGeom& g, int imgs) {
   return B;
 }
 
-void conv_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, const std::vector<int64_t>& geom,
-              c10::optional<torch::Tensor> part) {
+// defer: split-K slabs are left in `part` for the consumer; returns how many (1 = y final)
+int64_t conv_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, const std::vector<int64_t>& geom,
+                 c10::optional<torch::Tensor> part, bool defer) {
   const ndp::ConvGeom g = conv_geom(geom);
   const int cls = ndp::conv_direct_class(g);
   const int B = conv_batch(x, g, ndp::conv_fwd_imgs(cls));
@@ -550,12 +572,14 @@ void conv_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, const std::vect
   conv_check(y, "y", B, g.Co, g.OH, g.OW);
   const int ks = ndp::conv_ksplit(cls, g, B, false);
   float* pp = conv_part(part, ks, y.numel(), "conv_fwd");
-  ndp::launch_conv_fwd(x.data_ptr<float>(), w.data_ptr<float>(), y.data_ptr<float>(), B, g, pp, cur_stream());
+  const int left = ndp::launch_conv_fwd(x.data_ptr<float>(), w.data_ptr<float>(), y.data_ptr<float>(), B, g, pp,
+                                        cur_stream(), defer);
   check_launch("launch_conv_fwd");
+  return left;
 }
 
-void conv_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, const std::vector<int64_t>& geom,
-                c10::optional<torch::Tensor> part, c10::optional<torch::Tensor> addend) {
+int64_t conv_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, const std::vector<int64_t>& geom,
+                   c10::optional<torch::Tensor> part, c10::optional<torch::Tensor> addend, bool defer) {
   const ndp::ConvGeom g = conv_geom(geom);
   const int cls = ndp::conv_direct_class(g);
   TORCH_CHECK(cls >= 0 && ndp::conv_dgrad_direct(cls), "conv_dgrad: no direct grad-x kernel for this geometry");
@@ -575,8 +599,10 @@ void conv_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, const std::
     TORCH_CHECK((reinterpret_cast<uintptr_t>(addend->data_ptr()) & 15) == 0, "conv_dgrad: 16-B aligned addend");
     ap = addend->data_ptr<float>();
   }
-  ndp::launch_conv_dgrad(dy.data_ptr<float>(), w.data_ptr<float>(), dx.data_ptr<float>(), B, g, pp, cur_stream(), ap);
+  const int left = ndp::launch_conv_dgrad(dy.data_ptr<float>(), w.data_ptr<float>(), dx.data_ptr<float>(), B, g, pp,
+                                          cur_stream(), ap, defer && cls != 4);
   check_launch("launch_conv_dgrad");
+  return left;
 }
 
 // dw None: write the per-slice partial slabs only (the caller sums them, batched)
@@ -610,6 +636,37 @@ void colsum(torch::Tensor g, torch::Tensor out) {
   auto part = torch::empty({(int64_t)ndp::colsum_chunks(M, N) * N}, g.options());
   ndp::launch_colsum(g.data_ptr<float>(), M, N, part.data_ptr<float>(), out.data_ptr<float>(), cur_stream());
   check_launch("launch_colsum");
+}
+
+// fused cross-entropy forward: loss (0-d), dl [B, K] saved gradient; scratch = rowloss [B] + inv [1]
+void ce_fwd(torch::Tensor x, torch::Tensor tgt, torch::Tensor dl, torch::Tensor scratch, torch::Tensor loss,
+            torch::Tensor ctr, int64_t ignore_index) {
+  check_f32(x, "logits"); check_f32(dl, "dl"); check_f32(scratch, "scratch"); check_f32(loss, "loss");
+  check_dev(tgt, "target"); check_dev(ctr, "ctr");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && dl.sizes() == x.sizes() && dl.is_contiguous(),
+              "ce_fwd: logits / dl must be contiguous [B, K]");
+  TORCH_CHECK(tgt.scalar_type() == torch::kInt64 && tgt.is_contiguous() && tgt.numel() == x.size(0),
+              "ce_fwd: target must be contiguous int64 [B]");
+  TORCH_CHECK(scratch.numel() >= x.size(0) + 1 && loss.numel() == 1, "ce_fwd: scratch / loss size");
+  TORCH_CHECK(ctr.scalar_type() == torch::kInt32 && ctr.numel() >= 1, "ce_fwd: int32 counter");
+  TORCH_CHECK(x.size(0) >= 1 && x.size(0) < (1LL << 31) && x.size(1) >= 1, "ce_fwd: empty batch");
+  const int B = (int)x.size(0);
+  float* sp = scratch.data_ptr<float>();
+  ndp::launch_ce_fwd(x.data_ptr<float>(), tgt.data_ptr<int64_t>(), B, (int)x.size(1), ignore_index,
+                     dl.data_ptr<float>(), sp, loss.data_ptr<float>(), sp + B,
+                     reinterpret_cast<unsigned*>(ctr.data_ptr<int32_t>()), cur_stream());
+  check_launch("launch_ce_fwd");
+}
+
+void ce_bwd(torch::Tensor dl, torch::Tensor g, torch::Tensor scratch, torch::Tensor dx) {
+  check_f32(dl, "dl"); check_f32(g, "grad"); check_f32(scratch, "scratch"); check_f32(dx, "dx");
+  TORCH_CHECK(dl.is_contiguous() && dx.is_contiguous() && dx.sizes() == dl.sizes() && dl.dim() == 2, "ce_bwd: shapes");
+  TORCH_CHECK(g.numel() == 1 && scratch.numel() >= dl.size(0) + 1, "ce_bwd: scalar grad / scratch");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(dl.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(dx.data_ptr()) & 15) == 0,
+              "ce_bwd: 16-B aligned tensors");
+  ndp::launch_ce_bwd(dl.data_ptr<float>(), g.data_ptr<float>(), scratch.data_ptr<float>() + dl.size(0),
+                     dx.data_ptr<float>(), dl.numel(), cur_stream());
+  check_launch("launch_ce_bwd");
 }
 
 void embedding_backward(torch::Tensor ids, torch::Tensor gout, torch::Tensor gw, int64_t pad, torch::Tensor perm,
@@ -720,9 +777,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sgd_momentum", &sgd_momentum);
   m.def("add", &add);
   m.def("delay_ns", &delay_ns);
-  m.def("bn_fwd", &bn_fwd);
-  m.def("bn_bwd", &bn_bwd);
+  m.def("bn_fwd", &bn_fwd, py::arg("x"), py::arg("res"), py::arg("y"), py::arg("gamma"), py::arg("beta"),
+        py::arg("rmean"), py::arg("rvar"), py::arg("nbt"), py::arg("save_mean"), py::arg("save_invstd"),
+        py::arg("part"), py::arg("eps"), py::arg("momentum"), py::arg("relu"), py::arg("training"),
+        py::arg("single"), py::arg("xpart") = py::none(), py::arg("nslab") = 0);
+  m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("gamma"), py::arg("save_mean"),
+        py::arg("save_invstd"), py::arg("dx"), py::arg("dres"), py::arg("dgamma"), py::arg("dbeta"), py::arg("part"),
+        py::arg("relu"), py::arg("single"), py::arg("dypart") = py::none(), py::arg("nslab") = 0);
   m.def("bn_slices", &bn_slices);
+  m.def("slab_sum", &slab_sum);
   m.def("bn_part_numel", &bn_part_numel);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
@@ -735,12 +798,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("toeplitz_fold_many", &toeplitz_fold_many);
   m.def("slab_sum_many", &slab_sum_many);
   m.def("conv_plan", &conv_plan, py::arg("geom"), py::arg("batch"));
-  m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("geom"), py::arg("part") = py::none());
+  m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("geom"), py::arg("part") = py::none(),
+        py::arg("defer") = false);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("geom"),
-        py::arg("part") = py::none(), py::arg("addend") = py::none());
+        py::arg("part") = py::none(), py::arg("addend") = py::none(), py::arg("defer") = false);
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("part"), py::arg("dw"), py::arg("geom"));
   m.def("embedding_backward", &embedding_backward);
   m.def("colsum", &colsum);
+  m.def("ce_fwd", &ce_fwd);
+  m.def("ce_bwd", &ce_bwd);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   register_comm(m);

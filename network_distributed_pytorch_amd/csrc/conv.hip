@@ -753,8 +753,8 @@ static void set_lds(KernelT k, size_t bytes) {
 // (small per-GPU batches: the strong-scaling shapes 512 / N).
 template <int R, int S, int ST, int PD, int H, int W, int CK, int BM, int IMGS, int WM, int NBUF, int KB, bool TRANSW,
           bool VEC, int UPS = 1>
-static void run_fwd(const float* x, const float* w, float* y, int B, int Cin, int Kout, int ksplit, float* part,
-                    hipStream_t s, const float* addend = nullptr) {
+static int run_fwd(const float* x, const float* w, float* y, int B, int Cin, int Kout, int ksplit, float* part,
+                   hipStream_t s, const float* addend = nullptr, bool defer = false) {
   using G = ConvFwdCfg<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW>;
   auto k = conv_fwd_kernel<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW, VEC, UPS>;
   static bool attr = false;  // once per instantiation (> 64 KiB of LDS needs the opt-in)
@@ -766,6 +766,9 @@ static void run_fwd(const float* x, const float* w, float* y, int B, int Cin, in
   const int64_t slab = (int64_t)B * Kout * G::PQ;  // compact partial tile layout
   hipLaunchKernelGGL(k, dim3(B / IMGS, Kout / BM, ksplit), dim3(256), G::LDS_BYTES, s, x, w, y, part, Cin, Kout, cps,
                      slab, ksplit > 1 ? nullptr : addend);
+  // defer: leave the ksplit slabs for the consumer (the fused BN kernel sums them while it
+  // reads its input, ops/slablink.py) — one launch fewer per conv
+  if (ksplit > 1 && defer && UPS == 1 && addend == nullptr) return ksplit;
   if (ksplit > 1) {
     if constexpr (UPS == 1)
       hipLaunchKernelGGL(conv_slab_sum_kernel, dim3((unsigned)((slab / 4 + 15) / 16)), dim3(256), 0, s, part, y, slab,
@@ -774,6 +777,12 @@ static void run_fwd(const float* x, const float* w, float* y, int B, int Cin, in
       hipLaunchKernelGGL(conv_slab_sum_ups_kernel, dim3((unsigned)((slab + 255) / 256)), dim3(256), 0, s, part, y, slab,
                          ksplit);
   }
+  return 1;
+}
+
+void launch_slab_sum(const float* part, float* out, int64_t n, int nslab, hipStream_t s) {
+  hipLaunchKernelGGL(conv_slab_sum_kernel, dim3((unsigned)((n / 4 + 15) / 16)), dim3(256), 0, s, part, out, n, nslab,
+                     nullptr);
 }
 
 template <int R, int S, int ST, int PD, int H, int W, int CB, int BM, int NW, int NBPW, int KB>
@@ -859,36 +868,73 @@ int conv_ksplit(int cls, const ConvGeom& g, int B, bool dgrad) {
   return pow2_floor(ks);
 }
 bool conv_dgrad_direct(int cls) { return cls == 0 || cls == 1 || cls == 4; }
-void launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s) {
+// NDP_CONV_VARIANT (benchmarking only): 1 = two images per layer1 tile; 2 = 16-channel
+// chunks (half the chunk barriers, twice the MFMA work behind each prefetch) for the 3x3
+// classes 0-2; 3 = 16-channel chunks for classes 1-2 only (already one workgroup per CU)
+static bool ck16(int cls) {
+  const int v = conv_variant();
+  return (v == 2 && cls <= 2) || (v == 3 && (cls == 1 || cls == 2));
+}
+
+int launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s,
+                    bool defer) {
   const int cls = conv_direct_class(g);
   const int ks = conv_ksplit(cls, g, B, false);
+  const bool c16 = ck16(cls);
   switch (cls) {
     case 0:
-      if (conv_variant() == 1) run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 2, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s);
-      else run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s);
-      break;
-    case 1: run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s); break;
-    case 2: run_fwd<3, 3, 2, 1, 8, 8, 8, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s); break;
-    case 3: run_fwd<7, 7, 2, 3, 32, 32, 4, 64, 1, 2, 1, 7, false, false>(x, w, y, B, g.C, g.Co, 1, nullptr, s); break;
-    case 4: run_fwd<1, 1, 2, 0, 8, 8, 8, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s); break;
-    default: break;
+      if (conv_variant() == 1)
+        return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 2, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s, nullptr,
+                                                                         defer);
+      if (c16)
+        return run_fwd<3, 3, 1, 1, 8, 8, 16, 64, 1, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s,
+                                                                          nullptr, defer);
+      return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s, nullptr,
+                                                                       defer);
+    case 1:
+      if (c16)
+        return run_fwd<3, 3, 1, 1, 4, 4, 16, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s,
+                                                                          nullptr, defer);
+      return run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s, nullptr,
+                                                                       defer);
+    case 2:
+      if (c16)
+        return run_fwd<3, 3, 2, 1, 8, 8, 16, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s,
+                                                                          nullptr, defer);
+      return run_fwd<3, 3, 2, 1, 8, 8, 8, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s, nullptr,
+                                                                       defer);
+    case 3: return run_fwd<7, 7, 2, 3, 32, 32, 4, 64, 1, 2, 1, 7, false, false>(x, w, y, B, g.C, g.Co, 1, nullptr, s);
+    case 4:
+      return run_fwd<1, 1, 2, 0, 8, 8, 8, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s, nullptr,
+                                                                       defer);
+    default: return 1;
   }
 }
 
 // dx[B, C, H, W] from dy[B, Co, OH, OW] (stride-1 classes only)
-void launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, float* part,
-                       hipStream_t s, const float* addend) {
+int launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, float* part,
+                      hipStream_t s, const float* addend, bool defer) {
   const int cls = conv_direct_class(g);
   const int ks = conv_ksplit(cls, g, B, true);
+  const bool c16 = ck16(cls);
   switch (cls) {
     case 0:
       if (conv_variant() == 1)
-        run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 2, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s, addend);
-      else run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s, addend);
-      break;
-    case 1: run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s, addend); break;
-    case 4: run_fwd<1, 1, 1, 0, 4, 4, 8, 64, 4, 2, 2, 4, true, true, 2>(dy, w, dx, B, g.Co, g.C, ks, part, s); break;
-    default: break;
+        return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 2, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s, addend,
+                                                                        defer);
+      if (c16)
+        return run_fwd<3, 3, 1, 1, 8, 8, 16, 64, 1, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s,
+                                                                         addend, defer);
+      return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s, addend,
+                                                                      defer);
+    case 1:
+      if (c16)
+        return run_fwd<3, 3, 1, 1, 4, 4, 16, 64, 4, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s,
+                                                                         addend, defer);
+      return run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s, addend,
+                                                                      defer);
+    case 4: return run_fwd<1, 1, 1, 0, 4, 4, 8, 64, 4, 2, 2, 4, true, true, 2>(dy, w, dx, B, g.Co, g.C, ks, part, s);
+    default: return 1;
   }
 }
 

@@ -8,7 +8,9 @@
 //   pass 1: workgroup (column strip of 256 columns, row chunk) — 64 lanes own 4 columns
 //           each (float4 loads, whole rows coalesced), 4 lane groups stride the chunk's
 //           rows; the 4 group sums are added in LDS in fixed order -> part[chunk][n];
-//   pass 2: db[n] = sum over chunks in order.
+//   pass 2: db[n] = sum over chunks (conv.hip's split-K slab sum: 16 chunk groups per float4
+//           column, group sums added in fixed order — a serial per-column loop here took 18 µs
+//           per DistilBERT Linear, profiles/r2/distilbert_psgd_r8_graph_kernels.md).
 // Fixed summation order everywhere: bitwise reproducible, no atomics, no semaphores.
 #include <hip/hip_runtime.h>
 #include "ndp_kernels.h"
@@ -39,15 +41,6 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __rest
   }
 }
 
-__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int chunks, int N,
-                                                           float* __restrict__ out) {
-  const int n = blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
-  float s = 0.f;
-  for (int c = 0; c < chunks; ++c) s += part[(int64_t)c * N + n];
-  out[n] = s;
-}
-
 int colsum_chunks(int64_t M, int N) {
   const int strips = (N / 4 + 63) / 64;
   int chunks = (256 + strips - 1) / strips;          // ~256 workgroups in pass 1
@@ -61,7 +54,7 @@ void launch_colsum(const float* g, int64_t M, int N, float* part, float* out, hi
   const int rpc = (int)((M + chunks - 1) / chunks);
   const int strips = (N / 4 + 63) / 64;
   hipLaunchKernelGGL(colsum_partial_kernel, dim3(strips, chunks), dim3(256), 0, s, g, M, N, rpc, part);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((N + 255) / 256), dim3(256), 0, s, part, chunks, N, out);
+  launch_slab_sum(part, out, N, chunks, s);
 }
 
 }  // namespace ndp

@@ -118,10 +118,13 @@ int64_t bn_part_numel(int N, int C, int HW);
 void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamma, const float* beta,
                    float* rmean, float* rvar, int64_t* nbt, float* save_mean, float* save_invstd,
                    double* part, int N, int C, int HW, int S, float eps, float momentum, int relu,
-                   int training, int single, hipStream_t s);
+                   int training, int single, hipStream_t s, const float* xpart = nullptr, int nslab = 0);
+// xpart / dypart (nullable): the input x (forward) / dy (backward) is the sum of `nslab`
+// split-K slabs of numel(x) floats (a deferred conv sum); the forward also writes the sum to x
 void launch_bn_bwd(const float* dy, const float* y, const float* x, const float* gamma, const float* save_mean,
                    const float* save_invstd, float* dx, float* dres, float* dgamma, float* dbeta, double* part,
-                   int N, int C, int HW, int S, int relu, int single, hipStream_t s);
+                   int N, int C, int HW, int S, int relu, int single, hipStream_t s, const float* dypart = nullptr,
+                   int nslab = 0);
 }  // namespace ndp
 
 // ---- embedding backward (embedding.hip) -------------------------------------------------
@@ -135,6 +138,16 @@ int colsum_chunks(int64_t M, int N);
 void launch_colsum(const float* g, int64_t M, int N, float* part, float* out, hipStream_t s);
 void launch_embedding_backward(const int64_t* ids, int T, const float* gout, int V, int D, int pad, int* perm,
                                int* row_start, int* row_cnt, float* gw, hipStream_t s);
+}  // namespace ndp
+
+// ---- fused softmax cross-entropy, mean reduction (loss.hip) -----------------------------
+// x [B, K] logits, tgt [B] int64; dl [B, K] saved gradient (unscaled softmax - onehot),
+// rowloss [B] scratch, loss / inv device scalars, ctr: one zeroed uint32 (re-armed by the kernel)
+namespace ndp {
+void launch_ce_fwd(const float* x, const int64_t* tgt, int B, int K, int64_t ignore, float* dl, float* rowloss,
+                   float* loss, float* inv, unsigned* ctr, hipStream_t s);
+// dx = dl * (g[0] * inv[0])
+void launch_ce_bwd(const float* dl, const float* g, const float* inv, float* dx, int64_t n, hipStream_t s);
 }  // namespace ndp
 
 // ---- convolutions, NCHW fp32 (conv.hip) -------------------------------------------------
@@ -187,10 +200,15 @@ bool conv_dgrad_direct(int cls);
 // launchers need `part` scratch of ksplit * (compact output) floats: B * outC * OH * OW
 // (the stride-2 1x1 grad-x: B * C * 4 * 4 before its even-pixel scatter)
 int conv_ksplit(int cls, const ConvGeom& g, int B, bool dgrad);
-void launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s);
-// addend (nullable, stride-1 classes): dx += addend in the epilogue / split-K sum
-void launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, float* part,
-                       hipStream_t s, const float* addend = nullptr);
+// defer: with split-K, skip the slab sum and return the number of slabs left in `part`
+// (compact output layout, slab = numel(out)); returns 1 when `y` / `dx` holds the result
+int launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s,
+                    bool defer = false);
+// addend (nullable, stride-1 classes): dx += addend in the epilogue / split-K sum (never deferred)
+int launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, float* part,
+                      hipStream_t s, const float* addend = nullptr, bool defer = false);
+// out[i] = sum_{z < nslab} part[z * n + i] in z order (n % 4 == 0), same order as the split-K sums
+void launch_slab_sum(const float* part, float* out, int64_t n, int nslab, hipStream_t s);
 // part: (B / conv_wgrad_imgs(cls, g, B)) * Co*C*KH*KW floats of scratch
 void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, int B, const ConvGeom& g,
                        hipStream_t s);

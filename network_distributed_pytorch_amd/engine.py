@@ -29,6 +29,7 @@ import torch
 import torch.distributed as dist
 
 from .ops import gemm_tuning
+from .ops.loss import CrossEntropyLoss
 from .models import build_model
 from .parallel.comm import LINK_PRESETS, Communicator
 from .parallel.trainer import build_grad_sync
@@ -186,7 +187,7 @@ def run_task(config) -> Dict[str, Any]:
     if config["task"] == "mlp":
         model_name = "mlp"
     model = build_model(model_name, config["num_classes"] if config["task"] != "imdb" else 2).to(device)
-    crit = torch.nn.CrossEntropyLoss().to(device)
+    crit = CrossEntropyLoss().to(device)  # fused gfx950 kernel on device (ops/loss.py)
     link = None if config.get("link", "none") == "none" else LINK_PRESETS[config["link"]]
     comm = Communicator(link=link, emulate_world=config.get("emulate_world"),
                         device=device if device.type == "cuda" else None)

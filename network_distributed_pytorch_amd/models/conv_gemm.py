@@ -205,9 +205,12 @@ class GemmConv2d(nn.Conv2d):
                 self._maps[key] = (src, dst, oh, ow, sub, None)
         return self._maps[key]
 
-    def forward(self, x, link=None):
+    def forward(self, x, link=None, slab_out=None, grad_slab=None):
         """``link`` (ops/gradlink.GradLink): a residual-branch gradient to add into this
-        conv's grad-x (fused into the kernel / GEMM where the path allows)."""
+        conv's grad-x (fused into the kernel / GEMM where the path allows).
+        ``slab_out`` / ``grad_slab`` (ops/slablink.SlabLink, direct kernels only): the
+        forward / grad-x split-K slabs go to the neighbouring fused BN instead of a sum
+        launch (other paths leave the links empty)."""
         if not (self.gemm and x.is_cuda and self.groups == 1 and self.dilation == (1, 1) and self.bias is None
                 and self.stride[0] == self.stride[1] and self.padding[0] == self.padding[1]
                 and self.padding_mode == "zeros" and x.dtype == torch.float32):
@@ -218,7 +221,7 @@ class GemmConv2d(nn.Conv2d):
         if self.direct:
             plan = direct_plan(x, self.weight, s, p)
             if plan is not None:
-                return DirectConvFn.apply(x, self.weight, plan, link)
+                return DirectConvFn.apply(x, self.weight, plan, link, slab_out, grad_slab)
         oh = (H + 2 * p - kh) // s + 1
         ow = (W + 2 * p - kw) // s + 1
         if not eligible(H, W, oh, ow):

@@ -26,6 +26,7 @@ import torch.nn.functional as F
 from ..ops.attention import attention, fused_ok
 from ..ops.embedding import Embedding
 from ..ops.linear import Linear
+from ..ops.loss import cross_entropy as native_ce
 
 __all__ = ["DistilBertConfig", "DistilBertForSequenceClassification", "distilbert_base"]
 
@@ -190,7 +191,9 @@ class DistilBertForSequenceClassification(nn.Module):
         pooled = self.dropout(F.relu(self.pre_classifier(hidden[:, 0])))
         logits = self.classifier(pooled)
         if labels is not None:
-            loss = F.cross_entropy(logits.view(-1, self.config.num_labels), labels.view(-1))
+            lg, lb = logits.view(-1, self.config.num_labels), labels.view(-1)
+            # native kernels on: the fused gfx950 cross-entropy (ops/loss.py), same math
+            loss = native_ce(lg, lb) if self.config.fused_attention else F.cross_entropy(lg, lb)
             return SequenceClassifierOutput((loss, logits))
         return SequenceClassifierOutput((logits,))
 

@@ -20,6 +20,7 @@ direction (same parameters/buffers/state_dict keys as ``nn.BatchNorm2d``).
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Type, Union
 
 import torch
@@ -28,10 +29,15 @@ import torch.nn as nn
 from ..ops.batchnorm import BatchNormAct2d
 from ..ops.gradlink import GradLink
 from ..ops.pool import MaxPool2d
+from ..ops.slablink import SlabLink
 from .conv_gemm import GemmConv2d, ToeplitzBank
 
 __all__ = ["ResNet", "BasicBlock", "Bottleneck", "resnet18", "resnet34", "resnet50", "resnet101",
            "resnet152", "build_resnet"]
+
+# split-K slab hand-off between direct convs and fused BN (ops/slablink.py; NDP_SLAB_LINKS=0
+# or tests flip it for A/B)
+SLAB_LINKS = os.environ.get("NDP_SLAB_LINKS", "1") != "0"
 
 
 def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -59,14 +65,27 @@ class BasicBlock(nn.Module):
         self.fused = norm is BatchNormAct2d
 
     def forward(self, x):
-        identity = x if self.downsample is None else self.downsample(x)
         if self.fused:  # conv -> BN+ReLU ; conv -> BN + identity + ReLU (fused kernels)
+            train = x.is_cuda and torch.is_grad_enabled() and self.training
             # identity block: BN2's residual gradient is folded into conv1's grad-x
             # (ops/gradlink.py) instead of an autograd add of the two branches
-            link = (GradLink() if self.downsample is None and x.is_cuda and torch.is_grad_enabled()
-                    and x.requires_grad and self.training else None)
-            out = self.bn1(self.conv1(x, link=link) if link is not None else self.conv1(x), relu=True)
-            return self.bn2(self.conv2(out), residual=identity, relu=True, link=link)
+            link = GradLink() if self.downsample is None and train and x.requires_grad else None
+            # split-K conv slabs summed inside the neighbouring BN kernels (ops/slablink.py):
+            # conv1 -> bn1, conv2 -> bn2, downsample conv -> its BN (forward), and conv2's
+            # grad-x -> the gradient bn1's backward reads
+            s1, s2, g1, sd = ((SlabLink(), SlabLink(), SlabLink(), SlabLink()) if train and SLAB_LINKS
+                              else (None,) * 4)
+            identity = x
+            if self.downsample is not None:
+                ds = self.downsample
+                if train and len(ds) == 2 and isinstance(ds[0], GemmConv2d) and isinstance(ds[1], BatchNormAct2d):
+                    identity = ds[1](ds[0](x, slab_out=sd), slab_in=sd)
+                else:
+                    identity = ds(x)
+            out = self.bn1(self.conv1(x, link=link, slab_out=s1), relu=True, slab_in=s1, grad_slab=g1)
+            return self.bn2(self.conv2(out, slab_out=s2, grad_slab=g1), residual=identity, relu=True, link=link,
+                            slab_in=s2)
+        identity = x if self.downsample is None else self.downsample(x)
         out = self.relu(self.bn1(self.conv1(x)))
         out = self.bn2(self.conv2(out))
         return self.relu(out + identity)

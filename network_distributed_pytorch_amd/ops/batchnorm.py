@@ -27,7 +27,7 @@ __all__ = ["BatchNormAct2d", "bn_act"]
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, res, weight, bias, running_mean, running_var, nbt, part, eps, momentum, relu, single=False,
-                link=None):
+                link=None, slab_in=None, grad_slab=None):
         X = ext()
         x = x.contiguous()
         if res is not None:
@@ -36,8 +36,10 @@ class _BNActFn(torch.autograd.Function):
         y = torch.empty_like(x)
         save_mean = torch.empty(C, device=x.device, dtype=torch.float32)
         save_invstd = torch.empty(C, device=x.device, dtype=torch.float32)
+        xpart, nslab = slab_in.take_fwd() if slab_in is not None else (None, 0)
         X.bn_fwd(x, res, y, weight, bias, running_mean, running_var, nbt, save_mean, save_invstd, part,
-                 float(eps), float(momentum), bool(relu), True, bool(single))
+                 float(eps), float(momentum), bool(relu), True, bool(single), xpart, nslab)
+        ctx.grad_slab = grad_slab  # ops/slablink.py: dy may arrive as the next conv's grad-x slabs
         ctx.relu = bool(relu)
         ctx.single = bool(single)
         ctx.has_res = res is not None
@@ -55,17 +57,23 @@ class _BNActFn(torch.autograd.Function):
         dres = torch.empty_like(x) if ctx.has_res else None
         dgamma = torch.empty_like(weight) if ctx.has_w else None
         dbeta = torch.empty_like(weight) if ctx.has_w else None
-        ext().bn_bwd(dy, y, x, weight, save_mean, save_invstd, dx, dres, dgamma, dbeta, part, ctx.relu, ctx.single)
+        dypart, nslab = ctx.grad_slab.take_bwd() if ctx.grad_slab is not None else (None, 0)
+        ext().bn_bwd(dy, y, x, weight, save_mean, save_invstd, dx, dres, dgamma, dbeta, part, ctx.relu, ctx.single,
+                     dypart, nslab)
         if ctx.link is not None and dres is not None:
             ctx.link.put(dres)
             dres = None
-        return dx, dres, dgamma, dbeta, None, None, None, None, None, None, None, None, None
+        return dx, dres, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None
 
 
 def bn_act(x, weight, bias, running_mean, running_var, nbt, part, training, momentum, eps,
-           residual=None, relu=False, single=False, link=None):
+           residual=None, relu=False, single=False, link=None, slab_in=None, grad_slab=None):
     needs_grad = torch.is_grad_enabled() and (x.requires_grad or (weight is not None and weight.requires_grad)
                                               or (residual is not None and residual.requires_grad))
+    fused = x.is_cuda and training and x.dtype == torch.float32
+    if slab_in is not None and slab_in.fwd is not None and not fused:  # no fused consumer: finish the sum
+        sp, n = slab_in.take_fwd()
+        ext().slab_sum(sp, x, n)
     if x.is_cuda and (training or not needs_grad):  # eval + autograd: differentiable torch path below
         if x.dtype != torch.float32:  # bf16 autocast: normalise in fp32 (stats are fp64 anyway)
             x = x.float()
@@ -74,7 +82,7 @@ def bn_act(x, weight, bias, running_mean, running_var, nbt, part, training, mome
             if link is not None and residual is not None:
                 residual = residual.detach()  # its gradient travels through `link`
             return _BNActFn.apply(x, residual, weight, bias, running_mean, running_var, nbt, part, eps,
-                                  momentum, relu, single, link)
+                                  momentum, relu, single, link, slab_in, grad_slab)
         y = torch.empty_like(x := x.contiguous())
         C = x.shape[1]
         sm = torch.empty(C, device=x.device)
@@ -111,9 +119,16 @@ class BatchNormAct2d(nn.BatchNorm2d):
                 self._part = torch.zeros(need, dtype=torch.float64, device=x.device)
             self._part_key = key
 
-    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, relu: bool = False, link=None):
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, relu: bool = False, link=None,
+                slab_in=None, grad_slab=None):
         """``link`` (ops/gradlink.GradLink, training on device only): deposit the residual's
-        gradient there instead of returning it (the caller's conv absorbs it)."""
+        gradient there instead of returning it (the caller's conv absorbs it).
+        ``slab_in`` / ``grad_slab`` (ops/slablink.SlabLink): x / the gradient of the output
+        may arrive as a direct conv's unsummed split-K slabs (summed inside the BN kernel)."""
+        if slab_in is not None and slab_in.fwd is not None and (
+                self.momentum is None or not self.track_running_stats):
+            sp, n = slab_in.take_fwd()
+            ext().slab_sum(sp, x, n)
         if self.momentum is None or not self.track_running_stats:
             y = super().forward(x)
             if residual is not None:
@@ -124,4 +139,4 @@ class BatchNormAct2d(nn.BatchNorm2d):
             self._ensure_part(x)
         return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var,
                       self.num_batches_tracked if training else None, self._part, training, self.momentum,
-                      self.eps, residual, relu, x.is_cuda and self.fused_small, link)
+                      self.eps, residual, relu, x.is_cuda and self.fused_small, link, slab_in, grad_slab)

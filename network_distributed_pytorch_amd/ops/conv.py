@@ -68,9 +68,12 @@ def direct_plan(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int
 
 class DirectConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, plan, link=None):
+    def forward(ctx, x, weight, plan, link=None, slab_out=None, grad_slab=None):
+        """``slab_out`` / ``grad_slab`` (ops/slablink.py): leave the forward / grad-x split-K
+        slabs for the fused BN kernel that consumes them instead of summing them here."""
         wparam = weight
         ctx.link = link  # ops/gradlink.py: residual-branch gradient folded into grad-x
+        ctx.grad_slab = grad_slab
         geom, _, wgrad_imgs, dgrad_direct, ks_fwd, _ = plan
         C, H, W, Co, KH, KW, s, p = geom
         x = x.contiguous()
@@ -80,7 +83,9 @@ class DirectConvFn(torch.autograd.Function):
         OW = (W + 2 * p - KW) // s + 1
         y = torch.empty(B, Co, OH, OW, device=x.device, dtype=x.dtype)
         part = torch.empty(ks_fwd * y.numel(), device=x.device, dtype=x.dtype) if ks_fwd > 1 else None
-        ext().conv_fwd(x, weight, y, list(geom), part)
+        left = ext().conv_fwd(x, weight, y, list(geom), part, slab_out is not None and part is not None)
+        if left > 1:
+            slab_out.put_fwd(part, left)  # y is filled by the consuming BN kernel
         ctx.save_for_backward(x, weight)
         ctx.plan = plan
         ctx.weight = wparam  # the Parameter itself: its .grad is where a deferred sum lands
@@ -115,7 +120,11 @@ class DirectConvFn(torch.autograd.Function):
                 if ks_dgrad > 1:  # compact partials: numel(dy) * C / Co floats per split
                     part = torch.empty(ks_dgrad * (dy.numel() // geom[3]) * geom[0], device=x.device, dtype=x.dtype)
                 fuse = addend is not None and geom[6] == 1  # stride-1 classes take the addend in-kernel
-                ext().conv_dgrad(dy, weight, dx, list(geom), part, addend.contiguous() if fuse else None)
+                defer = ctx.grad_slab is not None and part is not None and addend is None
+                left = ext().conv_dgrad(dy, weight, dx, list(geom), part, addend.contiguous() if fuse else None,
+                                        defer)
+                if left > 1:
+                    ctx.grad_slab.put_bwd(part, left)  # dx stays unwritten: the BN backward sums the slabs
                 if fuse:
                     addend = None
             else:
@@ -125,11 +134,11 @@ class DirectConvFn(torch.autograd.Function):
                 dx = dx + addend
         if fork:
             main.wait_stream(side)
-        return dx, dw, None, None
+        return dx, dw, None, None, None, None
 
 
 def conv2d_direct(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int, plan=None,
-                  link=None) -> torch.Tensor:
+                  link=None, slab_out=None, grad_slab=None) -> torch.Tensor:
     plan = plan if plan is not None else direct_plan(x, weight, stride, padding)
     assert plan is not None, "no direct kernel for this convolution"
-    return DirectConvFn.apply(x, weight, plan, link)
+    return DirectConvFn.apply(x, weight, plan, link, slab_out, grad_slab)

@@ -1,0 +1,48 @@
+"""Hand a direct convolution's split-K partial slabs to the fused BN kernel next to it.
+
+At the strong-scaling per-GPU batches (512 / N = 64 ... 256) the direct conv kernels of
+ResNet layer1 / layer2 split their reduction over input channels (``conv_ksplit``) to fill
+the 256 CUs, and a separate ``conv_slab_sum`` launch adds the slabs.  Every such conv
+feeds exactly one BatchNorm: in forward conv -> BN, in backward conv2's grad-x -> the
+grad of BN1's output.  With a :class:`SlabLink` the conv leaves its slabs in scratch
+(``defer=True``) and the fused single-launch BN kernel sums them while it reads its input
+(csrc/batchnorm.hip ``src``), in the same slab order as ``conv_slab_sum`` (bitwise-equal
+values): one launch fewer per conv, ~5 µs each on MI355X.  The forward BN also stores the
+sum to the conv's output buffer (BN saves its input for backward).  Where no fused BN
+kernel covers the shape, ``launch_bn_fwd`` / ``launch_bn_bwd`` run the plain slab sum
+themselves first, so a deferred sum is always finished.
+
+Only wired inside the fused ResNet blocks (models/resnet.py), where each conv output /
+grad-x has exactly that one consumer.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+__all__ = ["SlabLink"]
+
+
+class SlabLink:
+    __slots__ = ("fwd", "bwd")
+
+    def __init__(self):
+        self.fwd: Optional[Tuple[torch.Tensor, int]] = None  # conv output slabs -> BN forward
+        self.bwd: Optional[Tuple[torch.Tensor, int]] = None  # conv grad-x slabs -> BN backward
+
+    def put_fwd(self, part: torch.Tensor, n: int) -> None:
+        assert self.fwd is None, "SlabLink: forward slabs deposited twice"
+        self.fwd = (part, int(n))
+
+    def take_fwd(self) -> Tuple[Optional[torch.Tensor], int]:
+        v, self.fwd = self.fwd, None
+        return v if v is not None else (None, 0)
+
+    def put_bwd(self, part: torch.Tensor, n: int) -> None:
+        assert self.bwd is None, "SlabLink: grad-x slabs deposited twice"
+        self.bwd = (part, int(n))
+
+    def take_bwd(self) -> Tuple[Optional[torch.Tensor], int]:
+        v, self.bwd = self.bwd, None
+        return v if v is not None else (None, 0)
