@@ -180,18 +180,14 @@ class Workload:
             from network_distributed_pytorch_amd.utils.graph import StepRunner
 
             static = {k: v.clone() for k, v in pool[0].items()}
-            loss_static = torch.zeros((), device=device)
 
             def pre():
                 sync.zero_grad()
                 loss = loss_of(static)
                 loss.backward()
-                loss_static.copy_(loss.detach())
+                loss_acc.add_(loss.detach())  # one add, no copy into a static loss
 
-            def post():
-                loss_acc.add_(loss_static)
-
-            runner = StepRunner(pre, sync, mode=graph_mode, warmup=3, post=post,
+            runner = StepRunner(pre, sync, mode=graph_mode, warmup=3,
                                 state_tensors=list(model.buffers()))
             graph_mode = runner.mode
 

@@ -704,6 +704,11 @@ int64_t bn_part_numel(int N, int C, int HW) {
 }
 
 // ----------------------------------- launchers -------------------------------------------
+// Deferred conv slabs are summed inside the single-launch BN kernel only up to this many:
+// ResNet-18 step on 1x MI355X, layer2 (HW 16) at per-GPU batch 256 (2 slabs) 1.4968 ->
+// 1.4688 ms, batch 128 (4) 1.2158 -> 1.2176 (even), batch 64 (8 slabs) 1.0689 -> 1.0746 (the
+// BN's 128 workgroups read 8 slabs slower than the 256-CU sum kernel plus a launch).
+constexpr int kMaxFusedSlabs = 4;
 int bn_slices(int N, int C, int HW) {
   // ~4 workgroups per CU over the whole launch, >= ~2K elements per workgroup
   int64_t s = (1024 + C - 1) / C;
@@ -719,6 +724,10 @@ void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamm
                    double* part, int N, int C, int HW, int S, float eps, float momentum, int relu,
                    int training, int single, hipStream_t s, const float* xpart, int nslab) {
   if (xpart != nullptr && nslab < 2) xpart = nullptr;
+  if (xpart != nullptr && nslab > kMaxFusedSlabs) {  // many slabs: the wide sum kernel first
+    launch_slab_sum(xpart, const_cast<float*>(x), (int64_t)N * C * HW, nslab, s);
+    xpart = nullptr;
+  }
   if (training && single && bn_fused_ok(N, C, HW)) {
     launch_small_fused<0>(HW, x, res, nullptr, nullptr, gamma, beta, rmean, rvar, nbt, save_mean, save_invstd,
                           nullptr, nullptr, y, nullptr, N, C, eps, momentum, relu, s, xpart, nslab);
@@ -757,6 +766,10 @@ void launch_bn_bwd(const float* dy, const float* y, const float* x, const float*
                    int N, int C, int HW, int S, int relu, int single, hipStream_t s, const float* dypart,
                    int nslab) {
   if (dypart != nullptr && nslab < 2) dypart = nullptr;
+  if (dypart != nullptr && nslab > kMaxFusedSlabs) {
+    launch_slab_sum(dypart, const_cast<float*>(dy), (int64_t)N * C * HW, nslab, s);
+    dypart = nullptr;
+  }
   if (single && bn_fused_ok(N, C, HW)) {
     launch_small_fused<1>(HW, x, nullptr, dy, y, gamma, nullptr, nullptr, nullptr, nullptr,
                           const_cast<float*>(save_mean), const_cast<float*>(save_invstd), dgamma, dbeta, dx, dres, N, C,

@@ -669,6 +669,41 @@ void ce_bwd(torch::Tensor dl, torch::Tensor g, torch::Tensor scratch, torch::Ten
   check_launch("launch_ce_bwd");
 }
 
+// fused residual add + LayerNorm (last dim D): y, s (= a + b), mean, rstd are outputs
+void ln_fwd(torch::Tensor a, c10::optional<torch::Tensor> b, torch::Tensor gamma, torch::Tensor beta, torch::Tensor y,
+            torch::Tensor s, torch::Tensor mean, torch::Tensor rstd, double eps) {
+  check_f32(a, "a"); check_f32(gamma, "gamma"); check_f32(beta, "beta"); check_f32(y, "y"); check_f32(s, "s");
+  check_f32(mean, "mean"); check_f32(rstd, "rstd");
+  const int D = (int)a.size(-1);
+  TORCH_CHECK(ndp::ln_supported(D) && gamma.numel() == D && beta.numel() == D, "ln_fwd: unsupported D");
+  const int64_t R = a.numel() / D;
+  for (auto* t : {&a, &y, &s}) TORCH_CHECK(t->is_contiguous() && t->numel() == R * D, "ln_fwd: contiguous [R, D]");
+  if (b.has_value()) {
+    check_f32(*b, "b");
+    TORCH_CHECK(b->is_contiguous() && b->sizes() == a.sizes(), "ln_fwd: residual shape");
+  }
+  TORCH_CHECK(mean.numel() == R && rstd.numel() == R, "ln_fwd: stats size");
+  ndp::launch_ln_fwd(a.data_ptr<float>(), opt_f32(b, "b"), gamma.data_ptr<float>(), beta.data_ptr<float>(),
+                     y.data_ptr<float>(), s.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(), R, D,
+                     (float)eps, cur_stream());
+  check_launch("launch_ln_fwd");
+}
+
+void ln_bwd(torch::Tensor dy, torch::Tensor s, torch::Tensor mean, torch::Tensor rstd, torch::Tensor gamma,
+            torch::Tensor dx, torch::Tensor dgb) {
+  check_f32(dy, "dy"); check_f32(s, "s"); check_f32(mean, "mean"); check_f32(rstd, "rstd"); check_f32(gamma, "gamma");
+  check_f32(dx, "dx"); check_f32(dgb, "dgb");
+  const int D = (int)s.size(-1);
+  const int64_t R = s.numel() / D;
+  TORCH_CHECK(ndp::ln_supported(D) && gamma.numel() == D && dgb.numel() == 2 * D, "ln_bwd: unsupported D");
+  for (auto* t : {&dy, &s, &dx}) TORCH_CHECK(t->is_contiguous() && t->numel() == R * D, "ln_bwd: contiguous [R, D]");
+  auto part = torch::empty({(int64_t)ndp::ln_bwd_wgs(R) * 2 * D}, s.options());
+  ndp::launch_ln_bwd(dy.data_ptr<float>(), s.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                     gamma.data_ptr<float>(), dx.data_ptr<float>(), part.data_ptr<float>(), dgb.data_ptr<float>(), R, D,
+                     cur_stream());
+  check_launch("launch_ln_bwd");
+}
+
 void embedding_backward(torch::Tensor ids, torch::Tensor gout, torch::Tensor gw, int64_t pad, torch::Tensor perm,
                         torch::Tensor row_start, torch::Tensor row_cnt) {
   check_dev(ids, "ids"); check_f32(gout, "grad_out"); check_f32(gw, "grad_weight");
@@ -806,6 +841,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embedding_backward", &embedding_backward);
   m.def("colsum", &colsum);
   m.def("ce_fwd", &ce_fwd);
+  m.def("ln_fwd", &ln_fwd);
+  m.def("ln_bwd", &ln_bwd);
   m.def("ce_bwd", &ce_bwd);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);

@@ -150,6 +150,18 @@ void launch_ce_fwd(const float* x, const int64_t* tgt, int B, int K, int64_t ign
 void launch_ce_bwd(const float* dl, const float* g, const float* inv, float* dx, int64_t n, hipStream_t s);
 }  // namespace ndp
 
+// ---- fused residual add + LayerNorm over the last dim (layernorm.hip) --------------------
+namespace ndp {
+bool ln_supported(int D);  // D in {256, 512, 768, 1024}
+// y = LN(a (+ b)) * gamma + beta; s = a (+ b), mean / rstd [R] saved for backward
+void launch_ln_fwd(const float* a, const float* b, const float* gamma, const float* beta, float* y, float* s,
+                   float* mean, float* rstd, int64_t R, int D, float eps, hipStream_t st);
+int ln_bwd_wgs(int64_t R);
+// dx [R, D]; part: ln_bwd_wgs(R) * 2D floats of scratch; dgb: [dgamma | dbeta] (2D floats)
+void launch_ln_bwd(const float* dy, const float* s, const float* mean, const float* rstd, const float* gamma,
+                   float* dx, float* part, float* dgb, int64_t R, int D, hipStream_t st);
+}  // namespace ndp
+
 // ---- convolutions, NCHW fp32 (conv.hip) -------------------------------------------------
 namespace ndp {
 struct ConvGeom {

@@ -110,7 +110,7 @@ class _ToeplitzConv(torch.autograd.Function):
     tests): the same maps as index tensors."""
 
     @staticmethod
-    def forward(ctx, x, weight, src, dst, oh, ow, geom=None, bank=None, layer=None, link=None):
+    def forward(ctx, x, weight, src, dst, oh, ow, geom=None, bank=None, layer=None, link=None, branch=None):
         B = x.shape[0]
         co = weight.shape[0]
         X = x.reshape(B, -1)
@@ -130,6 +130,9 @@ class _ToeplitzConv(torch.autograd.Function):
         ctx.geom = geom
         ctx.weight = weight  # the Parameter: a deferred fold writes its adopted .grad
         ctx.link = link      # ops/gradlink.py: residual-branch gradient, folded in by addmm
+        ctx.branch = branch if (branch is not None and x.is_cuda and geom is not None) else None
+        if ctx.branch is not None:
+            ctx.branch.join()  # ops/gradlink.BranchLink: grad-x shared with a sibling conv
         ctx.x_shape = x.shape
         ctx.w_shape = weight.shape
         return out.view(B, co, oh, ow)
@@ -156,20 +159,31 @@ class _ToeplitzConv(torch.autograd.Function):
                         ext().toeplitz_fold(dwt, dw, list(ctx.geom))
             if ctx.needs_input_grad[0]:
                 addend = ctx.link.take() if ctx.link is not None else None
-                if addend is not None:  # dx = addend + G @ W_big in one GEMM (beta = 1)
-                    dx = torch.addmm(addend.reshape(G.shape[0], -1), G, w_big).view(ctx.x_shape)
+                br = ctx.branch if ctx.branch is not None and ctx.branch.active() else None
+                if br is not None:
+                    other = br.take()
+                    if addend is None:
+                        addend = other
+                    elif other is not None:
+                        addend = addend + other
+                if addend is not None:  # dx = addend + G @ W_big in one GEMM (beta = 1), in place:
+                    # the addend is a gradient buffer nothing else reads (no copy of it into dx)
+                    dx = addend.reshape(G.shape[0], -1).addmm_(G, w_big).view(ctx.x_shape)
                 else:
                     dx = (G @ w_big).view(ctx.x_shape)
+                    if br is not None and other is None:  # first of the two: the sibling adds onto it
+                        br.put(dx)
+                        dx = None
             if fork:
                 main.wait_stream(side)
-            return dx, dw, None, None, None, None, None, None, None, None
+            return dx, dw, None, None, None, None, None, None, None, None, None
         if ctx.needs_input_grad[0]:
             dx = (G @ w_big.t()).view(ctx.x_shape)
         if ctx.needs_input_grad[1]:
             dw_big = X.t() @ G                                    # [K, N]
             ext_ = torch.cat([dw_big.reshape(-1), dw_big.new_zeros(1)])
             dw = ext_[dst].sum(-1).view(ctx.w_shape)              # fixed-order, deterministic
-        return dx, dw, None, None, None, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None, None, None, None
 
 
 class GemmConv2d(nn.Conv2d):
@@ -205,12 +219,13 @@ class GemmConv2d(nn.Conv2d):
                 self._maps[key] = (src, dst, oh, ow, sub, None)
         return self._maps[key]
 
-    def forward(self, x, link=None, slab_out=None, grad_slab=None):
+    def forward(self, x, link=None, slab_out=None, grad_slab=None, branch=None):
         """``link`` (ops/gradlink.GradLink): a residual-branch gradient to add into this
         conv's grad-x (fused into the kernel / GEMM where the path allows).
         ``slab_out`` / ``grad_slab`` (ops/slablink.SlabLink, direct kernels only): the
         forward / grad-x split-K slabs go to the neighbouring fused BN instead of a sum
-        launch (other paths leave the links empty)."""
+        launch (other paths leave the links empty).  ``branch`` (ops/gradlink.BranchLink,
+        Toeplitz path only): grad-x shared with a sibling conv of the same input."""
         if not (self.gemm and x.is_cuda and self.groups == 1 and self.dilation == (1, 1) and self.bias is None
                 and self.stride[0] == self.stride[1] and self.padding[0] == self.padding[1]
                 and self.padding_mode == "zeros" and x.dtype == torch.float32):
@@ -231,4 +246,5 @@ class GemmConv2d(nn.Conv2d):
             x = x[:, :, ::sub, ::sub]
         if link is not None and geom is None:  # CPU index-map path: plain add in backward
             x, link = InjectGrad.apply(x, link), None
-        return _ToeplitzConv.apply(x.contiguous(), self.weight, src, dst, oh2, ow2, geom, self.bank, self, link)
+        return _ToeplitzConv.apply(x.contiguous(), self.weight, src, dst, oh2, ow2, geom, self.bank, self, link,
+                                   branch)

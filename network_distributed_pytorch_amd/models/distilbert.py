@@ -25,6 +25,7 @@ import torch.nn.functional as F
 
 from ..ops.attention import attention, fused_ok
 from ..ops.embedding import Embedding
+from ..ops.layernorm import AddLayerNorm
 from ..ops.linear import Linear
 from ..ops.loss import cross_entropy as native_ce
 
@@ -55,7 +56,8 @@ class Embeddings(nn.Module):
         # native deterministic backward (graph-replayable; ops/embedding.py)
         self.word_embeddings = Embedding(c.vocab_size, c.dim, padding_idx=c.pad_token_id)
         self.position_embeddings = nn.Embedding(c.max_position_embeddings, c.dim)
-        self.LayerNorm = nn.LayerNorm(c.dim, eps=c.layer_norm_eps)
+        self.LayerNorm = AddLayerNorm(c.dim, eps=c.layer_norm_eps)
+        self.LayerNorm.native = c.fused_attention  # native kernels on/off together
         self.dropout = nn.Dropout(c.dropout)
 
     def forward(self, input_ids):
@@ -116,13 +118,15 @@ class TransformerBlock(nn.Module):
     def __init__(self, c: DistilBertConfig):
         super().__init__()
         self.attention = MultiHeadSelfAttention(c)
-        self.sa_layer_norm = nn.LayerNorm(c.dim, eps=c.layer_norm_eps)
+        # residual add + LayerNorm fused into one gfx950 kernel per direction (ops/layernorm.py)
+        self.sa_layer_norm = AddLayerNorm(c.dim, eps=c.layer_norm_eps)
         self.ffn = FFN(c)
-        self.output_layer_norm = nn.LayerNorm(c.dim, eps=c.layer_norm_eps)
+        self.output_layer_norm = AddLayerNorm(c.dim, eps=c.layer_norm_eps)
+        self.sa_layer_norm.native = self.output_layer_norm.native = c.fused_attention
 
     def forward(self, x, mask):
-        x = self.sa_layer_norm(self.attention(x, mask) + x)
-        return self.output_layer_norm(self.ffn(x) + x)
+        x = self.sa_layer_norm(self.attention(x, mask), residual=x)
+        return self.output_layer_norm(self.ffn(x), residual=x)
 
 
 class Transformer(nn.Module):

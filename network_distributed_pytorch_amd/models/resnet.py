@@ -27,7 +27,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.batchnorm import BatchNormAct2d
-from ..ops.gradlink import GradLink
+from ..ops.gradlink import BranchLink, GradLink
 from ..ops.pool import MaxPool2d
 from ..ops.slablink import SlabLink
 from .conv_gemm import GemmConv2d, ToeplitzBank
@@ -38,6 +38,8 @@ __all__ = ["ResNet", "BasicBlock", "Bottleneck", "resnet18", "resnet34", "resnet
 # split-K slab hand-off between direct convs and fused BN (ops/slablink.py; NDP_SLAB_LINKS=0
 # or tests flip it for A/B)
 SLAB_LINKS = os.environ.get("NDP_SLAB_LINKS", "1") != "0"
+# downsample blocks: conv1 / downsample grad-x accumulated in place (ops/gradlink.BranchLink)
+BRANCH_LINKS = os.environ.get("NDP_BRANCH_LINKS", "1") != "0"
 
 
 def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -76,13 +78,17 @@ class BasicBlock(nn.Module):
             s1, s2, g1, sd = ((SlabLink(), SlabLink(), SlabLink(), SlabLink()) if train and SLAB_LINKS
                               else (None,) * 4)
             identity = x
+            # downsample block: conv1 and the 1x1 downsample share one grad-x buffer (Toeplitz
+            # layers; ops/gradlink.BranchLink) instead of an autograd add of the two
+            br = (BranchLink() if BRANCH_LINKS and train and self.downsample is not None and x.requires_grad
+                  else None)
             if self.downsample is not None:
                 ds = self.downsample
                 if train and len(ds) == 2 and isinstance(ds[0], GemmConv2d) and isinstance(ds[1], BatchNormAct2d):
-                    identity = ds[1](ds[0](x, slab_out=sd), slab_in=sd)
+                    identity = ds[1](ds[0](x, slab_out=sd, branch=br), slab_in=sd)
                 else:
                     identity = ds(x)
-            out = self.bn1(self.conv1(x, link=link, slab_out=s1), relu=True, slab_in=s1, grad_slab=g1)
+            out = self.bn1(self.conv1(x, link=link, slab_out=s1, branch=br), relu=True, slab_in=s1, grad_slab=g1)
             return self.bn2(self.conv2(out, slab_out=s2, grad_slab=g1), residual=identity, relu=True, link=link,
                             slab_in=s2)
         identity = x if self.downsample is None else self.downsample(x)

@@ -14,7 +14,7 @@ from typing import Optional
 
 import torch
 
-__all__ = ["GradLink", "InjectGrad"]
+__all__ = ["GradLink", "InjectGrad", "BranchLink"]
 
 
 class GradLink:
@@ -45,3 +45,32 @@ class InjectGrad(torch.autograd.Function):
     def backward(ctx, g):
         extra = ctx.link.take()
         return (g if extra is None else g + extra), None
+
+
+class BranchLink:
+    """Two convolutions reading the same input — a downsample block's conv1 and its 1x1
+    downsample: autograd would sum their two grad-x tensors with an elementwise add launch.
+    Every conv that takes the link in forward ``join``s it; in backward (either order) the
+    first member deposits its grad-x and returns None (a zero gradient to autograd), the
+    second accumulates its product onto the deposit in place (``addmm_``, beta = 1) and
+    returns the sum.  With fewer than two members the link is inert."""
+
+    __slots__ = ("members", "grad")
+
+    def __init__(self):
+        self.members = 0
+        self.grad: Optional[torch.Tensor] = None
+
+    def join(self) -> None:
+        self.members += 1
+
+    def active(self) -> bool:
+        return self.members == 2
+
+    def put(self, g: torch.Tensor) -> None:
+        assert self.grad is None, "BranchLink: grad-x deposited twice"
+        self.grad = g
+
+    def take(self) -> Optional[torch.Tensor]:
+        g, self.grad = self.grad, None
+        return g

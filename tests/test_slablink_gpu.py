@@ -83,3 +83,25 @@ def test_slab_sum_matches_sequential(device):
     for z in range(1, 8):
         ref += parts[z]
     assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("batch", [64, 512])
+def test_resnet18_branch_links_match(device, batch, monkeypatch):
+    """Downsample blocks: conv1 / downsample grad-x accumulated in place (BranchLink) equals
+    autograd's add of the two (GEMM beta = 1 may pick another library solution: tolerance)."""
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
+    torch.manual_seed(1)
+    m = build_resnet(18, 1000).to(device)
+    state = {k: v.clone() for k, v in m.state_dict().items()}
+    x = torch.rand(batch, 3, 32, 32, device=device) * 2 - 1
+    y = torch.randint(0, 10, (batch,), device=device)
+    runs = []
+    for on in (True, False):
+        monkeypatch.setattr(resnet_mod, "BRANCH_LINKS", on)
+        m.load_state_dict(state)
+        runs.append(_step(m, x, y))
+    (l1, g1), (l0, g0) = runs
+    assert torch.equal(l1, l0)
+    for n in g0:
+        scale = g0[n].abs().max().item() + 1e-12
+        torch.testing.assert_close(g1[n], g0[n], rtol=1e-4, atol=1e-5 * scale, msg=n)
