@@ -81,6 +81,7 @@ struct AttnArgs {
   const int32_t* seedp;          // device-resident seed (graph-replay safe), may be null
   uint32_t drop_thr;             // drop_thr = 0 -> no dropout
   float drop_scale;              // 1/(1-p)
+  int64_t ldq;                   // token row stride (floats) of q / k / v: H*D, or 3*H*D for a packed QKV
 };
 
 // ---------------------------------------------------------------------------------------
@@ -97,6 +98,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   const bool row_any = scan_mask(a.mask, b, a.S, blkv);
   const int64_t rs = (int64_t)a.H * kD;                       // row stride of [B,S,H,D]
   const int64_t base = (int64_t)b * a.S * rs + (int64_t)h * kD;
+  const int64_t qrs = a.ldq;                                  // q / k / v (+ grads) row stride
+  const int64_t qbase = (int64_t)b * a.S * qrs + (int64_t)h * kD;
   const int q = blockIdx.x * 64 + wave * 16 + c16;            // this lane's query
   const bool qok = q < a.S;
 
@@ -105,7 +108,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
   for (int cc = 0; cc < 4; ++cc) {
     f32x4 v4 = {0.f, 0.f, 0.f, 0.f};
-    if (qok) v4 = *reinterpret_cast<const f32x4*>(a.q + base + (int64_t)q * rs + 16 * cc + 4 * g);
+    if (qok) v4 = *reinterpret_cast<const f32x4*>(a.q + qbase + (int64_t)q * qrs + 16 * cc + 4 * g);
 #pragma unroll
     for (int t = 0; t < 4; ++t) Qr[cc][t] = v4[t] * a.scale;
   }
@@ -123,8 +126,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
       const int key = k0 + kr;
       f32x4 kv = {0.f, 0.f, 0.f, 0.f}, vv = {0.f, 0.f, 0.f, 0.f};
       if (key < a.S) {
-        kv = *reinterpret_cast<const f32x4*>(a.k + base + (int64_t)key * rs + dq);
-        vv = *reinterpret_cast<const f32x4*>(a.v + base + (int64_t)key * rs + dq);
+        kv = *reinterpret_cast<const f32x4*>(a.k + qbase + (int64_t)key * qrs + dq);
+        vv = *reinterpret_cast<const f32x4*>(a.v + qbase + (int64_t)key * qrs + dq);
       }
       *reinterpret_cast<f32x4*>(&Ks[kr * kLD + dq]) = kv;
 #pragma unroll
@@ -239,6 +242,7 @@ struct AttnBwdArgs {
   const int32_t* seedp;
   uint32_t drop_thr;
   float drop_scale;
+  int64_t ldq;                   // token row stride of q / k / v and dq / dk / dv (o / dout: H*D)
 };
 
 // Recompute one 16(query) x 64(key) probability tile in the S^T layout used by the forward:
@@ -256,6 +260,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
   const int bh = blockIdx.y, b = bh / a.H, h = bh - (bh / a.H) * a.H;
   const int64_t rs = (int64_t)a.H * kD;
   const int64_t base = (int64_t)b * a.S * rs + (int64_t)h * kD;
+  const int64_t qrs = a.ldq;                                  // q / k / v (+ grads) row stride
+  const int64_t qbase = (int64_t)b * a.S * qrs + (int64_t)h * kD;
   const int key = blockIdx.x * 64 + wave * 16 + c16;             // this lane's key
   const bool kok = key < a.S;
   const bool row_any = scan_mask(a.mask, b, a.S, blkv);
@@ -263,8 +269,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
     if (kok)
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        *reinterpret_cast<f32x4*>(a.dk + base + (int64_t)key * rs + 16 * dt + 4 * g) = f32x4{0.f, 0.f, 0.f, 0.f};
-        *reinterpret_cast<f32x4*>(a.dv + base + (int64_t)key * rs + 16 * dt + 4 * g) = f32x4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f32x4*>(a.dk + qbase + (int64_t)key * qrs + 16 * dt + 4 * g) = f32x4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f32x4*>(a.dv + qbase + (int64_t)key * qrs + 16 * dt + 4 * g) = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     return;
   }
@@ -276,8 +282,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
   for (int cc = 0; cc < 4; ++cc) {
     f32x4 kv = {0.f, 0.f, 0.f, 0.f}, vv = {0.f, 0.f, 0.f, 0.f};
     if (kok) {
-      kv = *reinterpret_cast<const f32x4*>(a.k + base + (int64_t)key * rs + 16 * cc + 4 * g);
-      vv = *reinterpret_cast<const f32x4*>(a.v + base + (int64_t)key * rs + 16 * cc + 4 * g);
+      kv = *reinterpret_cast<const f32x4*>(a.k + qbase + (int64_t)key * qrs + 16 * cc + 4 * g);
+      vv = *reinterpret_cast<const f32x4*>(a.v + qbase + (int64_t)key * qrs + 16 * cc + 4 * g);
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -299,7 +305,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
       const int qq = q0 + qr;
       f32x4 qv = {0.f, 0.f, 0.f, 0.f}, gv = {0.f, 0.f, 0.f, 0.f};
       if (qq < a.S) {
-        qv = *reinterpret_cast<const f32x4*>(a.q + base + (int64_t)qq * rs + dq) * a.scale;
+        qv = *reinterpret_cast<const f32x4*>(a.q + qbase + (int64_t)qq * qrs + dq) * a.scale;
         gv = *reinterpret_cast<const f32x4*>(a.dout + base + (int64_t)qq * rs + dq);
       }
       *reinterpret_cast<f32x4*>(&Qs[qr * kLD + dq]) = qv;
@@ -364,8 +370,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
   // dK^T tile: col = key (lane), rows d = 16dt + 4g + r.  Q was pre-scaled -> dK = dS^T (Q*scale)
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) {
-    *reinterpret_cast<f32x4*>(a.dk + base + (int64_t)key * rs + 16 * dt + 4 * g) = dK[dt];
-    *reinterpret_cast<f32x4*>(a.dv + base + (int64_t)key * rs + 16 * dt + 4 * g) = dV[dt];
+    *reinterpret_cast<f32x4*>(a.dk + qbase + (int64_t)key * qrs + 16 * dt + 4 * g) = dK[dt];
+    *reinterpret_cast<f32x4*>(a.dv + qbase + (int64_t)key * qrs + 16 * dt + 4 * g) = dV[dt];
   }
 }
 
@@ -382,6 +388,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   const bool row_any = scan_mask(a.mask, b, a.S, blkv);
   const int64_t rs = (int64_t)a.H * kD;
   const int64_t base = (int64_t)b * a.S * rs + (int64_t)h * kD;
+  const int64_t qrs = a.ldq;                                  // q / k / v (+ grads) row stride
+  const int64_t qbase = (int64_t)b * a.S * qrs + (int64_t)h * kD;
   const int q = blockIdx.x * 64 + wave * 16 + c16;
   const bool qok = q < a.S;
   float Qr[4][4], Gr[4][4];
@@ -389,7 +397,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   for (int cc = 0; cc < 4; ++cc) {
     f32x4 qv = {0.f, 0.f, 0.f, 0.f}, gv = {0.f, 0.f, 0.f, 0.f};
     if (qok) {
-      qv = *reinterpret_cast<const f32x4*>(a.q + base + (int64_t)q * rs + 16 * cc + 4 * g);
+      qv = *reinterpret_cast<const f32x4*>(a.q + qbase + (int64_t)q * qrs + 16 * cc + 4 * g);
       gv = *reinterpret_cast<const f32x4*>(a.dout + base + (int64_t)q * rs + 16 * cc + 4 * g);
     }
 #pragma unroll
@@ -413,8 +421,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
       const int key = k0 + kr;
       f32x4 kv = {0.f, 0.f, 0.f, 0.f}, vv = {0.f, 0.f, 0.f, 0.f};
       if (key < a.S) {
-        kv = *reinterpret_cast<const f32x4*>(a.k + base + (int64_t)key * rs + dq);
-        vv = *reinterpret_cast<const f32x4*>(a.v + base + (int64_t)key * rs + dq);
+        kv = *reinterpret_cast<const f32x4*>(a.k + qbase + (int64_t)key * qrs + dq);
+        vv = *reinterpret_cast<const f32x4*>(a.v + qbase + (int64_t)key * qrs + dq);
       }
       *reinterpret_cast<f32x4*>(&Ks[kr * kLD + dq]) = kv;
       *reinterpret_cast<f32x4*>(&Vs[kr * kLD + dq]) = vv;
@@ -465,13 +473,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   if (!qok) return;
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt)
-    *reinterpret_cast<f32x4*>(a.dq + base + (int64_t)q * rs + 16 * dt + 4 * g) = dQ[dt] * a.scale;
+    *reinterpret_cast<f32x4*>(a.dq + qbase + (int64_t)q * qrs + 16 * dt + 4 * g) = dQ[dt] * a.scale;
 }
 
 // ------------------------------------ launchers ------------------------------------------
 void launch_attn_fwd(const float* q, const float* k, const float* v, const int32_t* mask, float* o, float* lse,
-                     int B, int S, int H, float scale, const int32_t* seed, float p_drop, hipStream_t s) {
-  AttnArgs a{q, k, v, mask, o, lse, B, S, H, scale, seed, 0u, 1.f};
+                     int B, int S, int H, float scale, const int32_t* seed, float p_drop, hipStream_t s,
+                     int64_t ldq) {
+  AttnArgs a{q, k, v, mask, o, lse, B, S, H, scale, seed, 0u, 1.f, ldq > 0 ? ldq : (int64_t)H * kD};
   if (p_drop > 0.f) {
     a.drop_thr = (uint32_t)fminf(p_drop * 4294967296.0f, 4294967295.0f);
     a.drop_scale = 1.f / (1.f - p_drop);
@@ -481,10 +490,11 @@ void launch_attn_fwd(const float* q, const float* k, const float* v, const int32
 
 void launch_attn_bwd(const float* q, const float* k, const float* v, const int32_t* mask, const float* o,
                      const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv, int B,
-                     int S, int H, float scale, const int32_t* seed, float p_drop, hipStream_t s) {
+                     int S, int H, float scale, const int32_t* seed, float p_drop, hipStream_t s, int64_t ldq) {
   const int rows = B * S * H;
   hipLaunchKernelGGL(attn_bwd_delta_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, o, dout, delta, B, S, H);
-  AttnBwdArgs a{q, k, v, mask, dout, lse, delta, dq, dk, dv, B, S, H, scale, seed, 0u, 1.f};
+  AttnBwdArgs a{q, k, v, mask, dout, lse, delta, dq, dk, dv, B, S, H, scale, seed, 0u, 1.f,
+                ldq > 0 ? ldq : (int64_t)H * kD};
   if (p_drop > 0.f) {
     a.drop_thr = (uint32_t)fminf(p_drop * 4294967296.0f, 4294967295.0f);
     a.drop_scale = 1.f / (1.f - p_drop);

@@ -727,7 +727,19 @@ void embedding_backward(torch::Tensor ids, torch::Tensor gout, torch::Tensor gw,
 // q/k/v/o: [B, S, H, 64] fp32 contiguous (== the [B, S, H*64] projections); mask [B, S] int32 or None
 void attn_check(const torch::Tensor& t, const char* n, const torch::Tensor& q) {
   check_f32(t, n);
-  TORCH_CHECK(t.sizes() == q.sizes(), n, ": shape mismatch");
+  TORCH_CHECK(t.sizes() == q.sizes() && t.is_contiguous(), n, ": contiguous [B, S, H, 64] like q");
+}
+
+// q / k / v (and dq / dk / dv): [B, S, H, 64] with unit element / 64-float head strides and
+// a common token row stride ld (H*64 contiguous, 3*H*64 for views into a packed QKV)
+int64_t attn_ld(const torch::Tensor& t, const char* n, const torch::Tensor& q) {
+  TORCH_CHECK(t.is_cuda(), n, " must be a device (HIP) tensor");
+  TORCH_CHECK(t.scalar_type() == torch::kFloat32 && t.sizes() == q.sizes(), n, ": fp32 [B, S, H, 64] like q");
+  const int64_t S = t.size(1), H = t.size(2), ld = t.stride(1);
+  TORCH_CHECK(t.stride(3) == 1 && t.stride(2) == 64 && t.stride(0) == S * ld && ld >= H * 64 && ld % 4 == 0 &&
+                  (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0,
+              n, ": needs [B, S, H, 64] rows with a 16-B aligned token stride");
+  return ld;
 }
 
 const int32_t* attn_seed(const c10::optional<torch::Tensor>& seed, double p_drop) {
@@ -741,9 +753,10 @@ const int32_t* attn_seed(const c10::optional<torch::Tensor>& seed, double p_drop
 
 void attn_fwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, c10::optional<torch::Tensor> mask, torch::Tensor o,
               torch::Tensor lse, double scale, c10::optional<torch::Tensor> seed, double p_drop) {
-  check_f32(q, "q");
   TORCH_CHECK(q.dim() == 4 && q.size(3) == 64, "attn: q must be [B, S, H, 64]");
-  attn_check(k, "k", q); attn_check(v, "v", q); attn_check(o, "o", q); check_f32(lse, "lse");
+  const int64_t ld = attn_ld(q, "q", q);
+  TORCH_CHECK(attn_ld(k, "k", q) == ld && attn_ld(v, "v", q) == ld, "attn: q / k / v need one token stride");
+  attn_check(o, "o", q); check_f32(lse, "lse");
   const int B = (int)q.size(0), S = (int)q.size(1), H = (int)q.size(2);
   TORCH_CHECK(lse.numel() >= 2 * (int64_t)B * H * S, "attn: lse must hold 2*B*H*S floats");
   const int32_t* mp = nullptr;
@@ -755,17 +768,18 @@ void attn_fwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, c10::optional<t
   }
   const int32_t* sp = attn_seed(seed, p_drop);
   ndp::launch_attn_fwd(q.data_ptr<float>(), k.data_ptr<float>(), v.data_ptr<float>(), mp, o.data_ptr<float>(),
-                       lse.data_ptr<float>(), B, S, H, (float)scale, sp, (float)p_drop, cur_stream());
+                       lse.data_ptr<float>(), B, S, H, (float)scale, sp, (float)p_drop, cur_stream(), ld);
   check_launch("launch_attn_fwd");
 }
 
 void attn_bwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, c10::optional<torch::Tensor> mask, torch::Tensor o,
               torch::Tensor dout, torch::Tensor lse, torch::Tensor delta, torch::Tensor dq, torch::Tensor dk,
               torch::Tensor dv, double scale, c10::optional<torch::Tensor> seed, double p_drop) {
-  check_f32(q, "q");
   TORCH_CHECK(q.dim() == 4 && q.size(3) == 64, "attn: q must be [B, S, H, 64]");
-  attn_check(k, "k", q); attn_check(v, "v", q); attn_check(o, "o", q); attn_check(dout, "dout", q);
-  attn_check(dq, "dq", q); attn_check(dk, "dk", q); attn_check(dv, "dv", q);
+  const int64_t ld = attn_ld(q, "q", q);
+  for (auto* t : {&k, &v, &dq, &dk, &dv})
+    TORCH_CHECK(attn_ld(*t, "q/k/v grads", q) == ld, "attn: q / k / v and their grads need one token stride");
+  attn_check(o, "o", q); attn_check(dout, "dout", q);
   check_f32(lse, "lse"); check_f32(delta, "delta");
   const int B = (int)q.size(0), S = (int)q.size(1), H = (int)q.size(2);
   TORCH_CHECK(lse.numel() >= 2 * (int64_t)B * H * S && delta.numel() >= (int64_t)B * H * S,
@@ -781,7 +795,7 @@ void attn_bwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, c10::optional<t
   ndp::launch_attn_bwd(q.data_ptr<float>(), k.data_ptr<float>(), v.data_ptr<float>(), mp, o.data_ptr<float>(),
                        dout.data_ptr<float>(), lse.data_ptr<float>(), delta.data_ptr<float>(), dq.data_ptr<float>(),
                        dk.data_ptr<float>(), dv.data_ptr<float>(), B, S, H, (float)scale, sp,
-                       (float)p_drop, cur_stream());
+                       (float)p_drop, cur_stream(), ld);
   check_launch("launch_attn_bwd");
 }
 

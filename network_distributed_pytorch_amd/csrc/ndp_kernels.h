@@ -231,11 +231,14 @@ namespace ndp {
 // mask: [B, S] int32 (nonzero = attend) or null; lse: [B, H, S]; p_drop in [0, 1);
 // seed: device int32[1] read by the kernels (so a replayed hipGraph sees fresh seeds)
 void launch_attn_fwd(const float* q, const float* k, const float* v, const int32_t* mask, float* o, float* lse,
-                     int B, int S, int H, float scale, const int32_t* seed, float p_drop, hipStream_t s);
-// delta: [B, H, S] scratch
+                     int B, int S, int H, float scale, const int32_t* seed, float p_drop, hipStream_t s,
+                     int64_t ldq = 0);
+// ldq: token row stride of q / k / v (and dq / dk / dv): 0 = H*64 (contiguous), 3*H*64 for
+// views into a packed [B, S, 3, H, 64] QKV projection.  delta: [B, H, S] scratch
 void launch_attn_bwd(const float* q, const float* k, const float* v, const int32_t* mask, const float* o,
                      const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv, int B,
-                     int S, int H, float scale, const int32_t* seed, float p_drop, hipStream_t s);
+                     int S, int H, float scale, const int32_t* seed, float p_drop, hipStream_t s,
+                     int64_t ldq = 0);
 }  // namespace ndp
 
 // ---- max-pool 2-D, NCHW fp32, deterministic gather backward (pool.hip) ---------------

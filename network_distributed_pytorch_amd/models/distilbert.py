@@ -17,19 +17,26 @@ from __future__ import annotations
 
 import dataclasses
 import math
+import os
 from typing import Optional
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.attention import attention, fused_ok
+from ..ops.attention import attention, attention_qkv, fused_ok
 from ..ops.embedding import Embedding
+from ..ops.gradlink import GradLink
 from ..ops.layernorm import AddLayerNorm
-from ..ops.linear import Linear
+from ..ops.linear import Linear, linear
 from ..ops.loss import cross_entropy as native_ce
 
 __all__ = ["DistilBertConfig", "DistilBertForSequenceClassification", "distilbert_base"]
+
+# one packed QKV projection read in place by the attention kernels (NDP_PACKED_QKV=0: three)
+PACKED_QKV = os.environ.get("NDP_PACKED_QKV", "1") != "0"
+# LayerNorm residual gradients folded into the next GEMM (NDP_LN_LINKS=0: autograd adds)
+LN_LINKS = os.environ.get("NDP_LN_LINKS", "1") != "0"
 
 
 @dataclasses.dataclass
@@ -79,11 +86,22 @@ class MultiHeadSelfAttention(nn.Module):
         self.dropout = nn.Dropout(c.attention_dropout)
         self.fused = c.fused_attention
 
-    def forward(self, x, mask: Optional[torch.Tensor]):
+    def forward(self, x, mask: Optional[torch.Tensor], link=None):
+        """``link`` (ops/gradlink.GradLink): the block's residual gradient, folded into the
+        first projection's grad-x GEMM."""
         bs, s, d = x.shape
         h = self.n_heads
         dh = d // h
-        q4 = self.q_lin(x).view(bs, s, h, dh)
+        if self.fused and PACKED_QKV and x.is_cuda and x.dtype == torch.float32 and dh == 64:
+            # one packed projection GEMM [B*S, 3D] (the three weights concatenated per pass: a
+            # 7 MB copy; their gradients come back as views of one grad-W) read in place by
+            # the fused attention kernels (ops/attention.attention_qkv)
+            w = torch.cat([self.q_lin.weight, self.k_lin.weight, self.v_lin.weight])
+            bias = torch.cat([self.q_lin.bias, self.k_lin.bias, self.v_lin.bias])
+            qkv = linear(x, w, bias, link)
+            ctx = attention_qkv(qkv, h, mask, self.dropout.p if self.training else 0.0)
+            return self.out_lin(ctx.reshape(bs, s, d))
+        q4 = self.q_lin(x, link=link).view(bs, s, h, dh)
         if self.fused and fused_ok(q4):
             ctx = attention(q4, self.k_lin(x).view(bs, s, h, dh), self.v_lin(x).view(bs, s, h, dh), mask,
                             self.dropout.p if self.training else 0.0)
@@ -110,8 +128,8 @@ class FFN(nn.Module):
         self.lin2 = Linear(c.hidden_dim, c.dim)
         self.dropout = nn.Dropout(c.dropout)
 
-    def forward(self, x):
-        return self.dropout(self.lin2(F.gelu(self.lin1(x))))
+    def forward(self, x, link=None):
+        return self.dropout(self.lin2(F.gelu(self.lin1(x, link=link))))
 
 
 class TransformerBlock(nn.Module):
@@ -125,8 +143,17 @@ class TransformerBlock(nn.Module):
         self.sa_layer_norm.native = self.output_layer_norm.native = c.fused_attention
 
     def forward(self, x, mask):
-        x = self.sa_layer_norm(self.attention(x, mask), residual=x)
-        return self.output_layer_norm(self.ffn(x), residual=x)
+        # residual gradients: deposited by the fused LayerNorm backward, added in place by the
+        # sublayer's first GEMM (ops/gradlink.GradLink) instead of an autograd add
+        lk = self._link(self.sa_layer_norm, x)
+        x = self.sa_layer_norm(self.attention(x, mask, link=lk), residual=x, link=lk)
+        lk = self._link(self.output_layer_norm, x)
+        return self.output_layer_norm(self.ffn(x, link=lk), residual=x, link=lk)
+
+    def _link(self, ln, x):
+        if LN_LINKS and self.training and torch.is_grad_enabled() and x.requires_grad and ln.fused_ok(x, x):
+            return GradLink()
+        return None
 
 
 class Transformer(nn.Module):

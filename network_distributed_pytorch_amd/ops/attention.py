@@ -22,7 +22,7 @@ import torch
 
 from ._ext import ext
 
-__all__ = ["attention", "attention_reference", "dropout_keep_mask", "fused_ok"]
+__all__ = ["attention", "attention_qkv", "attention_reference", "dropout_keep_mask", "fused_ok"]
 
 _M32 = 0xFFFFFFFF
 
@@ -74,7 +74,7 @@ class _FusedAttention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, mask, seed, p_drop):
         B, S, H, _ = q.shape
-        o = torch.empty_like(q)
+        o = torch.empty(q.shape, device=q.device, dtype=q.dtype)
         lse = torch.empty(2, B, H, S, device=q.device, dtype=torch.float32)   # row max, log(sum)
         scale = 1.0 / math.sqrt(q.shape[-1])
         ext().attn_fwd(q, k, v, mask, o, lse, scale, seed, p_drop)
@@ -107,3 +107,56 @@ def attention(q, k, v, mask: Optional[torch.Tensor] = None, p_drop: float = 0.0,
     if p_drop > 0 and seed is None:
         seed = torch.randint(0, 2 ** 31 - 1, (1,), device=q.device, dtype=torch.int32)
     return _FusedAttention.apply(q, k, v, mask, seed, float(p_drop))
+
+
+class _FusedAttentionQKV(torch.autograd.Function):
+    """Attention straight off a packed QKV projection [B, S, 3 * H * 64] (one GEMM for the
+    three projections): the kernels read q / k / v in place with a 3*H*64 token stride and
+    the backward writes dq / dk / dv into ONE packed gradient — the projection's backward is
+    then one grad-x GEMM, one grad-W GEMM and one bias column sum instead of three each plus
+    two autograd adds of the three grad-x tensors."""
+
+    @staticmethod
+    def forward(ctx, qkv, H, mask, seed, p_drop):
+        B, S, D3 = qkv.shape
+        v5 = qkv.view(B, S, 3, H, 64)
+        q, k, v = v5[:, :, 0], v5[:, :, 1], v5[:, :, 2]
+        o = torch.empty(B, S, H, 64, device=qkv.device, dtype=qkv.dtype)
+        lse = torch.empty(2, B, H, S, device=qkv.device, dtype=torch.float32)
+        scale = 1.0 / 8.0  # 1 / sqrt(64)
+        ext().attn_fwd(q, k, v, mask, o, lse, scale, seed, p_drop)
+        ctx.save_for_backward(qkv, mask, o, lse, seed)
+        ctx.has_mask = mask is not None
+        ctx.p_drop = p_drop
+        ctx.scale = scale
+        ctx.H = H
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, mask, o, lse, seed = ctx.saved_tensors
+        do = do.contiguous()
+        B, S, D3 = qkv.shape
+        H = ctx.H
+        v5 = qkv.view(B, S, 3, H, 64)
+        dqkv = torch.empty_like(qkv)
+        d5 = dqkv.view(B, S, 3, H, 64)
+        delta = torch.empty(B, H, S, device=qkv.device, dtype=torch.float32)
+        ext().attn_bwd(v5[:, :, 0], v5[:, :, 1], v5[:, :, 2], mask if ctx.has_mask else None, o, do, lse, delta,
+                       d5[:, :, 0], d5[:, :, 1], d5[:, :, 2], ctx.scale, seed if ctx.p_drop > 0 else None,
+                       ctx.p_drop)
+        return dqkv, None, None, None, None
+
+
+def attention_qkv(qkv, n_heads: int, mask: Optional[torch.Tensor] = None, p_drop: float = 0.0,
+                  seed: Optional[torch.Tensor] = None):
+    """Fused attention on a packed projection ``qkv`` [B, S, 3 * n_heads * 64] (q | k | v
+    along the last dim) -> [B, S, n_heads, 64]."""
+    B, S, D3 = qkv.shape
+    assert D3 == 3 * n_heads * 64, "attention_qkv: packed q | k | v of 64-wide heads"
+    qkv = qkv.contiguous()
+    if mask is not None:
+        mask = mask.to(torch.int32).contiguous()
+    if p_drop > 0 and seed is None:
+        seed = torch.randint(0, 2 ** 31 - 1, (1,), device=qkv.device, dtype=torch.int32)
+    return _FusedAttentionQKV.apply(qkv, n_heads, mask, seed, float(p_drop))

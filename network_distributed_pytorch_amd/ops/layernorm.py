@@ -28,7 +28,7 @@ _WIDTHS = (256, 512, 768, 1024)
 
 class _AddLayerNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, residual, weight, bias, eps):
+    def forward(ctx, x, residual, weight, bias, eps, link=None):
         x = x.contiguous()
         r = residual.contiguous() if residual is not None else None
         D = x.shape[-1]
@@ -39,6 +39,7 @@ class _AddLayerNormFn(torch.autograd.Function):
         rstd = torch.empty(R, device=x.device, dtype=torch.float32)
         ext().ln_fwd(x, r, weight, bias, y, s, mean, rstd, float(eps))
         ctx.has_res = r is not None
+        ctx.link = link  # ops/gradlink.GradLink: the residual's gradient goes there instead
         ctx.save_for_backward(s, mean, rstd, weight)
         return y
 
@@ -49,17 +50,27 @@ class _AddLayerNormFn(torch.autograd.Function):
         D = s.shape[-1]
         dgb = torch.empty(2 * D, device=s.device, dtype=torch.float32)
         ext().ln_bwd(dy.contiguous(), s, mean, rstd, weight, dx, dgb)
-        # d(x + residual) reaches both inputs unchanged
-        return dx, (dx if ctx.has_res else None), dgb[:D].view_as(weight), dgb[D:].view_as(weight), None
+        # d(x + residual) reaches both inputs unchanged; with a link the residual's copy is
+        # added by the sublayer's first GEMM (after every reader of dx for x has run)
+        dres = dx if ctx.has_res else None
+        if ctx.link is not None and dres is not None:
+            ctx.link.put(dres)
+            dres = None
+        return dx, dres, dgb[:D].view_as(weight), dgb[D:].view_as(weight), None, None
 
 
 def add_layer_norm(x: torch.Tensor, residual: Optional[torch.Tensor], weight: torch.Tensor, bias: torch.Tensor,
-                   eps: float) -> torch.Tensor:
-    """``F.layer_norm(x + residual, (D,), weight, bias, eps)`` (residual may be None)."""
+                   eps: float, link=None) -> torch.Tensor:
+    """``F.layer_norm(x + residual, (D,), weight, bias, eps)`` (residual may be None).
+    ``link`` (ops/gradlink.GradLink, fused path only): the residual's gradient is deposited
+    there (the residual is taken detached) for the consumer GEMM that folds it in."""
     if (_ENABLED and x.is_cuda and x.dtype == torch.float32 and x.shape[-1] in _WIDTHS and weight is not None
             and bias is not None and weight.dtype == torch.float32
             and (residual is None or (residual.dtype == torch.float32 and residual.shape == x.shape))):
-        return _AddLayerNormFn.apply(x, residual, weight, bias, eps)
+        if link is not None and residual is not None:
+            residual = residual.detach()
+        return _AddLayerNormFn.apply(x, residual, weight, bias, eps, link)
+    assert link is None or link.grad is None
     h = x if residual is None else x + residual
     return F.layer_norm(h, (x.shape[-1],), weight, bias, eps)
 
@@ -70,7 +81,14 @@ class AddLayerNorm(nn.LayerNorm):
 
     native = True
 
-    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def fused_ok(self, x: torch.Tensor, residual: Optional[torch.Tensor]) -> bool:
+        """Whether forward(x, residual) takes the native kernel (a GradLink is only honoured there)."""
+        return (self.native and _ENABLED and len(self.normalized_shape) == 1 and self.elementwise_affine
+                and x.is_cuda and x.dtype == torch.float32 and x.shape[-1] in _WIDTHS
+                and (residual is None or (residual.dtype == torch.float32 and residual.shape == x.shape)))
+
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, link=None) -> torch.Tensor:
         if self.native and len(self.normalized_shape) == 1 and self.elementwise_affine:
-            return add_layer_norm(x, residual, self.weight, self.bias, self.eps)
+            return add_layer_norm(x, residual, self.weight, self.bias, self.eps, link if self.fused_ok(x, residual)
+                                  else None)
         return super().forward(x if residual is None else x + residual)

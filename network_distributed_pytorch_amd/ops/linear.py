@@ -13,14 +13,16 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ._ext import ext
+from .gradlink import InjectGrad
 
-__all__ = ["Linear"]
+__all__ = ["Linear", "linear"]
 
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, link=None):
         ctx.save_for_backward(x, weight)
+        ctx.link = link  # ops/gradlink.GradLink: a residual gradient added into grad-x (addmm_)
         return F.linear(x, weight, bias)
 
     @staticmethod
@@ -31,21 +33,39 @@ class _LinearFn(torch.autograd.Function):
         if not g2.is_contiguous():
             g2 = g2.contiguous()
         dx = dw = db = None
+        addend = ctx.link.take() if ctx.link is not None else None
         if ctx.needs_input_grad[0]:
-            dx = (g2 @ weight).view(x.shape)
+            if addend is not None:  # in place on the residual gradient buffer: GEMM with beta = 1
+                dx = addend.reshape(-1, k).addmm_(g2, weight).view(x.shape)
+            else:
+                dx = (g2 @ weight).view(x.shape)
+        elif addend is not None:
+            dx = addend.view(x.shape)
         if ctx.needs_input_grad[1]:
             dw = g2.t() @ x.reshape(-1, k)
         if ctx.needs_input_grad[2]:
             db = torch.empty(n, device=g.device, dtype=g.dtype)
             ext().colsum(g2, db)
-        return dx, dw, db
+        return dx, dw, db, None
+
+
+def _native_ok(x, weight, bias) -> bool:
+    return (x.is_cuda and bias is not None and x.dtype == torch.float32 and weight.dtype == torch.float32
+            and weight.shape[0] % 4 == 0 and torch.is_grad_enabled())
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, link=None) -> torch.Tensor:
+    """``F.linear`` with the native deterministic bias gradient where it applies.  ``link``
+    (ops/gradlink.GradLink): a residual-branch gradient folded into this layer's grad-x."""
+    if _native_ok(x, weight, bias):
+        return _LinearFn.apply(x, weight, bias, link)
+    return F.linear(InjectGrad.apply(x, link) if link is not None else x, weight, bias)
 
 
 class Linear(nn.Linear):
     """Drop-in ``nn.Linear`` (device fp32 with bias and out_features % 4 == 0 -> native bias grad)."""
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        if (x.is_cuda and self.bias is not None and x.dtype == torch.float32 and self.weight.dtype == torch.float32
-                and self.out_features % 4 == 0 and torch.is_grad_enabled()):
-            return _LinearFn.apply(x, self.weight, self.bias)
-        return super().forward(x)
+    def forward(self, x: torch.Tensor, link=None) -> torch.Tensor:
+        if _native_ok(x, self.weight, self.bias):
+            return _LinearFn.apply(x, self.weight, self.bias, link)
+        return super().forward(InjectGrad.apply(x, link) if link is not None else x)

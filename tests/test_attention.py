@@ -123,3 +123,29 @@ def test_fused_attention_distilbert_shape(device):
     gr = torch.autograd.grad(r, (qd, kd, vd), go.double())
     for x, y in zip(g, gr):
         _check(x, y, 5e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p_drop", [0.0, 0.1])
+def test_attention_packed_qkv_matches_separate(device, p_drop):
+    """attention_qkv reads q / k / v in place from a packed projection (token stride 3*H*64)
+    and writes one packed gradient: bitwise equal to the contiguous three-tensor path."""
+    from network_distributed_pytorch_amd.ops.attention import attention, attention_qkv
+
+    torch.manual_seed(7)
+    B, S, H = 2, 200, 4
+    qkv = torch.randn(B, S, 3 * H * 64, device=device, requires_grad=True)
+    mask = torch.ones(B, S, dtype=torch.int32, device=device)
+    mask[1, 150:] = 0
+    seed = torch.tensor([1234], dtype=torch.int32, device=device)
+    o1 = attention_qkv(qkv, H, mask, p_drop, seed=seed)
+    v5 = qkv.detach().view(B, S, 3, H, 64)
+    q, k, v = (v5[:, :, i].contiguous().requires_grad_(True) for i in range(3))
+    o2 = attention(q, k, v, mask, p_drop, seed=seed)
+    assert torch.equal(o1, o2)
+    g = torch.randn_like(o1)
+    o1.backward(g)
+    o2.backward(g)
+    d5 = qkv.grad.view(B, S, 3, H, 64)
+    for i, t in enumerate((q, k, v)):
+        assert torch.equal(d5[:, :, i], t.grad), i

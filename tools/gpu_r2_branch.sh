@@ -3,13 +3,18 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/gputests.log 2>&1 || { tail -30 gpurun_out/gputests.log; exit 1; }
-tail -2 gpurun_out/gputests.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > gpurun_out/gputests.log 2>&1
+rc=$?
+grep -E "FAILED|passed|failed" gpurun_out/gputests.log | tail -12
+case $rc in 0|1) ;; *) echo "pytest rc=$rc (crash/timeout): stopping"; exit 1 ;; esac
 b() {  # name, env..., -- bench args
   local name=$1; shift
   timeout -k 10 300 env "$@" > gpurun_out/ab_$name.json 2> gpurun_out/ab_$name.err || { tail -5 gpurun_out/ab_$name.err; return 1; }
   echo "$name $(python3 tools/jline.py gpurun_out/ab_$name.json)"
 }
+b bert8 python bench.py --model distilbert --rank 8 --steps 20 --warmup 5 &&
+b bert8_nolnk NDP_LN_LINKS=0 python bench.py --model distilbert --rank 8 --steps 20 --warmup 5 &&
+b bert8_noqkv NDP_PACKED_QKV=0 python bench.py --model distilbert --rank 8 --steps 20 --warmup 5 || exit 1
 for gb in 64 512; do
   b br_$gb python bench.py --global-batch $gb --steps 60 &&
   b nobr_$gb NDP_BRANCH_LINKS=0 python bench.py --global-batch $gb --steps 60 &&
