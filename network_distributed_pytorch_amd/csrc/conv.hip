@@ -289,8 +289,12 @@ struct ConvFwdCfg {
 // floats), grad-x rows W[c][m0:m0+BM][:] (BM*RS contiguous) with the taps flipped; both are
 // written transposed into the [kk][m] LDS image.  VEC=1 needs Cin % CK == 0 (float4 over
 // whole channels); the stem (Cin = 3 < CK) stages scalars.
+// SCH (instruction scheduling of the MFMA block, benchmarking variants): 0 = compiler default,
+// 1 = __builtin_amdgcn_iglp_opt(0), 2 = pinned interleave of one MFMA and one LDS read (the
+// default schedule waits on each operand read right before its MFMA: exposed LDS latency
+// at 1-2 waves per SIMD)
 template <int R, int S, int ST, int PD, int H, int W, int CK, int BM, int IMGS, int WM, int NBUF, int KB, bool TRANSW,
-          bool VEC, int UPS = 1>
+          bool VEC, int UPS = 1, int SCH = 0>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                        float* __restrict__ y, float* __restrict__ part, int Cin,
                                                        int Kout, int cps, int64_t slab,
@@ -436,6 +440,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
         for (int tn = 0; tn < G::TN; ++tn) bv[slot][i][tn] = B[b_base[tn] + offb];
       }
     };
+    if constexpr (SCH == 1) __builtin_amdgcn_iglp_opt(0);
     fetch(0, 0);
 #pragma unroll
     for (int blk = 0; blk < G::NBLK; ++blk) {
@@ -447,6 +452,13 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
 #pragma unroll
           for (int tn = 0; tn < G::TN; ++tn)
             acc[tm][tn] = mfma32(av[blk & 1][i][tm], bv[blk & 1][i][tn], acc[tm][tn]);
+    }
+    if constexpr (SCH == 2) {
+#pragma unroll
+      for (int i = 0; i < G::NSTEP * G::TM * G::TN; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // one LDS read
+      }
     }
     if (ch + 1 < nchunks) {
       if (NBUF == 2) {
@@ -752,11 +764,11 @@ static void set_lds(KernelT k, size_t bytes) {
 // (deterministic).  Used where B / IMGS * Kout / BM alone cannot fill the 256 CUs
 // (small per-GPU batches: the strong-scaling shapes 512 / N).
 template <int R, int S, int ST, int PD, int H, int W, int CK, int BM, int IMGS, int WM, int NBUF, int KB, bool TRANSW,
-          bool VEC, int UPS = 1>
+          bool VEC, int UPS = 1, int SCH = 0>
 static int run_fwd(const float* x, const float* w, float* y, int B, int Cin, int Kout, int ksplit, float* part,
                    hipStream_t s, const float* addend = nullptr, bool defer = false) {
   using G = ConvFwdCfg<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW>;
-  auto k = conv_fwd_kernel<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW, VEC, UPS>;
+  auto k = conv_fwd_kernel<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW, VEC, UPS, SCH>;
   static bool attr = false;  // once per instantiation (> 64 KiB of LDS needs the opt-in)
   if (!attr) { set_lds(k, G::LDS_BYTES); attr = true; }
   const int nchunks = (Cin + CK - 1) / CK;
@@ -868,6 +880,15 @@ int conv_ksplit(int cls, const ConvGeom& g, int B, bool dgrad) {
   return pow2_floor(ks);
 }
 bool conv_dgrad_direct(int cls) { return cls == 0 || cls == 1 || cls == 4; }
+// MFMA-block schedule of the layer1 / layer2 fwd + grad-x kernels (SCH template argument):
+// default 2 (pinned MFMA / LDS-read interleave): ResNet-18 step on 1x MI355X 2.0175 / 2.0154
+// -> 1.9981 / 1.9994 ms at batch 512, 1.0582 / 1.0627 -> 1.0546 / 1.0569 at batch 64;
+// NDP_CONV_VARIANT 5 = iglp_opt(0) (2.0043 / 1.0602), 7 = the compiler's schedule.
+static int conv_sched() {
+  const int v = conv_variant();
+  return v == 5 ? 1 : (v == 0 || v == 6) ? 2 : 0;
+}
+
 // NDP_CONV_VARIANT (benchmarking only): 1 = two images per layer1 tile; 2 = 16-channel
 // chunks (half the chunk barriers, twice the MFMA work behind each prefetch) for the 3x3
 // classes 0-2; 3 = 16-channel chunks for classes 1-2 only (already one workgroup per CU)
@@ -881,8 +902,15 @@ int launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvG
   const int cls = conv_direct_class(g);
   const int ks = conv_ksplit(cls, g, B, false);
   const bool c16 = ck16(cls);
+  const int sch = conv_sched();
   switch (cls) {
     case 0:
+      if (sch == 1)
+        return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, false, true, 1, 1>(x, w, y, B, g.C, g.Co, ks, part, s,
+                                                                               nullptr, defer);
+      if (sch == 2)
+        return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, false, true, 1, 2>(x, w, y, B, g.C, g.Co, ks, part, s,
+                                                                               nullptr, defer);
       if (conv_variant() == 1)
         return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 2, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s, nullptr,
                                                                          defer);
@@ -892,6 +920,12 @@ int launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvG
       return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s, nullptr,
                                                                        defer);
     case 1:
+      if (sch == 1)
+        return run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, false, true, 1, 1>(x, w, y, B, g.C, g.Co, ks, part, s,
+                                                                               nullptr, defer);
+      if (sch == 2)
+        return run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, false, true, 1, 2>(x, w, y, B, g.C, g.Co, ks, part, s,
+                                                                               nullptr, defer);
       if (c16)
         return run_fwd<3, 3, 1, 1, 4, 4, 16, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s,
                                                                           nullptr, defer);
@@ -917,8 +951,15 @@ int launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const C
   const int cls = conv_direct_class(g);
   const int ks = conv_ksplit(cls, g, B, true);
   const bool c16 = ck16(cls);
+  const int sch = conv_sched();
   switch (cls) {
     case 0:
+      if (sch == 1)
+        return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true, true, 1, 1>(dy, w, dx, B, g.Co, g.C, ks, part, s,
+                                                                              addend, defer);
+      if (sch == 2)
+        return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true, true, 1, 2>(dy, w, dx, B, g.Co, g.C, ks, part, s,
+                                                                              addend, defer);
       if (conv_variant() == 1)
         return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 2, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s, addend,
                                                                         defer);
@@ -928,6 +969,12 @@ int launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const C
       return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s, addend,
                                                                       defer);
     case 1:
+      if (sch == 1)
+        return run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, true, true, 1, 1>(dy, w, dx, B, g.Co, g.C, ks, part, s,
+                                                                              addend, defer);
+      if (sch == 2)
+        return run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, true, true, 1, 2>(dy, w, dx, B, g.Co, g.C, ks, part, s,
+                                                                              addend, defer);
       if (c16)
         return run_fwd<3, 3, 1, 1, 4, 4, 16, 64, 4, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s,
                                                                          addend, defer);
