@@ -180,11 +180,12 @@ class Workload:
             from network_distributed_pytorch_amd.utils.graph import StepRunner
 
             static = {k: v.clone() for k, v in pool[0].items()}
+            one = torch.ones((), device=device)  # backward seed outside the graph: no fill kernel
 
             def pre():
                 sync.zero_grad()
                 loss = loss_of(static)
-                loss.backward()
+                loss.backward(one)
                 loss_acc.add_(loss.detach())  # one add, no copy into a static loss
 
             runner = StepRunner(pre, sync, mode=graph_mode, warmup=3,

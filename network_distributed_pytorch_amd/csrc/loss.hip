@@ -36,6 +36,7 @@ __device__ __forceinline__ float wave_sum_f(float v) {
 }
 
 constexpr int kCeRowsPerWg = 4;
+constexpr int kCeRegs = 16;  // row length held in registers: K <= 1024
 
 __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ x, const int64_t* __restrict__ tgt,
                                                      int B, int K, int64_t ignore, float* __restrict__ dl,
@@ -48,16 +49,35 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ x
     float* dr = dl + (int64_t)b * K;
     const int64_t t = tgt[b];
     const bool valid = t != ignore;
-    float m = -INFINITY;
-    for (int k = lane; k < K; k += 64) m = fmaxf(m, xr[k]);
-    m = wave_max_f(m);
-    float s = 0.f;
-    for (int k = lane; k < K; k += 64) s += expf(xr[k] - m);
-    s = wave_sum_f(s);
-    const float lse = m + logf(s);
     const bool in_range = t >= 0 && t < K;
-    for (int k = lane; k < K; k += 64)
-      dr[k] = valid ? expf(xr[k] - lse) - (k == t ? 1.f : 0.f) : 0.f;
+    float m = -INFINITY, s = 0.f, lse;
+    if (K <= 64 * kCeRegs) {  // the row in registers: one load pass (ResNet's 1000 classes)
+      float v[kCeRegs];
+#pragma unroll
+      for (int i = 0; i < kCeRegs; ++i) {
+        const int k = lane + 64 * i;
+        v[i] = k < K ? xr[k] : -INFINITY;
+        m = fmaxf(m, v[i]);
+      }
+      m = wave_max_f(m);
+#pragma unroll
+      for (int i = 0; i < kCeRegs; ++i) s += lane + 64 * i < K ? expf(v[i] - m) : 0.f;
+      s = wave_sum_f(s);
+      lse = m + logf(s);
+#pragma unroll
+      for (int i = 0; i < kCeRegs; ++i) {
+        const int k = lane + 64 * i;
+        if (k < K) dr[k] = valid ? expf(v[i] - lse) - (k == t ? 1.f : 0.f) : 0.f;
+      }
+    } else {
+      for (int k = lane; k < K; k += 64) m = fmaxf(m, xr[k]);
+      m = wave_max_f(m);
+      for (int k = lane; k < K; k += 64) s += expf(xr[k] - m);
+      s = wave_sum_f(s);
+      lse = m + logf(s);
+      for (int k = lane; k < K; k += 64)
+        dr[k] = valid ? expf(xr[k] - lse) - (k == t ? 1.f : 0.f) : 0.f;
+    }
     if (lane == 0) rowloss[b] = !valid ? 0.f : (in_range ? lse - xr[t] : __builtin_nanf(""));
   }
   // last-arriving workgroup: fixed-order mean over the rows
