@@ -293,8 +293,12 @@ struct ConvFwdCfg {
 // 1 = __builtin_amdgcn_iglp_opt(0), 2 = pinned interleave of one MFMA and one LDS read (the
 // default schedule waits on each operand read right before its MFMA: exposed LDS latency
 // at 1-2 waves per SIMD)
+// IUPS = 2 (grad-x of the 3x3 stride-2 conv): the input is a (H/2) x (W/2) map staged onto
+// the even pixels of the H x W LDS image (the odd ones keep the zero fill), i.e. the stride-1
+// correlation of the zero-inserted dY with the flipped weights:
+//   dX[c, h, w] = sum_{k,r,s} W[k, c, 2-r, 2-s] * Z[k, h-1+r, w-1+s],  Z[k, 2p, 2q] = dY[k, p, q]
 template <int R, int S, int ST, int PD, int H, int W, int CK, int BM, int IMGS, int WM, int NBUF, int KB, bool TRANSW,
-          bool VEC, int UPS = 1, int SCH = 0>
+          bool VEC, int UPS = 1, int SCH = 0, int IUPS = 1>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                        float* __restrict__ y, float* __restrict__ part, int Cin,
                                                        int Kout, int cps, int64_t slab,
@@ -327,8 +331,12 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
     b_base[tn] = img * G::IMGSTR + h * (CK / 2) * G::HWp + p * ST * G::Wp + q * ST;
   }
 
+  // B staging: float4 of the (possibly half-size, IUPS) input planes
+  constexpr int IW = W / IUPS, IHW = (H / IUPS) * IW;
+  constexpr int B4I = IMGS * CK * IHW / 4, BPT = (B4I + 255) / 256;
+  static_assert(IW % 4 == 0 && (IUPS == 1 || (ST == 1 && UPS == 1)), "input staging");
   f32x4c ra[A_PER_T];
-  f32x4c rb[G::B_PER_T];
+  f32x4c rb[BPT];
   auto load = [&](int ch) {
     const int c0 = (ch0 + ch) * CK;
 #pragma unroll
@@ -355,14 +363,14 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
       ra[i] = v;
     }
 #pragma unroll
-    for (int i = 0; i < G::B_PER_T; ++i) {
-      const int e = tid + 256 * i;  // float4 index within the IMGS x CK x H x W block
+    for (int i = 0; i < BPT; ++i) {
+      const int e = tid + 256 * i;  // float4 index within the IMGS x CK x (input plane) block
       f32x4c v = {0.f, 0.f, 0.f, 0.f};
-      if (e < G::B4) {
-        const int img = e / (CK * G::HW / 4), rem4 = e - img * (CK * G::HW / 4);
-        const int c = (4 * rem4) / G::HW;
+      if (e < B4I) {
+        const int img = e / (CK * IHW / 4), rem4 = e - img * (CK * IHW / 4);
+        const int c = (4 * rem4) / IHW;
         if (c0 + c < Cin)
-          v = *reinterpret_cast<const f32x4c*>(x + ((int64_t)(b0 + img) * Cin + c0) * G::HW + 4 * rem4);
+          v = *reinterpret_cast<const f32x4c*>(x + ((int64_t)(b0 + img) * Cin + c0) * IHW + 4 * rem4);
       }
       rb[i] = v;
     }
@@ -397,14 +405,14 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
       }
     }
 #pragma unroll
-    for (int i = 0; i < G::B_PER_T; ++i) {
+    for (int i = 0; i < BPT; ++i) {
       const int e = tid + 256 * i;
-      if (e < G::B4) {
-        const int img = e / (CK * G::HW / 4), rem = 4 * (e - img * (CK * G::HW / 4));
-        const int c = rem / G::HW, hw = rem - c * G::HW;
-        const int hh = hw / W, ww = hw - hh * W;
-        float* d = B + img * G::IMGSTR + c * G::HWp + (hh + PD) * G::Wp + ww + PD;
-        d[0] = rb[i].x; d[1] = rb[i].y; d[2] = rb[i].z; d[3] = rb[i].w;
+      if (e < B4I) {
+        const int img = e / (CK * IHW / 4), rem = 4 * (e - img * (CK * IHW / 4));
+        const int c = rem / IHW, hw = rem - c * IHW;
+        const int hh = hw / IW, ww = hw - hh * IW;
+        float* d = B + img * G::IMGSTR + c * G::HWp + (IUPS * hh + PD) * G::Wp + IUPS * ww + PD;
+        d[0] = rb[i].x; d[IUPS] = rb[i].y; d[2 * IUPS] = rb[i].z; d[3 * IUPS] = rb[i].w;
       }
     }
   };
@@ -764,11 +772,11 @@ static void set_lds(KernelT k, size_t bytes) {
 // (deterministic).  Used where B / IMGS * Kout / BM alone cannot fill the 256 CUs
 // (small per-GPU batches: the strong-scaling shapes 512 / N).
 template <int R, int S, int ST, int PD, int H, int W, int CK, int BM, int IMGS, int WM, int NBUF, int KB, bool TRANSW,
-          bool VEC, int UPS = 1, int SCH = 0>
+          bool VEC, int UPS = 1, int SCH = 0, int IUPS = 1>
 static int run_fwd(const float* x, const float* w, float* y, int B, int Cin, int Kout, int ksplit, float* part,
                    hipStream_t s, const float* addend = nullptr, bool defer = false) {
   using G = ConvFwdCfg<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW>;
-  auto k = conv_fwd_kernel<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW, VEC, UPS, SCH>;
+  auto k = conv_fwd_kernel<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW, VEC, UPS, SCH, IUPS>;
   static bool attr = false;  // once per instantiation (> 64 KiB of LDS needs the opt-in)
   if (!attr) { set_lds(k, G::LDS_BYTES); attr = true; }
   const int nchunks = (Cin + CK - 1) / CK;
@@ -815,7 +823,8 @@ static void run_wgrad(const float* x, const float* dy, float* part, float* dw, i
 // Shape classes with a direct kernel (everything else stays on MIOpen / the Toeplitz path)
 //   id 0: 3x3 s1 p1 on 8x8   (ResNet layer1)           C, K % 64 == 0
 //   id 1: 3x3 s1 p1 on 4x4   (ResNet layer2)           C, K % 64 == 0
-//   id 2: 3x3 s2 p1 8x8->4x4 (layer2 first conv)       C % 32 == 0, K % 64 == 0
+//   id 2: 3x3 s2 p1 8x8->4x4 (layer2 first conv)       C, K % 64 == 0; grad-x = the id-0 kernel on
+//         the zero-inserted dY (IUPS = 2 staging)
 //   id 3: 7x7 s2 p3 32x32->16x16, C = 3 (stem)         K % 64 == 0
 //   id 4: 1x1 s2 p0 8x8->4x4 (layer2 downsample)        C % 32 == 0, K % 64 == 0;
 //         grad-x = the 1x1 transposed product on the 4x4 map, written to the even pixels
@@ -825,7 +834,7 @@ int conv_direct_class(const ConvGeom& g) {
     return 0;
   if (g.KH == 3 && g.KW == 3 && g.pad == 1 && g.stride == 1 && g.H == 4 && g.W == 4 && g.C % 64 == 0 && g.Co % 64 == 0)
     return 1;
-  if (g.KH == 3 && g.KW == 3 && g.pad == 1 && g.stride == 2 && g.H == 8 && g.W == 8 && g.C % 32 == 0 && g.Co % 64 == 0)
+  if (g.KH == 3 && g.KW == 3 && g.pad == 1 && g.stride == 2 && g.H == 8 && g.W == 8 && g.C % 64 == 0 && g.Co % 64 == 0)
     return 2;
   if (g.KH == 7 && g.KW == 7 && g.pad == 3 && g.stride == 2 && g.H == 32 && g.W == 32 && g.C == 3 && g.Co % 64 == 0)
     return 3;
@@ -873,13 +882,26 @@ int conv_wgrad_imgs(int cls, const ConvGeom& g, int B) {
 int conv_ksplit(int cls, const ConvGeom& g, int B, bool dgrad) {
   if (cls == 3 || (dgrad && !conv_dgrad_direct(cls))) return 1;
   const int inC = dgrad ? g.Co : g.C, outC = dgrad ? g.C : g.Co;
-  const int base = (B / conv_fwd_imgs(cls)) * (outC / 64);
+  const int imgs = (dgrad && cls == 2) ? 1 : conv_fwd_imgs(cls);  // class-2 grad-x: 8x8 tiles, 1 image
+  const int base = (B / imgs) * (outC / 64);
   const int nchunks = inC / 8;
   int ks = 1;
   while (ks * 2 <= nchunks && base * ks < kFillWgs) ks *= 2;
   return pow2_floor(ks);
 }
-bool conv_dgrad_direct(int cls) { return cls == 0 || cls == 1 || cls == 4; }
+// 3x3 stride-2 grad-x on the zero-inserted dY (NDP_CONV_DGRAD2=1): exact (tests/
+// test_conv_direct.py) but 4x the MFMA work of the sub-pixel form, measured on 1x MI355X
+// (ResNet-18 step) 2.006 / 2.005 vs MIOpen 1.991 ms at batch 512, 1.054 / 1.047 vs 1.051 at
+// 64, 1.443 / 1.445 vs 1.446 at 256 — MIOpen stays the default.
+static bool dgrad2_on() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("NDP_CONV_DGRAD2");
+    v = e ? atoi(e) : 0;
+  }
+  return v != 0;
+}
+bool conv_dgrad_direct(int cls) { return cls == 0 || cls == 1 || (cls == 2 && dgrad2_on()) || cls == 4; }
 // MFMA-block schedule of the layer1 / layer2 fwd + grad-x kernels (SCH template argument):
 // default 2 (pinned MFMA / LDS-read interleave): ResNet-18 step on 1x MI355X 2.0175 / 2.0154
 // -> 1.9981 / 1.9994 ms at batch 512, 1.0582 / 1.0627 -> 1.0546 / 1.0569 at batch 64;
@@ -980,6 +1002,9 @@ int launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const C
                                                                          addend, defer);
       return run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s, addend,
                                                                       defer);
+    case 2:  // 3x3 stride 2: the layer1 grad-x kernel on the zero-inserted dY (staged, not stored)
+      return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true, true, 1, 2, 2>(dy, w, dx, B, g.Co, g.C, ks, part, s,
+                                                                              addend, defer);
     case 4: return run_fwd<1, 1, 1, 0, 4, 4, 8, 64, 4, 2, 2, 4, true, true, 2>(dy, w, dx, B, g.Co, g.C, ks, part, s);
     default: return 1;
   }

@@ -4,9 +4,10 @@
 hand-written gfx950 kernels for the shape classes the extension reports through
 ``conv_plan`` (ResNet stem 7x7/2 on 32x32, layer1 3x3 on 8x8, layer2 3x3 on 4x4, its
 strided 8x8->4x4 entry conv and its 1x1/2 downsample).  Grad-input of the strided 3x3 class
-goes to MIOpen (``aten.convolution_backward``); the 1x1/2 downsample's grad-input is the
-transposed 1x1 product written to the even pixels (native); the stem's input never needs a
-gradient.
+goes to MIOpen by default; ``NDP_CONV_DGRAD2=1`` runs it natively as the layer1 grad-x kernel
+on the zero-inserted dY (zeros from the LDS staging; exact, but measured no faster);  the 1x1/2
+downsample's grad-input is the transposed 1x1 product written to the even pixels; the stem's
+input never needs a gradient.
 :func:`direct_plan` returns None for every other geometry, so callers keep their MIOpen /
 Toeplitz paths there.
 """
@@ -117,8 +118,10 @@ class DirectConvFn(torch.autograd.Function):
             if dgrad_direct:
                 dx = torch.empty_like(x)
                 part = None
-                if ks_dgrad > 1:  # compact partials: numel(dy) * C / Co floats per split
-                    part = torch.empty(ks_dgrad * (dy.numel() // geom[3]) * geom[0], device=x.device, dtype=x.dtype)
+                if ks_dgrad > 1:  # partials in dx layout (the 1x1 stride-2 class: its compact 4x4 map)
+                    ups = geom[4] == 1 and geom[6] == 2
+                    slab = (dy.numel() // geom[3]) * geom[0] if ups else x.numel()
+                    part = torch.empty(ks_dgrad * slab, device=x.device, dtype=x.dtype)
                 fuse = addend is not None and geom[6] == 1  # stride-1 classes take the addend in-kernel
                 defer = ctx.grad_slab is not None and part is not None and addend is None
                 left = ext().conv_dgrad(dy, weight, dx, list(geom), part, addend.contiguous() if fuse else None,

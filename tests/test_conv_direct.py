@@ -1,4 +1,6 @@
-"""Direct fp32-MFMA convolutions (csrc/conv.hip) vs an fp64 CPU oracle (F.conv2d)."""
+"""Direct fp32-MFMA convolutions (csrc/conv.hip) vs an fp64 CPU oracle (F.conv2d).
+(The 3x3 stride-2 native grad-x is opt-in, NDP_CONV_DGRAD2=1: run this file with it set to
+cover that kernel, as tools/gpu_r2_dgrad2.sh did.)"""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -7,7 +9,8 @@ import torch.nn.functional as F
 # small batches run split-K forward / grad-x (+ slab sum) and 1-image grad-W slices
 CASES = [(64, 64, 3, 1, 1, 8, 8), (128, 128, 3, 1, 1, 4, 16), (64, 128, 3, 2, 1, 8, 8), (3, 64, 7, 2, 3, 32, 4),
          (128, 64, 3, 1, 1, 8, 4), (64, 192, 3, 1, 1, 4, 16), (64, 64, 3, 1, 1, 8, 64), (128, 128, 3, 1, 1, 4, 64),
-         (64, 64, 3, 1, 1, 8, 6), (64, 128, 1, 2, 0, 8, 8), (64, 128, 1, 2, 0, 8, 64), (256, 512, 1, 2, 0, 8, 16)]
+         (64, 64, 3, 1, 1, 8, 6), (64, 128, 1, 2, 0, 8, 8), (64, 128, 1, 2, 0, 8, 64), (256, 512, 1, 2, 0, 8, 16),
+         (64, 128, 3, 2, 1, 8, 64), (128, 128, 3, 2, 1, 8, 32), (64, 128, 3, 2, 1, 8, 512)]
 
 
 @pytest.mark.gpu
