@@ -124,7 +124,8 @@ class Workload:
         if args.channels_last:
             self.model = self.model.to(memory_format=torch.channels_last)
         link = None if args.link == "none" else LINK_PRESETS[args.link]
-        self.comm = Communicator(link=link, emulate_world=args.emulate_world, device=device)
+        native = None if getattr(args, "native_comm", True) else False
+        self.comm = Communicator(link=link, emulate_world=args.emulate_world, device=device, native=native)
         kw = {}
         if args.reducer in ("powersgd", "dense"):
             if args.overlap != "auto":  # auto: overlap when a step has wire time (N > 1 / link emulation)
@@ -206,15 +207,15 @@ class Workload:
         self.graph_mode = graph_mode
         return step
 
-    def time(self, step, steps: int, warmup: int) -> float:
-        for i in range(warmup):
+    def time(self, step, steps: int, warmup: int, start: int = 0) -> float:
+        for i in range(start, start + warmup):
             step(i)
         if self.world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         self.comm.stats.reset()
         t0 = time.perf_counter()
-        for i in range(steps):
+        for i in range(start + warmup, start + warmup + steps):
             step(i)
         torch.cuda.synchronize()
         if self.world > 1:
@@ -225,6 +226,54 @@ class Workload:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
         return elapsed
+
+
+# N > 1: if building / capturing / warming the step raises on any rank, every rank moves to
+# the next, simpler configuration together (agreed by a c10d all-reduce MIN of a success flag):
+# the default (native RCCL communicator, step captured with the comm graph overlapping
+# backward) -> collectives captured serially in the step graph -> c10d data plane with the
+# collectives eager between captured phases -> eager.  The JSON line records any fallback.
+# Covers failures every rank hits (capture / build errors are shape- and code-determined, so
+# SPMD ranks fail alike); a rank failing alone while its peers sit in a collective still hangs.
+_FALLBACKS = [{}, {"overlap": "off"}, {"native_comm": False, "graph_mode": "auto"},
+              {"native_comm": False, "graph_mode": "none"}]
+
+
+def build_with_fallback(args, device, world, rank, per_gpu):
+    attempts = _FALLBACKS if world > 1 else _FALLBACKS[:1]
+    errors = []
+    for i, over in enumerate(attempts):
+        a = argparse.Namespace(**{**vars(args), **over})
+        if "overlap" in over:
+            a.overlap = over["overlap"]
+        ok, wl, step = 1, None, None
+        try:
+            if os.environ.get("NDP_BENCH_FAIL") in (f"{i}:{rank}", f"{i}:*"):  # test hook: inject a failure
+                raise RuntimeError(f"injected failure, attempt {i} rank {rank}")
+            torch.manual_seed(714)
+            wl = Workload(a, device, world, rank)
+            step = wl.make_step(per_gpu)
+            for j in range(args.warmup):
+                step(j)
+            torch.cuda.synchronize()
+        except Exception as e:  # noqa: BLE001 - any failure moves every rank to the next config
+            ok = 0
+            errors.append(f"{over or 'default'}: {repr(e)[:300]}")
+            print(f"[bench] rank {rank}: attempt {i} failed: {errors[-1]}", file=sys.stderr, flush=True)
+        if world > 1:
+            flag = torch.tensor([ok], dtype=torch.int32, device=device)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            ok = int(flag.item())
+        if ok:
+            return wl, step, ({"attempt": i, "config": over, "errors": errors} if i else None)
+        if wl is not None:
+            try:
+                wl.comm.close()
+            except Exception:  # noqa: BLE001
+                pass
+        del wl, step
+        torch.cuda.synchronize()
+    raise RuntimeError("every bench configuration failed: " + " | ".join(errors))
 
 
 def main(argv=None):
@@ -252,9 +301,8 @@ def main(argv=None):
         per_gpu = args.global_batch // world   # reference: bsz = int(512 / float(size))
     else:
         per_gpu = args.batch
-    wl = Workload(args, device, world, rank)
-    step = wl.make_step(per_gpu)
-    elapsed = wl.time(step, args.steps, args.warmup)
+    wl, step, fallback = build_with_fallback(args, device, world, rank, per_gpu)
+    elapsed = wl.time(step, args.steps, 0, start=args.warmup)  # warmed up inside the attempt
     graph_mode = wl.graph_mode
     comm_stats = wl.comm.stats.as_dict()
     final_loss = float(wl.loss_acc.item()) / max(1, args.warmup + args.steps)
@@ -323,6 +371,8 @@ def main(argv=None):
         }
         if weak is not None:
             rec["weak_scaling"] = weak
+        if fallback:
+            rec["fallback"] = fallback
         line = json.dumps(rec)
         print(line, flush=True)
         if args.json_out:

@@ -908,8 +908,10 @@ bool conv_dgrad_direct(int cls) { return cls == 0 || cls == 1 || (cls == 2 && dg
 // NDP_CONV_VARIANT 5 = iglp_opt(0) (2.0043 / 1.0602), 7 = the compiler's schedule.
 static int conv_sched() {
   const int v = conv_variant();
-  return v == 5 ? 1 : (v == 0 || v == 6) ? 2 : 0;
+  return v == 5 ? 1 : (v == 0 || v == 6 || v == 8) ? 2 : 0;
 }
+// NDP_CONV_VARIANT=8: the pinned interleave also for the stem, 3x3/2 and 1x1/2 forwards (A/B)
+static bool sched_all() { return conv_variant() == 8; }
 
 // NDP_CONV_VARIANT (benchmarking only): 1 = two images per layer1 tile; 2 = 16-channel
 // chunks (half the chunk barriers, twice the MFMA work behind each prefetch) for the 3x3
@@ -957,10 +959,19 @@ int launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvG
       if (c16)
         return run_fwd<3, 3, 2, 1, 8, 8, 16, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s,
                                                                           nullptr, defer);
+      if (sched_all())
+        return run_fwd<3, 3, 2, 1, 8, 8, 8, 64, 4, 2, 2, 4, false, true, 1, 2>(x, w, y, B, g.C, g.Co, ks, part, s,
+                                                                               nullptr, defer);
       return run_fwd<3, 3, 2, 1, 8, 8, 8, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s, nullptr,
                                                                        defer);
-    case 3: return run_fwd<7, 7, 2, 3, 32, 32, 4, 64, 1, 2, 1, 7, false, false>(x, w, y, B, g.C, g.Co, 1, nullptr, s);
+    case 3:
+      if (sched_all())
+        return run_fwd<7, 7, 2, 3, 32, 32, 4, 64, 1, 2, 1, 7, false, false, 1, 2>(x, w, y, B, g.C, g.Co, 1, nullptr, s);
+      return run_fwd<7, 7, 2, 3, 32, 32, 4, 64, 1, 2, 1, 7, false, false>(x, w, y, B, g.C, g.Co, 1, nullptr, s);
     case 4:
+      if (sched_all())
+        return run_fwd<1, 1, 2, 0, 8, 8, 8, 64, 4, 2, 2, 4, false, true, 1, 2>(x, w, y, B, g.C, g.Co, ks, part, s,
+                                                                               nullptr, defer);
       return run_fwd<1, 1, 2, 0, 8, 8, 8, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s, nullptr,
                                                                        defer);
     default: return 1;
