@@ -885,8 +885,13 @@ int conv_ksplit(int cls, const ConvGeom& g, int B, bool dgrad) {
   const int imgs = (dgrad && cls == 2) ? 1 : conv_fwd_imgs(cls);  // class-2 grad-x: 8x8 tiles, 1 image
   const int base = (B / imgs) * (outC / 64);
   const int nchunks = inC / 8;
+  static int maxks = -1;  // NDP_CONV_MAXKS (A/B only): cap the split, e.g. 4 keeps BN-fusable slabs
+  if (maxks < 0) {
+    const char* e = getenv("NDP_CONV_MAXKS");
+    maxks = e ? atoi(e) : 1 << 30;
+  }
   int ks = 1;
-  while (ks * 2 <= nchunks && base * ks < kFillWgs) ks *= 2;
+  while (ks * 2 <= nchunks && base * ks < kFillWgs && ks * 2 <= maxks) ks *= 2;
   return pow2_floor(ks);
 }
 // 3x3 stride-2 grad-x on the zero-inserted dY (NDP_CONV_DGRAD2=1): exact (tests/

@@ -28,6 +28,10 @@ _ENABLED = os.environ.get("NDP_FUSED_CE", "1") != "0"  # =0: PyTorch-ROCm's loss
 
 
 def _counter(device: torch.device) -> torch.Tensor:
+    """The kernel's last-workgroup counter, re-armed to 0 by every launch.  One per device:
+    per-stream counters would be created inside a graph capture (the warm-up runs on another
+    stream) and cost a memset node per replay; the framework never runs two losses of one
+    device concurrently."""
     idx = device.index if device.index is not None else torch.cuda.current_device()
     c = _CTR.get(idx)
     if c is None:  # first use is eager (warm-up), never inside a capture
