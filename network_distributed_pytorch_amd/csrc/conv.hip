@@ -871,6 +871,16 @@ static int pow2_floor(int v) {
 // grid has >= kFillWgs workgroups.  Workgroups per slice = (Kout / 32) * ceil(Cin / CB).
 int conv_wgrad_imgs(int cls, const ConvGeom& g, int B) {
   int def = cls == 0 ? (conv_variant() == 1 ? 2 : 4) : cls == 1 ? 16 : cls == 2 ? 8 : cls == 4 ? 8 : 2;
+  static int mul = -1;  // NDP_WGRAD_IMGS_MUL (A/B only): larger slices = fewer slabs to sum
+  if (mul < 0) {
+    const char* e = getenv("NDP_WGRAD_IMGS_MUL");
+    mul = e ? atoi(e) : 1;
+    if (mul < 1) mul = 1;
+  }
+  for (int m = mul; m > 1 && def * 2 <= B && B % (def * 2) == 0 &&
+                  (B / (def * 2)) * (g.Co / 32) * ((g.C + 31) / 32) >= kFillWgs;
+       m /= 2)
+    def *= 2;
   const int cb = cls == 3 ? 3 : 32;
   const int per_slice = (g.Co / 32) * ((g.C + cb - 1) / cb);
   while (def > 1 && (B / def) * per_slice < kFillWgs && B % (def / 2) == 0) def /= 2;
