@@ -638,6 +638,22 @@ void colsum(torch::Tensor g, torch::Tensor out) {
   check_launch("launch_colsum");
 }
 
+// DistilBERT FFN: dh = g * gelu'(h) and db = column sums of dh in one pass
+void gelu_bwd_colsum(torch::Tensor g, torch::Tensor h, torch::Tensor dh, torch::Tensor db) {
+  check_f32(g, "g"); check_f32(h, "h"); check_f32(dh, "dh"); check_f32(db, "db");
+  TORCH_CHECK(g.dim() == 2 && g.size(1) % 4 == 0 && h.sizes() == g.sizes() && dh.sizes() == g.sizes() &&
+                  db.numel() == g.size(1),
+              "gelu_bwd_colsum: g / h / dh [M, N] with N % 4 == 0, db [N]");
+  for (auto* t : {&g, &h, &dh})
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0, "gelu_bwd_colsum: 16-B aligned tensors");
+  const int64_t M = g.size(0);
+  const int N = (int)g.size(1);
+  auto part = torch::empty({(int64_t)ndp::colsum_chunks(M, N) * N}, g.options());
+  ndp::launch_gelu_bwd_colsum(g.data_ptr<float>(), h.data_ptr<float>(), dh.data_ptr<float>(), M, N,
+                              part.data_ptr<float>(), db.data_ptr<float>(), cur_stream());
+  check_launch("launch_gelu_bwd_colsum");
+}
+
 // fused cross-entropy forward: loss (0-d), dl [B, K] saved gradient; scratch = rowloss [B] + inv [1]
 void ce_fwd(torch::Tensor x, torch::Tensor tgt, torch::Tensor dl, torch::Tensor scratch, torch::Tensor loss,
             torch::Tensor ctr, int64_t ignore_index) {
@@ -854,6 +870,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("part"), py::arg("dw"), py::arg("geom"));
   m.def("embedding_backward", &embedding_backward);
   m.def("colsum", &colsum);
+  m.def("gelu_bwd_colsum", &gelu_bwd_colsum);
   m.def("ce_fwd", &ce_fwd);
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd);

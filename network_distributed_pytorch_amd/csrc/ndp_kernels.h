@@ -136,6 +136,9 @@ namespace ndp {
 // (linear.hip); part: colsum_chunks(M, N) * N floats of scratch
 int colsum_chunks(int64_t M, int N);
 void launch_colsum(const float* g, int64_t M, int N, float* part, float* out, hipStream_t s);
+// dh = g * gelu'(h) (exact GELU) and out = column sums of dh, one pass over g / h (+ slab sum)
+void launch_gelu_bwd_colsum(const float* g, const float* h, float* dh, int64_t M, int N, float* part, float* out,
+                            hipStream_t s);
 void launch_embedding_backward(const int64_t* ids, int T, const float* gout, int V, int D, int pad, int* perm,
                                int* row_start, int* row_cnt, float* gw, hipStream_t s);
 }  // namespace ndp

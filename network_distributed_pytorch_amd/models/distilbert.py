@@ -28,7 +28,7 @@ from ..ops.attention import attention, attention_qkv, fused_ok
 from ..ops.embedding import Embedding
 from ..ops.gradlink import GradLink
 from ..ops.layernorm import AddLayerNorm
-from ..ops.linear import Linear, linear
+from ..ops.linear import Linear, linear, linear_gelu
 from ..ops.loss import cross_entropy as native_ce
 
 __all__ = ["DistilBertConfig", "DistilBertForSequenceClassification", "distilbert_base"]
@@ -129,7 +129,8 @@ class FFN(nn.Module):
         self.dropout = nn.Dropout(c.dropout)
 
     def forward(self, x, link=None):
-        return self.dropout(self.lin2(F.gelu(self.lin1(x, link=link))))
+        # lin1 + exact GELU share one fused native backward pass (ops/linear.linear_gelu)
+        return self.dropout(self.lin2(linear_gelu(x, self.lin1.weight, self.lin1.bias, link)))
 
 
 class TransformerBlock(nn.Module):

@@ -8,6 +8,8 @@ and cost ~18 µs per call.  Same parameters / ``state_dict`` as ``nn.Linear``.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -15,7 +17,9 @@ import torch.nn.functional as F
 from ._ext import ext
 from .gradlink import InjectGrad
 
-__all__ = ["Linear", "linear"]
+__all__ = ["Linear", "linear", "linear_gelu"]
+
+_FUSED_GELU = os.environ.get("NDP_FUSED_GELU", "0") != "0"  # =1: fused native backward (A/B; validating)
 
 
 class _LinearFn(torch.autograd.Function):
@@ -47,6 +51,47 @@ class _LinearFn(torch.autograd.Function):
             db = torch.empty(n, device=g.device, dtype=g.dtype)
             ext().colsum(g2, db)
         return dx, dw, db, None
+
+
+class _LinearGeluFn(torch.autograd.Function):
+    """``gelu(linear(x))`` (exact GELU): forward = the library GEMM with bias epilogue + ATen's
+    GELU; backward = ONE native pass computing ``dh = da * gelu'(h)`` and the bias column sums
+    (csrc/linear.hip), then the grad-x (optionally onto a GradLink addend) and grad-W GEMMs."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, link=None):
+        h = F.linear(x, weight, bias)
+        ctx.save_for_backward(x, weight, h)
+        ctx.link = link
+        return F.gelu(h)
+
+    @staticmethod
+    def backward(ctx, da):
+        x, weight, h = ctx.saved_tensors
+        n, k = weight.shape
+        g2 = da.reshape(-1, n)
+        if not g2.is_contiguous():
+            g2 = g2.contiguous()
+        h2 = h.reshape(-1, n)
+        dh = torch.empty_like(h2)
+        db = torch.empty(n, device=da.device, dtype=da.dtype)
+        ext().gelu_bwd_colsum(g2, h2, dh, db)
+        addend = ctx.link.take() if ctx.link is not None else None
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = (addend.reshape(-1, k).addmm_(dh, weight) if addend is not None else dh @ weight).view(x.shape)
+        elif addend is not None:
+            dx = addend.view(x.shape)
+        if ctx.needs_input_grad[1]:
+            dw = dh.t() @ x.reshape(-1, k)
+        return dx, dw, (db if ctx.needs_input_grad[2] else None), None
+
+
+def linear_gelu(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, link=None) -> torch.Tensor:
+    """``F.gelu(F.linear(x, weight, bias))`` with the fused native backward where it applies."""
+    if _native_ok(x, weight, bias) and _FUSED_GELU:
+        return _LinearGeluFn.apply(x, weight, bias, link)
+    return F.gelu(linear(x, weight, bias, link))
 
 
 def _native_ok(x, weight, bias) -> bool:

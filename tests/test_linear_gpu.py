@@ -53,3 +53,26 @@ def test_linear_bias_grad_graph_replay(device):
         torch.cuda.synchronize()
         ref = gs[i % 3].double().sum(0)
         assert (lin.bias.grad.double() - ref).abs().max().item() < 1e-3, i
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(8192, 768, 3072), (100, 64, 256), (3, 8, 12)])
+def test_linear_gelu_fused_backward_vs_fp64(device, shape):
+    """gelu(linear(x)): one native pass for dh = da * gelu'(h) and the bias column sums."""
+    from network_distributed_pytorch_amd.ops.linear import linear_gelu
+
+    M, K, N = shape
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device=device, requires_grad=True)
+    w = (torch.randn(N, K, device=device) / K ** 0.5).requires_grad_(True)
+    b = torch.randn(N, device=device, requires_grad=True)
+    y = linear_gelu(x, w, b)
+    x64, w64, b64 = (t.detach().double().requires_grad_(True) for t in (x, w, b))
+    y64 = torch.nn.functional.gelu(torch.nn.functional.linear(x64, w64, b64))
+    torch.testing.assert_close(y.double(), y64, rtol=1e-4, atol=1e-4)
+    g = torch.randn_like(y)
+    y.backward(g)
+    y64.backward(g.double())
+    for got, ref, name in ((x.grad, x64.grad, "dx"), (w.grad, w64.grad, "dw"), (b.grad, b64.grad, "db")):
+        scale = ref.abs().max().item()
+        torch.testing.assert_close(got.double(), ref, rtol=1e-3, atol=2e-5 * scale * M ** 0.5, msg=name)
