@@ -871,7 +871,9 @@ static int pow2_floor(int v) {
 // grid has >= kFillWgs workgroups.  Workgroups per slice = (Kout / 32) * ceil(Cin / CB).
 int conv_wgrad_imgs(int cls, const ConvGeom& g, int B) {
   int def = cls == 0 ? (conv_variant() == 1 ? 2 : 4) : cls == 1 ? 16 : cls == 2 ? 8 : cls == 4 ? 8 : 2;
-  static int mul = -1;  // NDP_WGRAD_IMGS_MUL (A/B only): larger slices = fewer slabs to sum
+  // NDP_WGRAD_IMGS_MUL (A/B only): larger slices = fewer slabs to sum; measured slower (batch
+  // 512: x2 1.9937, x4 1.9969 vs 1.9904 / 1.9927 ms; batch 256: 1.4473 / 1.4444 vs 1.441)
+  static int mul = -1;
   if (mul < 0) {
     const char* e = getenv("NDP_WGRAD_IMGS_MUL");
     mul = e ? atoi(e) : 1;
@@ -895,10 +897,13 @@ int conv_ksplit(int cls, const ConvGeom& g, int B, bool dgrad) {
   const int imgs = (dgrad && cls == 2) ? 1 : conv_fwd_imgs(cls);  // class-2 grad-x: 8x8 tiles, 1 image
   const int base = (B / imgs) * (outC / 64);
   const int nchunks = inC / 8;
-  static int maxks = -1;  // NDP_CONV_MAXKS (A/B only): cap the split, e.g. 4 keeps BN-fusable slabs
+  // split cap (NDP_CONV_MAXKS to A/B): 4 keeps layer2's slabs summable inside the fused BN
+  // kernel (batchnorm.hip kMaxFusedSlabs) — ResNet-18 step on 1x MI355X, batch 128 1.216 / 1.197 ->
+  // 1.191 / 1.188 ms, batch 64 1.050 / 1.050 -> 1.049 / 1.046 (uncapped: 8 slabs at batch 64)
+  static int maxks = -1;
   if (maxks < 0) {
     const char* e = getenv("NDP_CONV_MAXKS");
-    maxks = e ? atoi(e) : 1 << 30;
+    maxks = e ? atoi(e) : 4;
   }
   int ks = 1;
   while (ks * 2 <= nchunks && base * ks < kFillWgs && ks * 2 <= maxks) ks *= 2;

@@ -19,7 +19,10 @@ from .gradlink import InjectGrad
 
 __all__ = ["Linear", "linear", "linear_gelu"]
 
-_FUSED_GELU = os.environ.get("NDP_FUSED_GELU", "0") != "0"  # =1: fused native backward (A/B; validating)
+# =1: the fused native GELU-backward + bias-sum pass.  Exact (tests/test_linear_gpu.py) but
+# measured slower on 1x MI355X, DistilBERT r=8: 21.39 / 21.41 vs 21.27 ms (its column-strip
+# grid has ~250 workgroups; ATen's GELU backward streams with the whole chip) -> off.
+_FUSED_GELU = os.environ.get("NDP_FUSED_GELU", "0") != "0"
 
 
 class _LinearFn(torch.autograd.Function):
