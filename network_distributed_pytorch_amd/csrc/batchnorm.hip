@@ -76,16 +76,27 @@ __device__ __forceinline__ BnSlice slice_of(int N, int S, int s) {
 }
 
 // ---- forward statistics -------------------------------------------------------------
+// src (nullable, VEC only): x is the sum of nslab split-K conv slabs (slab order, bitwise equal
+// to conv_slab_sum); the kernel adds them, writes x and takes its statistics in one pass.
 template <bool VEC>
 __global__ __launch_bounds__(256) void bn_fwd_stats_kernel(const float* __restrict__ x, double* __restrict__ part,
-                                                           int N, int C, int HW, int S) {
+                                                           int N, int C, int HW, int S,
+                                                           const float* __restrict__ src = nullptr, int nslab = 0) {
   __shared__ double red[16];
   const int s = blockIdx.x, c = blockIdx.y;
   const BnSlice sl = slice_of(N, S, s);
   double sum = 0.0, sq = 0.0;
   if (VEC) {
+    const int64_t slab = (int64_t)N * C * HW;
     for_slice<4>(sl.n0, sl.n1, C, c, HW, [&](int64_t o) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(x + o);
+      f32x4 v;
+      if (src != nullptr) {
+        v = *reinterpret_cast<const f32x4*>(src + o);
+        for (int z = 1; z < nslab; ++z) v += *reinterpret_cast<const f32x4*>(src + z * slab + o);
+        *reinterpret_cast<f32x4*>(const_cast<float*>(x) + o) = v;
+      } else {
+        v = *reinterpret_cast<const f32x4*>(x + o);
+      }
       // fp32 pair sums first (exact enough), fp64 across the slice
       const float s4 = (v[0] + v[1]) + (v[2] + v[3]);
       const float q4 = (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]);
@@ -166,21 +177,32 @@ __global__ __launch_bounds__(256) void bn_fwd_apply_kernel(
 }
 
 // ---- backward statistics ----------------------------------------------------------------
+// src (nullable, VEC only): dy is the sum of nslab split-K grad-x slabs; written back to dy
+// for the apply kernel.
 template <bool VEC>
 __global__ __launch_bounds__(256) void bn_bwd_stats_kernel(const float* __restrict__ dy, const float* __restrict__ y,
                                                            const float* __restrict__ x,
                                                            const float* __restrict__ save_mean,
                                                            const float* __restrict__ save_invstd,
                                                            double* __restrict__ part, int N, int C, int HW,
-                                                           int S, int relu) {
+                                                           int S, int relu, const float* __restrict__ src = nullptr,
+                                                           int nslab = 0) {
   __shared__ double red[16];
   const int s = blockIdx.x, c = blockIdx.y;
   const BnSlice sl = slice_of(N, S, s);
   const float mean = save_mean[c], invstd = save_invstd[c];
   double sdz = 0.0, sdzx = 0.0;
   if (VEC) {
+    const int64_t slab = (int64_t)N * C * HW;
     for_slice<4>(sl.n0, sl.n1, C, c, HW, [&](int64_t o) {
-      const f32x4 g = *reinterpret_cast<const f32x4*>(dy + o);
+      f32x4 g;
+      if (src != nullptr) {
+        g = *reinterpret_cast<const f32x4*>(src + o);
+        for (int z = 1; z < nslab; ++z) g += *reinterpret_cast<const f32x4*>(src + z * slab + o);
+        *reinterpret_cast<f32x4*>(const_cast<float*>(dy) + o) = g;
+      } else {
+        g = *reinterpret_cast<const f32x4*>(dy + o);
+      }
       const f32x4 xv = *reinterpret_cast<const f32x4*>(x + o);
       f32x4 yv = {1.f, 1.f, 1.f, 1.f};
       if (relu) yv = *reinterpret_cast<const f32x4*>(y + o);
@@ -709,6 +731,16 @@ int64_t bn_part_numel(int N, int C, int HW) {
 // 1.4688 ms, batch 128 (4) 1.2158 -> 1.2176 (even), batch 64 (8 slabs) 1.0689 -> 1.0746 (the
 // BN's 128 workgroups read 8 slabs slower than the 256-CU sum kernel plus a launch).
 constexpr int kMaxFusedSlabs = 4;
+// Two-kernel path (8x8 maps of layer1): the statistics pass adds the deferred slabs and writes
+// the summed tensor (NDP_BN_STATS_SLABS; default set by the A/B in profiles/README.md).
+static bool bn_stats_slabs() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("NDP_BN_STATS_SLABS");
+    v = e ? atoi(e) : 0;
+  }
+  return v != 0;
+}
 int bn_slices(int N, int C, int HW) {
   // ~4 workgroups per CU over the whole launch, >= ~2K elements per workgroup
   int64_t s = (1024 + C - 1) / C;
@@ -733,8 +765,13 @@ void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamm
                           nullptr, nullptr, y, nullptr, N, C, eps, momentum, relu, s, xpart, nslab);
     return;
   }
-  if (xpart != nullptr)  // no fused consumer for this shape: finish the conv's split-K sum here
+  const bool vec_ok = (HW % 4) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 &&
+                      (res == nullptr || ((uintptr_t)res & 15) == 0) && ((uintptr_t)xpart & 15) == 0;
+  if (xpart != nullptr && !(bn_stats_slabs() && training && vec_ok && !bn_small_path(N, C, HW))) {
+    // no fused consumer for this shape: finish the conv's split-K sum here
     launch_slab_sum(xpart, const_cast<float*>(x), (int64_t)N * C * HW, nslab, s);
+    xpart = nullptr;
+  }
   if (training && bn_small_path(N, C, HW)) {
     const int Ss = bn_small_slices(N, C, HW);
     double* coef = part + (int64_t)C * Ss * 2;
@@ -749,9 +786,9 @@ void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamm
   const bool vec = (HW % 4) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 &&
                    (res == nullptr || ((uintptr_t)res & 15) == 0);
   const dim3 grid(S, C);
-  if (training) {
-    if (vec) hipLaunchKernelGGL(bn_fwd_stats_kernel<true>, grid, dim3(256), 0, s, x, part, N, C, HW, S);
-    else hipLaunchKernelGGL(bn_fwd_stats_kernel<false>, grid, dim3(256), 0, s, x, part, N, C, HW, S);
+  if (training) {  // the statistics pass also adds deferred conv slabs (xpart) and writes x
+    if (vec) hipLaunchKernelGGL(bn_fwd_stats_kernel<true>, grid, dim3(256), 0, s, x, part, N, C, HW, S, xpart, nslab);
+    else hipLaunchKernelGGL(bn_fwd_stats_kernel<false>, grid, dim3(256), 0, s, x, part, N, C, HW, S, nullptr, 0);
   }
   if (vec)
     hipLaunchKernelGGL(bn_fwd_apply_kernel<true>, grid, dim3(256), 0, s, x, res, y, gamma, beta, rmean, rvar, nbt,
@@ -776,8 +813,14 @@ void launch_bn_bwd(const float* dy, const float* y, const float* x, const float*
                           0.f, 0.f, relu, s, dypart, nslab);
     return;
   }
-  if (dypart != nullptr)  // no fused consumer: finish the conv's split-K grad-x sum into dy
+  const bool vec_ok = (HW % 4) == 0 && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)x & 15) == 0 &&
+                      ((uintptr_t)dx & 15) == 0 && (!relu || ((uintptr_t)y & 15) == 0) &&
+                      (dres == nullptr || ((uintptr_t)dres & 15) == 0) && ((uintptr_t)dypart & 15) == 0;
+  if (dypart != nullptr && !(bn_stats_slabs() && vec_ok && !bn_small_path(N, C, HW))) {
+    // no fused consumer: finish the conv's split-K grad-x sum into dy
     launch_slab_sum(dypart, const_cast<float*>(dy), (int64_t)N * C * HW, nslab, s);
+    dypart = nullptr;
+  }
   if (bn_small_path(N, C, HW)) {
     const int Ss = bn_small_slices(N, C, HW);
     double* coef = part + (int64_t)C * Ss * 2;
@@ -794,9 +837,9 @@ void launch_bn_bwd(const float* dy, const float* y, const float* x, const float*
                    ((uintptr_t)dx & 15) == 0 && (!relu || ((uintptr_t)y & 15) == 0) &&
                    (dres == nullptr || ((uintptr_t)dres & 15) == 0);
   const dim3 grid(S, C);
-  if (vec) {
+  if (vec) {  // the statistics pass also adds deferred grad-x slabs (dypart) and writes dy
     hipLaunchKernelGGL(bn_bwd_stats_kernel<true>, grid, dim3(256), 0, s, dy, y, x, save_mean, save_invstd, part, N, C,
-                       HW, S, relu);
+                       HW, S, relu, dypart, nslab);
     hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, grid, dim3(256), 0, s, dy, y, x, gamma, save_mean, save_invstd, dx,
                        dres, dgamma, dbeta, part, N, C, HW, S, relu);
   } else {
