@@ -732,12 +732,13 @@ int64_t bn_part_numel(int N, int C, int HW) {
 // BN's 128 workgroups read 8 slabs slower than the 256-CU sum kernel plus a launch).
 constexpr int kMaxFusedSlabs = 4;
 // Two-kernel path (8x8 maps of layer1): the statistics pass adds the deferred slabs and writes
-// the summed tensor (NDP_BN_STATS_SLABS; default set by the A/B in profiles/README.md).
+// the summed tensor, no separate sum launch (NDP_BN_STATS_SLABS=0 to A/B).  ResNet-18 step on
+// 1x MI355X: batch 128 1.196 / 1.198 -> 1.164 / 1.165 ms, batch 64 1.061 / 1.058 -> 1.046 / 1.053.
 static bool bn_stats_slabs() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("NDP_BN_STATS_SLABS");
-    v = e ? atoi(e) : 0;
+    v = e ? atoi(e) : 1;
   }
   return v != 0;
 }
