@@ -13,11 +13,22 @@ The whole step is ONE hipGraph; the PowerSGD group pipelines (gfx950 kernels + R
 collectives) run on a side stream that overlaps backward.  fp32 everywhere (the
 reference's dtype), random-init weights, synthetic device-resident data.
 
+Launch + failure model (utils/supervisor.py).  The process started by the user or by
+torchrun is a SUPERVISOR that never touches the GPU: it starts the GPU worker(s) as child
+processes (``python bench.py --gpus N`` alone starts all N ranks itself; under torchrun
+each rank's supervisor starts its one worker), each worker running ONE configuration
+level of the fallback ladder below.  A worker fails its attempt by exiting non-zero
+(exception, failed health check) or by stalling past the allowance of its current phase
+(heartbeat file); then every worker of the attempt is killed and all ranks restart at the
+next level on a fresh rendezvous.  Health checks after warm-up and after the timed steps:
+RCCL async errors, the compute/comm graph flag-wait error word, finite loss, and a
+cross-rank fp64 checksum of the parameters (``replicas_equal``).  A number is printed
+only for a verified step; if every level fails the exit code is non-zero.
+
 Scaling: **strong** by default for the CIFAR workloads, exactly like the reference — the
 global batch is fixed at 512 (PowerSGD, ddp_powersgd_guide_cifar10/ddp_init.py:52) and
 each of the N ranks trains on 512/N.  DistilBERT is weak in the reference (16 per rank,
-ddp_powersgd_distillBERT_IMDb/ddp_init.py:92).  For N > 1 strong runs the bench also
-times the weak configuration (512 per GPU) and reports it under ``weak_scaling``.
+ddp_powersgd_distillBERT_IMDb/ddp_init.py:92).
 
 Rank 0 prints ONE JSON line.  ``value`` = whole-job samples/s (max step time over ranks).
 ``bytes_per_step`` = bytes all-reduced per rank per step with the reference's accounting.
@@ -30,9 +41,6 @@ import os
 import sys
 import time
 
-import torch
-import torch.distributed as dist
-
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 METRIC = "samples/sec + bytes/step all-reduced, ResNet18 CIFAR10 PowerSGD r=4, 1/2/4/8 GPU"
@@ -40,7 +48,7 @@ METRIC = "samples/sec + bytes/step all-reduced, ResNet18 CIFAR10 PowerSGD r=4, 1
 
 def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="ranks (default: WORLD_SIZE from a launcher, else 1)")
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--model", default="resnet18", help="resnet18/34/50/101/152 | distilbert")
@@ -51,8 +59,8 @@ def parse(argv=None):
     ap.add_argument("--global-batch", type=int, default=512, help="strong scaling: global batch (reference 512)")
     ap.add_argument("--batch", type=int, default=None,
                     help="per-GPU batch; implies weak scaling. Default 512 ResNet, 16 DistilBERT (reference)")
-    ap.add_argument("--weak-too", choices=["auto", "on", "off"], default="auto",
-                    help="N>1 strong runs: also time the weak config (per-GPU 512) as an extra field")
+    ap.add_argument("--weak-too", choices=["on", "off"], default="off",
+                    help="strong runs: also time the weak config (per-GPU 512) as an extra field")
     ap.add_argument("--seq-len", type=int, default=512)
     ap.add_argument("--reducer", choices=["powersgd", "dense", "dense-ref", "powersgd-ref", "powersgd-api"],
                     default="powersgd")
@@ -77,6 +85,9 @@ def parse(argv=None):
                          "link is emulated)")
     ap.add_argument("--no-overlap", action="store_true", help="= --overlap off")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--no-supervise", action="store_true",
+                    help="run the step in this process (no supervisor / fallback; for profilers)")
+    ap.add_argument("--level", type=int, default=0, help="first fallback level to try (see FALLBACKS_*)")
     ap.add_argument("--graph-mode", default="auto", choices=["auto", "full", "piecewise", "none"],
                     help="hipGraph capture of the step: full (native RCCL / N=1), piecewise (collectives "
                          "eager between captured compute; c10d data plane), none")
@@ -109,6 +120,8 @@ class Workload:
     """Model + gradient sync + a timed-step factory for one per-GPU batch size."""
 
     def __init__(self, args, device, world, rank):
+        import torch
+
         from network_distributed_pytorch_amd.models import build_model
         from network_distributed_pytorch_amd.parallel.comm import LINK_PRESETS, Communicator
         from network_distributed_pytorch_amd.parallel.trainer import build_grad_sync
@@ -140,8 +153,11 @@ class Workload:
         self.crit = torch.nn.CrossEntropyLoss() if args.stock else CrossEntropyLoss()
         self.loss_acc = torch.zeros((), device=device)
         self.graph_mode = None
+        self.runner = None
 
     def make_step(self, batch: int):
+        import torch
+
         args, device, model = self.args, self.device, self.model
         g = torch.Generator(device=device)
         g.manual_seed(1234 + self.rank)
@@ -192,6 +208,7 @@ class Workload:
             runner = StepRunner(pre, sync, mode=graph_mode, warmup=3,
                                 state_tensors=list(model.buffers()))
             graph_mode = runner.mode
+            self.runner = runner
 
             def step(i):
                 for k, v in pool[i % n_pool].items():
@@ -208,6 +225,9 @@ class Workload:
         return step
 
     def time(self, step, steps: int, warmup: int, start: int = 0) -> float:
+        import torch
+        import torch.distributed as dist
+
         for i in range(start, start + warmup):
             step(i)
         if self.world > 1:
@@ -228,61 +248,75 @@ class Workload:
         return elapsed
 
 
-# N > 1: if building / capturing / warming the step raises on any rank, every rank moves to
-# the next, simpler configuration together (agreed by a c10d all-reduce MIN of a success flag):
-# the default (native RCCL communicator, step captured with the comm graph overlapping
-# backward) -> collectives captured serially in the step graph -> c10d data plane with the
-# collectives eager between captured phases -> eager.  The JSON line records any fallback.
-# Covers failures every rank hits (capture / build errors are shape- and code-determined, so
-# SPMD ranks fail alike); a rank failing alone while its peers sit in a collective still hangs.
-_FALLBACKS = [{}, {"overlap": "off"}, {"native_comm": False, "graph_mode": "auto"},
-              {"native_comm": False, "graph_mode": "none"}]
+
+# Fallback ladder (one level per supervised attempt).  N > 1: native RCCL communicator with
+# the step captured as compute + comm graphs overlapping backward -> collectives captured
+# serially in the step graph -> c10d data plane with eager collectives between captured
+# phases -> eager.  N = 1: captured (as configured) -> no overlap -> eager.
+FALLBACKS_MULTI = [{}, {"overlap": "off"}, {"native_comm": False, "graph_mode": "auto"},
+                   {"native_comm": False, "graph_mode": "none"}]
+FALLBACKS_SINGLE = [{}, {"overlap": "off"}, {"overlap": "off", "graph_mode": "none"}]
 
 
-def build_with_fallback(args, device, world, rank, per_gpu):
-    attempts = _FALLBACKS if world > 1 else _FALLBACKS[:1]
-    errors = []
-    for i, over in enumerate(attempts):
-        a = argparse.Namespace(**{**vars(args), **over})
-        if "overlap" in over:
-            a.overlap = over["overlap"]
-        ok, wl, step = 1, None, None
-        try:
-            if os.environ.get("NDP_BENCH_FAIL") in (f"{i}:{rank}", f"{i}:*"):  # test hook: inject a failure
-                raise RuntimeError(f"injected failure, attempt {i} rank {rank}")
-            torch.manual_seed(714)
-            wl = Workload(a, device, world, rank)
-            step = wl.make_step(per_gpu)
-            for j in range(args.warmup):
-                step(j)
-            torch.cuda.synchronize()
-        except Exception as e:  # noqa: BLE001 - any failure moves every rank to the next config
-            ok = 0
-            errors.append(f"{over or 'default'}: {repr(e)[:300]}")
-            print(f"[bench] rank {rank}: attempt {i} failed: {errors[-1]}", file=sys.stderr, flush=True)
-        if world > 1:
-            flag = torch.tensor([ok], dtype=torch.int32, device=device)
-            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-            ok = int(flag.item())
-        if ok:
-            return wl, step, ({"attempt": i, "config": over, "errors": errors} if i else None)
-        if wl is not None:
-            try:
-                wl.comm.close()
-            except Exception:  # noqa: BLE001
-                pass
-        del wl, step
-        torch.cuda.synchronize()
-    raise RuntimeError("every bench configuration failed: " + " | ".join(errors))
+def fallbacks(world: int):
+    return FALLBACKS_MULTI if world > 1 else FALLBACKS_SINGLE
 
 
-def main(argv=None):
-    args = parse(argv)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+class HealthError(RuntimeError):
+    pass
+
+
+def health_check(wl, world: int, where: str) -> dict:
+    """Fail loudly unless the step just run is trustworthy on every rank (see module doc)."""
+    import math
+
+    import torch
+    import torch.distributed as dist
+
+    from network_distributed_pytorch_amd.ops import checksum
+
+    if wl.runner is not None:
+        wl.runner.join()
+    torch.cuda.synchronize()
+    flag_errors = wl.comm.flag_error()
+    wl.comm.check()  # RCCL async error / flag-wait timeout -> raises
+    if hasattr(wl.sync, "check_errors"):
+        wl.sync.check_errors()  # MGS barrier timeouts
+    flat = getattr(getattr(wl.sync, "opt", None), "x", None)
+    if flat is None:
+        flat = getattr(getattr(wl.sync, "ddp", None), "x", None)
+    if flat is None:
+        flat = torch.cat([p.detach().reshape(-1) for p in wl.model.parameters()])
+    local = checksum(flat)
+    sums = [local]
+    if world > 1:
+        t = torch.tensor([local], dtype=torch.float64, device=wl.device)
+        outs = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(outs, t)
+        sums = [float(o.item()) for o in outs]
+    equal = all(s == sums[0] for s in sums) and math.isfinite(sums[0])
+    loss = float(wl.loss_acc.item())
+    if not equal:
+        raise HealthError(f"{where}: replicas differ (parameter checksums {sums})")
+    if not math.isfinite(loss):
+        raise HealthError(f"{where}: non-finite loss accumulator {loss}")
+    return {"replicas_equal": equal, "flag_errors": flag_errors, "checksum": sums[0]}
+
+
+def worker(args, level: int, world: int, rank: int, local: int) -> None:
+    """One configuration level on this rank (a supervised child, or in-process unsupervised)."""
+    from network_distributed_pytorch_amd.utils.supervisor import Heartbeat
+
+    hb = Heartbeat(rank)
+    hb.beat("import", 900)
+    import torch
+    import torch.distributed as dist
+
+    over = fallbacks(world)[level]
+    a = argparse.Namespace(**{**vars(args), **over})
     # one process per GPU; NDP_BACKEND=gloo lets several ranks share one GPU (testing only)
     backend = os.environ.get("NDP_BACKEND", "nccl")
+    hb.beat("init", 600)
     dev_index = local % max(1, torch.cuda.device_count())
     device = torch.device("cuda", dev_index)
     torch.cuda.set_device(device)
@@ -295,93 +329,158 @@ def main(argv=None):
             dist.init_process_group(backend)
     torch.manual_seed(714)
     torch.backends.cudnn.benchmark = True
+    if os.environ.get("NDP_BENCH_FAIL") in (f"{level}:{rank}", f"{level}:*"):  # test hook
+        raise RuntimeError(f"injected failure, level {level} rank {rank}")
 
     if args.scaling == "strong":
         assert args.global_batch % world == 0, "global batch must divide by the world size"
         per_gpu = args.global_batch // world   # reference: bsz = int(512 / float(size))
     else:
         per_gpu = args.batch
-    wl, step, fallback = build_with_fallback(args, device, world, rank, per_gpu)
-    elapsed = wl.time(step, args.steps, 0, start=args.warmup)  # warmed up inside the attempt
-    graph_mode = wl.graph_mode
+    hb.beat("build+capture", 600)
+    wl = Workload(a, device, world, rank)
+    step = wl.make_step(per_gpu)
+    for j in range(args.warmup):
+        step(j)
+        torch.cuda.synchronize()
+        hb.beat(f"warmup {j + 1}/{args.warmup}", 300)
+    hb.beat("check:warmup", 300)
+    health_check(wl, world, "after warm-up")
+    hb.beat("timed", 300 + 30 * args.steps)
+    elapsed = wl.time(step, args.steps, 0, start=args.warmup)  # warmed up above
+    hb.beat("check:timed", 300)
+    health = health_check(wl, world, "after the timed steps")
     comm_stats = wl.comm.stats.as_dict()
     final_loss = float(wl.loss_acc.item()) / max(1, args.warmup + args.steps)
 
     weak = None
-    want_weak = args.weak_too == "on" or (args.weak_too == "auto" and world > 1)
-    if args.scaling == "strong" and want_weak and not wl.is_bert:
-        try:
-            wb = args.global_batch  # per-GPU batch of the N=1 config, fixed as N grows
-            wstep = wl.make_step(wb)
-            we = wl.time(wstep, args.steps, args.warmup)
-            weak = {"value": round(wb * world * args.steps / we, 2), "unit": "samples/s",
-                    "ms_per_step": round(1e3 * we / args.steps, 4), "per_gpu_batch": wb,
-                    "global_batch": wb * world}
-        except Exception as e:  # the extra arm must never cost the headline line
-            weak = {"error": repr(e)[:200]}
+    if args.weak_too == "on" and args.scaling == "strong" and not wl.is_bert:
+        hb.beat("weak arm", 600 + 30 * args.steps)
+        wb = args.global_batch  # per-GPU batch of the N=1 config, fixed as N grows
+        wstep = wl.make_step(wb)
+        we = wl.time(wstep, args.steps, args.warmup)
+        health_check(wl, world, "after the weak-scaling arm")
+        weak = {"value": round(wb * world * args.steps / we, 2), "unit": "samples/s",
+                "ms_per_step": round(1e3 * we / args.steps, 4), "per_gpu_batch": wb, "global_batch": wb * world}
 
     if rank == 0:
-        global_batch = per_gpu * world
-        sps = global_batch * args.steps / elapsed
-        is_bert = wl.is_bert
-        rec = {
-            "metric": metric_name(args),
-            "value": round(sps, 2),
-            "unit": "samples/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(1e3 * elapsed / args.steps, 4),
-            "higher_is_better": True,
-            "scaling": args.scaling,
-            "vs_baseline": None,
-            "dtype": "fp32" if args.amp == "none" else "bf16-autocast (fp32 params/grads/reducer)",
-            "data": ("synthetic IMDb-shape (512-token ids + masks, 2 labels)" if is_bert else
-                     "synthetic CIFAR-10-shape (3x32x32, 10 labels)") + ", random-init weights",
-            "bytes_per_step": wl.sync.bytes_per_step,
-            "dense_bytes_per_step": 4 * sum(p.numel() for p in wl.model.parameters()),
-            "collectives_per_step": wl.sync.collectives_per_step,
-            "comm_backend": wl.comm.backend,
-            "config": {
-                "model": args.model,
-                "num_classes": args.num_classes if args.num_classes is not None else (2 if is_bert else 1000),
-                "global_batch": global_batch,
-                "per_gpu_batch": per_gpu,
-                "seq_len": args.seq_len if is_bert else None,
-                "image": None if is_bert else [3, 32, 32],
-                "parallelism": f"dp{world}",
-                "reducer": args.reducer,
-                "powersgd_rank": args.rank if "powersgd" in args.reducer else None,
-                "overlap": getattr(getattr(wl.sync, "opt", getattr(wl.sync, "ddp", None)), "overlap", None),
-                "link_emulation": args.link,
-                "emulate_world": args.emulate_world,
-                "channels_last": args.channels_last,
-                "stock_model_ops": bool(args.no_fused_bn and args.no_gemm_convs),
-                "hip_graph": graph_mode,
-                "tuned_gemms": wl.tuned_gemms,
-                "fused_attention": (not args.no_fused_attn) if is_bert else None,
-            },
-            "comm_stats_timed": comm_stats,
-            "collective_payloads": wl.sync.collective_payloads() if hasattr(wl.sync, "collective_payloads") else None,
-            "link_model_s_per_step": (sum(wl.comm.link.seconds(b, wl.comm.paced_world)
-                                          for b in wl.sync.collective_payloads())
-                                      if wl.comm.link is not None and hasattr(wl.sync, "collective_payloads")
-                                      else None),
-            "mean_loss": round(final_loss, 5),
-        }
-        if weak is not None:
-            rec["weak_scaling"] = weak
-        if fallback:
-            rec["fallback"] = fallback
-        line = json.dumps(rec)
-        print(line, flush=True)
+        line = json.dumps(record(args, a, wl, world, per_gpu, elapsed, comm_stats, final_loss, health, level,
+                                 weak))
+        hb.result(line)
+        if not hb.enabled:
+            print(line, flush=True)
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
+    hb.done()
+    hb.beat("teardown", 120)
     wl.comm.close()
     if dist.is_initialized():
         dist.destroy_process_group()
 
 
+def record(args, a, wl, world, per_gpu, elapsed, comm_stats, final_loss, health, level, weak) -> dict:
+    global_batch = per_gpu * world
+    sps = global_batch * args.steps / elapsed
+    is_bert = wl.is_bert
+    native = wl.comm.native
+    rec = {
+        "metric": metric_name(args),
+        "value": round(sps, 2),
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": args.scaling,
+        "vs_baseline": None,
+        "dtype": "fp32" if args.amp == "none" else "bf16-autocast (fp32 params/grads/reducer)",
+        "data": ("synthetic IMDb-shape (512-token ids + masks, 2 labels)" if is_bert else
+                 "synthetic CIFAR-10-shape (3x32x32, 10 labels)") + ", random-init weights",
+        "bytes_per_step": wl.sync.bytes_per_step,
+        "dense_bytes_per_step": 4 * sum(p.numel() for p in wl.model.parameters()),
+        "collectives_per_step": wl.sync.collectives_per_step,
+        "comm_backend": wl.comm.backend,
+        "rccl_nranks": native.nranks if native is not None else None,
+        "replicas_equal": health["replicas_equal"],
+        "flag_errors": health["flag_errors"],
+        "param_checksum": health["checksum"],
+        "fallback": ({"level": level, "config": fallbacks(world)[level]} if level else None),
+        "config": {
+            "model": args.model,
+            "num_classes": args.num_classes if args.num_classes is not None else (2 if is_bert else 1000),
+            "global_batch": global_batch,
+            "per_gpu_batch": per_gpu,
+            "seq_len": args.seq_len if is_bert else None,
+            "image": None if is_bert else [3, 32, 32],
+            "parallelism": f"dp{world}",
+            "reducer": args.reducer,
+            "powersgd_rank": args.rank if "powersgd" in args.reducer else None,
+            "overlap": getattr(getattr(wl.sync, "opt", getattr(wl.sync, "ddp", None)), "overlap", None),
+            "link_emulation": args.link,
+            "emulate_world": args.emulate_world,
+            "channels_last": args.channels_last,
+            "stock_model_ops": bool(a.no_fused_bn and a.no_gemm_convs),
+            "hip_graph": wl.graph_mode,
+            "tuned_gemms": wl.tuned_gemms,
+            "fused_attention": (not args.no_fused_attn) if is_bert else None,
+        },
+        "comm_stats_timed": comm_stats,
+        "collective_payloads": wl.sync.collective_payloads() if hasattr(wl.sync, "collective_payloads") else None,
+        "link_model_s_per_step": (sum(wl.comm.link.seconds(b, wl.comm.paced_world)
+                                      for b in wl.sync.collective_payloads())
+                                  if wl.comm.link is not None and hasattr(wl.sync, "collective_payloads")
+                                  else None),
+        "mean_loss": round(final_loss, 5),
+    }
+    if weak is not None:
+        rec["weak_scaling"] = weak
+    return rec
+
+
+def resolve_world(args) -> int:
+    env = os.environ.get("WORLD_SIZE")
+    if env is not None:
+        if args.gpus is not None and int(env) != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env} (launcher and flag disagree)")
+        return int(env)
+    return args.gpus if args.gpus is not None else 1
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse(argv)
+    from network_distributed_pytorch_amd.utils.supervisor import run_supervised, worker_env_info
+
+    role, level, _ = worker_env_info()
+    world = resolve_world(args)
+    if role == "worker":
+        rank, local = int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+        try:
+            worker(args, level, world, rank, local)
+        except BaseException as e:  # noqa: BLE001 - report, then fail the attempt
+            import traceback
+
+            from network_distributed_pytorch_amd.utils.supervisor import Heartbeat
+
+            tb = traceback.format_exc()
+            print(tb, file=sys.stderr, flush=True)
+            Heartbeat(rank).error(f"{type(e).__name__}: {str(e)[:1500]}")
+            os._exit(1)  # no teardown: a peer may be stuck in a collective with us
+        return 0
+    if args.no_supervise:  # in-process, one level, no fallback (debugging / profilers)
+        if os.environ.get("WORLD_SIZE") is None and world > 1:
+            raise SystemExit("--no-supervise with --gpus N > 1 needs a launcher (torchrun)")
+        worker(args, args.level, world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")))
+        return 0
+    cmd = [sys.executable, "-u", os.path.abspath(__file__)] + argv
+    levels = fallbacks(world)
+    start = max(0, min(args.level, len(levels) - 1))
+    code = run_supervised(cmd, world, len(levels), describe=lambda i: str(levels[i]),
+                          first_level=start)
+    return code
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -131,8 +131,12 @@ __global__ void delay_kernel(int64_t ticks) {
 // comm graph's first kernel of each piece spins on it (agent-scope acquire, s_sleep), so
 // the comm queue reacts within microseconds.  Each wait consumes exactly one bump
 // (`seen` is private to the waiting queue), so the same captured graphs replay forever.
-// A wall-clock-bounded spin (s_memrealtime, 100 MHz) reports through `err` instead of
-// hanging (e.g. if both streams ever shared one hardware queue, or a wait has no signaller).
+// A wall-clock-bounded spin (s_memrealtime, 100 MHz) never hangs the GPU: on timeout it sets
+// the error word and proceeds.  The error is STICKY — once set, every later wait proceeds at
+// once (a broken ordering costs one timeout, not one per wait) — and it is fatal on the
+// host: Communicator.check() raises, the bench's health checks fail the attempt and the
+// supervisor falls back (bench.py), the engine checks it at its logging cadence.  Results
+// of a step run after a timed-out wait are never reported.
 __global__ void flag_signal_kernel(unsigned* ctr) {
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -145,6 +149,7 @@ __global__ void flag_wait_kernel(unsigned* ctr, unsigned* seen, unsigned* err, u
     const unsigned want = __hip_atomic_load(seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while ((int)(__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
+      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;  // sticky
       __builtin_amdgcn_s_sleep(2);
       if (__builtin_amdgcn_s_memrealtime() - t0 > max_ticks) {
         __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

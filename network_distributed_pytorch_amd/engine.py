@@ -53,7 +53,7 @@ def default_config(**over) -> Dict[str, Any]:
         dataset_size=None, data_seed=0, max_steps_per_epoch=None, graph_mode="auto", link="none",
         emulate_world=None, bucket_mb=None, reuse_query=True, overlap=None, psgd_groups=None,
         checkpoint_dir=None, resume=None, log_file=None, log_every=1, check_replicas_every=0,
-        write_grad=False, verbose=True, trace_phases=False,
+        check_health_every=50, write_grad=False, verbose=True, trace_phases=False,
     )
     cfg.update(over)
     return cfg
@@ -237,11 +237,13 @@ def run_task(config) -> Dict[str, Any]:
         graph_mode = runner.mode
         if graph_mode == "none":
             runner = None
-    # a captured step needs a fixed batch shape: drop the ragged last batch in graph mode
-    loader = DeviceLoader(part, bsz, shuffle=True, seed=config["seed"] + rank, device=device,
-                          drop_last=runner is not None)
+    # every batch is trained, the ragged last one too (the reference's DataLoader keeps it,
+    # ddp_powersgd_guide_cifar10/ddp_init.py:53,142): in graph mode a batch whose shape
+    # differs from the captured one runs as an eager step (see _eager_step)
+    loader = DeviceLoader(part, bsz, shuffle=True, seed=config["seed"] + rank, device=device, drop_last=False)
     loader.set_epoch(start_epoch)
-    num_batches = math.ceil(len(part) / float(bsz))
+    num_batches = math.ceil(len(part) / float(bsz))  # reference: ceil(len(partition) / bsz)
+    health_every = int(config.get("check_health_every") or 0)
 
     timer = PhaseTimer() if (config.get("trace_phases") and runner is None) else None
     losses = []
@@ -255,7 +257,15 @@ def run_task(config) -> Dict[str, Any]:
         for batch in loader:
             if config.get("max_steps_per_epoch") and i >= config["max_steps_per_epoch"]:
                 break
-            if runner is not None:
+            if runner is not None and "batch" in static and not _same_shape(static["batch"], batch):
+                runner.join()  # ragged batch: eager step, ordered after the last replay
+                sync.zero_grad()
+                loss = loss_fn(batch)
+                epoch_loss += loss.detach()
+                loss.backward()
+                sync.step()
+                loss_static.copy_(loss.detach())
+            elif runner is not None:
                 if "batch" not in static:
                     static["batch"] = _clone_batch(batch)
                 else:
@@ -289,6 +299,10 @@ def run_task(config) -> Dict[str, Any]:
                 if runner is not None and step % checker.every == 0:
                     runner.join()
                 checker.check(step)
+            if health_every and step % health_every == 0 and hasattr(sync, "check_errors"):
+                if runner is not None:
+                    runner.join()
+                sync.check_errors()  # flag-wait timeouts / MGS barrier / RCCL async errors: fatal
             if log_every and step % log_every == 0:  # per-step record (host sync at this cadence)
                 loss_now = float((loss_static if runner is not None else loss.detach()).item())
                 now = time.perf_counter()
@@ -306,7 +320,9 @@ def run_task(config) -> Dict[str, Any]:
                 last_log = (now, comm.stats.payload_bytes, comm.stats.wire_bytes, step)
         if runner is not None:
             runner.join()  # parameters / sync state are read below (checks, checkpoint)
-        mean = float(epoch_loss.item()) / max(1, i)
+        # reference: epoch_loss / num_batches (ddp_powersgd_guide_cifar10/ddp_init.py:118,183);
+        # a step cap (max_steps_per_epoch, an addition) divides by the steps actually run
+        mean = float(epoch_loss.item()) / max(1, num_batches if i == num_batches else i)
         if hasattr(sync, "check_errors"):
             sync.check_errors()  # MGS barrier timeouts / RCCL async errors (epoch cadence)
         losses.append(mean)
@@ -343,6 +359,12 @@ def run_task(config) -> Dict[str, Any]:
 
 def _ring_wire(payload: int, n: int) -> float:
     return 0.0 if n <= 1 else 2.0 * (n - 1) / n * payload
+
+
+def _same_shape(a, b) -> bool:
+    if isinstance(a, dict):
+        return all(a[k].shape == b[k].shape for k in a)
+    return all(x.shape == y.shape for x, y in zip(a, b))
 
 
 def _clone_batch(b):

@@ -49,6 +49,7 @@ __all__ = [
     "Communicator",
     "LINK_PRESETS",
     "create_native_comm",
+    "FlagTimeout",
 ]
 
 
@@ -126,6 +127,10 @@ class CommStats:
         return dataclasses.asdict(self)
 
 
+class FlagTimeout(RuntimeError):
+    """A compute/comm graph ordering wait timed out (see :meth:`Communicator.check`)."""
+
+
 class _PacedWork:
     """Async handle that applies link pacing when waited on (c10d data plane)."""
 
@@ -157,7 +162,12 @@ class _StreamWork:
 
 _MAX_FLAGS = 256
 _DONE, _ERR = 2 * _MAX_FLAGS, 2 * _MAX_FLAGS + 2
-_WAIT_US = 2_000_000  # a flag wait reports a timeout after 2 s (device wall clock) instead of hanging
+# A flag wait gives up after this long (device wall clock) instead of hanging the GPU, sets
+# the sticky error word and lets the step run unordered; that step's results are never used:
+# check() raises on the word (bench health checks, engine logging cadence).  30 s covers rank
+# skew (a peer writing a checkpoint, capture skew) and emulated 1 Gb steps (3.75 s for dense
+# DistilBERT); NDP_FLAG_WAIT_US lowers it to inject a timeout in tests.
+_WAIT_US = int(os.environ.get("NDP_FLAG_WAIT_US", "30000000"))
 _SIDE_LINKS = {}
 _KEEPALIVE = []
 
@@ -470,8 +480,9 @@ class Communicator:
         if self._native is not None:
             self._native.check()
         if self.flag_error():
-            raise RuntimeError("compute/comm graph ordering: a device-flag wait timed out "
-                               "(the two streams may share a hardware queue); results of that step are unordered")
+            raise FlagTimeout("compute/comm graph ordering: a device-flag wait timed out after "
+                              f"{_WAIT_US / 1e6:.3g} s (a stalled peer, or the two streams share a hardware "
+                              "queue); the steps since are unordered and must not be used")
 
     def close(self):
         """Destroy the native communicator — unless a captured graph contains its

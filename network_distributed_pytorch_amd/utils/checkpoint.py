@@ -14,6 +14,8 @@ Layout of a checkpoint ``<path>``:
 Loading: the model from ``<path>``; the sync state and RNG from ``<path>.rank<r>`` when it
 exists (same world size), else from ``<path>`` (a world-size-1 checkpoint, or a resume
 at a different world size: the EF residual then restarts from rank 0's, with a warning).
+Both files carry the epoch / step counters; a per-rank file from a different save than the
+rank-0 file (a crash between the ranks' writes) raises :class:`CheckpointMismatch`.
 Writes are atomic (tmp file + rename).  Files contain only tensors and plain containers
 and are read back with ``torch.load(weights_only=True)``.
 """
@@ -27,7 +29,11 @@ import torch
 
 from ..parallel.comm import get_rank, world_size
 
-__all__ = ["save_checkpoint", "load_checkpoint", "rank_file"]
+__all__ = ["save_checkpoint", "load_checkpoint", "rank_file", "CheckpointMismatch"]
+
+
+class CheckpointMismatch(RuntimeError):
+    """The per-rank file and the rank-0 file of a checkpoint come from different saves."""
 
 FORMAT = "network_distributed_pytorch_amd/ckpt-v2"
 
@@ -92,6 +98,12 @@ def load_checkpoint(path: str, model: torch.nn.Module, sync=None, strict: bool =
     rf = rank_file(path, rank)
     if os.path.exists(rf):
         own = torch.load(rf, map_location="cpu", weights_only=True)
+        if (own.get("epoch"), own.get("step")) != (state["epoch"], state["step"]):
+            # a partial save (crash between the ranks' atomic writes) would otherwise mix
+            # epoch-e weights with another epoch's EF residual / momentum / RNG
+            raise CheckpointMismatch(
+                f"{rf} is from epoch {own.get('epoch')} step {own.get('step')}, {path} from epoch "
+                f"{state['epoch']} step {state['step']}: the checkpoint set is from different saves")
         if own.get("world", world) == world:
             local = own
         else:

@@ -68,6 +68,7 @@ class TrainConfig:
     log_file: Optional[str] = None
     log_every: int = 1
     check_replicas_every: int = 0
+    check_health_every: int = 50  # host check of flag-wait / MGS / RCCL errors (fatal), 0 = epoch end only
     write_grad: bool = False
     verbose: bool = True
     trace_phases: bool = False
