@@ -626,6 +626,85 @@ void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor part, c10::opti
   check_launch("launch_conv_wgrad");
 }
 
+// ---- strided / tabled implicit-GEMM convolutions (tgemm.hip) -----------------------------
+// (class, fwd slabs, grad-x slabs, grad-W slabs) for batch B, or class -1 (no tgemm path)
+py::tuple tg_plan(const std::vector<int64_t>& geom, int64_t B) {
+  const ndp::ConvGeom g = conv_geom(geom);
+  const int cls = ndp::tg_class(g);
+  const int64_t ny = B * g.Co * g.OH * g.OW, nx = B * g.C * g.H * g.W;
+  const int64_t nw = cls == ndp::TG_POINTWISE ? (int64_t)g.Co * g.C : (int64_t)g.Co * g.OH * g.OW * g.C * g.H * g.W;
+  // split-K slab sums run on float4: every output must hold a multiple of 4 floats
+  if (cls < 0 || B <= 0 || ny % 4 || nx % 4 || nw % 4) return py::make_tuple(-1, 1, 1, 1);
+  return py::make_tuple(cls, ndp::tg_splits(g, (int)B, 0), ndp::tg_splits(g, (int)B, 1), ndp::tg_splits(g, (int)B, 2));
+}
+
+static int tg_batch(const torch::Tensor& t, const ndp::ConvGeom& g, const char* who) {
+  TORCH_CHECK(ndp::tg_class(g) >= 0, who, ": no tgemm path for this geometry");
+  return (int)t.size(0);
+}
+
+static float* tg_part(const c10::optional<torch::Tensor>& part, int splits, int64_t slab, const char* who) {
+  if (splits <= 1) return nullptr;
+  TORCH_CHECK(part.has_value(), who, ": split-K needs a part scratch tensor");
+  check_f32(*part, "part");
+  TORCH_CHECK(part->numel() >= splits * slab && slab % 4 == 0, who, ": part scratch too small / slab % 4");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(part->data_ptr()) & 15) == 0, who, ": 16-B aligned part");
+  return part->data_ptr<float>();
+}
+
+int64_t tg_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, const std::vector<int64_t>& geom,
+               c10::optional<torch::Tensor> part, bool defer) {
+  const ndp::ConvGeom g = conv_geom(geom);
+  const int B = tg_batch(x, g, "tg_fwd");
+  conv_check(x, "x", B, g.C, g.H, g.W);
+  conv_check(w, "w", g.Co, g.C, g.KH, g.KW);
+  conv_check(y, "y", B, g.Co, g.OH, g.OW);
+  float* pp = tg_part(part, ndp::tg_splits(g, B, 0), y.numel(), "tg_fwd");
+  const int left = ndp::launch_tg_fwd(x.data_ptr<float>(), w.data_ptr<float>(), y.data_ptr<float>(), B, g, pp,
+                                      cur_stream(), defer);
+  check_launch("launch_tg_fwd");
+  return left;
+}
+
+int64_t tg_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, const std::vector<int64_t>& geom,
+                 c10::optional<torch::Tensor> part, c10::optional<torch::Tensor> addend, bool defer) {
+  const ndp::ConvGeom g = conv_geom(geom);
+  const int B = tg_batch(dy, g, "tg_dgrad");
+  conv_check(dy, "dy", B, g.Co, g.OH, g.OW);
+  conv_check(w, "w", g.Co, g.C, g.KH, g.KW);
+  conv_check(dx, "dx", B, g.C, g.H, g.W);
+  float* pp = tg_part(part, ndp::tg_splits(g, B, 1), dx.numel(), "tg_dgrad");
+  const float* ap = nullptr;
+  if (addend.has_value()) {
+    conv_check(*addend, "addend", B, g.C, g.H, g.W);
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(addend->data_ptr()) & 15) == 0, "tg_dgrad: 16-B aligned addend");
+    ap = addend->data_ptr<float>();
+  }
+  const int left = ndp::launch_tg_dgrad(dy.data_ptr<float>(), w.data_ptr<float>(), dx.data_ptr<float>(), B, g, pp,
+                                        cur_stream(), ap, defer);
+  check_launch("launch_tg_dgrad");
+  return left;
+}
+
+// out: dW [Co, C, 1, 1] (pointwise) or dWbig^T [Co*OH*OW, C*H*W] (small map); returns the
+// number of slabs left in part (defer, pointwise only) or 1
+int64_t tg_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor out, const std::vector<int64_t>& geom,
+                 c10::optional<torch::Tensor> part, bool defer) {
+  const ndp::ConvGeom g = conv_geom(geom);
+  const int B = tg_batch(x, g, "tg_wgrad");
+  conv_check(x, "x", B, g.C, g.H, g.W);
+  conv_check(dy, "dy", B, g.Co, g.OH, g.OW);
+  check_f32(out, "out");
+  const bool pw = ndp::tg_class(g) == ndp::TG_POINTWISE;
+  const int64_t n = pw ? (int64_t)g.Co * g.C : (int64_t)g.Co * g.OH * g.OW * g.C * g.H * g.W;
+  TORCH_CHECK(out.numel() == n, "tg_wgrad: out must hold ", n, " floats");
+  float* pp = tg_part(part, ndp::tg_splits(g, B, 2), n, "tg_wgrad");
+  const int left = ndp::launch_tg_wgrad(x.data_ptr<float>(), dy.data_ptr<float>(), out.data_ptr<float>(), B, g, pp,
+                                        cur_stream(), defer && pw);
+  check_launch("launch_tg_wgrad");
+  return left;
+}
+
 // db = g.sum(0) for g [M, N] contiguous fp32, N % 4 == 0 (deterministic, graph-safe)
 void colsum(torch::Tensor g, torch::Tensor out) {
   check_f32(g, "g"); check_f32(out, "out");
@@ -868,6 +947,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("geom"),
         py::arg("part") = py::none(), py::arg("addend") = py::none(), py::arg("defer") = false);
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("part"), py::arg("dw"), py::arg("geom"));
+  m.def("tg_plan", &tg_plan);
+  m.def("tg_fwd", &tg_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("geom"), py::arg("part") = py::none(),
+        py::arg("defer") = false);
+  m.def("tg_dgrad", &tg_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("geom"),
+        py::arg("part") = py::none(), py::arg("addend") = py::none(), py::arg("defer") = false);
+  m.def("tg_wgrad", &tg_wgrad, py::arg("x"), py::arg("dy"), py::arg("out"), py::arg("geom"),
+        py::arg("part") = py::none(), py::arg("defer") = false);
   m.def("embedding_backward", &embedding_backward);
   m.def("colsum", &colsum);
   m.def("gelu_bwd_colsum", &gelu_bwd_colsum);

@@ -800,9 +800,9 @@ static int run_fwd(const float* x, const float* w, float* y, int B, int Cin, int
   return 1;
 }
 
-void launch_slab_sum(const float* part, float* out, int64_t n, int nslab, hipStream_t s) {
+void launch_slab_sum(const float* part, float* out, int64_t n, int nslab, hipStream_t s, const float* addend) {
   hipLaunchKernelGGL(conv_slab_sum_kernel, dim3((unsigned)((n / 4 + 15) / 16)), dim3(256), 0, s, part, out, n, nslab,
-                     nullptr);
+                     addend);
 }
 
 template <int R, int S, int ST, int PD, int H, int W, int CB, int BM, int NW, int NBPW, int KB>

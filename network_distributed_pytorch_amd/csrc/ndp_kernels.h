@@ -222,11 +222,50 @@ int launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvG
 // addend (nullable, stride-1 classes): dx += addend in the epilogue / split-K sum (never deferred)
 int launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, float* part,
                       hipStream_t s, const float* addend = nullptr, bool defer = false);
-// out[i] = sum_{z < nslab} part[z * n + i] in z order (n % 4 == 0), same order as the split-K sums
-void launch_slab_sum(const float* part, float* out, int64_t n, int nslab, hipStream_t s);
+// out[i] = sum_{z < nslab} part[z * n + i] (+ addend[i]) in z order (n % 4 == 0), same order as
+// the split-K sums; out may alias addend
+void launch_slab_sum(const float* part, float* out, int64_t n, int nslab, hipStream_t s,
+                     const float* addend = nullptr);
 // part: (B / conv_wgrad_imgs(cls, g, B)) * Co*C*KH*KW floats of scratch
 void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, int B, const ConvGeom& g,
                        hipStream_t s);
+
+// ---- strided / tabled implicit-GEMM convolutions (tgemm.hip) ------------------------------
+// operand index i -> element offset (i >> sh) * so + (i & (2^sh - 1)) * si
+struct TgIndex {
+  int64_t so, si;
+  int32_t sh, pad;
+};
+// C[m, n] (+)= sum_k A[m, k] B[k, n];  A(m,k) = a[am(m) + ak(k)], B(k,n) = b[bk(k) + bn(n)] or,
+// gathered, b[(k >> bk.sh) * bk.so + (n >> bn.sh) * bn.so + tab[(k & kmask) << bn.sh | (n & nmask)]]
+// (tab < 0: zero); C(m,n) = c[cm(m) + cn(n)]; split z writes part + z * slab when part != null
+struct TgArgs {
+  const float* a;
+  const float* b;
+  float* c;
+  float* part;
+  const float* addend;  // C += addend (same offsets; may alias c); single-split launches only
+  TgIndex am, ak, bk, bn, cm, cn;
+  int32_t M, N, K, kchunk;
+  int64_t slab;
+  int32_t gather, pad;
+  int8_t tab[64];
+};
+constexpr int TG_POINTWISE = 0;  // 1x1 stride-1, power-of-two map
+constexpr int TG_SMALL = 1;      // input map <= 16, output map <= 4 pixels (powers of two)
+int tg_class(const ConvGeom& g);
+// split-K slabs of direction dir (0 fwd, 1 grad-x, 2 grad-W) for batch B (1 = no scratch)
+int tg_splits(const ConvGeom& g, int B, int dir);
+// defer: leave the split-K slabs in part and return their count (1 = y / dx final)
+int launch_tg_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s,
+                  bool defer = false);
+// addend (nullable, may alias dx): dx = grad-x + addend (never deferred)
+int launch_tg_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, float* part,
+                    hipStream_t s, const float* addend = nullptr, bool defer = false);
+// POINTWISE: out = dW; SMALL: out = dWbig^T [Co*OH*OW, C*H*W] (fold with toeplitz_fold).
+// defer: leave the split-K slabs in part, return their count (1 = out final)
+int launch_tg_wgrad(const float* x, const float* dy, float* out, int B, const ConvGeom& g, float* part,
+                    hipStream_t s, bool defer = false);
 }  // namespace ndp
 
 // ---- fused fp32 attention, q/k/v/o [B, S, H, 64] (attention.hip) ------------------------

@@ -1,0 +1,330 @@
+// Strided / tabled implicit-GEMM convolutions on v_mfma_f32_32x32x2_f32 (exact f32, gfx950).
+//
+// Two conv families that the direct kernels (conv.hip) do not cover, both NCHW fp32:
+//
+//  * POINTWISE: 1x1 stride-1 convolutions on any power-of-two map (the bottleneck conv1 /
+//    conv3 and the stride-1 downsample of ResNet-50/101/152 — the reference's own models,
+//    ddp_guide_cifar10/ddp_init.py:108, ddp_powersgd_guide_cifar10/ddp_init.py:111):
+//      forward  Y[co, (b,p)]  = sum_c  W[co, c]  X[c, (b,p)]        M = Co, N = B*HW, K = C
+//      grad-x   dX[c, (b,p)]  = sum_co W[co, c]  dY[co, (b,p)]      M = C,  N = B*HW, K = Co
+//      grad-W   dW[co, c]     = sum_(b,p) dY[co, (b,p)] X[c, (b,p)] M = Co, N = C,    K = B*HW
+//  * SMALL MAP ("Toeplitz" form without materialising W_big): any KHxKW / stride / pad conv
+//    with an input map of <= 16 and an output map of <= 4 pixels (ResNet layer3 / layer4 on
+//    32x32 inputs).  With T = KH*KW and tap(ipix, opix) the kernel tap joining an input and an
+//    output pixel (-1: none),
+//      forward  Y[b, (co,o)] = sum_(c,i) X[b, (c,i)] * W[co, c, tap(i, o)]
+//      grad-x   dX[b, (c,i)] = sum_(co,o) dY[b, (co,o)] * W[co, c, tap(i, o)]
+//    the weight operand is GATHERED from W through a <= 64-entry tap table held in the kernel
+//    arguments (no W_big expand launch, no W_big buffer, no zero MACs beyond the table's);
+//      grad-W   dWbig^T[(co,o), (c,i)] = sum_b dY[b, (co,o)] X[b, (c,i)]
+//    folded into dW by the existing deterministic fold (conv.hip toeplitz_fold_many,
+//    batched per backward by ops/gradfinish.py).
+//
+// One kernel serves all six: C[m, n] = sum_k A[m, k] B[k, n] with every operand index
+// split as (i >> sh) * so + (i & (2^sh - 1)) * si — NCHW's (image, pixel) pairs are such
+// composites when the map is a power of two — and an optional tap-table gather for B.
+// Tiles: 64 x 64 x 32, 4 waves of 32 x 32 (one f32x16 accumulator each), operands staged
+// in LDS as [k][m] / [k][n] with an odd row stride (conflict-free transposing stores and
+// broadcast-free MFMA reads), register double buffering: the global loads of tile t+1 are
+// in flight while the MFMAs of tile t issue; one barrier per tile.  The load mapping walks
+// the operand's contiguous index across lanes (template AKF / BNF) so every global access is
+// a coalesced 256-B wave transaction.  Split-K (blockIdx.z) writes slabs that
+// conv_slab_sum adds in z order: deterministic, no atomics.
+#include <hip/hip_runtime.h>
+
+#include "ndp_kernels.h"
+
+namespace ndp {
+
+namespace {
+
+constexpr int TBM = 64, TBN = 64, TBK = 32;
+typedef float f32x16t __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ int64_t tg_off(const TgIndex& t, int i) {
+  return (int64_t)(i >> t.sh) * t.so + (int64_t)(i & ((1 << t.sh) - 1)) * t.si;
+}
+
+template <bool AKF, bool BNF, bool GATHER>
+__global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
+  __shared__ float As[2][TBK][TBM + 1];
+  __shared__ float Bs[2][TBK][TBN + 1];
+  __shared__ int8_t stab[64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (GATHER && tid < 64) stab[tid] = g.tab[tid];  // made visible by the first tile's barrier
+  const int h = lane >> 5, l32 = lane & 31;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int n0 = blockIdx.x * TBN, m0 = blockIdx.y * TBM;
+  const int kbeg = blockIdx.z * g.kchunk;
+  const int kend = min(g.K, kbeg + g.kchunk);
+  constexpr int PER = TBM * TBK / 256;  // 8 elements of each operand per thread and tile
+
+  // fixed per-thread tile coordinates; the m / n parts of the addresses are tile-invariant
+  int am[PER], ak[PER], bk[PER], bn[PER];
+  int64_t aoff[PER], boff[PER];
+  bool aok[PER], bok[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = tid + 256 * i;
+    if (AKF) { am[i] = e / TBK; ak[i] = e % TBK; } else { ak[i] = e / TBM; am[i] = e % TBM; }
+    if (BNF) { bk[i] = e / TBN; bn[i] = e % TBN; } else { bn[i] = e / TBK; bk[i] = e % TBK; }
+    const int gm = m0 + am[i], gn = n0 + bn[i];
+    aok[i] = gm < g.M;
+    bok[i] = gn < g.N;
+    aoff[i] = aok[i] ? tg_off(g.am, gm) : 0;
+    boff[i] = bok[i] ? (GATHER ? (int64_t)(gn >> g.bn.sh) * g.bn.so : tg_off(g.bn, gn)) : 0;
+  }
+  const int nmask = (1 << g.bn.sh) - 1, kmask = (1 << g.bk.sh) - 1;
+
+  float ra[PER], rb[PER];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int gk = k0 + ak[i];
+      ra[i] = (aok[i] && gk < kend) ? g.a[aoff[i] + tg_off(g.ak, gk)] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int gk = k0 + bk[i];
+      float v = 0.f;
+      if (bok[i] && gk < kend) {
+        if constexpr (GATHER) {
+          const int t = stab[((gk & kmask) << g.bn.sh) | ((n0 + bn[i]) & nmask)];
+          if (t >= 0) v = g.b[boff[i] + (int64_t)(gk >> g.bk.sh) * g.bk.so + t];
+        } else {
+          v = g.b[boff[i] + tg_off(g.bk, gk)];
+        }
+      }
+      rb[i] = v;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) As[buf][ak[i]][am[i]] = ra[i];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) Bs[buf][bk[i]][bn[i]] = rb[i];
+  };
+
+  f32x16t acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+
+  const int ntiles = kend > kbeg ? (kend - kbeg + TBK - 1) / TBK : 0;
+  if (GATHER) __syncthreads();  // stab
+  if (ntiles > 0) {
+    load(kbeg);
+    store(0);
+    __syncthreads();
+    for (int t = 0; t < ntiles; ++t) {
+      const int cur = t & 1;
+      if (t + 1 < ntiles) load(kbeg + (t + 1) * TBK);
+#pragma unroll
+      for (int kp = 0; kp < TBK / 2; ++kp) {
+        const float a = As[cur][2 * kp + h][wm * 32 + l32];
+        const float b = Bs[cur][2 * kp + h][wn * 32 + l32];
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+      }
+      if (t + 1 < ntiles) store(cur ^ 1);
+      __syncthreads();
+    }
+  }
+
+  float* out = g.part != nullptr ? g.part + (int64_t)blockIdx.z * g.slab : g.c;
+  const int n = n0 + wn * 32 + l32;
+  if (n < g.N) {
+    const int64_t noff = tg_off(g.cn, n);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (m < g.M) {
+        const int64_t o = tg_off(g.cm, m) + noff;
+        out[o] = g.addend != nullptr && g.part == nullptr ? acc[r] + g.addend[o] : acc[r];
+      }
+    }
+  }
+}
+
+int ilog2_exact(int v) {
+  int s = 0;
+  while ((1 << s) < v) ++s;
+  return (1 << s) == v ? s : -1;
+}
+
+TgIndex plain(int64_t stride) { return TgIndex{0, stride, 30, 0}; }  // i < 2^30: outer part always 0
+TgIndex comp(int sh, int64_t outer, int64_t inner) { return TgIndex{outer, inner, sh, 0}; }
+
+constexpr int kTgFill = 256;  // one workgroup per CU at least
+
+// split-K factor: power of two so that tiles * splits >= kTgFill, each split >= 2 k-tiles
+int tg_pick_splits(int M, int N, int K, int cap) {
+  const int tiles = ((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN);
+  const int ktiles = (K + TBK - 1) / TBK;
+  int s = 1;
+  while (s * 2 <= cap && tiles * s < kTgFill && ktiles >= 4 * s) s *= 2;
+  return s;
+}
+
+int tg_cap() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("NDP_TG_MAXSPLIT");
+    v = e ? atoi(e) : 16;
+    if (v < 1) v = 1;
+  }
+  return v;
+}
+
+// returns the number of split-K slabs left in a.part (defer), or 1 when final_out is written
+int run(TgArgs a, bool akf, bool bnf, int splits, float* final_out, hipStream_t s, bool defer = false) {
+  const int ktiles = (a.K + TBK - 1) / TBK;
+  const int per = (ktiles + splits - 1) / splits;
+  a.kchunk = per * TBK;
+  splits = (ktiles + per - 1) / per;
+  if (splits <= 1) a.part = nullptr;
+  const dim3 grid((a.N + TBN - 1) / TBN, (a.M + TBM - 1) / TBM, splits);
+  const bool gather = a.gather != 0;
+#define NDP_TG_LAUNCH(AK, BN_, GA) hipLaunchKernelGGL((tgemm_kernel<AK, BN_, GA>), grid, dim3(256), 0, s, a)
+  if (gather) {
+    if (akf) NDP_TG_LAUNCH(true, false, true); else NDP_TG_LAUNCH(false, false, true);
+  } else if (akf && bnf) NDP_TG_LAUNCH(true, true, false);
+  else if (akf) NDP_TG_LAUNCH(true, false, false);
+  else if (bnf) NDP_TG_LAUNCH(false, true, false);
+  else NDP_TG_LAUNCH(false, false, false);
+#undef NDP_TG_LAUNCH
+  if (splits <= 1) return 1;
+  if (defer && a.addend == nullptr) return splits;  // the consumer (fused BN, gradfinish) sums them
+  launch_slab_sum(a.part, final_out, a.slab, splits, s, a.addend);
+  return 1;
+}
+
+// tap(i, o) of a small-map conv, row-major [rows][cols] as the kernel reads it
+void fill_tab(TgArgs& a, const ConvGeom& g, bool by_input_rows) {
+  const int IHW = g.H * g.W, OHW = g.OH * g.OW;
+  for (int i = 0; i < 64; ++i) a.tab[i] = -1;
+  for (int i = 0; i < IHW; ++i)
+    for (int o = 0; o < OHW; ++o) {
+      const int ih = i / g.W, iw = i % g.W, oh = o / g.OW, ow = o % g.OW;
+      const int kh = ih - oh * g.stride + g.pad, kw = iw - ow * g.stride + g.pad;
+      const int t = (kh >= 0 && kh < g.KH && kw >= 0 && kw < g.KW) ? kh * g.KW + kw : -1;
+      if (by_input_rows) a.tab[i * OHW + o] = (int8_t)t;
+      else a.tab[o * IHW + i] = (int8_t)t;
+    }
+}
+
+}  // namespace
+
+int tg_class(const ConvGeom& g) {
+  const int hw = g.H * g.W;
+  if (g.KH == 1 && g.KW == 1 && g.stride == 1 && g.pad == 0 && ilog2_exact(hw) >= 0) return TG_POINTWISE;
+  const int ohw = g.OH * g.OW;
+  if (hw <= 16 && ohw <= 4 && ilog2_exact(hw) >= 0 && ilog2_exact(ohw) >= 0 && g.KH * g.KW <= 127 &&
+      g.OH >= 1 && g.OW >= 1)
+    return TG_SMALL;
+  return -1;
+}
+
+// slabs `part` must hold for direction dir (0 fwd, 1 grad-x, 2 grad-W); 1 = no scratch
+int tg_splits(const ConvGeom& g, int B, int dir) {
+  const int cls = tg_class(g);
+  const int hw = g.H * g.W, ohw = g.OH * g.OW;
+  if (cls == TG_POINTWISE) {
+    if (dir == 0) return tg_pick_splits(g.Co, B * hw, g.C, tg_cap());
+    if (dir == 1) return tg_pick_splits(g.C, B * hw, g.Co, tg_cap());
+    return tg_pick_splits(g.Co, g.C, B * hw, 64);
+  }
+  if (cls == TG_SMALL) {
+    if (dir == 0) return tg_pick_splits(B, g.Co * ohw, g.C * hw, tg_cap());
+    if (dir == 1) return tg_pick_splits(B, g.C * hw, g.Co * ohw, tg_cap());
+    return tg_pick_splits(g.Co * ohw, g.C * hw, B, tg_cap());
+  }
+  return 1;
+}
+
+// y [B, Co, OH, OW] = conv(x [B, C, H, W], w); part: tg_splits(g, B, 0) * numel(y) floats (or null if 1)
+int launch_tg_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s,
+                  bool defer) {
+  const int cls = tg_class(g);
+  const int hw = g.H * g.W, ohw = g.OH * g.OW, T = g.KH * g.KW;
+  TgArgs a{};
+  a.part = part;
+  a.c = y;
+  if (cls == TG_POINTWISE) {
+    const int sh = ilog2_exact(hw);
+    a.a = w; a.am = plain(g.C); a.ak = plain(1);                       // W [Co][C]
+    a.b = x; a.bk = plain(hw); a.bn = comp(sh, (int64_t)g.C * hw, 1);   // X [b][c][p]
+    a.cm = plain(hw); a.cn = comp(sh, (int64_t)g.Co * hw, 1);          // Y [b][co][p]
+    a.M = g.Co; a.N = B * hw; a.K = g.C;
+    a.slab = (int64_t)B * g.Co * hw;
+    return run(a, true, hw >= 4, tg_splits(g, B, 0), y, s, defer);
+  }
+  {
+    a.a = x; a.am = plain((int64_t)g.C * hw); a.ak = plain(1);         // X [b][(c,i)]
+    a.b = w; a.gather = 1;                                             // W[co, c, tap(i, o)]
+    a.bk = comp(ilog2_exact(hw), T, 0); a.bn = comp(ilog2_exact(ohw), (int64_t)g.C * T, 0);
+    fill_tab(a, g, true);                                              // rows: i (k inner), cols: o (n inner)
+    a.cm = plain((int64_t)g.Co * ohw); a.cn = plain(1);                // Y [b][(co,o)]
+    a.M = B; a.N = g.Co * ohw; a.K = g.C * hw;
+    a.slab = (int64_t)B * g.Co * ohw;
+    return run(a, true, false, tg_splits(g, B, 0), y, s, defer);
+  }
+}
+
+// dx [B, C, H, W] from dy [B, Co, OH, OW]; part: tg_splits(g, B, 1) * numel(dx) floats
+int launch_tg_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, float* part,
+                    hipStream_t s, const float* addend, bool defer) {
+  const int cls = tg_class(g);
+  const int hw = g.H * g.W, ohw = g.OH * g.OW, T = g.KH * g.KW;
+  TgArgs a{};
+  a.part = part;
+  a.c = dx;
+  a.addend = addend;
+  if (cls == TG_POINTWISE) {
+    const int sh = ilog2_exact(hw);
+    a.a = w; a.am = plain(1); a.ak = plain(g.C);                       // W^T: A[c][co] = W[co][c]
+    a.b = dy; a.bk = plain(hw); a.bn = comp(sh, (int64_t)g.Co * hw, 1);
+    a.cm = plain(hw); a.cn = comp(sh, (int64_t)g.C * hw, 1);
+    a.M = g.C; a.N = B * hw; a.K = g.Co;
+    a.slab = (int64_t)B * g.C * hw;
+    return run(a, false, hw >= 4, tg_splits(g, B, 1), dx, s, defer);
+  }
+  {
+    a.a = dy; a.am = plain((int64_t)g.Co * ohw); a.ak = plain(1);      // dY [b][(co,o)]
+    a.b = w; a.gather = 1;                                             // B[(co,o), (c,i)] = W[co, c, tap(i, o)]
+    a.bk = comp(ilog2_exact(ohw), (int64_t)g.C * T, 0); a.bn = comp(ilog2_exact(hw), T, 0);
+    fill_tab(a, g, false);                                             // rows: o (k inner), cols: i (n inner)
+    a.cm = plain((int64_t)g.C * hw); a.cn = plain(1);
+    a.M = B; a.N = g.C * hw; a.K = g.Co * ohw;
+    a.slab = (int64_t)B * g.C * hw;
+    return run(a, true, false, tg_splits(g, B, 1), dx, s, defer);
+  }
+}
+
+// POINTWISE: out = dW [Co, C]; SMALL: out = dWbig^T [Co*OH*OW, C*H*W] (fold it into dW with
+// toeplitz_fold).  part: tg_splits(g, B, 2) * numel(out) floats.  defer: leave the split-K
+// slabs in `part` and return how many (1 = `out` final).
+int launch_tg_wgrad(const float* x, const float* dy, float* out, int B, const ConvGeom& g, float* part, hipStream_t s,
+                    bool defer) {
+  const int cls = tg_class(g);
+  const int hw = g.H * g.W, ohw = g.OH * g.OW;
+  TgArgs a{};
+  a.part = part;
+  a.c = out;
+  const int splits = tg_splits(g, B, 2);
+  if (cls == TG_POINTWISE) {
+    const int sh = ilog2_exact(hw);
+    a.a = dy; a.am = plain(hw); a.ak = comp(sh, (int64_t)g.Co * hw, 1);  // A[co][(b,p)]
+    a.b = x; a.bk = comp(sh, (int64_t)g.C * hw, 1); a.bn = plain(hw);    // B[(b,p)][c]
+    a.cm = plain(g.C); a.cn = plain(1);
+    a.M = g.Co; a.N = g.C; a.K = B * hw;
+    a.slab = (int64_t)g.Co * g.C;
+    return run(a, hw >= 4, hw == 1, splits, out, s, defer);
+  }
+  a.a = dy; a.am = plain(1); a.ak = plain((int64_t)g.Co * ohw);       // A[(co,o)][b]
+  a.b = x; a.bk = plain((int64_t)g.C * hw); a.bn = plain(1);          // B[b][(c,i)]
+  a.cm = plain((int64_t)g.C * hw); a.cn = plain(1);
+  a.M = g.Co * ohw; a.N = g.C * hw; a.K = B;
+  a.slab = (int64_t)g.Co * ohw * g.C * hw;
+  return run(a, false, true, splits, out, s, false);
+}
+
+}  // namespace ndp

@@ -18,8 +18,11 @@ the input is subsampled first.
 input geometry, the fastest native path:
   1. a direct fp32-MFMA kernel (csrc/conv.hip via ops/conv.py) for the ResNet CIFAR shapes
      it covers (stem 7x7/2 on 32x32, 3x3 on 8x8 and 4x4, 3x3/2 8x8->4x4);
-  2. the Toeplitz GEMM form where it pays: input H*W <= 16 and output OH*OW <= 4;
-  3. MIOpen otherwise.
+  2. the strided / tabled MFMA GEMM kernel (csrc/tgemm.hip via ops/tgconv.py): 1x1 stride-1
+     convs on any power-of-two map, and the small-map Toeplitz product (input H*W <= 16,
+     output OH*OW <= 4) with the weight gathered in-kernel (no W_big);
+  3. the hipBLASLt Toeplitz GEMM form (``NDP_TG=0``), and the CPU path;
+  4. MIOpen otherwise.
 """
 from __future__ import annotations
 
@@ -34,6 +37,7 @@ from ..ops._ext import ext
 from ..ops import conv as _conv
 from ..ops.conv import DirectConvFn, direct_plan, side_stream
 from ..ops.gradlink import InjectGrad
+from ..ops.tgconv import TgConvFn, tg_plan
 
 __all__ = ["GemmConv2d", "ToeplitzBank", "toeplitz_maps", "eligible"]
 
@@ -237,6 +241,9 @@ class GemmConv2d(nn.Conv2d):
             plan = direct_plan(x, self.weight, s, p)
             if plan is not None:
                 return DirectConvFn.apply(x, self.weight, plan, link, slab_out, grad_slab)
+            tplan = tg_plan(x, self.weight, s, p)
+            if tplan is not None:  # pointwise 1x1 / small-map tabled GEMM (csrc/tgemm.hip)
+                return TgConvFn.apply(x, self.weight, tplan, link, branch, slab_out, grad_slab)
         oh = (H + 2 * p - kh) // s + 1
         ow = (W + 2 * p - kw) // s + 1
         if not eligible(H, W, oh, ow):

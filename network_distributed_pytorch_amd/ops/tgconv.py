@@ -1,0 +1,137 @@
+"""Strided / tabled implicit-GEMM convolutions (csrc/tgemm.hip) behind an autograd Function.
+
+Two shape families the direct kernels (ops/conv.py) do not cover, forward / grad-x / grad-W
+all on one hand-written gfx950 MFMA GEMM kernel:
+
+* ``pointwise`` — 1x1 stride-1 convs on any power-of-two map: the bottleneck conv1 / conv3
+  and stride-1 downsample of ResNet-50/101/152, the reference's own models
+  (ddp_guide_cifar10/ddp_init.py:108, ddp_powersgd_guide_cifar10/ddp_init.py:111), which
+  otherwise run on MIOpen;
+* ``small`` — any conv from a <= 16-pixel map to a <= 4-pixel map (ResNet layer3 / layer4 on
+  32x32 inputs): the Toeplitz product with the weight operand gathered through a tap table
+  in the kernel arguments, so there is no W_big buffer and no expand launch; grad-W is
+  W_big's gradient folded by the existing deterministic fold (batched, ops/gradfinish.py).
+
+Split-K slabs are summed in a fixed order (deterministic) — by the kernel's own slab sum,
+by the fused BN kernel that consumes the conv (``slab_out`` / ``grad_slab``,
+ops/slablink.py) or by gradfinish's batched sum (grad-W).  ``NDP_TG=0`` disables the path
+(``NDP_TG_SMALL=0`` / ``NDP_TG_PW=0`` one family), restoring Toeplitz / MIOpen.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional, Tuple
+
+import torch
+
+from . import gradfinish
+from ._ext import ext
+
+__all__ = ["tg_plan", "TgConvFn", "enabled"]
+
+_PLANS: dict = {}
+_ON = os.environ.get("NDP_TG", "1") != "0"
+_SMALL = os.environ.get("NDP_TG_SMALL", "1") != "0"
+_PW = os.environ.get("NDP_TG_PW", "1") != "0"
+POINTWISE, SMALL = 0, 1
+
+
+def enabled() -> bool:
+    return _ON
+
+
+def tg_plan(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int) -> Optional[Tuple]:
+    """(geom, cls, fwd_slabs, dgrad_slabs, wgrad_slabs) if the tgemm path covers this conv."""
+    if not (_ON and x.is_cuda and x.dtype == torch.float32 and weight.dtype == torch.float32 and x.dim() == 4):
+        return None
+    B, C, H, W = x.shape
+    Co, Ci, KH, KW = weight.shape
+    if Ci != C or KH * KW > 9:  # the grad-W fold handles <= 3x3 kernels
+        return None
+    geom = (C, H, W, Co, KH, KW, int(stride), int(padding))
+    key = (geom, int(B))
+    if key not in _PLANS:
+        cls, fs, ds, ws = ext().tg_plan(list(geom), int(B))
+        ok = cls >= 0 and ((cls == POINTWISE and _PW) or (cls == SMALL and _SMALL))
+        _PLANS[key] = (geom, int(cls), int(fs), int(ds), int(ws)) if ok else None
+    return _PLANS[key]
+
+
+def _scratch(n_slabs: int, numel: int, like: torch.Tensor) -> Optional[torch.Tensor]:
+    return torch.empty(n_slabs * numel, device=like.device, dtype=like.dtype) if n_slabs > 1 else None
+
+
+class TgConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, plan, link=None, branch=None, slab_out=None, grad_slab=None):
+        geom, cls, fs, _, _ = plan
+        C, H, W, Co, KH, KW, s, p = geom
+        x = x.contiguous()
+        w = weight.contiguous()
+        B = x.shape[0]
+        OH = (H + 2 * p - KH) // s + 1
+        OW = (W + 2 * p - KW) // s + 1
+        y = torch.empty(B, Co, OH, OW, device=x.device, dtype=x.dtype)
+        part = _scratch(fs, y.numel(), x)
+        left = ext().tg_fwd(x, w, y, list(geom), part, slab_out is not None)
+        if left > 1:
+            slab_out.put_fwd(part, left)  # y is filled by the consuming fused BN kernel
+        ctx.save_for_backward(x, w)
+        ctx.plan = plan
+        ctx.weight = weight  # the Parameter: a deferred grad-W finish writes its adopted .grad
+        ctx.link = link      # ops/gradlink.GradLink: residual-branch gradient added in the epilogue
+        ctx.grad_slab = grad_slab
+        ctx.branch = branch
+        if branch is not None:
+            branch.join()    # ops/gradlink.BranchLink: grad-x shared with a sibling conv
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        geom, cls, _, ds, ws = ctx.plan
+        C, H, W, Co, KH, KW, s, p = geom
+        dy = dy.contiguous()
+        dx = dw = None
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty_like(w)
+            defer = gradfinish.can_defer(ctx.weight)
+            if cls == POINTWISE:
+                part = _scratch(ws, dw.numel(), x)
+                left = ext().tg_wgrad(x, dy, dw, list(geom), part, defer)
+                if left > 1:
+                    gradfinish.defer_slab(part, dw, left)
+            else:
+                OH = (H + 2 * p - KH) // s + 1
+                OW = (W + 2 * p - KW) // s + 1
+                dwt = torch.empty(Co * OH * OW, C * H * W, device=x.device, dtype=x.dtype)
+                ext().tg_wgrad(x, dy, dwt, list(geom), _scratch(ws, dwt.numel(), x), False)
+                if defer:
+                    gradfinish.defer_fold(dwt, dw, geom)
+                else:
+                    ext().toeplitz_fold(dwt, dw, list(geom))
+        if ctx.needs_input_grad[0]:
+            addend = ctx.link.take() if ctx.link is not None else None
+            br = ctx.branch if ctx.branch is not None and ctx.branch.active() else None
+            other = None
+            if br is not None:
+                other = br.take()
+                if addend is None:
+                    addend = other
+                elif other is not None:
+                    addend = addend + other
+            part = _scratch(ds, x.numel(), x)
+            if addend is not None:  # dx = grad-x + addend, written in place over the addend buffer
+                addend = addend.contiguous()
+                ext().tg_dgrad(dy, w, addend, list(geom), part, addend, False)
+                dx = addend
+            else:
+                dx = torch.empty_like(x)
+                defer = ctx.grad_slab is not None and br is None
+                left = ext().tg_dgrad(dy, w, dx, list(geom), part, None, defer)
+                if left > 1:
+                    ctx.grad_slab.put_bwd(part, left)  # dx stays unwritten: the BN backward sums the slabs
+                if br is not None and other is None:  # first of the two: the sibling adds onto it
+                    br.put(dx)
+                    dx = None
+        return dx, dw, None, None, None, None, None
