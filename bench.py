@@ -290,7 +290,8 @@ def health_check(wl, world: int, where: str) -> dict:
     local = checksum(flat)
     sums = [local]
     if world > 1:
-        t = torch.tensor([local], dtype=torch.float64, device=wl.device)
+        on = "cpu" if dist.get_backend() == "gloo" else wl.device
+        t = torch.tensor([local], dtype=torch.float64, device=on)
         outs = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(outs, t)
         sums = [float(o.item()) for o in outs]

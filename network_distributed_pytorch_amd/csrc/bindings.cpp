@@ -897,6 +897,7 @@ void attn_bwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, c10::optional<t
 }  // namespace
 
 void register_comm(py::module& m);  // comm.cpp
+void register_ipc(py::module& m);   // ipc.hip
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "network_distributed_pytorch_amd native gfx950 kernels + plan builder";
@@ -964,4 +965,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   register_comm(m);
+  register_ipc(m);
 }

@@ -1,0 +1,245 @@
+// Peer-memory one-shot all-reduce over HIP IPC (latency path for small
+// collectives), an opt-in data plane (NDP_COMM=ipc, parallel/comm.py).
+//
+// The reference's collectives (ddp_powersgd_guide_cifar10/reducer.py:126,132,145) are a few
+// 0.1-1 MB all-reduces per step: latency-bound.  Here every rank owns one symmetric device
+// buffer (data + flag words), exports it with hipIpcGetMemHandle, exchanges the handles
+// through the c10d store and maps every peer's buffer with hipIpcOpenMemHandle (dmabuf IPC:
+// HSA_ENABLE_IPC_MODE_LEGACY=0).  One kernel per collective, no host synchronisation,
+// hipGraph-capturable:
+//   workgroup w owns the fixed 16-KB chunk w of the buffer (the chunk -> workgroup mapping
+//   never changes, so each workgroup's flags order only its own chunk, and no workgroup
+//   waits for another workgroup of its own kernel: no co-residency assumption);
+//   with e = this chunk's use count (a device counter, so captured graphs replay):
+//     1. wait until every peer has finished reading my chunk w of use e-1 (done flags);
+//     2. copy my input chunk into my buffer, release (system scope), write `ready = e` into
+//        every peer's flag array;
+//     3. wait for every peer's ready flag, acquire, and sum the N chunks in rank order
+//        0..N-1 — every rank performs the identical fp32 additions, so the results are
+//        bitwise identical across ranks (replica consistency);
+//     4. write `done = e` into every peer's flag array.
+// Spins are wall-clock bounded (s_memrealtime): a timeout sets a sticky error word, later
+// collectives skip, and the host check (Communicator.check) fails the run — never a hang.
+// Works between processes sharing one GPU (the multi-process test of the captured overlap
+// path on a one-GPU box) and between GPUs over xGMI.
+#include <ATen/hip/HIPContext.h>
+#include <hip/hip_runtime.h>
+#include <torch/extension.h>
+
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace {
+
+constexpr int kIpcMaxRanks = 16;
+constexpr int kIpcChunk = 4096;  // floats per workgroup chunk (16 KB)
+constexpr int kIpcThreads = 256;
+
+#define NDP_IPC_CHECK(expr)                                                                \
+  do {                                                                                     \
+    hipError_t _e = (expr);                                                                \
+    TORCH_CHECK(_e == hipSuccess, "HIP error in ", #expr, ": ", hipGetErrorString(_e));     \
+  } while (0)
+
+struct IpcArgs {
+  float* data[kIpcMaxRanks];        // every rank's buffer, mapped into this process
+  unsigned* ready[kIpcMaxRanks];    // rank j's ready flags [src rank][chunk]
+  unsigned* done[kIpcMaxRanks];     // rank j's done flags  [src rank][chunk]
+  float* t;                         // in/out (this launch's segment)
+  int64_t n;                        // floats in this segment
+  unsigned* ctr;                    // per-chunk use counters (local)
+  unsigned* err;                    // sticky error word (local)
+  uint64_t max_ticks;               // spin bound, 100 MHz ticks
+  float scale;                      // 1 (sum) or 1/N (avg)
+  int rank, nranks, gmax;
+};
+
+__device__ __forceinline__ bool spin_until(const unsigned* p, unsigned want, unsigned* err, uint64_t max_ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while ((int)(__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - want) < 0) {
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return false;
+    __builtin_amdgcn_s_sleep(1);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > max_ticks) {
+      __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+  }
+  return true;
+}
+
+__global__ __launch_bounds__(kIpcThreads) void ipc_allreduce_kernel(IpcArgs a) {
+  __shared__ unsigned s_e;
+  __shared__ int s_skip;
+  const int w = blockIdx.x, tid = threadIdx.x;
+  if (tid == 0) {
+    s_e = a.ctr[w] + 1u;
+    s_skip = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+  }
+  __syncthreads();
+  if (s_skip) return;  // sticky error: the host check reports it
+  const unsigned e = s_e;
+  const int R = a.rank, N = a.nranks;
+  const int64_t base = (int64_t)w * kIpcChunk;
+  const int cnt = (int)min((int64_t)kIpcChunk, a.n - base);
+
+  // 1. peers are done reading my chunk w of the previous use
+  if (tid < N && tid != R && e > 1u) spin_until(a.done[R] + tid * a.gmax + w, e - 1u, a.err, a.max_ticks);
+  __syncthreads();
+  // 2. stage my contribution, publish it
+  float* mine = a.data[R] + base;
+  const float* src = a.t + base;
+  for (int i = tid; i < cnt; i += kIpcThreads) mine[i] = src[i];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // every wave: its stores reach memory (system scope)
+  __syncthreads();
+  if (tid < N) __hip_atomic_store(a.ready[tid] + R * a.gmax + w, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  // 3. every contribution is there: fixed-order sum
+  if (tid < N) spin_until(a.ready[R] + tid * a.gmax + w, e, a.err, a.max_ticks);
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  float* dst = a.t + base;
+  for (int i = tid; i < cnt; i += kIpcThreads) {
+    float acc = a.data[0][base + i];
+    for (int j = 1; j < N; ++j) acc += a.data[j][base + i];
+    dst[i] = a.scale == 1.f ? acc : acc * a.scale;
+  }
+  __syncthreads();
+  // 4. I am done reading everyone's chunk w
+  if (tid < N) __hip_atomic_store(a.done[tid] + R * a.gmax + w, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (tid == 0) a.ctr[w] = e;
+}
+
+class IpcComm {
+ public:
+  IpcComm(int rank, int nranks, int device, int64_t capacity_bytes)
+      : rank_(rank), nranks_(nranks), device_(device) {
+    TORCH_CHECK(nranks >= 1 && nranks <= kIpcMaxRanks && rank >= 0 && rank < nranks, "IpcComm: bad rank/nranks");
+    gmax_ = (int)std::max<int64_t>(1, capacity_bytes / (kIpcChunk * (int64_t)sizeof(float)));
+    cap_floats_ = (int64_t)gmax_ * kIpcChunk;
+    const size_t flags = 2 * (size_t)kIpcMaxRanks * gmax_ * sizeof(unsigned);
+    bytes_ = cap_floats_ * sizeof(float) + flags;
+    NDP_IPC_CHECK(hipSetDevice(device));
+    NDP_IPC_CHECK(hipMalloc(&base_, bytes_));
+    NDP_IPC_CHECK(hipMemset(base_, 0, bytes_));
+    NDP_IPC_CHECK(hipMalloc(&local_, (gmax_ + 1) * sizeof(unsigned)));
+    NDP_IPC_CHECK(hipMemset(local_, 0, (gmax_ + 1) * sizeof(unsigned)));
+    NDP_IPC_CHECK(hipDeviceSynchronize());  // zeroed before any peer can map it
+    peers_.assign(nranks, nullptr);
+    peers_[rank] = base_;
+    const char* t = std::getenv("NDP_FLAG_WAIT_US");
+    timeout_us_ = t ? std::atoll(t) : 30000000LL;
+  }
+  ~IpcComm() = default;  // released by destroy() (captured graphs may still reference the buffers)
+
+  py::bytes handle() const {
+    hipIpcMemHandle_t h;
+    NDP_IPC_CHECK(hipIpcGetMemHandle(&h, base_));
+    return py::bytes(h.reserved, HIP_IPC_HANDLE_SIZE);
+  }
+
+  void open(const std::vector<std::string>& handles) {
+    TORCH_CHECK((int)handles.size() == nranks_, "IpcComm.open: one handle per rank");
+    NDP_IPC_CHECK(hipSetDevice(device_));
+    for (int j = 0; j < nranks_; ++j) {
+      if (j == rank_) continue;
+      TORCH_CHECK(handles[j].size() == HIP_IPC_HANDLE_SIZE, "IpcComm.open: bad handle size");
+      hipIpcMemHandle_t h;
+      std::memcpy(h.reserved, handles[j].data(), HIP_IPC_HANDLE_SIZE);
+      void* p = nullptr;
+      NDP_IPC_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+      peers_[j] = p;
+    }
+    opened_ = true;
+  }
+
+  void all_reduce(torch::Tensor t, const std::string& op, int64_t stream) {
+    TORCH_CHECK(opened_, "IpcComm: open() the peer handles first");
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == torch::kFloat32 && t.get_device() == device_,
+                "IpcComm: contiguous float32 tensors on the communicator's device");
+    TORCH_CHECK(op == "sum" || op == "avg", "IpcComm: sum / avg only");
+    hipStream_t s = stream == 0 ? at::hip::getCurrentHIPStream().stream() : reinterpret_cast<hipStream_t>(stream);
+    IpcArgs a{};
+    for (int j = 0; j < nranks_; ++j) {
+      char* b = static_cast<char*>(peers_[j]);
+      a.data[j] = reinterpret_cast<float*>(b);
+      a.ready[j] = reinterpret_cast<unsigned*>(b + cap_floats_ * sizeof(float));
+      a.done[j] = a.ready[j] + (size_t)kIpcMaxRanks * gmax_;
+    }
+    a.ctr = static_cast<unsigned*>(local_);
+    a.err = a.ctr + gmax_;
+    a.max_ticks = (uint64_t)(timeout_us_ > 0 ? timeout_us_ : 0) * 100u;
+    a.scale = op == "avg" ? 1.f / nranks_ : 1.f;
+    a.rank = rank_;
+    a.nranks = nranks_;
+    a.gmax = gmax_;
+    float* p = t.data_ptr<float>();
+    for (int64_t off = 0; off < t.numel(); off += cap_floats_) {  // segments of the buffer capacity
+      a.t = p + off;
+      a.n = std::min<int64_t>(cap_floats_, t.numel() - off);
+      const int g = (int)((a.n + kIpcChunk - 1) / kIpcChunk);
+      hipLaunchKernelGGL(ipc_allreduce_kernel, dim3(g), dim3(kIpcThreads), 0, s, a);
+    }
+    NDP_IPC_CHECK(hipGetLastError());
+  }
+
+  void all_reduce_many(const std::vector<torch::Tensor>& ts, const std::string& op, int64_t stream) {
+    for (const auto& t : ts) all_reduce(t, op, stream);
+  }
+
+  // host-synchronising: 0 or the sticky error word
+  int64_t error() const {
+    unsigned v = 0;
+    NDP_IPC_CHECK(hipMemcpy(&v, static_cast<unsigned*>(local_) + gmax_, sizeof(unsigned), hipMemcpyDeviceToHost));
+    return v;
+  }
+  void check() const {
+    TORCH_CHECK(error() == 0, "IPC all-reduce: a peer wait timed out after ", timeout_us_ / 1e6,
+                " s (a stalled or diverged peer); the results since are invalid");
+  }
+  void destroy() {
+    if (base_ == nullptr) return;
+    for (int j = 0; j < nranks_; ++j)
+      if (j != rank_ && peers_[j] != nullptr) (void)hipIpcCloseMemHandle(peers_[j]);
+    (void)hipFree(base_);
+    (void)hipFree(local_);
+    base_ = local_ = nullptr;
+    opened_ = false;
+  }
+  int rank() const { return rank_; }
+  int nranks() const { return nranks_; }
+  int device() const { return device_; }
+  int64_t capacity() const { return cap_floats_ * sizeof(float); }
+  bool alive() const { return base_ != nullptr; }
+
+ private:
+  int rank_, nranks_, device_;
+  int gmax_ = 0;
+  int64_t cap_floats_ = 0;
+  size_t bytes_ = 0;
+  int64_t timeout_us_ = 0;
+  void* base_ = nullptr;
+  void* local_ = nullptr;
+  bool opened_ = false;
+  std::vector<void*> peers_;
+};
+
+}  // namespace
+
+void register_ipc(py::module& m) {
+  py::class_<IpcComm, std::shared_ptr<IpcComm>>(m, "IpcComm")
+      .def(py::init<int, int, int, int64_t>(), py::arg("rank"), py::arg("nranks"), py::arg("device"),
+           py::arg("capacity_bytes") = 8 << 20)
+      .def("handle", &IpcComm::handle)
+      .def("open", &IpcComm::open)
+      .def("all_reduce", &IpcComm::all_reduce, py::arg("t"), py::arg("op") = "sum", py::arg("stream") = 0)
+      .def("all_reduce_many", &IpcComm::all_reduce_many, py::arg("ts"), py::arg("op") = "sum", py::arg("stream") = 0)
+      .def("error", &IpcComm::error)
+      .def("check", &IpcComm::check)
+      .def("destroy", &IpcComm::destroy)
+      .def_property_readonly("rank", &IpcComm::rank)
+      .def_property_readonly("nranks", &IpcComm::nranks)
+      .def_property_readonly("device", &IpcComm::device)
+      .def_property_readonly("capacity", &IpcComm::capacity)
+      .def_property_readonly("alive", &IpcComm::alive);
+}

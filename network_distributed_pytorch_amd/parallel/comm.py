@@ -26,6 +26,10 @@ MI355X design:
     (:attr:`Communicator.active`): a one-GPU rehearsal of the N > 1 RCCL path whose sums
     are the identity, so results match the world-size-1 no-op path.
   * ``NDP_NATIVE_COMM=0`` forces the c10d data plane.
+  * ``NDP_COMM=ipc`` (opt-in) replaces RCCL with :class:`IpcDataPlane`: one-shot all-reduce
+    kernels on HIP IPC peer memory (csrc/ipc.hip) — stream-ordered and graph-capturable like
+    the RCCL plane, and usable by several ranks sharing ONE GPU (RCCL refuses that), which is
+    how the captured, backward-overlapped multi-rank step is exercised on a one-GPU box.
 """
 from __future__ import annotations
 
@@ -189,6 +193,61 @@ def _native_wanted() -> bool:
     return os.environ.get("NDP_NATIVE_COMM", "1") != "0"
 
 
+def _comm_kind() -> str:
+    return os.environ.get("NDP_COMM", "rccl")
+
+
+class IpcDataPlane:
+    """Stream-ordered data plane on HIP IPC peer memory (csrc/ipc.hip): one-shot
+    fixed-order all-reduce kernels, graph-capturable, bitwise identical on every rank.
+    Opt-in (``NDP_COMM=ipc``) and usable where RCCL is not — several ranks sharing one GPU
+    (gloo process group for the bootstrap).  broadcast / all_gather (init-time only) go
+    through the c10d group, blocking."""
+
+    def __init__(self, group, device: torch.device, capacity_bytes: int = 8 << 20):
+        from ..ops import ext
+
+        X = ext()
+        ranks = dist.get_process_group_ranks(group) if group is not None else list(range(dist.get_world_size()))
+        self.group = group
+        self.rank_in_group = dist.get_rank(group)
+        self._c = X.IpcComm(self.rank_in_group, len(ranks), device.index if device.index is not None else 0,
+                            int(capacity_bytes))
+        store = dist.distributed_c10d._get_default_store()
+        IpcDataPlane._n = getattr(IpcDataPlane, "_n", 0) + 1
+        key = "ndp_ipc/{}/{}".format("-".join(map(str, ranks)), IpcDataPlane._n)
+        store.set(f"{key}/{self.rank_in_group}", self._c.handle())
+        handles = [store.get(f"{key}/{r}") for r in range(len(ranks))]
+        self._c.open(handles)
+        dist.barrier(group=group)  # every rank mapped every buffer before the first collective
+
+    @property
+    def nranks(self) -> int:
+        return self._c.nranks
+
+    def all_reduce(self, t: torch.Tensor, op: str = "sum"):
+        self._c.all_reduce(t, op)
+
+    def all_reduce_many(self, ts):
+        self._c.all_reduce_many(list(ts))
+
+    def broadcast(self, t: torch.Tensor, src: int = 0):
+        torch.cuda.current_stream().synchronize()
+        dist.broadcast(t, src=src, group=self.group)
+
+    def all_gather(self, out: torch.Tensor, t: torch.Tensor):
+        # through host memory: gloo gathers no device tensors (init-time / check-time only)
+        host = [torch.empty(t.numel(), dtype=t.dtype) for _ in range(self.nranks)]
+        dist.all_gather(host, t.reshape(-1).cpu(), group=self.group)
+        out.copy_(torch.cat(host).to(out.device))
+
+    def check(self):
+        self._c.check()
+
+    def destroy(self):
+        self._c.destroy()
+
+
 def create_native_comm(group=None, device: Optional[torch.device] = None):
     """Bootstrap an :class:`RcclComm` over ``group`` (collective: every rank must call it).
 
@@ -198,14 +257,17 @@ def create_native_comm(group=None, device: Optional[torch.device] = None):
     """
     if not (_native_wanted() and dist.is_available() and dist.is_initialized() and torch.cuda.is_available()):
         return None
+    from ..ops import native_available, ext
+
+    if not native_available():
+        return None
+    if _comm_kind() == "ipc":  # opt-in peer-memory data plane (any bootstrap backend)
+        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        return IpcDataPlane(group, dev)
     try:
         if dist.get_backend(group) != "nccl":
             return None
     except Exception:
-        return None
-    from ..ops import native_available, ext
-
-    if not native_available():
         return None
     X = ext()
     dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -272,7 +334,7 @@ class Communicator:
     @property
     def backend(self) -> str:
         if self._native is not None:
-            return "rccl-native"
+            return "ipc-native" if isinstance(self._native, IpcDataPlane) else "rccl-native"
         if not self.active:
             return "none"
         try:

@@ -39,8 +39,11 @@ class ReplicaChecker:
     def check(self, step: int, force: bool = False) -> bool:
         if not force and step % self.every:
             return True
-        local = torch.tensor([checksum(self.flat)], dtype=torch.float64,
-                             device=self.flat.device if self.comm.world_size > 1 and self.flat.is_cuda else "cpu")
+        on_dev = self.comm.world_size > 1 and self.flat.is_cuda
+        if on_dev:
+            import torch.distributed as dist
+            on_dev = dist.get_backend(self.comm.group) != "gloo"  # gloo gathers host tensors only
+        local = torch.tensor([checksum(self.flat)], dtype=torch.float64, device=self.flat.device if on_dev else "cpu")
         outs = [torch.zeros_like(local) for _ in range(self.comm.world_size)]
         if self.comm.world_size > 1:
             import torch.distributed as dist

@@ -17,7 +17,7 @@ CSRC = os.path.join("network_distributed_pytorch_amd", "csrc")
 SOURCES = [os.path.join(CSRC, f) for f in ("bindings.cpp", "plan.cpp", "comm.cpp", "powersgd.hip", "orth.hip",
                                                 "multitensor.hip", "batchnorm.hip", "attention.hip", "conv.hip",
                                                 "pool.hip", "embedding.hip", "linear.hip", "loss.hip", "layernorm.hip",
-                                                "tgemm.hip")]
+                                                "tgemm.hip", "ipc.hip")]
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 # RCCL: link the copy torch already loads (SONAME librccl.so.1), so the process holds ONE
 # RCCL whether c10d or the native communicator (csrc/comm.cpp) creates a communicator

@@ -4,7 +4,7 @@ cd $GRAFT_REPO_ROOT
 O=gpurun_out/r3tg
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_tgconv_gpu.py tests/test_bench_gpu.py -x -v --timeout 200 --timeout-method thread > $O/pytest.log 2>&1
+timeout -k 10 700 python -u -m pytest tests/test_tgconv_gpu.py tests/test_bench_gpu.py tests/test_ipc_gpu.py -x -v --timeout 200 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|Error|error" $O/pytest.log | tail -15
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 for cfg in "--global-batch 512" "--global-batch 64" "--model resnet50 --reducer dense" "--model resnet152"; do
