@@ -185,8 +185,8 @@ void psgd_q(torch::Tensor geom, torch::Tensor ptrs, torch::Tensor items, torch::
   check_launch("launch_psgd_q");
 }
 
-// scratch: float32 tensor of >= 2*n_items*kMaxRank partials; ctr: int32 tensor of
-// >= n_mats + 1 words (counters, then the error word at index n_mats)
+// scratch: float32 tensor of >= 2*n_items*kMaxRank partials; ctr: int64 tensor of
+// >= n_mats + 1 words (64-bit counters, then the uint32 error word in word n_mats)
 // items may be a slice of the plan's full item list (one PowerSGD group); n_items_total
 // (the full list's length, -1 = this slice) fixes the double-buffered slab layout
 void psgd_orth(torch::Tensor geom, torch::Tensor items, torch::Tensor p, double p_div, double eps,
@@ -199,12 +199,14 @@ void psgd_orth(torch::Tensor geom, torch::Tensor items, torch::Tensor p, double 
   TORCH_CHECK(n_total >= n_items, "orth: n_items_total smaller than the item slice");
   const int n_mats = (int)n_of(geom, sizeof(MatGeom));
   TORCH_CHECK(scratch.numel() >= 2LL * n_total * ndp::kMaxRank, "orth scratch too small");
-  TORCH_CHECK(ctr.numel() * ctr.element_size() >= 4LL * (n_mats + 1), "orth counters too small");
-  auto* c = reinterpret_cast<unsigned*>(ctr.data_ptr());
+  // [n_mats x uint64 barrier counters][uint32 error word]
+  TORCH_CHECK(ctr.numel() * ctr.element_size() >= 8LL * n_mats + 4, "orth counters too small");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(ctr.data_ptr()) & 7) == 0, "orth counters: 8-B aligned");
+  auto* c = reinterpret_cast<unsigned long long*>(ctr.data_ptr());
   ndp::launch_psgd_orth(reinterpret_cast<const MatGeom*>(geom.data_ptr()),
                         reinterpret_cast<const ndp::OrthItem*>(items.data_ptr()), n_items, n_mats,
                         p.data_ptr<float>(), (float)p_div, (float)eps, max_rank,
-                        scratch.data_ptr<float>(), c, c + n_mats, n_total,
+                        scratch.data_ptr<float>(), c, reinterpret_cast<unsigned*>(c + n_mats), n_total,
                         max_spins < 0 ? ndp::kOrthMaxSpins : (unsigned)max_spins, cur_stream());
   check_launch("launch_psgd_orth");
 }

@@ -72,10 +72,10 @@ void launch_psgd_p(const MatGeom* geom, const MatPtrs* ptrs, const PItem* items,
                    const float* q_warm, float* p_part, int fuse_ef, int max_rank, hipStream_t s);
 void launch_psgd_q(const MatGeom* geom, const MatPtrs* ptrs, const QItem* items, int n_items,
                    const float* p_hat, float* q_part, int max_rank, hipStream_t s);
-// partial: 2 * n_items_total * kMaxRank floats; counters: n_mats uint32 (zeroed by the launcher);
+// partial: 2 * n_items_total * kMaxRank floats; counters: n_mats uint64 (zeroed once, never reset);
 // items may be a slice [k0, k0 + n_items) of an n_items_total list (slab0 indexes are global)
 void launch_psgd_orth(const MatGeom* geom, const OrthItem* items, int n_items, int n_mats, float* p,
-                      float p_div, float eps, int max_rank, float* partial, unsigned* counters,
+                      float p_div, float eps, int max_rank, float* partial, unsigned long long* counters,
                       unsigned* err, int n_items_total, unsigned max_spins, hipStream_t s);
 int orth_rows_per_thread(int max_rank);
 // workgroups of ONE matrix the MGS barrier may span: occupancy x CUs / 2 (-1: no device)

@@ -9,6 +9,9 @@
 //  * ONE launch for every matrix.  Matrix i is split into nwg_i workgroups of 256*RPT rows;
 //    each thread keeps its RPT rows x RMAX columns in VGPRs for the whole factorisation
 //    (P is read once and written once; every column step is register work + reductions).
+//  * One column reduction per step (r cross-workgroup barriers per launch, not 2r - 1): the
+//    norm and every projection coefficient of column i come from the same dot products
+//    <u_i, v_j>, j >= i, taken before u_i is normalised.
 //  * Column reductions: wave butterfly (bitwise-identical in every lane) -> fixed-order LDS
 //    combine -> for nwg_i > 1 a fixed-order sum of per-workgroup partial slabs exchanged
 //    through the agent-scope release / acquire protocol of cdna_hip_programming.md §6
@@ -17,8 +20,8 @@
 //    rank (same plan), computes the bitwise-identical result: replicas stay consistent.
 //  * Partial slabs are double-buffered by barrier parity (a fast workgroup can be at most
 //    one barrier ahead).  Counters are never reset (no memset node per launch): every
-//    workgroup increments its matrix counter exactly once per barrier, so a launch moves it
-//    by period = (2r - 1) * nwg and each launch starts on a multiple of the period; a
+//    workgroup increments its 64-bit matrix counter exactly once per barrier, so a launch
+//    moves it by period = r * nwg and each launch starts on a multiple of the period; a
 //    workgroup reads its base on entry (before barrier 0 can complete, so the counter is
 //    then in [base, base + nwg)).  Spins are bounded and report through an error word
 //    instead of hanging the GPU.
@@ -58,7 +61,7 @@ __device__ __forceinline__ void block_sum_o(float (&v)[K], float* red /*[4][K]*/
 
 struct OrthCtx {
   float* partial;     // [2][n_items][kMaxRank]
-  unsigned* ctr;      // [n_mats]
+  unsigned long long* ctr;  // [n_mats], 64-bit: never wraps
   unsigned* err;      // [1]
   int n_items;
   unsigned max_spins; // barrier spin bound (s_sleep 2 each) before reporting a timeout
@@ -67,7 +70,7 @@ struct OrthCtx {
 // Sum v[] over all workgroups of the matrix (deterministic, identical everywhere).
 template <int K>
 __device__ __forceinline__ void group_sum(float (&v)[K], float* red, const OrthItem& it, const OrthCtx& cx,
-                                          int& bar, unsigned base, int* bad) {
+                                          int& bar, unsigned long long base, int* bad) {
   block_sum_o<K>(v, red);
   if (it.nwg == 1) return;
   float* slab = cx.partial + ((size_t)(bar & 1) * cx.n_items + it.slab0) * kMaxRank;
@@ -81,10 +84,10 @@ __device__ __forceinline__ void group_sum(float (&v)[K], float* red, const OrthI
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(cx.ctr + it.mat, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned target = base + (unsigned)(bar + 1) * (unsigned)it.nwg;
+    __hip_atomic_fetch_add(cx.ctr + it.mat, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long target = base + (unsigned long long)(bar + 1) * (unsigned long long)it.nwg;
     unsigned spins = 0;
-    while ((int)(__hip_atomic_load(cx.ctr + it.mat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+    while ((long long)(__hip_atomic_load(cx.ctr + it.mat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
       __builtin_amdgcn_s_sleep(2);
       if (++spins > cx.max_spins) {  // report (and poison, below) instead of hanging
         __hip_atomic_fetch_or(cx.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -118,14 +121,14 @@ __global__ __launch_bounds__(256) void psgd_orth_mw_kernel(const MatGeom* __rest
   const int r = g.r;
   float* P = p + g.p_off;
   const int tid = threadIdx.x;
-  __shared__ unsigned base_s;
+  __shared__ unsigned long long base_s;
   if (tid == 0 && it.nwg > 1) {
-    const unsigned period = (unsigned)(2 * r - 1) * (unsigned)it.nwg;
-    const unsigned c0 = __hip_atomic_load(cx.ctr + it.mat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long period = (unsigned long long)r * (unsigned long long)it.nwg;  // r barriers per launch
+    const unsigned long long c0 = __hip_atomic_load(cx.ctr + it.mat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     base_s = c0 - c0 % period;
   }
   __syncthreads();
-  const unsigned base = it.nwg > 1 ? base_s : 0u;
+  const unsigned long long base = it.nwg > 1 ? base_s : 0ull;
 
   float v[RPT][RMAX];
 #pragma unroll
@@ -137,41 +140,48 @@ __global__ __launch_bounds__(256) void psgd_orth_mw_kernel(const MatGeom* __rest
   }
 
   int bar = 0;
+  // one reduction per column (r barriers, not 2r - 1): with u = column i before its
+  // normalisation, q[j] = <u, v_j> for j >= i gives the norm (j = i) and every projection
+  // coefficient at once: v_i = u / (sqrt(q[i]) + eps), v_j -= (q[j] / (sqrt(q[i]) + eps)) v_i
   for (int i = 0; i < r; ++i) {
-    float s[1] = {0.f};
+    float ui[RPT];
 #pragma unroll
-    for (int k = 0; k < RPT; ++k)
+    for (int k = 0; k < RPT; ++k) {
+      ui[k] = 0.f;
 #pragma unroll
       for (int c = 0; c < RMAX; ++c)
-        if (c == i) s[0] += v[k][c] * v[k][c];
-    group_sum<1>(s, red, it, cx, bar, base, &bad);
-    const float nrm = sqrtf(s[0]) + eps;
+        if (c == i) ui[k] = v[k][c];
+    }
+    float q[RMAX];
+#pragma unroll
+    for (int j = 0; j < RMAX; ++j) {
+      q[j] = 0.f;
+#pragma unroll
+      for (int k = 0; k < RPT; ++k)
+        if (j >= i) q[j] += ui[k] * v[k][j];
+    }
+    group_sum<RMAX>(q, red, it, cx, bar, base, &bad);
+    float qi = 0.f;
+#pragma unroll
+    for (int c = 0; c < RMAX; ++c)
+      if (c == i) qi = q[c];
+    const float nrm = sqrtf(qi) + eps;
     float vi[RPT];
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
-      vi[k] = 0.f;
+      vi[k] = ui[k] / nrm;
 #pragma unroll
       for (int c = 0; c < RMAX; ++c)
-        if (c == i) {
-          v[k][c] = v[k][c] / nrm;
-          vi[k] = v[k][c];
-        }
+        if (c == i) v[k][c] = vi[k];
     }
-    if (i + 1 >= r) break;
-    float d[RMAX];
 #pragma unroll
     for (int j = 0; j < RMAX; ++j) {
-      d[j] = 0.f;
+      if (j > i && j < r) {
+        const float d = q[j] / nrm;
 #pragma unroll
-      for (int k = 0; k < RPT; ++k)
-        if (j > i) d[j] += vi[k] * v[k][j];
+        for (int k = 0; k < RPT; ++k) v[k][j] = v[k][j] - d * vi[k];
+      }
     }
-    group_sum<RMAX>(d, red, it, cx, bar, base, &bad);
-#pragma unroll
-    for (int k = 0; k < RPT; ++k)
-#pragma unroll
-      for (int j = 0; j < RMAX; ++j)
-        if (j > i && j < r) v[k][j] = v[k][j] - d[j] * vi[k];
   }
 
   __syncthreads();
@@ -195,7 +205,7 @@ int orth_rows_per_thread(int max_rank) {
 }
 
 void launch_psgd_orth(const MatGeom* geom, const OrthItem* items, int n_items, int n_mats, float* p,
-                      float p_div, float eps, int max_rank, float* partial, unsigned* counters,
+                      float p_div, float eps, int max_rank, float* partial, unsigned long long* counters,
                       unsigned* err, int n_items_total, unsigned max_spins, hipStream_t s) {
   if (n_items <= 0) return;
   OrthCtx cx{partial, counters, err, n_items_total, max_spins};

@@ -86,7 +86,7 @@ def orthogonalize(matrix: torch.Tensor, eps: float = 1e-8) -> torch.Tensor:
         X = ext()
         geom, items, n_items, max_rank = X.make_orth_geom([(int(n), int(m), 0)])
         scratch = torch.empty(2 * n_items * X.MAX_RANK, dtype=torch.float32, device=matrix.device)
-        ctr = torch.zeros(2, dtype=torch.int32, device=matrix.device)
+        ctr = torch.zeros(2, dtype=torch.int64, device=matrix.device)
         X.psgd_orth(geom.to(matrix.device), items.to(matrix.device), matrix.view(-1), 1.0, float(eps),
                     int(max_rank), scratch, ctr)
         return matrix
@@ -162,7 +162,8 @@ class _PlanBuffers:
             self.item_start = {k: d[k + "_item_start"] for k in ("p", "q", "u", "orth")}
             self.orth_items = d["orth_items"].to(device)
             self.orth_scratch = torch.zeros(max(1, 2 * d["n_orth_items"] * X.MAX_RANK), **f32)
-            self.orth_ctr = torch.zeros(len(shapes) + 1, dtype=torch.int32, device=device)
+            # 64-bit MGS barrier counters (never wrap) + the error word (low half of the last)
+            self.orth_ctr = torch.zeros(len(shapes) + 1, dtype=torch.int64, device=device)
             nb = max(1, len(shapes)) * X.SIZEOF_MATGEOM
             self.geom = torch.zeros(nb, dtype=torch.uint8, device=device)
             self.ptrs = torch.zeros(nb, dtype=torch.uint8, device=device)
