@@ -338,18 +338,18 @@ def worker(args, level: int, world: int, rank: int, local: int) -> None:
         per_gpu = args.global_batch // world   # reference: bsz = int(512 / float(size))
     else:
         per_gpu = args.batch
-    hb.beat("build+capture", 600)
+    hb.beat("build+capture", 300)
     wl = Workload(a, device, world, rank)
     step = wl.make_step(per_gpu)
     for j in range(args.warmup):
         step(j)
         torch.cuda.synchronize()
-        hb.beat(f"warmup {j + 1}/{args.warmup}", 300)
-    hb.beat("check:warmup", 300)
+        hb.beat(f"warmup {j + 1}/{args.warmup}", 120)
+    hb.beat("check:warmup", 120)
     health_check(wl, world, "after warm-up")
-    hb.beat("timed", 300 + 30 * args.steps)
+    hb.beat("timed", 120 + 10 * args.steps)
     elapsed = wl.time(step, args.steps, 0, start=args.warmup)  # warmed up above
-    hb.beat("check:timed", 300)
+    hb.beat("check:timed", 120)
     health = health_check(wl, world, "after the timed steps")
     comm_stats = wl.comm.stats.as_dict()
     final_loss = float(wl.loss_acc.item()) / max(1, args.warmup + args.steps)

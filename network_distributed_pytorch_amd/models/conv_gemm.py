@@ -36,6 +36,7 @@ from ..ops import gradfinish
 from ..ops._ext import ext
 from ..ops import conv as _conv
 from ..ops.conv import DirectConvFn, direct_plan, side_stream
+from ..ops.gradarena import grad_buffer
 from ..ops.gradlink import InjectGrad
 from ..ops.tgconv import TgConvFn, tg_plan
 
@@ -151,7 +152,7 @@ class _ToeplitzConv(torch.autograd.Function):
             main = torch.cuda.current_stream()
             fork = _conv.FORK_WGRAD and ctx.needs_input_grad[0] and ctx.needs_input_grad[1]
             if ctx.needs_input_grad[1]:
-                dw = torch.empty(ctx.w_shape, device=G.device, dtype=G.dtype)
+                dw = grad_buffer(ctx.weight)  # the dense arm's arena slice when registered
                 dwt = torch.empty(w_big.shape, device=G.device, dtype=G.dtype)
                 side = side_stream(G.device) if fork else main
                 side.wait_stream(main)

@@ -20,6 +20,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ._ext import ext
+from .gradarena import grad_buffer
 
 __all__ = ["BatchNormAct2d", "bn_act"]
 
@@ -45,6 +46,7 @@ class _BNActFn(torch.autograd.Function):
         ctx.has_res = res is not None
         ctx.link = link  # ops/gradlink.py: the residual gradient goes here, not to `res`
         ctx.has_w = weight is not None
+        ctx.params = (weight, bias)  # the Parameters: their arena slices take the gradients
         ctx.save_for_backward(x, y if relu else None, weight, save_mean, save_invstd, part)
         ctx.mark_non_differentiable(save_mean, save_invstd)
         return y
@@ -55,8 +57,9 @@ class _BNActFn(torch.autograd.Function):
         dy = dy.contiguous()
         dx = torch.empty_like(x)
         dres = torch.empty_like(x) if ctx.has_res else None
-        dgamma = torch.empty_like(weight) if ctx.has_w else None
-        dbeta = torch.empty_like(weight) if ctx.has_w else None
+        # the dense arm's arena slices when registered (ops/gradarena.py)
+        dgamma = grad_buffer(ctx.params[0], weight) if ctx.has_w else None
+        dbeta = grad_buffer(ctx.params[1], weight) if ctx.has_w else None
         dypart, nslab = ctx.grad_slab.take_bwd() if ctx.grad_slab is not None else (None, 0)
         ext().bn_bwd(dy, y, x, weight, save_mean, save_invstd, dx, dres, dgamma, dbeta, part, ctx.relu, ctx.single,
                      dypart, nslab)

@@ -20,6 +20,7 @@ import torch
 
 from . import gradfinish
 from ._ext import ext
+from .gradarena import grad_buffer
 
 __all__ = ["direct_plan", "conv2d_direct", "DirectConvFn", "side_stream"]
 
@@ -103,7 +104,7 @@ class DirectConvFn(torch.autograd.Function):
         fork = FORK_WGRAD and ctx.needs_input_grad[0] and ctx.needs_input_grad[1]
         if ctx.needs_input_grad[1]:
             B = x.shape[0]
-            dw = torch.empty_like(weight)
+            dw = grad_buffer(ctx.weight, weight)  # the dense arm's arena slice when registered
             part = torch.empty((B // wgrad_imgs) * weight.numel(), device=x.device, dtype=x.dtype)
             side = side_stream(x.device) if fork else main
             side.wait_stream(main)

@@ -26,6 +26,7 @@ import torch
 
 from . import gradfinish
 from ._ext import ext
+from .gradarena import grad_buffer
 
 __all__ = ["tg_plan", "TgConvFn", "enabled"]
 
@@ -94,7 +95,7 @@ class TgConvFn(torch.autograd.Function):
         dy = dy.contiguous()
         dx = dw = None
         if ctx.needs_input_grad[1]:
-            dw = torch.empty_like(w)
+            dw = grad_buffer(ctx.weight, w)  # the dense arm's arena slice when registered
             defer = gradfinish.can_defer(ctx.weight)
             if cls == POINTWISE:
                 part = _scratch(ws, dw.numel(), x)

@@ -3,8 +3,11 @@ backward-overlapped MI355X arm.
 
 * :func:`average_gradients` — reference semantics (ddp_guide_cifar10/ddp_init.py:57-62):
   one blocking SUM all-reduce per parameter followed by ``grad /= world_size``.
-* :class:`BucketedDataParallel` — gradients are flattened into ONE arena laid out in
-  reverse parameter order (≈ backward production order) and cut into contiguous buckets.
+* :class:`BucketedDataParallel` — gradients live in ONE arena laid out in reverse
+  parameter order (≈ backward production order) and cut into contiguous buckets.  The
+  native conv / BN backwards write their parameters' gradients straight into the arena
+  slices (ops/gradarena.py, adopted by autograd as ``.grad``); only gradients produced
+  elsewhere (ATen Linear, MIOpen) are copied in by the bucket's flatten launch.
   A post-accumulate-grad hook launches each bucket as soon as its last gradient lands, in
   bucket order on every rank:
     - stream-ordered data plane (native RCCL communicator, csrc/comm.cpp; or world size
@@ -31,7 +34,7 @@ from typing import List, Optional
 
 import torch
 
-from ..ops import SegPlan, capturing, gradfinish, sgd_momentum_
+from ..ops import SegPlan, capturing, gradarena, gradfinish, sgd_momentum_
 from .comm import Communicator, all_reduce, world_size
 
 __all__ = ["average_gradients", "BucketedDataParallel", "DEFAULT_BUCKET_MB"]
@@ -86,6 +89,11 @@ class BucketedDataParallel:
                 p.grad = None
         if broadcast_params:
             self.comm.broadcast(self.x, src=0)
+        # the native backwards write these parameters' gradients straight into their arena
+        # slices (ops/gradarena.py): no flatten copy for them
+        if self.device.type == "cuda":
+            for p in self.params:
+                gradarena.register(p, self.g, offs[id(p)])
         # buckets: contiguous arena ranges in backward order
         cap = max(1, int(bucket_mb * 1024 * 1024 / 4))
         self.buckets = []  # [start, end, [params]]
@@ -103,6 +111,7 @@ class BucketedDataParallel:
         if cur:
             self.buckets.append([start, cur_end, cur])
         self._segs = [SegPlan([], self.device, capacity=len(b[2])) for b in self.buckets]
+        self._copies = [True] * len(self.buckets)
         self._ready = [0] * len(self.buckets)
         self._works = [None] * len(self.buckets)
         self._launched = [False] * len(self.buckets)
@@ -130,19 +139,27 @@ class BucketedDataParallel:
         """Bytes of every bucket all-reduce of one step (link-model input)."""
         return [4 * (e - s) for s, e, _ in self.buckets]
 
-    def _bind(self, b: int):
+    def _bind(self, b: int) -> bool:
+        """Copy table of bucket b's gradients that are NOT already in the arena; False if
+        every gradient was written in place (no flatten launch)."""
         _, _, ps = self.buckets[b]
         specs = []
         for p in ps:
-            if p.grad is None:
-                p.grad = torch.zeros_like(p)
             o = self.offsets[id(p)]
-            specs.append((p.grad.reshape(-1), self.g[o: o + p.numel()], 1, 0, 1.0))
+            dst = self.g[o: o + p.numel()]
+            if p.grad is None:  # unused parameter: zero gradient, in place
+                p.grad = dst.view_as(p)
+                p.grad.zero_()
+            if p.grad.data_ptr() == dst.data_ptr():
+                continue
+            specs.append((p.grad.reshape(-1), dst, 1, 0, 1.0))
         self._segs[b].set(specs)
+        self._copies[b] = bool(specs)
+        return self._copies[b]
 
     def _flatten(self, b: int):
-        self._bind(b)
-        self._segs[b].run()            # one flatten launch per bucket
+        if self._bind(b):
+            self._segs[b].run()        # one flatten launch per bucket (only copied gradients)
 
     def _allreduce(self, b: int):
         s, e, _ = self.buckets[b]
@@ -152,10 +169,11 @@ class BucketedDataParallel:
     def _launch(self, b: int):
         gradfinish.flush()  # deferred conv grad-W sums / folds (launches on the compute stream)
         if self.stream_mode:
-            self._bind(b)              # table upload on the compute stream, before the fork
+            copies = self._bind(b)     # table upload on the compute stream, before the fork
 
             def flatten_reduce():
-                self._segs[b].run()
+                if copies:
+                    self._segs[b].run()
                 self._allreduce(b)     # ddp_guide_cifar10/ddp_init.py:61, one per bucket
             self.comm.side_launch(flatten_reduce)
         else:

@@ -1,0 +1,36 @@
+"""Dense arm: native conv / BN backwards write gradients straight into the bucket arena
+(ops/gradarena.py) — no flatten copy for them — with the same update as
+the reference arm (per-parameter all-reduce + torch SGD, ddp_guide_cifar10/ddp_init.py:57-62,111)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def test_dense_arena_gradients_in_place(device):
+    from network_distributed_pytorch_amd.models import build_model
+    from network_distributed_pytorch_amd.parallel.ddp import BucketedDataParallel
+
+    torch.manual_seed(0)
+    ours = build_model("resnet18", 10).to(device)
+    ref = build_model("resnet18", 10).to(device)
+    ref.load_state_dict(ours.state_dict())
+    ddp = BucketedDataParallel(ours, lr=0.1, momentum=0.9)
+    opt = torch.optim.SGD(ref.parameters(), lr=0.1, momentum=0.9)
+    lo, hi = ddp.g.data_ptr(), ddp.g.data_ptr() + ddp.g.numel() * 4
+    for step in range(3):
+        x = torch.randn(32, 3, 32, 32, device=device)
+        y = torch.randint(0, 10, (32,), device=device)
+        ddp.zero_grad()
+        F.cross_entropy(ours(x), y).backward()
+        if step == 0:
+            inside = {n: lo <= p.grad.data_ptr() < hi for n, p in ours.named_parameters()}
+            assert all(v for n, v in inside.items() if ".bn" in n or "conv" in n or "downsample" in n), inside
+            assert not inside["fc.weight"]  # ATen Linear: copied by the bucket flatten
+        ddp.step()
+        opt.zero_grad()
+        F.cross_entropy(ref(x), y).backward()
+        opt.step()
+    for (n, a), (_, b) in zip(ours.named_parameters(), ref.named_parameters()):
+        assert torch.allclose(a, b, rtol=1e-4, atol=1e-5), n
