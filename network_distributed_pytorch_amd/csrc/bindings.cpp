@@ -640,6 +640,25 @@ py::tuple tg_plan(const std::vector<int64_t>& geom, int64_t B) {
   return py::make_tuple(cls, ndp::tg_splits(g, (int)B, 0), ndp::tg_splits(g, (int)B, 1), ndp::tg_splits(g, (int)B, 2));
 }
 
+// the GEMM description tgemm launches for (geom, B, dir) — host-side, for the CPU emulation
+// test of the index algebra (tests/test_tgemm_cpu.py)
+py::dict tg_describe(const std::vector<int64_t>& geom, int64_t B, int64_t dir) {
+  const ndp::ConvGeom g = conv_geom(geom);
+  TORCH_CHECK(ndp::tg_class(g) >= 0, "tg_describe: no tgemm path");
+  bool akf = false, bnf = false;
+  const ndp::TgArgs a = ndp::tg_args(g, (int)B, (int)dir, &akf, &bnf);
+  auto idx = [](const ndp::TgIndex& t) { return py::make_tuple(t.so, t.si, t.sh); };
+  py::dict d;
+  d["am"] = idx(a.am); d["ak"] = idx(a.ak); d["bk"] = idx(a.bk); d["bn"] = idx(a.bn);
+  d["cm"] = idx(a.cm); d["cn"] = idx(a.cn);
+  d["M"] = a.M; d["N"] = a.N; d["K"] = a.K; d["slab"] = a.slab; d["gather"] = a.gather;
+  std::vector<int> tab(a.tab, a.tab + 64);
+  d["tab"] = tab;
+  d["akf"] = akf; d["bnf"] = bnf;
+  d["splits"] = ndp::tg_splits(g, (int)B, (int)dir);
+  return d;
+}
+
 static int tg_batch(const torch::Tensor& t, const ndp::ConvGeom& g, const char* who) {
   TORCH_CHECK(ndp::tg_class(g) >= 0, who, ": no tgemm path for this geometry");
   return (int)t.size(0);
@@ -951,6 +970,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("part") = py::none(), py::arg("addend") = py::none(), py::arg("defer") = false);
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("part"), py::arg("dw"), py::arg("geom"));
   m.def("tg_plan", &tg_plan);
+  m.def("tg_describe", &tg_describe);
   m.def("tg_fwd", &tg_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("geom"), py::arg("part") = py::none(),
         py::arg("defer") = false);
   m.def("tg_dgrad", &tg_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("geom"),

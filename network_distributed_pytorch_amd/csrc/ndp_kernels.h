@@ -254,6 +254,8 @@ struct TgArgs {
 constexpr int TG_POINTWISE = 0;  // 1x1 stride-1, power-of-two map
 constexpr int TG_SMALL = 1;      // input map <= 16, output map <= 4 pixels (powers of two)
 int tg_class(const ConvGeom& g);
+// the GEMM description of direction dir (pointers null) + the load mappings of its launch
+TgArgs tg_args(const ConvGeom& g, int B, int dir, bool* akf, bool* bnf);
 // split-K slabs of direction dir (0 fwd, 1 grad-x, 2 grad-W) for batch B (1 = no scratch)
 int tg_splits(const ConvGeom& g, int B, int dir);
 // defer: leave the split-K slabs in part and return their count (1 = y / dx final)

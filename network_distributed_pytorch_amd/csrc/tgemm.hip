@@ -241,90 +241,103 @@ int tg_splits(const ConvGeom& g, int B, int dir) {
 }
 
 // y [B, Co, OH, OW] = conv(x [B, C, H, W], w); part: tg_splits(g, B, 0) * numel(y) floats (or null if 1)
-int launch_tg_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s,
-                  bool defer) {
+// the GEMM description of one direction (operand pointers / scratch left null), and the
+// load mappings (A k-fast, B n-fast) the launch uses
+TgArgs tg_args(const ConvGeom& g, int B, int dir, bool* akf, bool* bnf) {
   const int cls = tg_class(g);
   const int hw = g.H * g.W, ohw = g.OH * g.OW, T = g.KH * g.KW;
   TgArgs a{};
-  a.part = part;
-  a.c = y;
-  if (cls == TG_POINTWISE) {
+  if (dir == 0 && cls == TG_POINTWISE) {
     const int sh = ilog2_exact(hw);
-    a.a = w; a.am = plain(g.C); a.ak = plain(1);                       // W [Co][C]
-    a.b = x; a.bk = plain(hw); a.bn = comp(sh, (int64_t)g.C * hw, 1);   // X [b][c][p]
-    a.cm = plain(hw); a.cn = comp(sh, (int64_t)g.Co * hw, 1);          // Y [b][co][p]
+    a.am = plain(g.C); a.ak = plain(1);                         // W [Co][C]
+    a.bk = plain(hw); a.bn = comp(sh, (int64_t)g.C * hw, 1);    // X [b][c][p]
+    a.cm = plain(hw); a.cn = comp(sh, (int64_t)g.Co * hw, 1);   // Y [b][co][p]
     a.M = g.Co; a.N = B * hw; a.K = g.C;
     a.slab = (int64_t)B * g.Co * hw;
-    return run(a, true, hw >= 4, tg_splits(g, B, 0), y, s, defer);
-  }
-  {
-    a.a = x; a.am = plain((int64_t)g.C * hw); a.ak = plain(1);         // X [b][(c,i)]
-    a.b = w; a.gather = 1;                                             // W[co, c, tap(i, o)]
+    *akf = true; *bnf = hw >= 4;
+  } else if (dir == 0) {
+    a.am = plain((int64_t)g.C * hw); a.ak = plain(1);           // X [b][(c,i)]
+    a.gather = 1;                                               // W[co, c, tap(i, o)]
     a.bk = comp(ilog2_exact(hw), T, 0); a.bn = comp(ilog2_exact(ohw), (int64_t)g.C * T, 0);
-    fill_tab(a, g, true);                                              // rows: i (k inner), cols: o (n inner)
-    a.cm = plain((int64_t)g.Co * ohw); a.cn = plain(1);                // Y [b][(co,o)]
+    fill_tab(a, g, true);                                       // rows: i (k inner), cols: o (n inner)
+    a.cm = plain((int64_t)g.Co * ohw); a.cn = plain(1);         // Y [b][(co,o)]
     a.M = B; a.N = g.Co * ohw; a.K = g.C * hw;
     a.slab = (int64_t)B * g.Co * ohw;
-    return run(a, true, false, tg_splits(g, B, 0), y, s, defer);
+    *akf = true; *bnf = false;
+  } else if (dir == 1 && cls == TG_POINTWISE) {
+    const int sh = ilog2_exact(hw);
+    a.am = plain(1); a.ak = plain(g.C);                         // W^T: A[c][co] = W[co][c]
+    a.bk = plain(hw); a.bn = comp(sh, (int64_t)g.Co * hw, 1);   // dY [b][co][p]
+    a.cm = plain(hw); a.cn = comp(sh, (int64_t)g.C * hw, 1);    // dX [b][c][p]
+    a.M = g.C; a.N = B * hw; a.K = g.Co;
+    a.slab = (int64_t)B * g.C * hw;
+    *akf = false; *bnf = hw >= 4;
+  } else if (dir == 1) {
+    a.am = plain((int64_t)g.Co * ohw); a.ak = plain(1);         // dY [b][(co,o)]
+    a.gather = 1;                                               // B[(co,o), (c,i)] = W[co, c, tap(i, o)]
+    a.bk = comp(ilog2_exact(ohw), (int64_t)g.C * T, 0); a.bn = comp(ilog2_exact(hw), T, 0);
+    fill_tab(a, g, false);                                      // rows: o (k inner), cols: i (n inner)
+    a.cm = plain((int64_t)g.C * hw); a.cn = plain(1);           // dX [b][(c,i)]
+    a.M = B; a.N = g.C * hw; a.K = g.Co * ohw;
+    a.slab = (int64_t)B * g.C * hw;
+    *akf = true; *bnf = false;
+  } else if (cls == TG_POINTWISE) {
+    const int sh = ilog2_exact(hw);
+    a.am = plain(hw); a.ak = comp(sh, (int64_t)g.Co * hw, 1);   // dY as A[co][(b,p)]
+    a.bk = comp(sh, (int64_t)g.C * hw, 1); a.bn = plain(hw);    // X as B[(b,p)][c]
+    a.cm = plain(g.C); a.cn = plain(1);                         // dW [co][c]
+    a.M = g.Co; a.N = g.C; a.K = B * hw;
+    a.slab = (int64_t)g.Co * g.C;
+    *akf = hw >= 4; *bnf = hw == 1;
+  } else {
+    a.am = plain(1); a.ak = plain((int64_t)g.Co * ohw);         // dY as A[(co,o)][b]
+    a.bk = plain((int64_t)g.C * hw); a.bn = plain(1);           // X as B[b][(c,i)]
+    a.cm = plain((int64_t)g.C * hw); a.cn = plain(1);           // dWbig^T [(co,o)][(c,i)]
+    a.M = g.Co * ohw; a.N = g.C * hw; a.K = B;
+    a.slab = (int64_t)g.Co * ohw * g.C * hw;
+    *akf = false; *bnf = true;
   }
+  return a;
+}
+
+int launch_tg_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s,
+                  bool defer) {
+  bool akf, bnf;
+  TgArgs a = tg_args(g, B, 0, &akf, &bnf);
+  const bool pw = tg_class(g) == TG_POINTWISE;
+  a.a = pw ? w : x;
+  a.b = pw ? x : w;
+  a.c = y;
+  a.part = part;
+  return run(a, akf, bnf, tg_splits(g, B, 0), y, s, defer);
 }
 
 // dx [B, C, H, W] from dy [B, Co, OH, OW]; part: tg_splits(g, B, 1) * numel(dx) floats
 int launch_tg_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, float* part,
                     hipStream_t s, const float* addend, bool defer) {
-  const int cls = tg_class(g);
-  const int hw = g.H * g.W, ohw = g.OH * g.OW, T = g.KH * g.KW;
-  TgArgs a{};
-  a.part = part;
+  bool akf, bnf;
+  TgArgs a = tg_args(g, B, 1, &akf, &bnf);
+  const bool pw = tg_class(g) == TG_POINTWISE;
+  a.a = pw ? w : dy;
+  a.b = pw ? dy : w;
   a.c = dx;
+  a.part = part;
   a.addend = addend;
-  if (cls == TG_POINTWISE) {
-    const int sh = ilog2_exact(hw);
-    a.a = w; a.am = plain(1); a.ak = plain(g.C);                       // W^T: A[c][co] = W[co][c]
-    a.b = dy; a.bk = plain(hw); a.bn = comp(sh, (int64_t)g.Co * hw, 1);
-    a.cm = plain(hw); a.cn = comp(sh, (int64_t)g.C * hw, 1);
-    a.M = g.C; a.N = B * hw; a.K = g.Co;
-    a.slab = (int64_t)B * g.C * hw;
-    return run(a, false, hw >= 4, tg_splits(g, B, 1), dx, s, defer);
-  }
-  {
-    a.a = dy; a.am = plain((int64_t)g.Co * ohw); a.ak = plain(1);      // dY [b][(co,o)]
-    a.b = w; a.gather = 1;                                             // B[(co,o), (c,i)] = W[co, c, tap(i, o)]
-    a.bk = comp(ilog2_exact(ohw), (int64_t)g.C * T, 0); a.bn = comp(ilog2_exact(hw), T, 0);
-    fill_tab(a, g, false);                                             // rows: o (k inner), cols: i (n inner)
-    a.cm = plain((int64_t)g.C * hw); a.cn = plain(1);
-    a.M = B; a.N = g.C * hw; a.K = g.Co * ohw;
-    a.slab = (int64_t)B * g.C * hw;
-    return run(a, true, false, tg_splits(g, B, 1), dx, s, defer);
-  }
+  return run(a, akf, bnf, tg_splits(g, B, 1), dx, s, defer);
 }
 
 // POINTWISE: out = dW [Co, C]; SMALL: out = dWbig^T [Co*OH*OW, C*H*W] (fold it into dW with
-// toeplitz_fold).  part: tg_splits(g, B, 2) * numel(out) floats.  defer: leave the split-K
-// slabs in `part` and return how many (1 = `out` final).
+// toeplitz_fold).  part: tg_splits(g, B, 2) * numel(out) floats.  defer (pointwise): leave
+// the split-K slabs in `part` and return how many (1 = `out` final).
 int launch_tg_wgrad(const float* x, const float* dy, float* out, int B, const ConvGeom& g, float* part, hipStream_t s,
                     bool defer) {
-  const int cls = tg_class(g);
-  const int hw = g.H * g.W, ohw = g.OH * g.OW;
-  TgArgs a{};
-  a.part = part;
+  bool akf, bnf;
+  TgArgs a = tg_args(g, B, 2, &akf, &bnf);
+  a.a = dy;
+  a.b = x;
   a.c = out;
-  const int splits = tg_splits(g, B, 2);
-  if (cls == TG_POINTWISE) {
-    const int sh = ilog2_exact(hw);
-    a.a = dy; a.am = plain(hw); a.ak = comp(sh, (int64_t)g.Co * hw, 1);  // A[co][(b,p)]
-    a.b = x; a.bk = comp(sh, (int64_t)g.C * hw, 1); a.bn = plain(hw);    // B[(b,p)][c]
-    a.cm = plain(g.C); a.cn = plain(1);
-    a.M = g.Co; a.N = g.C; a.K = B * hw;
-    a.slab = (int64_t)g.Co * g.C;
-    return run(a, hw >= 4, hw == 1, splits, out, s, defer);
-  }
-  a.a = dy; a.am = plain(1); a.ak = plain((int64_t)g.Co * ohw);       // A[(co,o)][b]
-  a.b = x; a.bk = plain((int64_t)g.C * hw); a.bn = plain(1);          // B[b][(c,i)]
-  a.cm = plain((int64_t)g.C * hw); a.cn = plain(1);
-  a.M = g.Co * ohw; a.N = g.C * hw; a.K = B;
-  a.slab = (int64_t)g.Co * ohw * g.C * hw;
-  return run(a, false, true, splits, out, s, false);
+  a.part = part;
+  return run(a, akf, bnf, tg_splits(g, B, 2), out, s, defer && tg_class(g) == TG_POINTWISE);
 }
 
 }  // namespace ndp

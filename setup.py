@@ -19,6 +19,32 @@ SOURCES = [os.path.join(CSRC, f) for f in ("bindings.cpp", "plan.cpp", "comm.cpp
                                                 "pool.hip", "embedding.hip", "linear.hip", "loss.hip", "layernorm.hip",
                                                 "tgemm.hip", "ipc.hip")]
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+
+
+def _invalidate_on_header_change():
+    """hipcc-compiled objects carry no header dependency info for ninja: when a shared header
+    changes, drop the object directory so every translation unit is rebuilt (a stale object
+    compiled against an old declaration would leave an undefined symbol in _C*.so)."""
+    import glob
+    import hashlib
+    import shutil
+
+    h = hashlib.sha256()
+    for f in sorted(glob.glob(os.path.join(CSRC, "*.h"))):
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    digest = h.hexdigest()
+    stamp = os.path.join("build", ".headers.sha256")
+    old = open(stamp).read().strip() if os.path.exists(stamp) else None
+    if old != digest:
+        for d in glob.glob(os.path.join("build", "temp.*")):
+            shutil.rmtree(d, ignore_errors=True)
+        os.makedirs("build", exist_ok=True)
+        with open(stamp, "w") as fh:
+            fh.write(digest)
+
+
+_invalidate_on_header_change()
 # RCCL: link the copy torch already loads (SONAME librccl.so.1), so the process holds ONE
 # RCCL whether c10d or the native communicator (csrc/comm.cpp) creates a communicator
 TORCH_LIB = os.path.join(os.path.dirname(torch.__file__), "lib")
