@@ -167,8 +167,10 @@ int tg_pick_splits(int M, int N, int K, int cap) {
 int tg_cap() {
   static int v = -1;
   if (v < 0) {
+    // 4 = batchnorm.hip kMaxFusedSlabs: forward / grad-x slabs up to 4 are summed inside the
+    // fused BN kernel that consumes the conv (ops/slablink.py), i.e. at no extra launch
     const char* e = getenv("NDP_TG_MAXSPLIT");
-    v = e ? atoi(e) : 16;
+    v = e ? atoi(e) : 4;
     if (v < 1) v = 1;
   }
   return v;
