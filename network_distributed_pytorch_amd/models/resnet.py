@@ -28,6 +28,7 @@ import torch.nn as nn
 
 from ..ops.batchnorm import BatchNormAct2d
 from ..ops.gradlink import BranchLink, GradLink
+from ..ops.linear import Linear
 from ..ops.pool import MaxPool2d
 from ..ops.slablink import SlabLink
 from .conv_gemm import GemmConv2d, ToeplitzBank
@@ -143,7 +144,9 @@ class ResNet(nn.Module):
         self.layer3 = self._make_layer(block, 256, layers[2], stride=2)
         self.layer4 = self._make_layer(block, 512, layers[3], stride=2)
         self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
-        self.fc = nn.Linear(512 * block.expansion, num_classes)
+        # native deterministic bias gradient (ops/linear.py; ATen's multi-block reduce was
+        # found unreliable under hipGraph replay), same parameters / state_dict as nn.Linear
+        self.fc = (Linear if fused_bn else nn.Linear)(512 * block.expansion, num_classes)
         bank = ToeplitzBank()  # every Toeplitz layer's W_big in one launch per forward
         for m in self.modules():
             if isinstance(m, GemmConv2d):

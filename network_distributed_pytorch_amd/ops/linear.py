@@ -15,6 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ._ext import ext
+from .gradarena import grad_buffer
 from .gradlink import InjectGrad
 
 __all__ = ["Linear", "linear", "linear_gelu"]
@@ -30,6 +31,7 @@ class _LinearFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, link=None):
         ctx.save_for_backward(x, weight)
         ctx.link = link  # ops/gradlink.GradLink: a residual gradient added into grad-x (addmm_)
+        ctx.params = (weight, bias)  # the Parameters (ops/gradarena.py)
         return F.linear(x, weight, bias)
 
     @staticmethod
@@ -48,10 +50,10 @@ class _LinearFn(torch.autograd.Function):
                 dx = (g2 @ weight).view(x.shape)
         elif addend is not None:
             dx = addend.view(x.shape)
-        if ctx.needs_input_grad[1]:
-            dw = g2.t() @ x.reshape(-1, k)
+        if ctx.needs_input_grad[1]:  # straight into the dense arm's arena slice when registered
+            dw = torch.mm(g2.t(), x.reshape(-1, k), out=grad_buffer(ctx.params[0]))
         if ctx.needs_input_grad[2]:
-            db = torch.empty(n, device=g.device, dtype=g.dtype)
+            db = grad_buffer(ctx.params[1])
             ext().colsum(g2, db)
         return dx, dw, db, None
 
