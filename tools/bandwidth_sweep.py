@@ -34,7 +34,7 @@ sys.path.insert(0, ROOT)
 def run_bench(args, reducer, link, gpus, emulate=None):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(args.steps), "--warmup", str(args.warmup),
            "--model", args.model, "--reducer", reducer, "--rank", str(args.rank), "--link", link,
-           "--weak-too", "off"]
+           "--weak-too", "off", "--overlap", args.overlap]
     if args.batch:
         cmd += ["--batch", str(args.batch)]
     if emulate:
@@ -65,6 +65,9 @@ def main():
     ap.add_argument("--links", default="none,100g,10g,1g")
     ap.add_argument("--reducers", default="powersgd,dense")
     ap.add_argument("--jsonl", default=None, help="append every bench record here")
+    ap.add_argument("--overlap", choices=["auto", "on", "off"], default="on",
+                    help="gradient sync overlapped with backward on EVERY arm, the 'none' link included "
+                         "(the shipped N > 1 default), so the rows differ only in the link")
     args = ap.parse_args()
     from network_distributed_pytorch_amd.parallel.comm import LINK_PRESETS
 
