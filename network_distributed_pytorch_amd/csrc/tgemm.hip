@@ -49,9 +49,7 @@ template <bool AKF, bool BNF, bool GATHER>
 __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
   __shared__ float As[2][TBK][TBM + 1];
   __shared__ float Bs[2][TBK][TBN + 1];
-  __shared__ int8_t stab[64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (GATHER && tid < 64) stab[tid] = g.tab[tid];  // made visible by the first tile's barrier
   const int h = lane >> 5, l32 = lane & 31;
   const int wm = wave & 1, wn = wave >> 1;
   const int n0 = blockIdx.x * TBN, m0 = blockIdx.y * TBM;
@@ -59,50 +57,67 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
   const int kend = min(g.K, kbeg + g.kchunk);
   constexpr int PER = TBM * TBK / 256;  // 8 elements of each operand per thread and tile
 
-  // fixed per-thread tile coordinates; the m / n parts of the addresses are tile-invariant
-  int am[PER], ak[PER], bk[PER], bn[PER];
+  // Fixed per-thread tile coordinates.  Every operand offset splits into a tile-invariant
+  // per-element part and a per-tile part that is uniform across the workgroup: tiles start
+  // at multiples of TBK and every composite inner extent is a power of two, so
+  // off(k0 + kk) = off(k0) + off(kk) for kk < TBK (if the extent E >= TBK the tile stays
+  // inside one E-block; if E < TBK, k0 is a multiple of E).  The gathered tap is therefore
+  // fixed per element too (the k inner extent, a map of <= 16 pixels, divides TBK).  Only a
+  // scalar base moves per tile: no per-element index arithmetic in the K loop.
+  int ak[PER], bk[PER];
   int64_t aoff[PER], boff[PER];
   bool aok[PER], bok[PER];
+  const int nmask = (1 << g.bn.sh) - 1, kmask = (1 << g.bk.sh) - 1;
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int e = tid + 256 * i;
-    if (AKF) { am[i] = e / TBK; ak[i] = e % TBK; } else { ak[i] = e / TBM; am[i] = e % TBM; }
-    if (BNF) { bk[i] = e / TBN; bn[i] = e % TBN; } else { bn[i] = e / TBK; bk[i] = e % TBK; }
-    const int gm = m0 + am[i], gn = n0 + bn[i];
+    int am, bn;
+    if (AKF) { am = e / TBK; ak[i] = e % TBK; } else { ak[i] = e / TBM; am = e % TBM; }
+    if (BNF) { bk[i] = e / TBN; bn = e % TBN; } else { bn = e / TBK; bk[i] = e % TBK; }
+    const int gm = m0 + am, gn = n0 + bn;
     aok[i] = gm < g.M;
     bok[i] = gn < g.N;
-    aoff[i] = aok[i] ? tg_off(g.am, gm) : 0;
-    boff[i] = bok[i] ? (GATHER ? (int64_t)(gn >> g.bn.sh) * g.bn.so : tg_off(g.bn, gn)) : 0;
+    aoff[i] = aok[i] ? tg_off(g.am, gm) + tg_off(g.ak, ak[i]) : 0;
+    if (GATHER) {
+      const int t = g.tab[((bk[i] & kmask) << g.bn.sh) | (gn & nmask)];
+      bok[i] = bok[i] && t >= 0;  // no tap joins these pixels: a structural zero
+      boff[i] = bok[i] ? (int64_t)(gn >> g.bn.sh) * g.bn.so + (int64_t)(bk[i] >> g.bk.sh) * g.bk.so + t : 0;
+    } else {
+      boff[i] = bok[i] ? tg_off(g.bn, gn) + tg_off(g.bk, bk[i]) : 0;
+    }
   }
-  const int nmask = (1 << g.bn.sh) - 1, kmask = (1 << g.bk.sh) - 1;
 
   float ra[PER], rb[PER];
   auto load = [&](int k0) {
+    const int64_t abase = tg_off(g.ak, k0);
+    const int64_t bbase = GATHER ? (int64_t)(k0 >> g.bk.sh) * g.bk.so : tg_off(g.bk, k0);
+    const float* pa = g.a + abase;
+    const float* pb = g.b + bbase;
+    if (k0 + TBK <= kend) {  // whole tile inside the K range (uniform branch)
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int gk = k0 + ak[i];
-      ra[i] = (aok[i] && gk < kend) ? g.a[aoff[i] + tg_off(g.ak, gk)] : 0.f;
-    }
+      for (int i = 0; i < PER; ++i) ra[i] = aok[i] ? pa[aoff[i]] : 0.f;
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int gk = k0 + bk[i];
-      float v = 0.f;
-      if (bok[i] && gk < kend) {
-        if constexpr (GATHER) {
-          const int t = stab[((gk & kmask) << g.bn.sh) | ((n0 + bn[i]) & nmask)];
-          if (t >= 0) v = g.b[boff[i] + (int64_t)(gk >> g.bk.sh) * g.bk.so + t];
-        } else {
-          v = g.b[boff[i] + tg_off(g.bk, gk)];
-        }
-      }
-      rb[i] = v;
+      for (int i = 0; i < PER; ++i) rb[i] = bok[i] ? pb[boff[i]] : 0.f;
+    } else {
+#pragma unroll
+      for (int i = 0; i < PER; ++i) ra[i] = (aok[i] && k0 + ak[i] < kend) ? pa[aoff[i]] : 0.f;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) rb[i] = (bok[i] && k0 + bk[i] < kend) ? pb[boff[i]] : 0.f;
     }
   };
   auto store = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < PER; ++i) As[buf][ak[i]][am[i]] = ra[i];
+    for (int i = 0; i < PER; ++i) {
+      const int e = tid + 256 * i;
+      const int am = AKF ? e / TBK : e % TBM;
+      As[buf][ak[i]][am] = ra[i];
+    }
 #pragma unroll
-    for (int i = 0; i < PER; ++i) Bs[buf][bk[i]][bn[i]] = rb[i];
+    for (int i = 0; i < PER; ++i) {
+      const int e = tid + 256 * i;
+      const int bn = BNF ? e % TBN : e / TBK;
+      Bs[buf][bk[i]][bn] = rb[i];
+    }
   };
 
   f32x16t acc;
@@ -110,7 +125,6 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 
   const int ntiles = kend > kbeg ? (kend - kbeg + TBK - 1) / TBK : 0;
-  if (GATHER) __syncthreads();  // stab
   if (ntiles > 0) {
     load(kbeg);
     store(0);

@@ -34,6 +34,7 @@ _PLANS: dict = {}
 _ON = os.environ.get("NDP_TG", "1") != "0"
 _SMALL = os.environ.get("NDP_TG_SMALL", "1") != "0"
 _PW = os.environ.get("NDP_TG_PW", "1") != "0"
+_PW1 = os.environ.get("NDP_TG_PW1", "0") != "0"  # pointwise on 1x1 maps (measured slower: off)
 POINTWISE, SMALL = 0, 1
 
 
@@ -49,6 +50,8 @@ def tg_plan(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int) ->
     Co, Ci, KH, KW = weight.shape
     if Ci != C or KH * KW > 9:  # the grad-W fold handles <= 3x3 kernels
         return None
+    if KH == KW == 1 and stride == 1 and H * W == 1 and not _PW1:
+        return None  # 1x1 conv on a 1x1 map: the plain hipBLASLt GEMM (Toeplitz path) is faster
     geom = (C, H, W, Co, KH, KW, int(stride), int(padding))
     key = (geom, int(B))
     if key not in _PLANS:

@@ -37,7 +37,13 @@ def _run(device, case, addend=False):
     g = torch.Generator(device="cpu").manual_seed(hash(case) % 1000)
     x = torch.randn(B, C, H, W, generator=g).to(device)
     w = (torch.randn(Co, C, k, k, generator=g) / (C * k * k) ** 0.5).to(device)
-    plan = tg_plan(x, w, s, p)
+    from network_distributed_pytorch_amd.ops import tgconv
+
+    old_pw1, tgconv._PW1 = tgconv._PW1, True  # the 1x1-map pointwise case is off by default
+    try:
+        plan = tg_plan(x, w, s, p)
+    finally:
+        tgconv._PW1 = old_pw1
     assert plan is not None, case
     xr = x.double().requires_grad_()
     wr = w.double().requires_grad_()
@@ -112,18 +118,22 @@ def test_tgconv_deterministic(device, case):
         assert torch.equal(a[0], b[0])
 
 
-def test_resnet50_native_convs_match_stock(device):
-    """ResNet-50 forward + backward with every conv native (direct / tgemm) vs stock MIOpen."""
+def test_resnet50_native_convs_match_fp64(device):
+    """ResNet-50 forward + backward with every conv on a native path (direct / tgemm /
+    Toeplitz) vs the same network in fp64 on the CPU (torch math): normwise gradient error."""
     from network_distributed_pytorch_amd.models import build_model
 
     torch.manual_seed(0)
     ours = build_model("resnet50", 10).to(device)
-    ref = build_model("resnet50", 10, fused_bn=False, gemm_convs=False).to(device)
+    ref = build_model("resnet50", 10).double()
     ref.load_state_dict(ours.state_dict())
-    x = torch.randn(8, 3, 32, 32, device=device)
-    y = torch.randint(0, 10, (8,), device=device)
-    for m in (ours, ref):
-        F.cross_entropy(m(x), y).backward()
+    x = torch.randn(32, 3, 32, 32)
+    y = torch.randint(0, 10, (32,))
+    F.cross_entropy(ours(x.to(device)), y.to(device)).backward()
+    F.cross_entropy(ref(x.double()), y).backward()
+    worst = 0.0
     for (n, a), (_, b) in zip(ours.named_parameters(), ref.named_parameters()):
-        scale = b.grad.abs().max().item() + 1e-12
-        assert (a.grad - b.grad).abs().max().item() / scale < 5e-3, n
+        err = ((a.grad.double().cpu() - b.grad).norm() / (b.grad.norm() + 1e-30)).item()
+        worst = max(worst, err)
+        assert err < 1e-2, (n, err)
+    assert worst < 1e-2
