@@ -45,8 +45,23 @@ __device__ __forceinline__ int64_t tg_off(const TgIndex& t, int i) {
   return (int64_t)(i >> t.sh) * t.so + (int64_t)(i & ((1 << t.sh) - 1)) * t.si;
 }
 
-template <bool AKF, bool BNF, bool GATHER>
+template <int W>
+struct VecT { typedef float __attribute__((ext_vector_type(W))) type; };
+template <>
+struct VecT<1> { typedef float type; };
+
+template <int W>
+__device__ __forceinline__ float vget(const typename VecT<W>::type& v, int j) {
+  if constexpr (W == 1) return v;
+  else return v[j];
+}
+
+// WA / WB: elements per global load of A / B along the operand's unit-stride index (4 =
+// one 16-B load; the host checks contiguity, alignment and extents); GATHER implies WB = 1
+template <bool AKF, bool BNF, bool GATHER, int WA, int WB>
 __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
+  typedef typename VecT<WA>::type VA;
+  typedef typename VecT<WB>::type VB;
   __shared__ float As[2][TBK][TBM + 1];
   __shared__ float Bs[2][TBK][TBN + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -56,6 +71,8 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
   const int kbeg = blockIdx.z * g.kchunk;
   const int kend = min(g.K, kbeg + g.kchunk);
   constexpr int PER = TBM * TBK / 256;  // 8 elements of each operand per thread and tile
+  constexpr int NVA = PER / WA, NVB = PER / WB;
+  constexpr int FA = (AKF ? TBK : TBM) / WA, FB = (BNF ? TBN : TBK) / WB;  // vectors per fast row
 
   // Fixed per-thread tile coordinates.  Every operand offset splits into a tile-invariant
   // per-element part and a per-tile part that is uniform across the workgroup: tiles start
@@ -64,60 +81,71 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
   // inside one E-block; if E < TBK, k0 is a multiple of E).  The gathered tap is therefore
   // fixed per element too (the k inner extent, a map of <= 16 pixels, divides TBK).  Only a
   // scalar base moves per tile: no per-element index arithmetic in the K loop.
-  int ak[PER], bk[PER];
-  int64_t aoff[PER], boff[PER];
-  bool aok[PER], bok[PER];
+  int ak[NVA], am[NVA], bk[NVB], bn[NVB];
+  int64_t aoff[NVA], boff[NVB];
+  bool aok[NVA], bok[NVB];
   const int nmask = (1 << g.bn.sh) - 1, kmask = (1 << g.bk.sh) - 1;
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int e = tid + 256 * i;
-    int am, bn;
-    if (AKF) { am = e / TBK; ak[i] = e % TBK; } else { ak[i] = e / TBM; am = e % TBM; }
-    if (BNF) { bk[i] = e / TBN; bn = e % TBN; } else { bn = e / TBK; bk[i] = e % TBK; }
-    const int gm = m0 + am, gn = n0 + bn;
-    aok[i] = gm < g.M;
-    bok[i] = gn < g.N;
-    aoff[i] = aok[i] ? tg_off(g.am, gm) + tg_off(g.ak, ak[i]) : 0;
+  for (int v = 0; v < NVA; ++v) {
+    const int e = tid + 256 * v;
+    const int fast = (e % FA) * WA, slow = e / FA;
+    ak[v] = AKF ? fast : slow;
+    am[v] = AKF ? slow : fast;
+    const int gm = m0 + am[v];
+    aok[v] = gm < g.M;  // WA = 4 along m: M % 4 == 0, a vector is wholly in or out
+    aoff[v] = aok[v] ? tg_off(g.am, gm) + tg_off(g.ak, ak[v]) : 0;
+  }
+#pragma unroll
+  for (int v = 0; v < NVB; ++v) {
+    const int e = tid + 256 * v;
+    const int fast = (e % FB) * WB, slow = e / FB;
+    bn[v] = BNF ? fast : slow;
+    bk[v] = BNF ? slow : fast;
+    const int gn = n0 + bn[v];
+    bok[v] = gn < g.N;
     if (GATHER) {
-      const int t = g.tab[((bk[i] & kmask) << g.bn.sh) | (gn & nmask)];
-      bok[i] = bok[i] && t >= 0;  // no tap joins these pixels: a structural zero
-      boff[i] = bok[i] ? (int64_t)(gn >> g.bn.sh) * g.bn.so + (int64_t)(bk[i] >> g.bk.sh) * g.bk.so + t : 0;
+      const int t = g.tab[((bk[v] & kmask) << g.bn.sh) | (gn & nmask)];
+      bok[v] = bok[v] && t >= 0;  // no tap joins these pixels: a structural zero
+      boff[v] = bok[v] ? (int64_t)(gn >> g.bn.sh) * g.bn.so + (int64_t)(bk[v] >> g.bk.sh) * g.bk.so + t : 0;
     } else {
-      boff[i] = bok[i] ? tg_off(g.bn, gn) + tg_off(g.bk, bk[i]) : 0;
+      boff[v] = bok[v] ? tg_off(g.bn, gn) + tg_off(g.bk, bk[v]) : 0;
     }
   }
 
-  float ra[PER], rb[PER];
-  auto load = [&](int k0) {
-    const int64_t abase = tg_off(g.ak, k0);
-    const int64_t bbase = GATHER ? (int64_t)(k0 >> g.bk.sh) * g.bk.so : tg_off(g.bk, k0);
-    const float* pa = g.a + abase;
-    const float* pb = g.b + bbase;
-    if (k0 + TBK <= kend) {  // whole tile inside the K range (uniform branch)
+  // two register slots: the global loads of tile t+2 are in flight while tile t's MFMAs run
+  // and tile t+1 waits in registers for its LDS buffer
+  VA ra[2][NVA];
+  VB rb[2][NVB];
+  auto load = [&](int k0, int slot) {
+    const float* pa = g.a + tg_off(g.ak, k0);
+    const float* pb = g.b + (GATHER ? (int64_t)(k0 >> g.bk.sh) * g.bk.so : tg_off(g.bk, k0));
+    const bool full = k0 + TBK <= kend;  // whole tile inside the K range (uniform)
 #pragma unroll
-      for (int i = 0; i < PER; ++i) ra[i] = aok[i] ? pa[aoff[i]] : 0.f;
+    for (int v = 0; v < NVA; ++v) {
+      const bool ok = aok[v] && (full || k0 + ak[v] < kend);  // WA = 4 along k: K % 4 == 0
+      ra[slot][v] = ok ? *reinterpret_cast<const VA*>(pa + aoff[v]) : VA{};
+    }
 #pragma unroll
-      for (int i = 0; i < PER; ++i) rb[i] = bok[i] ? pb[boff[i]] : 0.f;
-    } else {
-#pragma unroll
-      for (int i = 0; i < PER; ++i) ra[i] = (aok[i] && k0 + ak[i] < kend) ? pa[aoff[i]] : 0.f;
-#pragma unroll
-      for (int i = 0; i < PER; ++i) rb[i] = (bok[i] && k0 + bk[i] < kend) ? pb[boff[i]] : 0.f;
+    for (int v = 0; v < NVB; ++v) {
+      const bool ok = bok[v] && (full || k0 + bk[v] < kend);
+      rb[slot][v] = ok ? *reinterpret_cast<const VB*>(pb + boff[v]) : VB{};
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, int slot) {
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int e = tid + 256 * i;
-      const int am = AKF ? e / TBK : e % TBM;
-      As[buf][ak[i]][am] = ra[i];
-    }
+    for (int v = 0; v < NVA; ++v)
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int e = tid + 256 * i;
-      const int bn = BNF ? e % TBN : e / TBK;
-      Bs[buf][bk[i]][bn] = rb[i];
-    }
+      for (int j = 0; j < WA; ++j) {
+        if (AKF) As[buf][ak[v] + j][am[v]] = vget<WA>(ra[slot][v], j);
+        else As[buf][ak[v]][am[v] + j] = vget<WA>(ra[slot][v], j);
+      }
+#pragma unroll
+    for (int v = 0; v < NVB; ++v)
+#pragma unroll
+      for (int j = 0; j < WB; ++j) {
+        if (BNF) Bs[buf][bk[v]][bn[v] + j] = vget<WB>(rb[slot][v], j);
+        else Bs[buf][bk[v] + j][bn[v]] = vget<WB>(rb[slot][v], j);
+      }
   };
 
   f32x16t acc;
@@ -126,19 +154,20 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
 
   const int ntiles = kend > kbeg ? (kend - kbeg + TBK - 1) / TBK : 0;
   if (ntiles > 0) {
-    load(kbeg);
-    store(0);
+    load(kbeg, 0);
+    if (ntiles > 1) load(kbeg + TBK, 1);
+    store(0, 0);
     __syncthreads();
     for (int t = 0; t < ntiles; ++t) {
       const int cur = t & 1;
-      if (t + 1 < ntiles) load(kbeg + (t + 1) * TBK);
+      if (t + 2 < ntiles) load(kbeg + (t + 2) * TBK, cur);  // slot `cur` (tile t) is in LDS already
 #pragma unroll
       for (int kp = 0; kp < TBK / 2; ++kp) {
         const float a = As[cur][2 * kp + h][wm * 32 + l32];
         const float b = Bs[cur][2 * kp + h][wn * 32 + l32];
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
       }
-      if (t + 1 < ntiles) store(cur ^ 1);
+      if (t + 1 < ntiles) store(cur ^ 1, cur ^ 1);  // LDS buffer cur^1 was released by the last barrier
       __syncthreads();
     }
   }
@@ -190,6 +219,24 @@ int tg_cap() {
   return v;
 }
 
+// 16-B loads along `fast` are legal when its 4 consecutive indices are 4 consecutive floats
+// (unit inner stride, outer steps and every stride of `slow` multiples of 4 floats), the base
+// is 16-B aligned and the fast extent is a multiple of 4 (tile origins are multiples of 32)
+bool vec_ok(const TgIndex& fast, const TgIndex& slow, const float* base, int extent) {
+  const bool unit = fast.si == 1 && (fast.sh == 30 || (fast.sh >= 2 && fast.so % 4 == 0));
+  const bool slow4 = slow.so % 4 == 0 && (slow.sh == 0 || slow.si % 4 == 0);
+  return unit && slow4 && (reinterpret_cast<uintptr_t>(base) & 15) == 0 && extent % 4 == 0;
+}
+
+bool tg_vec() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("NDP_TG_VEC");  // 0: scalar loads only (A/B)
+    v = e ? atoi(e) : 1;
+  }
+  return v != 0;
+}
+
 // returns the number of split-K slabs left in a.part (defer), or 1 when final_out is written
 int run(TgArgs a, bool akf, bool bnf, int splits, float* final_out, hipStream_t s, bool defer = false) {
   const int ktiles = (a.K + TBK - 1) / TBK;
@@ -199,13 +246,28 @@ int run(TgArgs a, bool akf, bool bnf, int splits, float* final_out, hipStream_t 
   if (splits <= 1) a.part = nullptr;
   const dim3 grid((a.N + TBN - 1) / TBN, (a.M + TBM - 1) / TBM, splits);
   const bool gather = a.gather != 0;
-#define NDP_TG_LAUNCH(AK, BN_, GA) hipLaunchKernelGGL((tgemm_kernel<AK, BN_, GA>), grid, dim3(256), 0, s, a)
+  const bool va = vec_ok(akf ? a.ak : a.am, akf ? a.am : a.ak, a.a, akf ? a.K : a.M) && tg_vec();
+  const bool vb = !gather && vec_ok(bnf ? a.bn : a.bk, bnf ? a.bk : a.bn, a.b, bnf ? a.N : a.K) && tg_vec();
+#define NDP_TG_LAUNCH(AK, BN_, GA, W1, W2) \
+  hipLaunchKernelGGL((tgemm_kernel<AK, BN_, GA, W1, W2>), grid, dim3(256), 0, s, a)
+#define NDP_TG_W(AK, BN_, GA)                                  \
+  do {                                                         \
+    if (va && vb) NDP_TG_LAUNCH(AK, BN_, GA, 4, 4);            \
+    else if (va) NDP_TG_LAUNCH(AK, BN_, GA, 4, 1);             \
+    else if (vb) NDP_TG_LAUNCH(AK, BN_, GA, 1, 4);             \
+    else NDP_TG_LAUNCH(AK, BN_, GA, 1, 1);                     \
+  } while (0)
   if (gather) {
-    if (akf) NDP_TG_LAUNCH(true, false, true); else NDP_TG_LAUNCH(false, false, true);
-  } else if (akf && bnf) NDP_TG_LAUNCH(true, true, false);
-  else if (akf) NDP_TG_LAUNCH(true, false, false);
-  else if (bnf) NDP_TG_LAUNCH(false, true, false);
-  else NDP_TG_LAUNCH(false, false, false);
+    if (akf) {
+      if (va) NDP_TG_LAUNCH(true, false, true, 4, 1); else NDP_TG_LAUNCH(true, false, true, 1, 1);
+    } else {
+      if (va) NDP_TG_LAUNCH(false, false, true, 4, 1); else NDP_TG_LAUNCH(false, false, true, 1, 1);
+    }
+  } else if (akf && bnf) NDP_TG_W(true, true, false);
+  else if (akf) NDP_TG_W(true, false, false);
+  else if (bnf) NDP_TG_W(false, true, false);
+  else NDP_TG_W(false, false, false);
+#undef NDP_TG_W
 #undef NDP_TG_LAUNCH
   if (splits <= 1) return 1;
   if (defer && a.addend == nullptr) return splits;  // the consumer (fused BN, gradfinish) sums them
