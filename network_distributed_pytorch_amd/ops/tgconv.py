@@ -32,7 +32,9 @@ __all__ = ["tg_plan", "TgConvFn", "enabled"]
 
 _PLANS: dict = {}
 _ON = os.environ.get("NDP_TG", "1") != "0"
-_SMALL = os.environ.get("NDP_TG_SMALL", "1") != "0"
+# small-map family off by default: measured 0.46-0.72x the hipBLASLt Toeplitz GEMMs on the
+# ResNet-18 layer3 / layer4 shapes at batch 64 / 512 (tools/tg_bench.py, profiles/r3/tg_bench.md)
+_SMALL = os.environ.get("NDP_TG_SMALL", "0") != "0"
 _PW = os.environ.get("NDP_TG_PW", "1") != "0"
 _PW1 = os.environ.get("NDP_TG_PW1", "0") != "0"  # pointwise on 1x1 maps (measured slower: off)
 POINTWISE, SMALL = 0, 1

@@ -39,11 +39,14 @@ def _run(device, case, addend=False):
     w = (torch.randn(Co, C, k, k, generator=g) / (C * k * k) ** 0.5).to(device)
     from network_distributed_pytorch_amd.ops import tgconv
 
-    old_pw1, tgconv._PW1 = tgconv._PW1, True  # the 1x1-map pointwise case is off by default
+    # the 1x1-map pointwise case and the small-map family are off by default (slower than the
+    # hipBLASLt GEMMs there): the kernels are still tested
+    saved = tgconv._PW1, tgconv._SMALL
+    tgconv._PW1 = tgconv._SMALL = True
     try:
         plan = tg_plan(x, w, s, p)
     finally:
-        tgconv._PW1 = old_pw1
+        tgconv._PW1, tgconv._SMALL = saved
     assert plan is not None, case
     xr = x.double().requires_grad_()
     wr = w.double().requires_grad_()
@@ -88,9 +91,15 @@ def test_tgconv_addend_in_place(device, case):
 
 def test_tgconv_split_k_used(device):
     # the N = 8 shapes must fill the GPU: split-K on the forward / grad-W of layer4
+    from network_distributed_pytorch_amd.ops import tgconv
+
     x = torch.empty(64, 512, 1, 1, device=device)
     w = torch.empty(512, 512, 3, 3, device=device)
-    plan = tg_plan(x, w, 1, 1)
+    saved, tgconv._SMALL = tgconv._SMALL, True
+    try:
+        plan = tg_plan(x, w, 1, 1)
+    finally:
+        tgconv._SMALL = saved
     assert plan[2] > 1 or plan[4] > 1, plan
 
 
@@ -104,8 +113,15 @@ def test_tgconv_branch_link_sums_two_convs(device):
     (F.conv2d(xr, w1.double(), stride=2, padding=1).sum() + 2 * F.conv2d(xr, w2.double(), stride=2).sum()).backward()
     xg = x.clone().requires_grad_()
     br = BranchLink()
-    a = TgConvFn.apply(xg, w1, tg_plan(x, w1, 2, 1), None, br)
-    b = TgConvFn.apply(xg, w2, tg_plan(x, w2, 2, 0), None, br)
+    from network_distributed_pytorch_amd.ops import tgconv
+
+    saved, tgconv._SMALL = tgconv._SMALL, True
+    try:
+        p1, p2 = tg_plan(x, w1, 2, 1), tg_plan(x, w2, 2, 0)
+    finally:
+        tgconv._SMALL = saved
+    a = TgConvFn.apply(xg, w1, p1, None, br)
+    b = TgConvFn.apply(xg, w2, p2, None, br)
     (a.sum() + 2 * b.sum()).backward()
     _close(xg.grad, xr.grad, "branch dgrad", "branch")
 
@@ -120,20 +136,27 @@ def test_tgconv_deterministic(device, case):
 
 def test_resnet50_native_convs_match_fp64(device):
     """ResNet-50 forward + backward with every conv on a native path (direct / tgemm /
-    Toeplitz) vs the same network in fp64 on the CPU (torch math): normwise gradient error."""
+    Toeplitz) vs the same network in fp64 on the CPU: the normwise gradient error of every
+    parameter is no worse than stock PyTorch-ROCm fp32 (MIOpen convs, nn.BatchNorm2d) shows
+    against the same fp64 reference (BN over 32 samples at layer4's 1x1 maps amplifies fp32
+    rounding towards the stem, for every implementation)."""
     from network_distributed_pytorch_amd.models import build_model
 
     torch.manual_seed(0)
     ours = build_model("resnet50", 10).to(device)
+    stock = build_model("resnet50", 10, fused_bn=False, gemm_convs=False).to(device)
     ref = build_model("resnet50", 10).double()
+    stock.load_state_dict(ours.state_dict())
     ref.load_state_dict(ours.state_dict())
     x = torch.randn(32, 3, 32, 32)
     y = torch.randint(0, 10, (32,))
-    F.cross_entropy(ours(x.to(device)), y.to(device)).backward()
+    for m in (ours, stock):
+        F.cross_entropy(m(x.to(device)), y.to(device)).backward()
     F.cross_entropy(ref(x.double()), y).backward()
-    worst = 0.0
-    for (n, a), (_, b) in zip(ours.named_parameters(), ref.named_parameters()):
-        err = ((a.grad.double().cpu() - b.grad).norm() / (b.grad.norm() + 1e-30)).item()
-        worst = max(worst, err)
-        assert err < 1e-2, (n, err)
-    assert worst < 1e-2
+
+    def err(a, b):
+        return ((a.grad.double().cpu() - b.grad).norm() / (b.grad.norm() + 1e-30)).item()
+
+    for (n, a), (_, s), (_, b) in zip(ours.named_parameters(), stock.named_parameters(), ref.named_parameters()):
+        e_ours, e_stock = err(a, b), err(s, b)
+        assert e_ours <= 2 * e_stock + 1e-4, (n, e_ours, e_stock)
