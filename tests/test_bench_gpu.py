@@ -6,6 +6,7 @@ import subprocess
 import sys
 
 import pytest
+import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -52,6 +53,7 @@ def test_engine_graph_mode_trains_ragged_last_batch(device, tmp_path):
     from network_distributed_pytorch_amd import engine
 
     def run(mode):
+        torch.manual_seed(0)  # the engine builds the model from the current RNG (setup() seeds it)
         cfg = engine.default_config(task="cifar", model="resnet18", num_classes=10, grad_sync="powersgd",
                                     training_epochs=1, dataset_size=100, global_batch=32, graph_mode=mode,
                                     verbose=False, log_file=str(tmp_path / f"{mode}.jsonl"))
