@@ -56,11 +56,13 @@ def tg_plan(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int) ->
         return None  # 1x1 conv on a 1x1 map: the plain hipBLASLt GEMM (Toeplitz path) is faster
     geom = (C, H, W, Co, KH, KW, int(stride), int(padding))
     key = (geom, int(B))
-    if key not in _PLANS:
+    if key not in _PLANS:  # the extension's answer is cached; the family switches apply per call
         cls, fs, ds, ws = ext().tg_plan(list(geom), int(B))
-        ok = cls >= 0 and ((cls == POINTWISE and _PW) or (cls == SMALL and _SMALL))
-        _PLANS[key] = (geom, int(cls), int(fs), int(ds), int(ws)) if ok else None
-    return _PLANS[key]
+        _PLANS[key] = (geom, int(cls), int(fs), int(ds), int(ws)) if cls >= 0 else None
+    plan = _PLANS[key]
+    if plan is None or not ((plan[1] == POINTWISE and _PW) or (plan[1] == SMALL and _SMALL)):
+        return None
+    return plan
 
 
 def _scratch(n_slabs: int, numel: int, like: torch.Tensor) -> Optional[torch.Tensor]:
