@@ -14,6 +14,7 @@ would alias it).  Used by the native conv (direct / tgemm / Toeplitz) and BN bac
 """
 from __future__ import annotations
 
+import os
 import weakref
 from typing import Iterable
 
@@ -22,6 +23,7 @@ import torch
 __all__ = ["register", "unregister", "grad_buffer", "registered"]
 
 _VIEWS: dict = {}
+_ON = os.environ.get("NDP_GRAD_ARENA", "1") != "0"
 
 
 def register(param: torch.Tensor, arena: torch.Tensor, offset: int) -> None:
@@ -41,7 +43,7 @@ def registered(param: torch.Tensor) -> bool:
 def grad_buffer(param: torch.Tensor, like: torch.Tensor = None) -> torch.Tensor:
     """Output buffer for ``param``'s gradient: its arena slice when registered and adoptable,
     else a fresh tensor like ``like`` (default ``param``)."""
-    e = _VIEWS.get(id(param))
+    e = _VIEWS.get(id(param)) if _ON else None
     if e is not None and param.grad is None and not torch.is_grad_enabled():
         ref, arena, off = e
         if ref() is param:
