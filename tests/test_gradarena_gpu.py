@@ -8,10 +8,12 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 
-def test_dense_arena_gradients_in_place(device):
+def test_dense_arena_gradients_in_place(device, monkeypatch):
     from network_distributed_pytorch_amd.models import build_model
     from network_distributed_pytorch_amd.parallel.ddp import BucketedDataParallel
 
+    # MIOpen's strided 3x3 grad-x (the one non-native kernel) may accumulate atomically
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
     torch.manual_seed(0)
     ours = build_model("resnet18", 10).to(device)
     ref = build_model("resnet18", 10).to(device)

@@ -1,5 +1,8 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=$GRAFT_REPO_ROOT/gpurun_out/iso; mkdir -p $O
-(cd _r2 && timeout -k 10 300 python -u -m pytest tests/test_conv_gemm.py -q --timeout 200 --timeout-method thread > $O/r2.log 2>&1; echo "r2 rc=$?"; tail -2 $O/r2.log)
-timeout -k 10 300 python -u -m pytest tests/test_conv_gemm.py -q --timeout 200 --timeout-method thread > $O/r3.log 2>&1; echo "r3 rc=$?"; tail -2 $O/r3.log
+run() { name=$1; shift; timeout -k 10 300 python -u -m pytest "$@" -q -m gpu --timeout 200 --timeout-method thread > $O/$name.log 2>&1; echo "$name rc=$? $(tail -1 $O/$name.log)"; grep FAILED $O/$name.log | head -3; }
+run G tests/test_graph_gpu.py
+run GA tests/test_gradarena_gpu.py tests/test_graph_gpu.py
+run BG tests/test_bench_gpu.py tests/test_graph_gpu.py
+run EARLY tests/test_attention.py tests/test_batchnorm_gpu.py tests/test_conv_direct.py tests/test_conv_gemm.py tests/test_distilbert_fusions_gpu.py tests/test_embedding_gpu.py tests/test_fuzz_gpu.py tests/test_gemm_tuning_gpu.py tests/test_graph_gpu.py
