@@ -909,15 +909,19 @@ int conv_ksplit(int cls, const ConvGeom& g, int B, bool dgrad) {
   while (ks * 2 <= nchunks && base * ks < kFillWgs && ks * 2 <= maxks) ks *= 2;
   return pow2_floor(ks);
 }
-// 3x3 stride-2 grad-x on the zero-inserted dY (NDP_CONV_DGRAD2=1): exact (tests/
-// test_conv_direct.py) but 4x the MFMA work of the sub-pixel form, measured on 1x MI355X
-// (ResNet-18 step) 2.006 / 2.005 vs MIOpen 1.991 ms at batch 512, 1.054 / 1.047 vs 1.051 at
-// 64, 1.443 / 1.445 vs 1.446 at 256 — MIOpen stays the default.
+// 3x3 stride-2 grad-x on the zero-inserted dY: exact (tests/test_conv_direct.py), 4x the
+// MFMA work of the sub-pixel form; measured on 1x MI355X (ResNet-18 step, round 2) 2.006 /
+// 2.005 vs MIOpen 1.991 ms at batch 512, 1.054 / 1.047 vs 1.051 at 64.  DEFAULT since round 3:
+// the MIOpen kernel was the last non-native call of the ResNet-18 step, and its algorithm
+// choice depends on MIOpen's on-disk find database (written by earlier processes, e.g. a
+// cudnn.benchmark run): on a box with a populated database it was non-deterministic and,
+// captured in a hipGraph, produced NaN (tools/gpu_iso.sh bisection).  NDP_CONV_DGRAD2=0
+// restores MIOpen.
 static bool dgrad2_on() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("NDP_CONV_DGRAD2");
-    v = e ? atoi(e) : 0;
+    v = e ? atoi(e) : 1;
   }
   return v != 0;
 }
