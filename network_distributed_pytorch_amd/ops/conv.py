@@ -4,8 +4,9 @@
 hand-written gfx950 kernels for the shape classes the extension reports through
 ``conv_plan`` (ResNet stem 7x7/2 on 32x32, layer1 3x3 on 8x8, layer2 3x3 on 4x4, its
 strided 8x8->4x4 entry conv and its 1x1/2 downsample).  Grad-input of the strided 3x3 class
-goes to MIOpen by default; ``NDP_CONV_DGRAD2=1`` runs it natively as the layer1 grad-x kernel
-on the zero-inserted dY (zeros from the LDS staging; exact, but measured no faster);  the 1x1/2
+runs natively as the layer1 grad-x kernel on the zero-inserted dY (zeros from the LDS staging;
+exact); ``NDP_CONV_DGRAD2=0`` sends it to MIOpen, whose find-database-dependent algorithm was
+found non-deterministic and NaN-producing under hipGraph capture;  the 1x1/2
 downsample's grad-input is the transposed 1x1 product written to the even pixels; the stem's
 input never needs a gradient.
 :func:`direct_plan` returns None for every other geometry, so callers keep their MIOpen /
