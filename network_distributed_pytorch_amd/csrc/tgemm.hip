@@ -38,7 +38,11 @@ namespace ndp {
 
 namespace {
 
-constexpr int TBM = 64, TBN = 64, TBK = 32;
+// tile shapes (BM, BN, BK): the 128 x 128 x 16 tile where both GEMM dimensions fill it
+struct TgTile {
+  int bm, bn, bk;
+};
+constexpr TgTile kSmallTile{64, 64, 32}, kBigTile{128, 128, 16};
 typedef float f32x16t __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ int64_t tg_off(const TgIndex& t, int i) {
@@ -56,12 +60,16 @@ __device__ __forceinline__ float vget(const typename VecT<W>::type& v, int j) {
   else return v[j];
 }
 
+// Tile TBM x TBN x TBK, 4 waves in 2 x 2, each wave (TBM/2) x (TBN/2) = TM x TN MFMA tiles of
+// 32 x 32 (64 x 64 x 32: one tile per wave; 128 x 128 x 16: 2 x 2 tiles per wave, one LDS read
+// per MFMA instead of two, half the global-load instructions per FLOP).
 // WA / WB: elements per global load of A / B along the operand's unit-stride index (4 =
 // one 16-B load; the host checks contiguity, alignment and extents); GATHER implies WB = 1
-template <bool AKF, bool BNF, bool GATHER, int WA, int WB>
+template <int TBM, int TBN, int TBK, bool AKF, bool BNF, bool GATHER, int WA, int WB>
 __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
   typedef typename VecT<WA>::type VA;
   typedef typename VecT<WB>::type VB;
+  constexpr int TM = TBM / 64, TN = TBN / 64;
   __shared__ float As[2][TBK][TBM + 1];
   __shared__ float Bs[2][TBK][TBN + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -148,9 +156,13 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
       }
   };
 
-  f32x16t acc;
+  f32x16t acc[TM][TN];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int ntiles = kend > kbeg ? (kend - kbeg + TBK - 1) / TBK : 0;
   if (ntiles > 0) {
@@ -163,9 +175,15 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
       if (t + 2 < ntiles) load(kbeg + (t + 2) * TBK, cur);  // slot `cur` (tile t) is in LDS already
 #pragma unroll
       for (int kp = 0; kp < TBK / 2; ++kp) {
-        const float a = As[cur][2 * kp + h][wm * 32 + l32];
-        const float b = Bs[cur][2 * kp + h][wn * 32 + l32];
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+        float a[TM], b[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) a[i] = As[cur][2 * kp + h][(wm * TM + i) * 32 + l32];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) b[j] = Bs[cur][2 * kp + h][(wn * TN + j) * 32 + l32];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
       }
       if (t + 1 < ntiles) store(cur ^ 1, cur ^ 1);  // LDS buffer cur^1 was released by the last barrier
       __syncthreads();
@@ -173,17 +191,22 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
   }
 
   float* out = g.part != nullptr ? g.part + (int64_t)blockIdx.z * g.slab : g.c;
-  const int n = n0 + wn * 32 + l32;
-  if (n < g.N) {
+  const bool add = g.addend != nullptr && g.part == nullptr;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + (wn * TN + j) * 32 + l32;
+    if (n >= g.N) continue;
     const int64_t noff = tg_off(g.cn, n);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (m < g.M) {
-        const int64_t o = tg_off(g.cm, m) + noff;
-        out[o] = g.addend != nullptr && g.part == nullptr ? acc[r] + g.addend[o] : acc[r];
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m < g.M) {
+          const int64_t o = tg_off(g.cm, m) + noff;
+          out[o] = add ? acc[i][j][r] + g.addend[o] : acc[i][j][r];
+        }
       }
-    }
   }
 }
 
@@ -198,10 +221,22 @@ TgIndex comp(int sh, int64_t outer, int64_t inner) { return TgIndex{outer, inner
 
 constexpr int kTgFill = 256;  // one workgroup per CU at least
 
+int tg_big() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("NDP_TG_BIG");  // 0: always the 64 x 64 tile (A/B)
+    v = e ? atoi(e) : 1;
+  }
+  return v;
+}
+
+TgTile tg_tile(int M, int N) { return (tg_big() && M >= 128 && N >= 128) ? kBigTile : kSmallTile; }
+
 // split-K factor: power of two so that tiles * splits >= kTgFill, each split >= 2 k-tiles
 int tg_pick_splits(int M, int N, int K, int cap) {
-  const int tiles = ((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN);
-  const int ktiles = (K + TBK - 1) / TBK;
+  const TgTile t = tg_tile(M, N);
+  const int tiles = ((M + t.bm - 1) / t.bm) * ((N + t.bn - 1) / t.bn);
+  const int ktiles = (K + t.bk - 1) / t.bk;
   int s = 1;
   while (s * 2 <= cap && tiles * s < kTgFill && ktiles >= 4 * s) s *= 2;
   return s;
@@ -237,19 +272,10 @@ bool tg_vec() {
   return v != 0;
 }
 
-// returns the number of split-K slabs left in a.part (defer), or 1 when final_out is written
-int run(TgArgs a, bool akf, bool bnf, int splits, float* final_out, hipStream_t s, bool defer = false) {
-  const int ktiles = (a.K + TBK - 1) / TBK;
-  const int per = (ktiles + splits - 1) / splits;
-  a.kchunk = per * TBK;
-  splits = (ktiles + per - 1) / per;
-  if (splits <= 1) a.part = nullptr;
-  const dim3 grid((a.N + TBN - 1) / TBN, (a.M + TBM - 1) / TBM, splits);
-  const bool gather = a.gather != 0;
-  const bool va = vec_ok(akf ? a.ak : a.am, akf ? a.am : a.ak, a.a, akf ? a.K : a.M) && tg_vec();
-  const bool vb = !gather && vec_ok(bnf ? a.bn : a.bk, bnf ? a.bk : a.bn, a.b, bnf ? a.N : a.K) && tg_vec();
+template <int BM, int BN, int BK>
+void launch_tile(const TgArgs& a, bool akf, bool bnf, bool va, bool vb, dim3 grid, hipStream_t s) {
 #define NDP_TG_LAUNCH(AK, BN_, GA, W1, W2) \
-  hipLaunchKernelGGL((tgemm_kernel<AK, BN_, GA, W1, W2>), grid, dim3(256), 0, s, a)
+  hipLaunchKernelGGL((tgemm_kernel<BM, BN, BK, AK, BN_, GA, W1, W2>), grid, dim3(256), 0, s, a)
 #define NDP_TG_W(AK, BN_, GA)                                  \
   do {                                                         \
     if (va && vb) NDP_TG_LAUNCH(AK, BN_, GA, 4, 4);            \
@@ -257,7 +283,7 @@ int run(TgArgs a, bool akf, bool bnf, int splits, float* final_out, hipStream_t 
     else if (vb) NDP_TG_LAUNCH(AK, BN_, GA, 1, 4);             \
     else NDP_TG_LAUNCH(AK, BN_, GA, 1, 1);                     \
   } while (0)
-  if (gather) {
+  if (a.gather) {
     if (akf) {
       if (va) NDP_TG_LAUNCH(true, false, true, 4, 1); else NDP_TG_LAUNCH(true, false, true, 1, 1);
     } else {
@@ -269,6 +295,21 @@ int run(TgArgs a, bool akf, bool bnf, int splits, float* final_out, hipStream_t 
   else NDP_TG_W(false, false, false);
 #undef NDP_TG_W
 #undef NDP_TG_LAUNCH
+}
+
+// returns the number of split-K slabs left in a.part (defer), or 1 when final_out is written
+int run(TgArgs a, bool akf, bool bnf, int splits, float* final_out, hipStream_t s, bool defer = false) {
+  const TgTile tile = tg_tile(a.M, a.N);
+  const int ktiles = (a.K + tile.bk - 1) / tile.bk;
+  const int per = (ktiles + splits - 1) / splits;
+  a.kchunk = per * tile.bk;
+  splits = (ktiles + per - 1) / per;
+  if (splits <= 1) a.part = nullptr;
+  const dim3 grid((a.N + tile.bn - 1) / tile.bn, (a.M + tile.bm - 1) / tile.bm, splits);
+  const bool va = vec_ok(akf ? a.ak : a.am, akf ? a.am : a.ak, a.a, akf ? a.K : a.M) && tg_vec();
+  const bool vb = !a.gather && vec_ok(bnf ? a.bn : a.bk, bnf ? a.bk : a.bn, a.b, bnf ? a.N : a.K) && tg_vec();
+  if (tile.bm == kBigTile.bm) launch_tile<kBigTile.bm, kBigTile.bn, kBigTile.bk>(a, akf, bnf, va, vb, grid, s);
+  else launch_tile<kSmallTile.bm, kSmallTile.bn, kSmallTile.bk>(a, akf, bnf, va, vb, grid, s);
   if (splits <= 1) return 1;
   if (defer && a.addend == nullptr) return splits;  // the consumer (fused BN, gradfinish) sums them
   launch_slab_sum(a.part, final_out, a.slab, splits, s, a.addend);
