@@ -224,8 +224,8 @@ constexpr int kTgFill = 256;  // one workgroup per CU at least
 int tg_big() {
   static int v = -1;
   if (v < 0) {
-    const char* e = getenv("NDP_TG_BIG");  // 0: always the 64 x 64 tile (A/B)
-    v = e ? atoi(e) : 1;
+    const char* e = getenv("NDP_TG_BIG");  // 1: 128 x 128 x 16 tile where M, N >= 128 (A/B only)
+    v = e ? atoi(e) : 0;  // measured slower on every r50 shape (profiles/r3/tg_bench.md)
   }
   return v;
 }
@@ -267,7 +267,7 @@ bool tg_vec() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("NDP_TG_VEC");  // 0: scalar loads only (A/B)
-    v = e ? atoi(e) : 1;
+    v = e ? atoi(e) : 0;  // measured slower on every r50 shape (profiles/r3/tg_bench.md)
   }
   return v != 0;
 }
