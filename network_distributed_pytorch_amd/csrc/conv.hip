@@ -252,7 +252,10 @@ struct ConvFwdCfg {
                                                                                        : 0;
   static constexpr int Hp = H + 2 * PD;
   static constexpr int Wp = LAYOUT == 1 ? 12 : LAYOUT == 2 ? 8 : LAYOUT == 3 ? 12 : W + 2 * PD;
-  static constexpr int HWp = Hp * Wp, HW = H * W;
+  // channel stride odd: the B staging stores (float4 per lane -> 4 scalar ds_write_b32, a
+  // 32-lane group spanning 2-8 channels) land on disjoint bank sets per channel (<= 2-way,
+  // which a b32 store absorbs); the reads of a half-wave stay inside one channel
+  static constexpr int HWp = (Hp * Wp) | 1, HW = H * W;
   static constexpr int IPAD0 = LAYOUT == 2 ? 4 : LAYOUT == 3 ? 1 : 0;  // target image stride mod 32
   static constexpr int IMGSTR = LAYOUT >= 2 ? (CK * HWp + 31) / 32 * 32 + IPAD0 : CK * HWp;
   static_assert(Wp >= W + 2 * PD, "row stride holds the zero border");
@@ -274,7 +277,11 @@ struct ConvFwdCfg {
   static constexpr int BN = IMGS * PQ;
   static constexpr int WN = 4 / WM;
   static constexpr int TM = BM / 32 / WM, TN = BN / 32 / WN;
-  static constexpr int LDA = BM + 1;    // [kk][m], odd stride: conflict-free transposing writes
+  // [kk][m] A image.  Reads (32 consecutive m) are conflict-free for any stride; the stride is
+  // picked for the transposing scalar stores: forward (m fastest over 4 lanes, then kk in
+  // float4 steps) LDA = 1 mod 32 -> <= 2-way; grad-x (TRANSW: 4 consecutive (m, tap) of a
+  // weight row per lane) LDA = 2 mod 32 -> <= 2-way (1 mod 32 was 5-way; PMC round 3)
+  static constexpr int LDA = TRANSW ? BM + 2 : BM + 1;
   static constexpr int A_SZ = KK * LDA;
   static constexpr int B_SZ = IMGS * IMGSTR;
   // A staging: float4 rows when every chunk is whole channels and rows are 16-B aligned
@@ -345,8 +352,8 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
       f32x4c v = {0.f, 0.f, 0.f, 0.f};
       if (e < AE) {
         if (VEC) {
-          if (!TRANSW) {
-            const int m = e / (G::KK / 4), k4 = e - m * (G::KK / 4);
+          if (!TRANSW) {  // lanes: 4 rows (m) fastest, then float4 k4 along the row
+            const int r = e >> 2, k4 = r % (G::KK / 4), m = 4 * (r / (G::KK / 4)) + (e & 3);
             v = *reinterpret_cast<const f32x4c*>(w + ((int64_t)(m0 + m) * Cin + c0) * G::RS + 4 * k4);
           } else {
             const int c = e / (BM * G::RS / 4), r4 = e - c * (BM * G::RS / 4);
@@ -384,8 +391,8 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
       if (e < AE) {
         if (VEC) {
           if (!TRANSW) {
-            const int m = e / (G::KK / 4), kk = 4 * (e - m * (G::KK / 4));
-            float* d = A + kk * G::LDA + m;
+            const int r = e >> 2, k4 = r % (G::KK / 4), m = 4 * (r / (G::KK / 4)) + (e & 3);
+            float* d = A + 4 * k4 * G::LDA + m;
             d[0] = ra[i].x; d[G::LDA] = ra[i].y; d[2 * G::LDA] = ra[i].z; d[3 * G::LDA] = ra[i].w;
           } else {
             const int c = e / (BM * G::RS / 4), f = 4 * (e - c * (BM * G::RS / 4));
@@ -537,8 +544,22 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
 template <int R, int S, int ST, int PD, int H, int W, int CB, int BM, int NW, int NBPW, int KB>
 struct ConvWgCfg {
   static constexpr int P = (H + 2 * PD - R) / ST + 1, Q = (W + 2 * PD - S) / ST + 1, PQ = P * Q;
-  static constexpr int Hp = H + 2 * PD, Wp = W + 2 * PD, HWp = Hp * Wp, HW = H * W;
+  // odd channel stride + tap-major columns (TAPMAJ: column j = rs * CB + c, so the 32 lanes of
+  // a B read are 32 channels at one tap): conflict-free B reads.  Channel-major (c * RS + rs)
+  // put 3-4 channels' 3x3 windows in one half-wave: 2-3-way conflicts (PMC round 3), and the
+  // even 8x8 1x1 stride was 32-way.
+  static constexpr int Hp = H + 2 * PD, Wp = W + 2 * PD, HWp = (Hp * Wp) | 1, HW = H * W;
   static constexpr int RS = R * S, J = CB * RS, JB = (J + 31) / 32, MB = BM / 32;
+  static constexpr bool TAPMAJ = CB % 32 == 0;
+  __device__ static __forceinline__ void col(int j, int& c, int& rs) {
+    if constexpr (TAPMAJ) {
+      rs = j / CB;
+      c = j - rs * CB;
+    } else {
+      c = j / RS;
+      rs = j - c * RS;
+    }
+  }
   static constexpr int NSTEP = PQ / 2, NBLK = NSTEP / KB;
   static constexpr int LDY = PQ + 1;
   static constexpr int A_SZ = BM * LDY;  // dY tile of one image: [m][pixel]
@@ -546,7 +567,13 @@ struct ConvWgCfg {
   static constexpr int NT = 64 * NW;
   static constexpr int A4 = BM * PQ / 4, B4 = CB * HW / 4;
   static constexpr int A_PER_T = (A4 + NT - 1) / NT, B_PER_T = (B4 + NT - 1) / NT;
-  static constexpr size_t LDS_BYTES = 2 * (size_t)(A_SZ + B_SZ) * sizeof(float);
+  // TAPMAJ epilogue: the dW tile goes through LDS back to channel-major rows ([BM][J], row
+  // stride LDJ, 16-B aligned) so the slab stores stay contiguous float4 (a lane-per-channel
+  // store at stride RS scattered every row over RS x 128 B and doubled the write bytes)
+  static constexpr int LDJ = J + 4;
+  static constexpr size_t MAIN_BYTES = 2 * (size_t)(A_SZ + B_SZ) * sizeof(float);
+  static constexpr size_t EPI_BYTES = TAPMAJ ? (size_t)BM * LDJ * sizeof(float) : 0;
+  static constexpr size_t LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
   static_assert(MB * JB == NW * NBPW, "every wave owns NBPW 32x32 blocks");
   static_assert(P % 2 == 0 && PQ % 4 == 0 && HW % 4 == 0 && NSTEP % KB == 0, "pixel pairing / float4 loads");
 };
@@ -573,7 +600,8 @@ __global__ __launch_bounds__(64 * NW) void conv_wgrad_kernel(const float* __rest
     const int mb = blk / G::JB, jb = blk - mb * G::JB;
     const int j = jb * 32 + l32;
     a_base[t] = (mb * 32 + l32) * G::LDY + h * (G::PQ / 2);
-    const int c = j / G::RS, rs = j - c * G::RS;
+    int c, rs;
+    G::col(j, c, rs);
     const int r = rs / S, s = rs - r * S;
     b_base[t] = (j < G::J) ? c * G::HWp + r * G::Wp + s + h * (G::P / 2) * ST * G::Wp : 0;
   }
@@ -662,16 +690,52 @@ __global__ __launch_bounds__(64 * NW) void conv_wgrad_kernel(const float* __rest
   }
 
   float* out = part + (int64_t)slice * Kout * Cin * G::RS;
+  if constexpr (G::TAPMAJ && G::RS > 1) {
+    // the loop's last barrier retired every LDS read: reuse the buffers as the staging tile
+    float* st = smem;
+#pragma unroll
+    for (int t = 0; t < NBPW; ++t) {
+      const int blk = wave * NBPW + t;
+      const int mb = blk / G::JB, jb = blk - mb * G::JB;
+      const int j = jb * 32 + l32;
+      int c, rs;
+      G::col(j, c, rs);
+      if (j < G::J) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          st[(mb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * G::LDJ + c * G::RS + rs] = acc[t][r];
+      }
+    }
+    __syncthreads();
+    const int lim = min(CB, Cin - c0) * G::RS;  // valid columns of a row (partial channel block)
+    constexpr int J4 = G::J / 4;
+    static_assert(G::J % 4 == 0, "float4 rows");
+    for (int i = tid; i < BM * J4; i += G::NT) {
+      const int mr = i / J4, q = 4 * (i - mr * J4);
+      const f32x4c v = *reinterpret_cast<const f32x4c*>(st + mr * G::LDJ + q);
+      float* o = out + ((int64_t)(m0 + mr) * Cin + c0) * G::RS + q;
+      if (q + 3 < lim) {
+        *reinterpret_cast<f32x4c*>(o) = v;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (q + k < lim) o[k] = v[k];
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < NBPW; ++t) {
     const int blk = wave * NBPW + t;
     const int mb = blk / G::JB, jb = blk - mb * G::JB;
     const int j = jb * 32 + l32;
-    if (j < G::J && c0 + j / G::RS < Cin) {
+    int c, rs;
+    G::col(j, c, rs);
+    if (j < G::J && c0 + c < Cin) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + mb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        out[((int64_t)m * Cin + c0) * G::RS + j] = acc[t][r];
+        out[((int64_t)m * Cin + c0 + c) * G::RS + rs] = acc[t][r];
       }
     }
   }
