@@ -213,7 +213,7 @@ void psgd_orth(torch::Tensor geom, torch::Tensor items, torch::Tensor p, double 
 
 void psgd_update(torch::Tensor geom, torch::Tensor ptrs, torch::Tensor items, torch::Tensor p_hat,
                  torch::Tensor q_sum, double q_div, c10::optional<torch::Tensor> q_warm, int mode,
-                 double lr, double momentum) {
+                 double lr, double momentum, int max_rank) {
   check_dev(geom, "geom"); check_dev(ptrs, "ptrs"); check_dev(items, "items");
   check_f32(p_hat, "p_hat"); check_f32(q_sum, "q_sum");
   float* qw = nullptr;
@@ -223,7 +223,7 @@ void psgd_update(torch::Tensor geom, torch::Tensor ptrs, torch::Tensor items, to
                           reinterpret_cast<const UItem*>(items.data_ptr()),
                           (int)n_of(items, sizeof(UItem)), p_hat.data_ptr<float>(),
                           q_sum.data_ptr<float>(), (float)q_div, qw, mode, (float)lr,
-                          (float)momentum, cur_stream());
+                          (float)momentum, max_rank, cur_stream());
   check_launch("launch_psgd_update");
 }
 

@@ -34,21 +34,50 @@ __global__ __launch_bounds__(256) void seg_reduce_kernel(const SegEntry* __restr
   const int64_t base = (blk - prefix[lo]) * kSegBlockElems;
   const bool scale = E.div != 1.0f;
   if (E.vec) {
+    // Split-K P / Q slabs (up to ~20 chunks): the chunk loads are issued kSegBatch at a time
+    // for both float4 of the thread before any add, so a block costs ~chunks / 8 memory
+    // round trips instead of one per chunk (the adds keep chunk order: bitwise unchanged).
+    constexpr int QN = kSegBlockElems / 1024;
+    constexpr int kSegBatch = 8;
+    int64_t kq[QN];
+    bool full[QN];
+    f32x4 acc[QN];
 #pragma unroll
-    for (int q = 0; q < kSegBlockElems / 1024; ++q) {
-      const int64_t k = base + (int64_t)(q * 256 + threadIdx.x) * 4;
-      if (k + 3 < E.numel) {
-        f32x4 acc = ld4(E.src + k);
-        for (int c = 1; c < E.chunks; ++c) acc += ld4(E.src + (int64_t)c * E.stride + k);
-        if (scale) acc = acc / E.div;
-        st4(E.dst + k, acc);
-      } else {
+    for (int q = 0; q < QN; ++q) {
+      kq[q] = base + (int64_t)(q * 256 + threadIdx.x) * 4;
+      full[q] = kq[q] + 3 < E.numel;
+      acc[q] = full[q] ? ld4(E.src + kq[q]) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    int c = 1;
+    for (; c + kSegBatch <= E.chunks; c += kSegBatch) {
+      f32x4 t[QN][kSegBatch];
+#pragma unroll
+      for (int j = 0; j < kSegBatch; ++j)
+#pragma unroll
+        for (int q = 0; q < QN; ++q)
+          t[q][j] = full[q] ? ld4(E.src + (int64_t)(c + j) * E.stride + kq[q]) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < QN; ++q)
+#pragma unroll
+        for (int j = 0; j < kSegBatch; ++j) acc[q] += t[q][j];
+    }
+    for (; c < E.chunks; ++c)
+#pragma unroll
+      for (int q = 0; q < QN; ++q)
+        if (full[q]) acc[q] += ld4(E.src + (int64_t)c * E.stride + kq[q]);
+#pragma unroll
+    for (int q = 0; q < QN; ++q) {
+      const int64_t k = kq[q];
+      if (full[q]) {
+        if (scale) acc[q] = acc[q] / E.div;
+        st4(E.dst + k, acc[q]);
+      } else if (k < E.numel) {
         for (int j = 0; j < 4; ++j) {
           if (k + j >= E.numel) break;
-          float acc = E.src[k + j];
-          for (int c = 1; c < E.chunks; ++c) acc += E.src[(int64_t)c * E.stride + k + j];
-          if (scale) acc = acc / E.div;
-          E.dst[k + j] = acc;
+          float t = E.src[k + j];
+          for (int z = 1; z < E.chunks; ++z) t += E.src[(int64_t)z * E.stride + k + j];
+          if (scale) t = t / E.div;
+          E.dst[k + j] = t;
         }
       }
     }

@@ -64,6 +64,10 @@ constexpr int kQCols = 256;   // columns per Q item (4 waves x 64)
 constexpr int kQRowsMax = 256;  // max rows per Q item (LDS: 256 x (16*NCG+pad) floats)
 constexpr int kURows = 64;
 constexpr int kUCols = 64;
+// plans whose max rank is <= kUWideMaxRank use 16 x 256 update tiles (psgd_update_wide_kernel)
+constexpr int kUWideRows = 16;
+constexpr int kUWideCols = 256;
+constexpr int kUWideMaxRank = 16;
 constexpr int kMaxRank = 64;
 constexpr int kSegBlockElems = 2048;  // elements per workgroup in seg_reduce
 
@@ -84,7 +88,8 @@ constexpr unsigned kOrthMaxSpins = 1u << 25;  // ~seconds of s_sleep 2
 // mode 0 = api (out/mem), 1 = engine (EF + momentum + SGD), 2 = engine + write grad
 void launch_psgd_update(const MatGeom* geom, const MatPtrs* ptrs, const UItem* items,
                         int n_items, const float* p_hat, const float* q_sum, float q_div,
-                        float* q_warm, int mode, float lr, float momentum, hipStream_t s);
+                        float* q_warm, int mode, float lr, float momentum, int max_rank,
+                        hipStream_t s);
 // rank-1 (<=1-D) group of the fused engine: out = buf/div; m = lam*m + out; x -= lr*(out+m)
 void launch_rank1_step(const float* buf, float div, float* mom, float* x, float* g,
                        int64_t n, float lr, float momentum, hipStream_t s);

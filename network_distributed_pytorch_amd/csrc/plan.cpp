@@ -8,7 +8,7 @@
 //     count are identical to the reference: SURVEY.md §2.7);
 //   * P items  : (matrix, 64-row block, 256-wide k-chunk)   -> split-K over m;
 //   * Q items  : (matrix, 256-col block, row chunk)          -> split-K over n;
-//   * U items  : (matrix, 64x64 tile)                        -> fused decompress/update;
+//   * U items  : (matrix, 16x256 tile; 64x64 above rank 16)  -> fused decompress/update;
 //   * split-K slab offsets for the deterministic seg_reduce.
 #include "plan.h"
 
@@ -25,6 +25,10 @@ Plan build_plan(const std::vector<std::pair<int64_t, int64_t>>& shapes, int rank
   Plan pl;
   pl.max_rank = 0;
   int64_t p_off = 0, q_off = 0, pp_off = 0, qp_off = 0;
+  int plan_rank = 1;  // max over matrices of min(n, m, rank): picks the update tile shape
+  for (const auto& s : shapes) plan_rank = std::max<int>(plan_rank, (int)std::min<int64_t>(std::min(s.first, s.second), rank));
+  const bool wide = plan_rank <= kUWideMaxRank;
+  const int64_t u_rows = wide ? kUWideRows : kURows, u_cols = wide ? kUWideCols : kUCols;
   for (size_t i = 0; i < shapes.size(); ++i) {
     const int64_t n = shapes[i].first, m = shapes[i].second;
     if (n < 1 || m < 1) throw std::invalid_argument("empty matrix in PowerSGD plan");
@@ -69,8 +73,8 @@ Plan build_plan(const std::vector<std::pair<int64_t, int64_t>>& shapes, int rank
         it.chunk = (int32_t)c;
         pl.q_items.push_back(it);
       }
-    for (int64_t row0 = 0; row0 < n; row0 += kURows)
-      for (int64_t col0 = 0; col0 < m; col0 += kUCols) {
+    for (int64_t row0 = 0; row0 < n; row0 += u_rows)
+      for (int64_t col0 = 0; col0 < m; col0 += u_cols) {
         UItem it{};
         it.mat = (int32_t)i;
         it.row0 = (int32_t)row0;

@@ -358,6 +358,128 @@ __global__ __launch_bounds__(256) void psgd_update_kernel(
   }
 }
 
+// ----------------------------------------------------------------------------------
+// Same stage for plans with max rank <= kUWideMaxRank (every ResNet / DistilBERT config the
+// reference runs): 16 x 256 tiles, one wave = 4 rows x 256 columns, lane = 4 consecutive
+// columns.  Each wave load instruction streams 1 KB of one row (the MFMA tile above reads 16
+// rows x 64 B per instruction), all 12 float4 loads of the HBM stream are issued before any
+// use, and the decompression out = P Q^T / N is r fmaf per element on the VALU: Q's 4 x r
+// values per lane are loaded once into registers, P's row is wave-uniform (scalar loads).
+// ----------------------------------------------------------------------------------
+constexpr int kURowsPerWave = kUWideRows / 4;
+
+template <int RQ>
+__global__ __launch_bounds__(256) void psgd_update_wide_kernel(
+    const MatGeom* __restrict__ geom, const MatPtrs* __restrict__ ptrs,
+    const UItem* __restrict__ items, const float* __restrict__ p_hat,
+    const float* __restrict__ q_sum, float q_div, float* __restrict__ q_warm, int mode,
+    float lr, float momentum) {
+  const UItem it = items[blockIdx.x];
+  const MatGeom g = geom[it.mat];
+  const MatPtrs pt = ptrs[it.mat];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = g.r, n = g.n, m = g.m;
+  const float* P = p_hat + g.p_off;
+  const float* Q = q_sum + g.q_off;
+
+  if (q_warm != nullptr && it.row0 == 0 && wave == 0) {
+    float* W = q_warm + g.q_off;
+    const int cnt = min(kUWideCols, m - it.col0) * r;
+    const int64_t base = (int64_t)it.col0 * r;
+    for (int idx = lane; idx < cnt; idx += 64) W[base + idx] = Q[base + idx] / q_div;
+  }
+
+  const int arow0 = it.row0 + wave * kURowsPerWave;
+  if (arow0 >= n) return;
+  const int b = it.col0 + 4 * lane;
+  const int nb = max(0, min(4, m - b));  // valid columns of this lane (vec: 0 or 4)
+  // the HBM stream first: M (= g + e), momentum, parameters of every row of the wave
+  f32x4 Mv[kURowsPerWave], Mm[kURowsPerWave], Xv[kURowsPerWave];
+  if (g.vec) {
+#pragma unroll
+    for (int i = 0; i < kURowsPerWave; ++i) {
+      const bool ok = nb == 4 && arow0 + i < n;
+      const int64_t o = (int64_t)(arow0 + i) * m + b;
+      Mv[i] = ok ? ld4(pt.mread + o) : f32x4{0.f, 0.f, 0.f, 0.f};
+      if (mode != 0) {
+        Mm[i] = ok ? ld4(pt.mom + o) : f32x4{0.f, 0.f, 0.f, 0.f};
+        Xv[i] = ok ? ld4(pt.x + o) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  }
+  // Qs = Q_sum / N for this lane's columns (reducer.py:147)
+  float qv[4][RQ];
+  const bool q4 = (r & 3) == 0 && (g.q_off & 3) == 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (q4) {
+#pragma unroll
+      for (int c = 0; c < RQ; c += 4) {
+        f32x4 t = (j < nb && c < r) ? ld4(Q + (int64_t)(b + j) * r + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) qv[j][c + u] = t[u] / q_div;
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < RQ; ++c) qv[j][c] = (j < nb && c < r) ? Q[(int64_t)(b + j) * r + c] / q_div : 0.f;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < kURowsPerWave; ++i) {
+    const int a = arow0 + i;
+    if (a >= n) break;  // wave-uniform
+    const float* prow = P + (int64_t)a * r;
+    f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < RQ; ++c) {
+      if (c >= r) break;
+      const float pv = prow[c];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = fmaf(pv, qv[j][c], o[j]);
+    }
+    const int64_t ro = (int64_t)a * m;
+    if (g.vec) {
+      if (nb != 4) continue;
+      const f32x4 M = Mv[i];
+      if (mode == 0) {
+        st4(pt.out + ro + b, o);
+        st4(pt.mem + ro + b, M - o);
+      } else {
+        f32x4 mm = Mm[i];
+        f32x4 xx = Xv[i];
+        st4(pt.e + ro + b, M - o);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) mm[j] = __fadd_rn(__fmul_rn(mm[j], momentum), o[j]);
+        const f32x4 up = o + mm;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xx[j] = fmaf(-lr, up[j], xx[j]);
+        st4(pt.mom + ro + b, mm);
+        st4(pt.x + ro + b, xx);
+        if (mode == 2) st4(pt.g + ro + b, up);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j >= nb) break;
+        const int64_t k = ro + b + j;
+        const float M = pt.mread[k];
+        if (mode == 0) {
+          pt.out[k] = o[j];
+          pt.mem[k] = M - o[j];
+        } else {
+          pt.e[k] = M - o[j];
+          const float mm = __fadd_rn(__fmul_rn(pt.mom[k], momentum), o[j]);
+          pt.mom[k] = mm;
+          const float up = o[j] + mm;
+          pt.x[k] = fmaf(-lr, up, pt.x[k]);
+          if (mode == 2) pt.g[k] = up;
+        }
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void rank1_step_kernel(const float* __restrict__ buf, float div,
                                                          float* __restrict__ mom,
                                                          float* __restrict__ x,
@@ -423,10 +545,22 @@ void launch_psgd_q(const MatGeom* geom, const MatPtrs* ptrs, const QItem* items,
 
 void launch_psgd_update(const MatGeom* geom, const MatPtrs* ptrs, const UItem* items,
                         int n_items, const float* p_hat, const float* q_sum, float q_div,
-                        float* q_warm, int mode, float lr, float momentum, hipStream_t s) {
+                        float* q_warm, int mode, float lr, float momentum, int max_rank,
+                        hipStream_t s) {
   if (n_items <= 0) return;
-  hipLaunchKernelGGL(psgd_update_kernel, dim3(n_items), dim3(256), 0, s, geom, ptrs, items,
-                     p_hat, q_sum, q_div, q_warm, mode, lr, momentum);
+  // the item tiles follow the plan's max rank (plan.cpp): wide 16 x 256 tiles up to rank 16
+  if (max_rank <= 4)
+    hipLaunchKernelGGL(psgd_update_wide_kernel<4>, dim3(n_items), dim3(256), 0, s, geom, ptrs,
+                       items, p_hat, q_sum, q_div, q_warm, mode, lr, momentum);
+  else if (max_rank <= 8)
+    hipLaunchKernelGGL(psgd_update_wide_kernel<8>, dim3(n_items), dim3(256), 0, s, geom, ptrs,
+                       items, p_hat, q_sum, q_div, q_warm, mode, lr, momentum);
+  else if (max_rank <= kUWideMaxRank)
+    hipLaunchKernelGGL(psgd_update_wide_kernel<kUWideMaxRank>, dim3(n_items), dim3(256), 0, s,
+                       geom, ptrs, items, p_hat, q_sum, q_div, q_warm, mode, lr, momentum);
+  else
+    hipLaunchKernelGGL(psgd_update_kernel, dim3(n_items), dim3(256), 0, s, geom, ptrs, items,
+                       p_hat, q_sum, q_div, q_warm, mode, lr, momentum);
 }
 
 void launch_rank1_step(const float* buf, float div, float* mom, float* x, float* g, int64_t n,

@@ -347,7 +347,7 @@ class PowerSGDReducer(Reducer):
             B.q_seg.run()
             self.comm.all_reduce(B.q_memory)                # reducer.py:145
             X.psgd_update(B.geom, B.ptrs, B.u_items, B.comm_buf, B.q_memory, float(N),
-                          B.q_warm, 0, 0.0, 0.0)
+                          B.q_warm, 0, 0.0, 0.0, B.max_rank)
         self._r1_unpack.run()                               # reducer.py:166-168
 
     # -- CPU / reference-semantics path --------------------------------------------------
@@ -587,7 +587,7 @@ class PowerSGDOptimizer:
             g.q_seg.run()
             self.comm.all_reduce(B.q_memory[q0:q1])                       # reducer.py:145 (group g)
             X.psgd_update(B.geom, B.ptrs, B.items("u", g.lo, g.hi), B.comm_buf, B.q_memory, float(N),
-                          B.q_warm, mode, lr, mom)
+                          B.q_warm, mode, lr, mom, B.max_rank)
         self.comm.side_launch(pipeline)
         g.launched = True
 
@@ -778,7 +778,7 @@ class PowerSGDOptimizer:
             X = ext()
             if B.shapes:
                 X.psgd_update(B.geom, B.ptrs, B.u_items, B.comm_buf, B.q_memory, float(N), B.q_warm,
-                              2 if self.write_grad else 1, self.lr, self.momentum)
+                              2 if self.write_grad else 1, self.lr, self.momentum, B.max_rank)
             if self.r1_numel:
                 r1 = slice(self.r1_start, self.arena_numel)
                 X.rank1_step(B.rank1_buf, float(N), self.m[r1], self.x[r1],

@@ -98,8 +98,9 @@ def test_native_plan_covers_every_element():
             cov[row0:row1, col0: col0 + 256] += 1
         assert (cov == 1).all()
         cov[:] = 0
+        ur, uc = (16, 256) if max(ranks) <= 16 else (64, 64)  # plan.cpp: wide tiles up to rank 16
         for mat, row0, col0, _ in U[U[:, 0] == i]:
-            cov[row0: row0 + 64, col0: col0 + 64] += 1
+            cov[row0: row0 + ur, col0: col0 + uc] += 1
         assert (cov == 1).all()
     assert d["q_chunks"][3] <= 128  # the tall embedding's Q slabs are capped
 
