@@ -3,6 +3,7 @@
 // Every entry point enqueues on the caller's current HIP stream (so the Python layer can
 // place work on a side stream, overlap it with backward and capture it in a hipGraph),
 // never synchronises and never allocates.
+#include <algorithm>
 #include <ATen/hip/HIPContext.h>
 #include <torch/extension.h>
 
@@ -637,6 +638,8 @@ py::tuple tg_plan(const std::vector<int64_t>& geom, int64_t B) {
   const int64_t nw = cls == ndp::TG_POINTWISE ? (int64_t)g.Co * g.C : (int64_t)g.Co * g.OH * g.OW * g.C * g.H * g.W;
   // split-K slab sums run on float4: every output must hold a multiple of 4 floats
   if (cls < 0 || B <= 0 || ny % 4 || nx % 4 || nw % 4) return py::make_tuple(-1, 1, 1, 1);
+  // tgemm addresses its operands with 32-bit byte offsets of raw buffer descriptors
+  if (std::max(std::max(ny, nx), (int64_t)g.Co * g.C * g.KH * g.KW) * 4 >= (1LL << 31)) return py::make_tuple(-1, 1, 1, 1);
   return py::make_tuple(cls, ndp::tg_splits(g, (int)B, 0), ndp::tg_splits(g, (int)B, 1), ndp::tg_splits(g, (int)B, 2));
 }
 
@@ -661,7 +664,10 @@ py::dict tg_describe(const std::vector<int64_t>& geom, int64_t B, int64_t dir) {
 
 static int tg_batch(const torch::Tensor& t, const ndp::ConvGeom& g, const char* who) {
   TORCH_CHECK(ndp::tg_class(g) >= 0, who, ": no tgemm path for this geometry");
-  return (int)t.size(0);
+  const int64_t B = t.size(0);
+  TORCH_CHECK(std::max(B * g.C * g.H * g.W, B * g.Co * g.OH * g.OW) * 4 < (1LL << 31), who,
+              ": operands >= 2 GB (tgemm uses 32-bit buffer offsets)");
+  return (int)B;
 }
 
 static float* tg_part(const c10::optional<torch::Tensor>& part, int splits, int64_t slab, const char* who) {

@@ -524,13 +524,26 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
       const int opix = UPS == 1 ? pp * G::Q + qq : pp * UPS * (UPS * G::Q) + qq * UPS;
       const int64_t yoff = (int64_t)(b0 + img) * Kout * OPQ + opix;
       float* yb = y + yoff;
+      // addend (UPS == 1 only): y += addend, e.g. the identity-branch gradient of a residual
+      // block added into conv1's grad-x (no separate add launch).  All 16 addends are loaded
+      // under ONE uniform branch before any store: a per-element `addend ? acc + addend[o]`
+      // compiled to 16 serial load + s_waitcnt vmcnt(0) round trips.
+      float ad[16];
+      if (addend != nullptr) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + (wm * G::TM + tm) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          ad[r] = addend[yoff + (int64_t)m * OPQ];
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) ad[r] = 0.f;
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + (wm * G::TM + tm) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         float* d = yb + (int64_t)m * OPQ;
-        // addend (UPS == 1 only): y += addend, e.g. the identity-branch gradient of a
-        // residual block added into conv1's grad-x (no separate add launch)
-        d[0] = addend ? acc[tm][tn][r] + addend[yoff + (int64_t)m * OPQ] : acc[tm][tn][r];
+        d[0] = acc[tm][tn][r] + ad[r];
         if constexpr (UPS == 2) {
           d[1] = 0.f;
           d[2 * G::Q] = 0.f;

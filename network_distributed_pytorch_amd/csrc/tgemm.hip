@@ -32,17 +32,21 @@
 // conv_slab_sum adds in z order: deterministic, no atomics.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "ndp_kernels.h"
 
 namespace ndp {
 
 namespace {
 
-// tile shapes (BM, BN, BK): the 128 x 128 x 16 tile where both GEMM dimensions fill it
+// tile shapes (BM, BN, BK): 64 x 64 x 32, or 64 x 64 x 64 (twice the MFMAs per barrier and
+// per prefetch round trip; NDP_TG_BK=64).  A 128 x 128 x 16 tile (2 x 2 MFMA tiles per wave)
+// was measured slower on every ResNet-50 shape and removed (profiles/r3/tg_bench.md).
 struct TgTile {
   int bm, bn, bk;
 };
-constexpr TgTile kSmallTile{64, 64, 32}, kBigTile{128, 128, 16};
+constexpr TgTile kSmallTile{64, 64, 32}, kDeepTile{64, 64, 64};
 typedef float f32x16t __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ int64_t tg_off(const TgIndex& t, int i) {
@@ -53,6 +57,16 @@ template <int W>
 struct VecT { typedef float __attribute__((ext_vector_type(W))) type; };
 template <>
 struct VecT<1> { typedef float type; };
+
+// W floats from byte offset `off` of a raw buffer (0 past the descriptor's range)
+template <int W>
+__device__ __forceinline__ typename VecT<W>::type bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  if constexpr (W == 1) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+  } else {
+    return __builtin_bit_cast(typename VecT<W>::type, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+  }
+}
 
 template <int W>
 __device__ __forceinline__ float vget(const typename VecT<W>::type& v, int j) {
@@ -121,22 +135,34 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
   }
 
   // two register slots: the global loads of tile t+2 are in flight while tile t's MFMAs run
-  // and tile t+1 waits in registers for its LDS buffer
+  // and tile t+1 waits in registers for its LDS buffer.
+  // Loads are raw BUFFER loads: a masked element gets an offset past the descriptor's range
+  // and the hardware returns 0.  A predicated `ok ? *p : 0` (or a select on the loaded value)
+  // makes hipcc turn each load into a branch + s_waitcnt vmcnt(0), which drained the prefetch
+  // right after issuing it and serialised every k-tile on a full memory round trip (8-10 %
+  // MFMA busy, profiles/r3/pmc_r50b512.md).  Offsets are 32-bit bytes (host-checked < 2 GB).
+  const __amdgpu_buffer_rsrc_t ra_src = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.a), 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb_src = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.b), 0, 0x7fffffff, 0x00020000);
+  constexpr uint32_t kOOB = 0xffffffffu;
+  uint32_t aoffb[NVA], boffb[NVB];
+#pragma unroll
+  for (int v = 0; v < NVA; ++v) aoffb[v] = aok[v] ? (uint32_t)(aoff[v] * 4) : kOOB;
+#pragma unroll
+  for (int v = 0; v < NVB; ++v) boffb[v] = bok[v] ? (uint32_t)(boff[v] * 4) : kOOB;
   VA ra[2][NVA];
   VB rb[2][NVB];
   auto load = [&](int k0, int slot) {
-    const float* pa = g.a + tg_off(g.ak, k0);
-    const float* pb = g.b + (GATHER ? (int64_t)(k0 >> g.bk.sh) * g.bk.so : tg_off(g.bk, k0));
-    const bool full = k0 + TBK <= kend;  // whole tile inside the K range (uniform)
+    const uint32_t ta = (uint32_t)(tg_off(g.ak, k0) * 4);
+    const uint32_t tb = (uint32_t)((GATHER ? (int64_t)(k0 >> g.bk.sh) * g.bk.so : tg_off(g.bk, k0)) * 4);
 #pragma unroll
     for (int v = 0; v < NVA; ++v) {
-      const bool ok = aok[v] && (full || k0 + ak[v] < kend);  // WA = 4 along k: K % 4 == 0
-      ra[slot][v] = ok ? *reinterpret_cast<const VA*>(pa + aoff[v]) : VA{};
+      const bool ok = (aoffb[v] != kOOB) & (k0 + ak[v] < kend);  // WA = 4 along k: K % 4 == 0
+      ra[slot][v] = bload<WA>(ra_src, ok ? aoffb[v] + ta : kOOB);
     }
 #pragma unroll
     for (int v = 0; v < NVB; ++v) {
-      const bool ok = bok[v] && (full || k0 + bk[v] < kend);
-      rb[slot][v] = ok ? *reinterpret_cast<const VB*>(pb + boff[v]) : VB{};
+      const bool ok = (boffb[v] != kOOB) & (k0 + bk[v] < kend);
+      rb[slot][v] = bload<WB>(rb_src, ok ? boffb[v] + tb : kOOB);
     }
   };
   auto store = [&](int buf, int slot) {
@@ -165,28 +191,43 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int ntiles = kend > kbeg ? (kend - kbeg + TBK - 1) / TBK : 0;
+  // One k-tile.  The loop is unrolled by two so the register slot / LDS buffer indices are
+  // compile-time constants (a runtime `t & 1` index into the register arrays forced hipcc to
+  // shuffle them through selects and drain the load queue), and its body is branch-free:
+  // loads past the K range are masked to 0 by the buffer descriptor, the extra LDS stores at
+  // the end are never read.
+  auto step = [&](auto curc, int t) {
+    constexpr int cur = decltype(curc)::value;
+    load(kbeg + (t + 2) * TBK, cur);  // slot `cur` (tile t) is in LDS already
+    // every fragment of the tile in registers first, then the MFMA chain
+    float a[TBK / 2][TM], b[TBK / 2][TN];
+#pragma unroll
+    for (int kp = 0; kp < TBK / 2; ++kp) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[kp][i] = As[cur][2 * kp + h][(wm * TM + i) * 32 + l32];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[kp][j] = Bs[cur][2 * kp + h][(wn * TN + j) * 32 + l32];
+    }
+#pragma unroll
+    for (int kp = 0; kp < TBK / 2; ++kp)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kp][i], b[kp][j], acc[i][j], 0, 0, 0);
+    store(cur ^ 1, cur ^ 1);  // LDS buffer cur^1 was released by the last barrier
+    __syncthreads();
+  };
   if (ntiles > 0) {
     load(kbeg, 0);
-    if (ntiles > 1) load(kbeg + TBK, 1);
+    load(kbeg + TBK, 1);
     store(0, 0);
     __syncthreads();
-    for (int t = 0; t < ntiles; ++t) {
-      const int cur = t & 1;
-      if (t + 2 < ntiles) load(kbeg + (t + 2) * TBK, cur);  // slot `cur` (tile t) is in LDS already
-#pragma unroll
-      for (int kp = 0; kp < TBK / 2; ++kp) {
-        float a[TM], b[TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) a[i] = As[cur][2 * kp + h][(wm * TM + i) * 32 + l32];
-#pragma unroll
-        for (int j = 0; j < TN; ++j) b[j] = Bs[cur][2 * kp + h][(wn * TN + j) * 32 + l32];
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
-      }
-      if (t + 1 < ntiles) store(cur ^ 1, cur ^ 1);  // LDS buffer cur^1 was released by the last barrier
-      __syncthreads();
+    for (int t = 0;; t += 2) {
+      step(std::integral_constant<int, 0>{}, t);
+      if (t + 1 >= ntiles) break;
+      step(std::integral_constant<int, 1>{}, t + 1);
+      if (t + 2 >= ntiles) break;
     }
   }
 
@@ -198,15 +239,26 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
     if (n >= g.N) continue;
     const int64_t noff = tg_off(g.cn, n);
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i) {
+      // addends loaded unconditionally (clamped address) before any store: no per-element
+      // branch + queue drain
+      float ad[16];
+      if (add) {  // uniform: one branch around the whole batch of loads
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          ad[r] = g.addend[tg_off(g.cm, m < g.M ? m : 0) + noff];
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) ad[r] = 0.f;
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (m < g.M) {
-          const int64_t o = tg_off(g.cm, m) + noff;
-          out[o] = add ? acc[i][j][r] + g.addend[o] : acc[i][j][r];
-        }
+        if (m < g.M) out[tg_off(g.cm, m) + noff] = acc[i][j][r] + ad[r];
       }
+    }
   }
 }
 
@@ -221,16 +273,17 @@ TgIndex comp(int sh, int64_t outer, int64_t inner) { return TgIndex{outer, inner
 
 constexpr int kTgFill = 256;  // one workgroup per CU at least
 
-int tg_big() {
+int tg_bk() {
   static int v = -1;
   if (v < 0) {
-    const char* e = getenv("NDP_TG_BIG");  // 1: 128 x 128 x 16 tile where M, N >= 128 (A/B only)
-    v = e ? atoi(e) : 0;  // measured slower on every r50 shape (profiles/r3/tg_bench.md)
+    const char* e = getenv("NDP_TG_BK");  // k-tile depth: 32 or 64
+    v = e ? atoi(e) : 32;
+    if (v != 64) v = 32;
   }
   return v;
 }
 
-TgTile tg_tile(int M, int N) { return (tg_big() && M >= 128 && N >= 128) ? kBigTile : kSmallTile; }
+TgTile tg_tile(int, int) { return tg_bk() == 64 ? kDeepTile : kSmallTile; }
 
 // split-K factor: power of two so that tiles * splits >= kTgFill, each split >= 2 k-tiles
 int tg_pick_splits(int M, int N, int K, int cap) {
@@ -308,7 +361,7 @@ int run(TgArgs a, bool akf, bool bnf, int splits, float* final_out, hipStream_t 
   const dim3 grid((a.N + tile.bn - 1) / tile.bn, (a.M + tile.bm - 1) / tile.bm, splits);
   const bool va = vec_ok(akf ? a.ak : a.am, akf ? a.am : a.ak, a.a, akf ? a.K : a.M) && tg_vec();
   const bool vb = !a.gather && vec_ok(bnf ? a.bn : a.bk, bnf ? a.bk : a.bn, a.b, bnf ? a.N : a.K) && tg_vec();
-  if (tile.bm == kBigTile.bm) launch_tile<kBigTile.bm, kBigTile.bn, kBigTile.bk>(a, akf, bnf, va, vb, grid, s);
+  if (tile.bk == kDeepTile.bk) launch_tile<kDeepTile.bm, kDeepTile.bn, kDeepTile.bk>(a, akf, bnf, va, vb, grid, s);
   else launch_tile<kSmallTile.bm, kSmallTile.bn, kSmallTile.bk>(a, akf, bnf, va, vb, grid, s);
   if (splits <= 1) return 1;
   if (defer && a.addend == nullptr) return splits;  // the consumer (fused BN, gradfinish) sums them
