@@ -79,7 +79,9 @@ __device__ __forceinline__ float vget(const typename VecT<W>::type& v, int j) {
 // per MFMA instead of two, half the global-load instructions per FLOP).
 // WA / WB: elements per global load of A / B along the operand's unit-stride index (4 =
 // one 16-B load; the host checks contiguity, alignment and extents); GATHER implies WB = 1
-template <int TBM, int TBN, int TBK, bool AKF, bool BNF, bool GATHER, int WA, int WB>
+// D: register prefetch slots.  The loads of tile t+1 are issued D-1 k-steps before its LDS
+// store, so D-1 MFMA phases (~1024 cycles each at one wave per SIMD) cover the memory latency.
+template <int TBM, int TBN, int TBK, bool AKF, bool BNF, bool GATHER, int WA, int WB, int D>
 __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
   typedef typename VecT<WA>::type VA;
   typedef typename VecT<WB>::type VB;
@@ -134,8 +136,8 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
     }
   }
 
-  // two register slots: the global loads of tile t+2 are in flight while tile t's MFMAs run
-  // and tile t+1 waits in registers for its LDS buffer.
+  // D register slots: the global loads of tiles t+1 .. t+D-1 are in flight while tile t's
+  // MFMAs run (tile t+1 is stored to the other LDS buffer at the end of the step).
   // Loads are raw BUFFER loads: a masked element gets an offset past the descriptor's range
   // and the hardware returns 0.  A predicated `ok ? *p : 0` (or a select on the loaded value)
   // makes hipcc turn each load into a branch + s_waitcnt vmcnt(0), which drained the prefetch
@@ -149,8 +151,8 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
   for (int v = 0; v < NVA; ++v) aoffb[v] = aok[v] ? (uint32_t)(aoff[v] * 4) : kOOB;
 #pragma unroll
   for (int v = 0; v < NVB; ++v) boffb[v] = bok[v] ? (uint32_t)(boff[v] * 4) : kOOB;
-  VA ra[2][NVA];
-  VB rb[2][NVB];
+  VA ra[D][NVA];
+  VB rb[D][NVB];
   auto load = [&](int k0, int slot) {
     const uint32_t ta = (uint32_t)(tg_off(g.ak, k0) * 4);
     const uint32_t tb = (uint32_t)((GATHER ? (int64_t)(k0 >> g.bk.sh) * g.bk.so : tg_off(g.bk, k0)) * 4);
@@ -191,14 +193,14 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int ntiles = kend > kbeg ? (kend - kbeg + TBK - 1) / TBK : 0;
-  // One k-tile.  The loop is unrolled by two so the register slot / LDS buffer indices are
-  // compile-time constants (a runtime `t & 1` index into the register arrays forced hipcc to
-  // shuffle them through selects and drain the load queue), and its body is branch-free:
+  // One k-tile.  The loop is unrolled by lcm(D, 2) so the register slot / LDS buffer indices
+  // are compile-time constants (a runtime `t & 1` index into the register arrays forced hipcc
+  // to shuffle them through selects and drain the load queue), and its body is branch-free:
   // loads past the K range are masked to 0 by the buffer descriptor, the extra LDS stores at
   // the end are never read.
-  auto step = [&](auto curc, int t) {
-    constexpr int cur = decltype(curc)::value;
-    load(kbeg + (t + 2) * TBK, cur);  // slot `cur` (tile t) is in LDS already
+  auto step = [&](auto slotc, auto bufc, int t) {
+    constexpr int slot = decltype(slotc)::value, cur = decltype(bufc)::value;
+    load(kbeg + (t + D) * TBK, slot);  // slot `slot` (tile t) is in LDS already
     // every fragment of the tile in registers first, then the MFMA chain
     float a[TBK / 2][TM], b[TBK / 2][TN];
 #pragma unroll
@@ -215,19 +217,27 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kp][i], b[kp][j], acc[i][j], 0, 0, 0);
-    store(cur ^ 1, cur ^ 1);  // LDS buffer cur^1 was released by the last barrier
+    store(cur ^ 1, (slot + 1) % D);  // LDS buffer cur^1 was released by the last barrier
     __syncthreads();
   };
+  constexpr int U = D % 2 == 0 ? D : 2 * D;
+  // steps t .. t+U-1 of one unrolled round; false once the last tile has been consumed
+  auto round = [&](auto self, auto uc, int t) -> bool {
+    constexpr int u = decltype(uc)::value;
+    if constexpr (u == U) {
+      return true;
+    } else {
+      step(std::integral_constant<int, u % D>{}, std::integral_constant<int, u % 2>{}, t + u);
+      if (t + u + 1 >= ntiles) return false;
+      return self(self, std::integral_constant<int, u + 1>{}, t);
+    }
+  };
   if (ntiles > 0) {
-    load(kbeg, 0);
-    load(kbeg + TBK, 1);
+#pragma unroll
+    for (int s = 0; s < D; ++s) load(kbeg + s * TBK, s);
     store(0, 0);
     __syncthreads();
-    for (int t = 0;; t += 2) {
-      step(std::integral_constant<int, 0>{}, t);
-      if (t + 1 >= ntiles) break;
-      step(std::integral_constant<int, 1>{}, t + 1);
-      if (t + 2 >= ntiles) break;
+    for (int t = 0; round(round, std::integral_constant<int, 0>{}, t); t += U) {
     }
   }
 
@@ -325,10 +335,20 @@ bool tg_vec() {
   return v != 0;
 }
 
-template <int BM, int BN, int BK>
+int tg_depth() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("NDP_TG_DEPTH");  // register prefetch slots: 2, 3 or 4
+    v = e ? atoi(e) : 2;
+    if (v < 2 || v > 4) v = 2;
+  }
+  return v;
+}
+
+template <int BM, int BN, int BK, int DEPTH>
 void launch_tile(const TgArgs& a, bool akf, bool bnf, bool va, bool vb, dim3 grid, hipStream_t s) {
 #define NDP_TG_LAUNCH(AK, BN_, GA, W1, W2) \
-  hipLaunchKernelGGL((tgemm_kernel<BM, BN, BK, AK, BN_, GA, W1, W2>), grid, dim3(256), 0, s, a)
+  hipLaunchKernelGGL((tgemm_kernel<BM, BN, BK, AK, BN_, GA, W1, W2, DEPTH>), grid, dim3(256), 0, s, a)
 #define NDP_TG_W(AK, BN_, GA)                                  \
   do {                                                         \
     if (va && vb) NDP_TG_LAUNCH(AK, BN_, GA, 4, 4);            \
@@ -361,8 +381,10 @@ int run(TgArgs a, bool akf, bool bnf, int splits, float* final_out, hipStream_t 
   const dim3 grid((a.N + tile.bn - 1) / tile.bn, (a.M + tile.bm - 1) / tile.bm, splits);
   const bool va = vec_ok(akf ? a.ak : a.am, akf ? a.am : a.ak, a.a, akf ? a.K : a.M) && tg_vec();
   const bool vb = !a.gather && vec_ok(bnf ? a.bn : a.bk, bnf ? a.bk : a.bn, a.b, bnf ? a.N : a.K) && tg_vec();
-  if (tile.bk == kDeepTile.bk) launch_tile<kDeepTile.bm, kDeepTile.bn, kDeepTile.bk>(a, akf, bnf, va, vb, grid, s);
-  else launch_tile<kSmallTile.bm, kSmallTile.bn, kSmallTile.bk>(a, akf, bnf, va, vb, grid, s);
+  if (tile.bk == kDeepTile.bk) launch_tile<kDeepTile.bm, kDeepTile.bn, kDeepTile.bk, 2>(a, akf, bnf, va, vb, grid, s);
+  else if (tg_depth() == 3) launch_tile<kSmallTile.bm, kSmallTile.bn, kSmallTile.bk, 3>(a, akf, bnf, va, vb, grid, s);
+  else if (tg_depth() == 4) launch_tile<kSmallTile.bm, kSmallTile.bn, kSmallTile.bk, 4>(a, akf, bnf, va, vb, grid, s);
+  else launch_tile<kSmallTile.bm, kSmallTile.bn, kSmallTile.bk, 2>(a, akf, bnf, va, vb, grid, s);
   if (splits <= 1) return 1;
   if (defer && a.addend == nullptr) return splits;  // the consumer (fused BN, gradfinish) sums them
   launch_slab_sum(a.part, final_out, a.slab, splits, s, a.addend);

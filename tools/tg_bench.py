@@ -28,6 +28,7 @@ SHAPES = {  # name: (C, H, W, Co, k, stride, pad)
     "r50.l1.pw_in": (256, 8, 8, 64, 1, 1, 0),
     "r50.l1.pw_out": (64, 8, 8, 256, 1, 1, 0),
     "r50.l2.pw_in": (512, 4, 4, 128, 1, 1, 0),
+    "r50.l3.pw_in": (1024, 2, 2, 256, 1, 1, 0),
     "r50.l3.pw_out": (256, 2, 2, 1024, 1, 1, 0),
     "r50.l4.pw_out": (512, 1, 1, 2048, 1, 1, 0),
 }
