@@ -60,6 +60,9 @@ struct SegEntry {
 
 constexpr int kPRows = 64;    // rows per P item (4 waves x 16)
 constexpr int kPK = 256;      // k-chunk of a P item
+// plans whose max rank is <= kUWideMaxRank use kPWRows x kPKW P items (psgd_p_wide_kernel)
+constexpr int kPWRows = 16;
+constexpr int kPKW = 1024;
 constexpr int kQCols = 256;   // columns per Q item (4 waves x 64)
 constexpr int kQRowsMax = 256;  // max rows per Q item (LDS: 256 x (16*NCG+pad) floats)
 constexpr int kURows = 64;

@@ -6,7 +6,7 @@
 // grouped kernel are computed ONCE per parameter set:
 //   * P / Q buffer offsets in reference order (so the all-reduced payload and its byte
 //     count are identical to the reference: SURVEY.md §2.7);
-//   * P items  : (matrix, 64-row block, 256-wide k-chunk)   -> split-K over m;
+//   * P items  : (matrix, 64-row block, 256-wide k-chunk; 16 x 1024 up to rank 16) -> split-K over m;
 //   * Q items  : (matrix, 256-col block, row chunk)          -> split-K over n;
 //   * U items  : (matrix, 16x256 tile; 64x64 above rank 16)  -> fused decompress/update;
 //   * split-K slab offsets for the deterministic seg_reduce.
@@ -41,7 +41,8 @@ Plan build_plan(const std::vector<std::pair<int64_t, int64_t>>& shapes, int rank
     g.vec = 0;
     g.p_off = (int32_t)p_off;
     g.q_off = (int32_t)q_off;
-    g.p_chunks = (int32_t)cdiv(m, kPK);
+    const int64_t p_rows = wide ? kPWRows : kPRows, p_k = wide ? kPKW : kPK;
+    g.p_chunks = (int32_t)cdiv(m, p_k);
     // Q split over n: 64-row chunks, but at most 64 chunks (cap the slab scratch), and
     // never more rows than the LDS tile holds.
     int64_t rc = 64;
@@ -53,13 +54,13 @@ Plan build_plan(const std::vector<std::pair<int64_t, int64_t>>& shapes, int rank
     pl.geom.push_back(g);
     pl.q_rows.push_back((int32_t)rc);
 
-    for (int64_t row0 = 0; row0 < n; row0 += kPRows)
+    for (int64_t row0 = 0; row0 < n; row0 += p_rows)
       for (int64_t c = 0; c < g.p_chunks; ++c) {
         PItem it{};
         it.mat = (int32_t)i;
         it.row0 = (int32_t)row0;
-        it.k0 = (int32_t)(c * kPK);
-        it.k1 = (int32_t)std::min<int64_t>(m, (c + 1) * kPK);
+        it.k0 = (int32_t)(c * p_k);
+        it.k1 = (int32_t)std::min<int64_t>(m, (c + 1) * p_k);
         it.chunk = (int32_t)c;
         pl.p_items.push_back(it);
       }

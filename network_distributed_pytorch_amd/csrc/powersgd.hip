@@ -155,6 +155,158 @@ __global__ __launch_bounds__(256) void psgd_p_kernel(const MatGeom* __restrict__
 }
 
 // ----------------------------------------------------------------------------------
+// Same stage for plans with max rank <= kUWideMaxRank: item = kPWRows rows x kPKW columns,
+// wave = 4 rows, lane = 4 consecutive columns of each 256-column slice, so every wave load
+// instruction streams 1 KB of ONE row (the MFMA tile above reads 16 rows x 64 B per
+// instruction).  The partial dot products (4 rows x r per lane) are FMA'd on the VALU and
+// reduced across the wave by recursive halving: each xor step exchanges half of the
+// remaining values, so 4r values cost 4r - 1 shuffles and lane groups end up holding one
+// total each (a fixed tree per value: bitwise reproducible).
+// ----------------------------------------------------------------------------------
+// after the call, v[0] of every lane holds the wave total of value index spread_index<V>(lane)
+template <int V>
+__device__ __forceinline__ void wave_reduce_spread(float (&v)[V], int lane) {
+  static_assert(V >= 1 && V <= 64 && (V & (V - 1)) == 0, "power of two <= 64 values");
+  int o = 32;
+#pragma unroll
+  for (int c = V; c > 1; c >>= 1, o >>= 1) {
+    const bool upper = (lane & o) != 0;
+#pragma unroll
+    for (int k = 0; k < c / 2; ++k) {
+      const float send = upper ? v[k] : v[k + c / 2];
+      const float keep = upper ? v[k + c / 2] : v[k];
+      v[k] = keep + __shfl_xor(send, o, 64);
+    }
+  }
+  for (; o > 0; o >>= 1) v[0] += __shfl_xor(v[0], o, 64);
+}
+
+template <int V>
+__device__ __forceinline__ int spread_index(int lane) {
+  int idx = 0, o = 32;
+#pragma unroll
+  for (int c = V; c > 1; c >>= 1, o >>= 1)
+    if (lane & o) idx += c / 2;
+  return idx;
+}
+
+// lanes whose spread index is owned by them alone (the lowest lane of each group)
+template <int V>
+__device__ __forceinline__ bool spread_writer(int lane) {
+  return (lane & (64 / V - 1)) == 0;  // the low 6 - log2(V) lane bits were plain butterflies
+}
+
+template <int RQ>
+__global__ __launch_bounds__(256) void psgd_p_wide_kernel(const MatGeom* __restrict__ geom,
+                                                          const MatPtrs* __restrict__ ptrs,
+                                                          const PItem* __restrict__ items,
+                                                          const float* __restrict__ q_warm,
+                                                          float* __restrict__ p_part, int fuse_ef) {
+  constexpr int NS = kPKW / 256;          // 256-column slices per item
+  constexpr int SB = RQ <= 8 ? NS : 2;    // slices whose loads are in flight together
+  constexpr int V = 4 * RQ;
+  const PItem it = items[blockIdx.x];
+  const MatGeom g = geom[it.mat];
+  const MatPtrs pt = ptrs[it.mat];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = g.r, n = g.n, m = g.m;
+  const int arow0 = it.row0 + wave * 4;
+  if (arow0 >= n) return;  // no barriers in this kernel
+  const float* Q = q_warm + g.q_off;
+  const bool q4 = (r & 3) == 0 && (g.q_off & 3) == 0;
+
+  float acc[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) acc[v] = 0.f;
+
+#pragma unroll
+  for (int s0 = 0; s0 < NS; s0 += SB) {
+    // the HBM stream of SB slices first: M = g [+ e] of the wave's 4 rows
+    f32x4 mv[4][SB];
+    if (g.vec) {
+      f32x4 ev[4][SB];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int sb = 0; sb < SB; ++sb) {
+          const int b = it.k0 + 256 * (s0 + sb) + 4 * lane;
+          const bool ok = arow0 + i < n && b < it.k1;  // vec: k1 - b >= 4 whenever b < k1
+          const int64_t o = (int64_t)(arow0 + i) * m + b;
+          mv[i][sb] = ok ? ld4(pt.min + o) : f32x4{0.f, 0.f, 0.f, 0.f};
+          ev[i][sb] = (ok && fuse_ef) ? ld4(pt.e + o) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      if (fuse_ef) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int sb = 0; sb < SB; ++sb) {
+            const int b = it.k0 + 256 * (s0 + sb) + 4 * lane;
+            mv[i][sb] = mv[i][sb] + ev[i][sb];  // send = g + e   (ddp_init.py:156-157)
+            if (arow0 + i < n && b < it.k1) st4(pt.e + (int64_t)(arow0 + i) * m + b, mv[i][sb]);
+          }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int sb = 0; sb < SB; ++sb) {
+          const int b = it.k0 + 256 * (s0 + sb) + 4 * lane;
+          float t[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float v = 0.f;
+            if (arow0 + i < n && b + j < it.k1) {
+              const int64_t o = (int64_t)(arow0 + i) * m + b + j;
+              v = pt.min[o];
+              if (fuse_ef) {
+                v = v + pt.e[o];
+                pt.e[o] = v;
+              }
+            }
+            t[j] = v;
+          }
+          mv[i][sb] = f32x4{t[0], t[1], t[2], t[3]};
+        }
+    }
+    // Q rows of this lane's columns (L2-resident: m x r floats per matrix)
+#pragma unroll
+    for (int sb = 0; sb < SB; ++sb) {
+      const int b = it.k0 + 256 * (s0 + sb) + 4 * lane;
+      float qv[4][RQ];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool okj = b + j < it.k1;
+        if (q4) {
+#pragma unroll
+          for (int c = 0; c < RQ; c += 4) {
+            const f32x4 t = (okj && c < r) ? ld4(Q + (int64_t)(b + j) * r + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) qv[j][c + u] = t[u];
+          }
+        } else {
+#pragma unroll
+          for (int c = 0; c < RQ; ++c) qv[j][c] = (okj && c < r) ? Q[(int64_t)(b + j) * r + c] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int c = 0; c < RQ; ++c) acc[i * RQ + c] = fmaf(mv[i][sb][j], qv[j][c], acc[i * RQ + c]);
+    }
+  }
+
+  wave_reduce_spread<V>(acc, lane);
+  if (!spread_writer<V>(lane)) return;
+  const int idx = spread_index<V>(lane);
+  const int i = idx / RQ, c = idx % RQ;
+  const int a = arow0 + i;
+  if (c < r && a < n) p_part[g.pp_off + (int64_t)it.chunk * n * r + (int64_t)a * r + c] = acc[0];
+}
+
+// ----------------------------------------------------------------------------------
 // Q partial:  q_part[chunk][b][c] = sum_{a in [row0,row1)} M[a][b] * Phat[a][c]
 // workgroup = [row0,row1) x 256 columns; wave w owns columns col0+64w..+63.
 // Lane l streams M[a][b0+4(l&15) .. +3] for row a = step + (l>>4): 4 rows x 256 B per
@@ -511,6 +663,20 @@ void launch_psgd_p(const MatGeom* geom, const MatPtrs* ptrs, const PItem* items,
                    const float* q_warm, float* p_part, int fuse_ef, int max_rank,
                    hipStream_t s) {
   if (n_items <= 0) return;
+  // the item shape follows the plan's max rank (plan.cpp): wide 16 x kPKW items up to rank 16
+  if (max_rank <= 4) {
+    hipLaunchKernelGGL(psgd_p_wide_kernel<4>, dim3(n_items), dim3(256), 0, s, geom, ptrs, items, q_warm, p_part, fuse_ef);
+    return;
+  }
+  if (max_rank <= 8) {
+    hipLaunchKernelGGL(psgd_p_wide_kernel<8>, dim3(n_items), dim3(256), 0, s, geom, ptrs, items, q_warm, p_part, fuse_ef);
+    return;
+  }
+  if (max_rank <= kUWideMaxRank) {
+    hipLaunchKernelGGL(psgd_p_wide_kernel<kUWideMaxRank>, dim3(n_items), dim3(256), 0, s, geom, ptrs, items, q_warm,
+                       p_part, fuse_ef);
+    return;
+  }
   const int ncg = ncg_for(max_rank);
   const size_t lds = sizeof(float) * 16 * ncg * (kPK + 4);
   if (ncg == 4) allow_lds(reinterpret_cast<const void*>(psgd_p_kernel<4>), lds);

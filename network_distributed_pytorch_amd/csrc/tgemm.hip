@@ -24,8 +24,8 @@
 // split as (i >> sh) * so + (i & (2^sh - 1)) * si — NCHW's (image, pixel) pairs are such
 // composites when the map is a power of two — and an optional tap-table gather for B.
 // Tiles: 64 x 64 x 32, 4 waves of 32 x 32 (one f32x16 accumulator each), operands staged
-// in LDS as [k][m] / [k][n] with an odd row stride (conflict-free transposing stores and
-// broadcast-free MFMA reads), register double buffering: the global loads of tile t+1 are
+// in LDS as [m][k] / [n][k] (k contiguous, padded rows: b128 fragment reads), register
+// double buffering: the global loads of tile t+1 are
 // in flight while the MFMAs of tile t issue; one barrier per tile.  The load mapping walks
 // the operand's contiguous index across lanes (template AKF / BNF) so every global access is
 // a coalesced 256-B wave transaction.  Split-K (blockIdx.z) writes slabs that
@@ -48,6 +48,7 @@ struct TgTile {
 };
 constexpr TgTile kSmallTile{64, 64, 32}, kDeepTile{64, 64, 64};
 typedef float f32x16t __attribute__((ext_vector_type(16)));
+typedef float f32x4t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int64_t tg_off(const TgIndex& t, int i) {
   return (int64_t)(i >> t.sh) * t.so + (int64_t)(i & ((1 << t.sh) - 1)) * t.si;
@@ -86,8 +87,16 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
   typedef typename VecT<WA>::type VA;
   typedef typename VecT<WB>::type VB;
   constexpr int TM = TBM / 64, TN = TBN / 64;
-  __shared__ float As[2][TBK][TBM + 1];
-  __shared__ float Bs[2][TBK][TBN + 1];
+  // LDS tiles are [m][k] / [n][k] with k contiguous (row stride TBK + 4: 16-B aligned rows, and
+  // 16 consecutive rows start 36 (or 68) words apart, i.e. in disjoint 4-bank groups).  Lane
+  // (h, l32) feeds MFMA kp with k = h * TBK/2 + kp — any k order works as long as A and B
+  // agree — so a lane's whole fragment of a tile is TBK/2 CONSECUTIVE floats: TBK/8
+  // ds_read_b128 per operand, all issued before the MFMA chain (a [k][m] layout needs one
+  // ds_read_b32 per MFMA, and hipcc interleaved those with the chain, exposing the LDS
+  // latency before every MFMA pair).
+  constexpr int LDK = TBK + 4;
+  __shared__ __attribute__((aligned(16))) float As[2][TBM][LDK];
+  __shared__ __attribute__((aligned(16))) float Bs[2][TBN][LDK];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, l32 = lane & 31;
   const int wm = wave & 1, wn = wave >> 1;
@@ -172,15 +181,15 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
     for (int v = 0; v < NVA; ++v)
 #pragma unroll
       for (int j = 0; j < WA; ++j) {
-        if (AKF) As[buf][ak[v] + j][am[v]] = vget<WA>(ra[slot][v], j);
-        else As[buf][ak[v]][am[v] + j] = vget<WA>(ra[slot][v], j);
+        if (AKF) As[buf][am[v]][ak[v] + j] = vget<WA>(ra[slot][v], j);
+        else As[buf][am[v] + j][ak[v]] = vget<WA>(ra[slot][v], j);
       }
 #pragma unroll
     for (int v = 0; v < NVB; ++v)
 #pragma unroll
       for (int j = 0; j < WB; ++j) {
-        if (BNF) Bs[buf][bk[v]][bn[v] + j] = vget<WB>(rb[slot][v], j);
-        else Bs[buf][bk[v] + j][bn[v]] = vget<WB>(rb[slot][v], j);
+        if (BNF) Bs[buf][bn[v] + j][bk[v]] = vget<WB>(rb[slot][v], j);
+        else Bs[buf][bn[v]][bk[v] + j] = vget<WB>(rb[slot][v], j);
       }
   };
 
@@ -201,35 +210,50 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
   auto step = [&](auto slotc, auto bufc, int t) {
     constexpr int slot = decltype(slotc)::value, cur = decltype(bufc)::value;
     load(kbeg + (t + D) * TBK, slot);  // slot `slot` (tile t) is in LDS already
+    // pin the loads at the top of the step: hipcc otherwise sinks them below the LDS stores
+    // at the end of the step, which leaves one MFMA phase (not D - 1) to hide their latency
+    __builtin_amdgcn_sched_barrier(0);
     // every fragment of the tile in registers first, then the MFMA chain
-    float a[TBK / 2][TM], b[TBK / 2][TN];
+    f32x4t a[TM][TBK / 8], b[TN][TBK / 8];
 #pragma unroll
-    for (int kp = 0; kp < TBK / 2; ++kp) {
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[kp][i] = As[cur][2 * kp + h][(wm * TM + i) * 32 + l32];
+      for (int q = 0; q < TBK / 8; ++q)
+        a[i][q] = *reinterpret_cast<const f32x4t*>(&As[cur][(wm * TM + i) * 32 + l32][h * (TBK / 2) + 4 * q]);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) b[kp][j] = Bs[cur][2 * kp + h][(wn * TN + j) * 32 + l32];
-    }
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < TBK / 8; ++q)
+        b[j][q] = *reinterpret_cast<const f32x4t*>(&Bs[cur][(wn * TN + j) * 32 + l32][h * (TBK / 2) + 4 * q]);
 #pragma unroll
     for (int kp = 0; kp < TBK / 2; ++kp)
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kp][i], b[kp][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][kp / 4][kp % 4], b[j][kp / 4][kp % 4], acc[i][j], 0, 0, 0);
     store(cur ^ 1, (slot + 1) % D);  // LDS buffer cur^1 was released by the last barrier
     __syncthreads();
   };
   constexpr int U = D % 2 == 0 ? D : 2 * D;
-  // steps t .. t+U-1 of one unrolled round; false once the last tile has been consumed
-  auto round = [&](auto self, auto uc, int t) -> bool {
+  // steps t .. t+U-1 of one unrolled round (no exit inside: a mid-round `break` gave the
+  // loop two exits, and the rotated loop then copied the prefetch registers between slots
+  // each round, i.e. waited for every load in flight: s_waitcnt vmcnt(0) per round)
+  auto round = [&](auto self, auto uc, int t) -> void {
     constexpr int u = decltype(uc)::value;
-    if constexpr (u == U) {
-      return true;
-    } else {
+    if constexpr (u < U) {
       step(std::integral_constant<int, u % D>{}, std::integral_constant<int, u % 2>{}, t + u);
-      if (t + u + 1 >= ntiles) return false;
-      return self(self, std::integral_constant<int, u + 1>{}, t);
+      self(self, std::integral_constant<int, u + 1>{}, t);
+    }
+  };
+  // the last ntiles % U steps, one at a time (slot / buffer indices continue the pattern)
+  auto tail = [&](auto self, auto uc, int t, int left) -> void {
+    constexpr int u = decltype(uc)::value;
+    if constexpr (u < U - 1) {
+      if (u < left) {
+        step(std::integral_constant<int, u % D>{}, std::integral_constant<int, u % 2>{}, t + u);
+        self(self, std::integral_constant<int, u + 1>{}, t, left);
+      }
     }
   };
   if (ntiles > 0) {
@@ -237,8 +261,9 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
     for (int s = 0; s < D; ++s) load(kbeg + s * TBK, s);
     store(0, 0);
     __syncthreads();
-    for (int t = 0; round(round, std::integral_constant<int, 0>{}, t); t += U) {
-    }
+    int t = 0;
+    for (; t + U <= ntiles; t += U) round(round, std::integral_constant<int, 0>{}, t);
+    tail(tail, std::integral_constant<int, 0>{}, t, ntiles - t);
   }
 
   float* out = g.part != nullptr ? g.part + (int64_t)blockIdx.z * g.slab : g.c;
@@ -281,7 +306,15 @@ int ilog2_exact(int v) {
 TgIndex plain(int64_t stride) { return TgIndex{0, stride, 30, 0}; }  // i < 2^30: outer part always 0
 TgIndex comp(int sh, int64_t outer, int64_t inner) { return TgIndex{outer, inner, sh, 0}; }
 
-constexpr int kTgFill = 256;  // one workgroup per CU at least
+int tg_fill() {  // split-K until tiles x splits reaches this many workgroups (NDP_TG_FILL)
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("NDP_TG_FILL");
+    v = e ? atoi(e) : 256;  // one workgroup per CU at least
+    if (v < 1) v = 256;
+  }
+  return v;
+}
 
 int tg_bk() {
   static int v = -1;
@@ -301,7 +334,7 @@ int tg_pick_splits(int M, int N, int K, int cap) {
   const int tiles = ((M + t.bm - 1) / t.bm) * ((N + t.bn - 1) / t.bn);
   const int ktiles = (K + t.bk - 1) / t.bk;
   int s = 1;
-  while (s * 2 <= cap && tiles * s < kTgFill && ktiles >= 4 * s) s *= 2;
+  while (s * 2 <= cap && tiles * s < tg_fill() && ktiles >= 4 * s) s *= 2;
   return s;
 }
 
