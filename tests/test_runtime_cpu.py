@@ -76,21 +76,24 @@ def test_reducer_world1_matches_oracle():
 
 
 @pytest.mark.skipif(not ops.native_available(), reason="extension not built")
-def test_native_plan_covers_every_element():
+@pytest.mark.parametrize("rank", [16, 32])
+def test_native_plan_covers_every_element(rank):
     X = ops.ext()
     shapes = [(64, 147), (1000, 512), (7, 5), (30522, 8), (300, 1030)]
-    d = X.build_plan(shapes, 16)
-    ranks, p_offs, q_offs, pt, qt = plan_layout(shapes, 16)
+    d = X.build_plan(shapes, rank)
+    ranks, p_offs, q_offs, pt, qt = plan_layout(shapes, rank)
     assert d["ranks"] == ranks and d["p_offs"] == p_offs and d["q_offs"] == q_offs
     assert d["p_total"] == pt and d["q_total"] == qt
     P = np.frombuffer(d["p_items"].numpy().tobytes(), dtype=np.int32).reshape(-1, 8)
     Q = np.frombuffer(d["q_items"].numpy().tobytes(), dtype=np.int32).reshape(-1, 8)
     U = np.frombuffer(d["u_items"].numpy().tobytes(), dtype=np.int32).reshape(-1, 4)
+    wide = max(ranks) <= 16  # plan.cpp: 16 x 1024 P items and 16 x 256 update tiles up to rank 16
+    pr, pk = (16, 1024) if wide else (64, 256)
     for i, (n, m) in enumerate(shapes):
         cov = np.zeros((n, m), np.int32)
         for mat, row0, k0, k1, chunk, *_ in P[P[:, 0] == i]:
-            cov[row0: row0 + 64, k0:k1] += 1
-            assert chunk == k0 // 256
+            cov[row0: row0 + pr, k0:k1] += 1
+            assert chunk == k0 // pk
         assert (cov == 1).all()
         cov[:] = 0
         for mat, col0, row0, row1, chunk, *_ in Q[Q[:, 0] == i]:
@@ -98,7 +101,7 @@ def test_native_plan_covers_every_element():
             cov[row0:row1, col0: col0 + 256] += 1
         assert (cov == 1).all()
         cov[:] = 0
-        ur, uc = (16, 256) if max(ranks) <= 16 else (64, 64)  # plan.cpp: wide tiles up to rank 16
+        ur, uc = (16, 256) if wide else (64, 64)
         for mat, row0, col0, _ in U[U[:, 0] == i]:
             cov[row0: row0 + ur, col0: col0 + uc] += 1
         assert (cov == 1).all()
