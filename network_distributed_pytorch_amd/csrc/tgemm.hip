@@ -40,13 +40,13 @@ namespace ndp {
 
 namespace {
 
-// tile shapes (BM, BN, BK): 64 x 64 x 32, or 64 x 64 x 64 (twice the MFMAs per barrier and
-// per prefetch round trip; NDP_TG_BK=64).  A 128 x 128 x 16 tile (2 x 2 MFMA tiles per wave)
-// was measured slower on every ResNet-50 shape and removed (profiles/r3/tg_bench.md).
+// tile shape (BM, BN, BK) = 64 x 64 x 32, one 32 x 32 accumulator per wave.  Measured and
+// removed (profiles/r3/tg_bench.md): 128 x 128 x 16; 64 x 128 / 128 x 64 (two accumulators per
+// wave: 3-5x slower on every shape); a 64-deep k-tile; 3-4 deep register prefetch.
 struct TgTile {
   int bm, bn, bk;
 };
-constexpr TgTile kSmallTile{64, 64, 32}, kDeepTile{64, 64, 64};
+constexpr TgTile kTile64{64, 64, 32};
 typedef float f32x16t __attribute__((ext_vector_type(16)));
 typedef float f32x4t __attribute__((ext_vector_type(4)));
 
@@ -103,8 +103,8 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
   const int n0 = blockIdx.x * TBN, m0 = blockIdx.y * TBM;
   const int kbeg = blockIdx.z * g.kchunk;
   const int kend = min(g.K, kbeg + g.kchunk);
-  constexpr int PER = TBM * TBK / 256;  // 8 elements of each operand per thread and tile
-  constexpr int NVA = PER / WA, NVB = PER / WB;
+  constexpr int PERA = TBM * TBK / 256, PERB = TBN * TBK / 256;  // elements per thread and tile
+  constexpr int NVA = PERA / WA, NVB = PERB / WB;
   constexpr int FA = (AKF ? TBK : TBM) / WA, FB = (BNF ? TBN : TBK) / WB;  // vectors per fast row
 
   // Fixed per-thread tile coordinates.  Every operand offset splits into a tile-invariant
@@ -176,20 +176,39 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
       rb[slot][v] = bload<WB>(rb_src, ok ? boffb[v] + tb : kOOB);
     }
   };
+  // A vector along m / n lands in 4 different rows of the [m][k] / [n][k] image.  Written
+  // component by component, the 16 lanes of a k-row (rows 4i + j, i = 0..15) hit only 4 bank
+  // groups (row stride 36 words: 144 i = 16 i mod 64), i.e. 4-way conflicts (profiles/r3/
+  // pmc_tgemm_micro.md).  Write w stores component j = (w + i / 4) & 3 instead: banks
+  // 16 (i & 3) + 36 j + k then cover all 64 (2-way at 32 vectors per row).
+  auto rot = [](int w, int fast) { return (w + (fast >> 4)) & 3; };
+  auto pick = [](const f32x4t& v, int j) { return j == 0 ? v[0] : (j == 1 ? v[1] : (j == 2 ? v[2] : v[3])); };
   auto store = [&](int buf, int slot) {
 #pragma unroll
     for (int v = 0; v < NVA; ++v)
 #pragma unroll
-      for (int j = 0; j < WA; ++j) {
-        if (AKF) As[buf][am[v]][ak[v] + j] = vget<WA>(ra[slot][v], j);
-        else As[buf][am[v] + j][ak[v]] = vget<WA>(ra[slot][v], j);
+      for (int w = 0; w < WA; ++w) {
+        if (AKF) {
+          As[buf][am[v]][ak[v] + w] = vget<WA>(ra[slot][v], w);
+        } else if constexpr (WA == 4) {
+          const int j = rot(w, am[v]);
+          As[buf][am[v] + j][ak[v]] = pick(ra[slot][v], j);
+        } else {
+          As[buf][am[v]][ak[v]] = vget<WA>(ra[slot][v], w);
+        }
       }
 #pragma unroll
     for (int v = 0; v < NVB; ++v)
 #pragma unroll
-      for (int j = 0; j < WB; ++j) {
-        if (BNF) Bs[buf][bn[v] + j][bk[v]] = vget<WB>(rb[slot][v], j);
-        else Bs[buf][bn[v]][bk[v] + j] = vget<WB>(rb[slot][v], j);
+      for (int w = 0; w < WB; ++w) {
+        if (!BNF) {
+          Bs[buf][bn[v]][bk[v] + w] = vget<WB>(rb[slot][v], w);
+        } else if constexpr (WB == 4) {
+          const int j = rot(w, bn[v]);
+          Bs[buf][bn[v] + j][bk[v]] = pick(rb[slot][v], j);
+        } else {
+          Bs[buf][bn[v]][bk[v]] = vget<WB>(rb[slot][v], w);
+        }
       }
   };
 
@@ -316,17 +335,7 @@ int tg_fill() {  // split-K until tiles x splits reaches this many workgroups (N
   return v;
 }
 
-int tg_bk() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("NDP_TG_BK");  // k-tile depth: 32 or 64
-    v = e ? atoi(e) : 32;
-    if (v != 64) v = 32;
-  }
-  return v;
-}
-
-TgTile tg_tile(int, int) { return tg_bk() == 64 ? kDeepTile : kSmallTile; }
+TgTile tg_tile(int, int) { return kTile64; }
 
 // split-K factor: power of two so that tiles * splits >= kTgFill, each split >= 2 k-tiles
 int tg_pick_splits(int M, int N, int K, int cap) {
@@ -363,19 +372,11 @@ bool tg_vec() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("NDP_TG_VEC");  // 0: scalar loads only (A/B)
-    v = e ? atoi(e) : 0;  // measured slower on every r50 shape (profiles/r3/tg_bench.md)
+    // on by default since the branch-free raw-buffer k-loop: R152 r=4 16.11 -> 15.45 ms,
+    // R50 dense 6.56 -> 6.31 ms (profiles/r3/tg_bench.md); slower with the old predicated loads
+    v = e ? atoi(e) : 1;
   }
   return v != 0;
-}
-
-int tg_depth() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("NDP_TG_DEPTH");  // register prefetch slots: 2, 3 or 4
-    v = e ? atoi(e) : 2;
-    if (v < 2 || v > 4) v = 2;
-  }
-  return v;
 }
 
 template <int BM, int BN, int BK, int DEPTH>
@@ -414,10 +415,7 @@ int run(TgArgs a, bool akf, bool bnf, int splits, float* final_out, hipStream_t 
   const dim3 grid((a.N + tile.bn - 1) / tile.bn, (a.M + tile.bm - 1) / tile.bm, splits);
   const bool va = vec_ok(akf ? a.ak : a.am, akf ? a.am : a.ak, a.a, akf ? a.K : a.M) && tg_vec();
   const bool vb = !a.gather && vec_ok(bnf ? a.bn : a.bk, bnf ? a.bk : a.bn, a.b, bnf ? a.N : a.K) && tg_vec();
-  if (tile.bk == kDeepTile.bk) launch_tile<kDeepTile.bm, kDeepTile.bn, kDeepTile.bk, 2>(a, akf, bnf, va, vb, grid, s);
-  else if (tg_depth() == 3) launch_tile<kSmallTile.bm, kSmallTile.bn, kSmallTile.bk, 3>(a, akf, bnf, va, vb, grid, s);
-  else if (tg_depth() == 4) launch_tile<kSmallTile.bm, kSmallTile.bn, kSmallTile.bk, 4>(a, akf, bnf, va, vb, grid, s);
-  else launch_tile<kSmallTile.bm, kSmallTile.bn, kSmallTile.bk, 2>(a, akf, bnf, va, vb, grid, s);
+  launch_tile<kTile64.bm, kTile64.bn, kTile64.bk, 2>(a, akf, bnf, va, vb, grid, s);
   if (splits <= 1) return 1;
   if (defer && a.addend == nullptr) return splits;  // the consumer (fused BN, gradfinish) sums them
   launch_slab_sum(a.part, final_out, a.slab, splits, s, a.addend);
