@@ -632,10 +632,28 @@ static int bn_colw() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("NDP_BN_COLW");
-    v = e ? atoi(e) : 8;  // ResNet-18 step: 4 -> 2.221 ms, 8 -> 2.182 ms, 16 -> 2.202 ms (1x MI355X)
-    if (v != 4 && v != 8 && v != 16) v = 8;
+    // 0 (default): per launch shape, bn_colw_for; 4 / 8 / 16: fixed (round 2 measured 8 best
+    // as a single global value: ResNet-18 step 4 -> 2.221 ms, 8 -> 2.182, 16 -> 2.202)
+    v = e ? atoi(e) : 0;
+    if (v != 0 && v != 4 && v != 8 && v != 16) v = 0;
   }
   return v;
+}
+
+// column-block width for one launch: the fixed NDP_BN_COLW, or (0) the widest block that still
+// gives >= 256 workgroups (one per CU), else the narrowest allowed one — 4 columns (16-B row
+// segments) only at per-GPU batch <= 128, where grid size matters more than segment width.
+// Measured (1x MI355X, profiles/r3/bn_colw.md) against the fixed 8: ResNet-18 r=4 batch 512
+// 1.945 -> 1.943 ms, batch 64 1.012 -> 1.000 ms, ResNet-152 r=4 15.19 -> 14.78 ms, ResNet-50
+// dense 6.246 -> 6.178 ms.
+static int bn_colw_for(int HW, int C, int N) {
+  const int mode = bn_colw();
+  if (mode != 0) return mode > HW ? mode : HW;
+  const int lo = N <= 128 ? 4 : 8;
+  const int64_t cols = (int64_t)C * HW;
+  for (int cw = 16; cw >= lo; cw >>= 1)
+    if (cw >= HW && cols / cw >= 256) return cw;
+  return HW > lo ? HW : lo;
 }
 
 template <int BWD, int CW>
@@ -671,7 +689,7 @@ static void launch_small_fused(int HW, const float* x, const float* res, const f
                        momentum, relu, src, nslab);
     return;
   }
-  switch (bn_colw() > HW ? bn_colw() : HW) {
+  switch (bn_colw_for(HW, C, N)) {
     case 16:
       launch_small_fused_cw<BWD, 16>(HW, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out,
                                      dres, N, C, eps, momentum, relu, s, src, nslab);
