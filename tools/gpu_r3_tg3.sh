@@ -21,3 +21,11 @@ for arm in "v0f256|NDP_TG_VEC=0" "v1f256|NDP_TG_VEC=1" "v1f512|NDP_TG_VEC=1,NDP_
   env $envs timeout -k 10 300 python bench.py --steps 10 --warmup 3 --model resnet50 --reducer dense > $O/r50_$label.json 2> $O/r50_$label.err || { echo "r50 $label failed"; tail -5 $O/r50_$label.err; exit 1; }
   echo "$label r152 $(python3 tools/jline.py $O/r152_$label.json)"; echo "$label r50 $(python3 tools/jline.py $O/r50_$label.json)"
 done
+# kernel tables at the shipped defaults (b512, b64)
+for cfg in "b512:" "b64:--global-batch 64"; do
+  tag=${cfg%%:*}; args=${cfg#*:}
+  timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/prof_$tag -o run -- python3 bench.py --no-supervise --steps 25 --warmup 5 $args > $O/prof_$tag.out 2>&1 || { echo "prof $tag failed"; tail -5 $O/prof_$tag.out; exit 1; }
+  f=$(find $O/prof_$tag -name '*kernel_trace.csv' | head -n 1)
+  python3 tools/prof_summary.py "$f" --steps 20 --marker 'conv_fwd_kernel<7, 7' --top 60 > $O/kernels_$tag.md && head -30 $O/kernels_$tag.md
+  rm -rf $O/prof_$tag
+done
