@@ -282,7 +282,15 @@ struct ConvFwdCfg {
   // float4 steps) LDA = 1 mod 32 -> <= 2-way; grad-x (TRANSW: 4 consecutive (m, tap) of a
   // weight row per lane) LDA = 2 mod 32 -> <= 2-way (1 mod 32 was 5-way; PMC round 3)
   static constexpr int LDA = TRANSW ? BM + 2 : BM + 1;
-  static constexpr int A_SZ = KK * LDA;
+  // AV: [m][kk] A image instead (kk contiguous, row stride LDAM with LDAM / 4 odd: the 16 rows
+  // of a ds_read_b128 phase start in disjoint 4-bank groups).  Lane half h consumes kk =
+  // h * NSTEP + t at MFMA step t, so KB consecutive steps are KB / 4 ds_read_b128 per tile
+  // instead of KB ds_read_b32 (each of which the MFMA chain waited on), and the forward's
+  // float4 weight loads land as one ds_write_b128.  Needs KB % 4 == 0 and NSTEP % 4 == 0
+  // (every 8x8 / 4x4 layer config; the 7x7 stem keeps [kk][m]).
+  static constexpr bool AV = KB % 4 == 0 && ((CK / 2) * RS) % 4 == 0;
+  static constexpr int LDAM = KK + (((KK / 4) % 2 == 0) ? 4 : 8);
+  static constexpr int A_SZ = AV ? BM * LDAM : KK * LDA;
   static constexpr int B_SZ = IMGS * IMGSTR;
   // A staging: float4 rows when every chunk is whole channels and rows are 16-B aligned
   static constexpr int B4 = IMGS * CK * HW / 4, B_PER_T = (B4 + 255) / 256;
@@ -329,7 +337,9 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
 
   int a_base[G::TM], b_base[G::TN];
 #pragma unroll
-  for (int tm = 0; tm < G::TM; ++tm) a_base[tm] = h * G::NSTEP * G::LDA + (wm * G::TM + tm) * 32 + l32;
+  for (int tm = 0; tm < G::TM; ++tm)
+    a_base[tm] = G::AV ? ((wm * G::TM + tm) * 32 + l32) * G::LDAM + h * G::NSTEP
+                       : h * G::NSTEP * G::LDA + (wm * G::TM + tm) * 32 + l32;
 #pragma unroll
   for (int tn = 0; tn < G::TN; ++tn) {
     const int n = (wn * G::TN + tn) * 32 + l32;
@@ -392,21 +402,30 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
         if (VEC) {
           if (!TRANSW) {
             const int r = e >> 2, k4 = r % (G::KK / 4), m = 4 * (r / (G::KK / 4)) + (e & 3);
-            float* d = A + 4 * k4 * G::LDA + m;
-            d[0] = ra[i].x; d[G::LDA] = ra[i].y; d[2 * G::LDA] = ra[i].z; d[3 * G::LDA] = ra[i].w;
+            if constexpr (G::AV) {
+              *reinterpret_cast<f32x4c*>(A + m * G::LDAM + 4 * k4) = ra[i];
+            } else {
+              float* d = A + 4 * k4 * G::LDA + m;
+              d[0] = ra[i].x; d[G::LDA] = ra[i].y; d[2 * G::LDA] = ra[i].z; d[3 * G::LDA] = ra[i].w;
+            }
           } else {
             const int c = e / (BM * G::RS / 4), f = 4 * (e - c * (BM * G::RS / 4));
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               const int m = (f + j) / G::RS, rs = (f + j) - m * G::RS;
-              A[(c * G::RS + (G::RS - 1 - rs)) * G::LDA + m] = ra[i][j];  // flip the taps
+              const int kk = c * G::RS + (G::RS - 1 - rs);  // flip the taps
+              if constexpr (G::AV) A[m * G::LDAM + kk] = ra[i][j];
+              else A[kk * G::LDA + m] = ra[i][j];
             }
           }
         } else {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int f = 4 * e + j, m = f / G::KK, kk = f - m * G::KK;
-            if (f < BM * G::KK) A[kk * G::LDA + m] = ra[i][j];
+            if (f < BM * G::KK) {
+              if constexpr (G::AV) A[m * G::LDAM + kk] = ra[i][j];
+              else A[kk * G::LDA + m] = ra[i][j];
+            }
           }
         }
       }
@@ -449,10 +468,22 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
         const int t = blk * KB + i;
         const int c = t / G::RS, rs = t - c * G::RS, r = rs / S, s = rs - r * S;
         const int offb = c * G::HWp + r * G::Wp + s;
+        if constexpr (!G::AV) {
 #pragma unroll
-        for (int tm = 0; tm < G::TM; ++tm) av[slot][i][tm] = A[a_base[tm] + t * G::LDA];
+          for (int tm = 0; tm < G::TM; ++tm) av[slot][i][tm] = A[a_base[tm] + t * G::LDA];
+        }
 #pragma unroll
         for (int tn = 0; tn < G::TN; ++tn) bv[slot][i][tn] = B[b_base[tn] + offb];
+      }
+      if constexpr (G::AV) {
+#pragma unroll
+        for (int tm = 0; tm < G::TM; ++tm)
+#pragma unroll
+          for (int q = 0; q < KB / 4; ++q) {
+            const f32x4c v = *reinterpret_cast<const f32x4c*>(A + a_base[tm] + blk * KB + 4 * q);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) av[slot][4 * q + j][tm] = v[j];
+          }
       }
     };
     if constexpr (SCH == 1) __builtin_amdgcn_iglp_opt(0);
