@@ -605,7 +605,10 @@ struct ConvWgCfg {
     }
   }
   static constexpr int NSTEP = PQ / 2, NBLK = NSTEP / KB;
-  static constexpr int LDY = PQ + 1;
+  // AVW: the dY row of a lane is read KB pixels at a time (ds_read_b128) — LDY / 4 odd, so
+  // the 16 rows of a b128 phase start in disjoint 4-bank groups; else LDY odd for b32 reads
+  static constexpr bool AVW = KB % 4 == 0 && (PQ / 2) % 4 == 0;
+  static constexpr int LDY = AVW ? PQ + (((PQ / 4) % 2 == 0) ? 4 : 8) : PQ + 1;
   static constexpr int A_SZ = BM * LDY;  // dY tile of one image: [m][pixel]
   static constexpr int B_SZ = CB * HWp;  // zero-bordered x planes of one image
   static constexpr int NT = 64 * NW;
@@ -677,7 +680,11 @@ __global__ __launch_bounds__(64 * NW) void conv_wgrad_kernel(const float* __rest
       if (e < G::A4) {
         const int m = (4 * e) / G::PQ, pq = 4 * e - m * G::PQ;
         float* d = A + m * G::LDY + pq;
-        d[0] = ra[i].x; d[1] = ra[i].y; d[2] = ra[i].z; d[3] = ra[i].w;
+        if constexpr (G::AVW) {
+          *reinterpret_cast<f32x4c*>(d) = ra[i];
+        } else {
+          d[0] = ra[i].x; d[1] = ra[i].y; d[2] = ra[i].z; d[3] = ra[i].w;
+        }
       }
     }
 #pragma unroll
@@ -715,9 +722,19 @@ __global__ __launch_bounds__(64 * NW) void conv_wgrad_kernel(const float* __rest
         const int p = t / G::Q, q = t - p * G::Q;
 #pragma unroll
         for (int u = 0; u < NBPW; ++u) {
-          av[slot][k][u] = A[a_base[u] + t];
+          if constexpr (!G::AVW) av[slot][k][u] = A[a_base[u] + t];
           bv[slot][k][u] = B[b_base[u] + p * ST * G::Wp + q * ST];
         }
+      }
+      if constexpr (G::AVW) {
+#pragma unroll
+        for (int u = 0; u < NBPW; ++u)
+#pragma unroll
+          for (int q4 = 0; q4 < KB / 4; ++q4) {
+            const f32x4c v = *reinterpret_cast<const f32x4c*>(A + a_base[u] + blk * KB + 4 * q4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) av[slot][4 * q4 + j][u] = v[j];
+          }
       }
     };
     fetch(0, 0);
