@@ -116,11 +116,28 @@ class Bottleneck(nn.Module):
         self.fused = norm is BatchNormAct2d
 
     def forward(self, x):
+        if self.fused:  # the BasicBlock plumbing, one conv / BN pair more
+            train = x.is_cuda and torch.is_grad_enabled() and self.training
+            # identity block: BN3's residual gradient is folded into conv1's grad-x (the tgemm
+            # pointwise epilogue / split-K sum) instead of an autograd add of the two branches
+            link = GradLink() if self.downsample is None and train and x.requires_grad else None
+            # split-K conv slabs summed inside the neighbouring BN kernels: conv1 -> bn1,
+            # conv2 -> bn2, conv3 -> bn3, downsample conv -> its BN (forward); conv2's grad-x ->
+            # bn1's backward, conv3's grad-x -> bn2's backward
+            s1, s2, s3, g1, g2, sd = (tuple(SlabLink() for _ in range(6)) if train and SLAB_LINKS
+                                      else (None,) * 6)
+            identity = x
+            if self.downsample is not None:
+                ds = self.downsample
+                if train and len(ds) == 2 and isinstance(ds[0], GemmConv2d) and isinstance(ds[1], BatchNormAct2d):
+                    identity = ds[1](ds[0](x, slab_out=sd), slab_in=sd)
+                else:
+                    identity = ds(x)
+            out = self.bn1(self.conv1(x, link=link, slab_out=s1), relu=True, slab_in=s1, grad_slab=g1)
+            out = self.bn2(self.conv2(out, slab_out=s2, grad_slab=g1), relu=True, slab_in=s2, grad_slab=g2)
+            return self.bn3(self.conv3(out, slab_out=s3, grad_slab=g2), residual=identity, relu=True, link=link,
+                            slab_in=s3)
         identity = x if self.downsample is None else self.downsample(x)
-        if self.fused:
-            out = self.bn1(self.conv1(x), relu=True)
-            out = self.bn2(self.conv2(out), relu=True)
-            return self.bn3(self.conv3(out), residual=identity, relu=True)
         out = self.relu(self.bn1(self.conv1(x)))
         out = self.relu(self.bn2(self.conv2(out)))
         out = self.bn3(self.conv3(out))

@@ -161,3 +161,29 @@ def test_resnet50_native_convs_match_fp64(device):
         e_ours, e_stock = err(a, b), err(s, b)
         # same order of magnitude as stock (measured: worst ratio ~2 on layer4's 1x1-map convs)
         assert e_ours <= 4 * e_stock + 2e-3, (n, e_ours, e_stock)
+
+
+@pytest.mark.gpu
+def test_bottleneck_links_match_unlinked(device, monkeypatch):
+    """ResNet-50 bottleneck blocks with the residual-gradient link (BN3 -> conv1 grad-x) and the
+    split-K slab links (conv -> BN, grad-x -> BN backward) == the same model without them: the
+    forward is bitwise equal (same sums, same order), gradients equal to fp32 add-order rounding."""
+    from network_distributed_pytorch_amd.models import build_model
+    from network_distributed_pytorch_amd.models import resnet as R
+
+    outs, losses = [], []
+    for linked in (True, False):
+        if not linked:
+            monkeypatch.setattr(R, "SLAB_LINKS", False)
+            monkeypatch.setattr(R, "GradLink", lambda: None)
+        torch.manual_seed(0)
+        m = build_model("resnet50", 10).to(device)
+        x = torch.randn(32, 3, 32, 32, device=device, generator=torch.Generator(device=device).manual_seed(1))
+        m.zero_grad()
+        loss = m(x).square().mean()
+        loss.backward()
+        losses.append(loss.detach())
+        outs.append([p.grad.clone() for p in m.parameters()])
+    assert torch.equal(losses[0], losses[1])
+    for a, b in zip(*outs):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
