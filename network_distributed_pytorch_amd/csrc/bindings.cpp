@@ -399,13 +399,25 @@ void flag_signal(torch::Tensor flags, int64_t i) {
   check_launch("launch_flag_signal");
 }
 
-void flag_wait(torch::Tensor flags, int64_t i, int64_t seen, int64_t err, int64_t timeout_us) {
+// host_err (optional): a pinned host int32 the wait mirrors a set error word into, so the
+// host sees a timed-out wait at its next replay without a device synchronisation
+void flag_wait(torch::Tensor flags, int64_t i, int64_t seen, int64_t err, int64_t timeout_us,
+               c10::optional<torch::Tensor> host_err) {
   check_dev(flags, "flags");
   TORCH_CHECK(flags.scalar_type() == torch::kInt32 && i >= 0 && i < flags.numel() && seen >= 0 &&
                   seen < flags.numel() && err >= 0 && err < flags.numel(),
               "flag_wait: bad flag indices");
   auto* f = reinterpret_cast<unsigned*>(flags.data_ptr<int32_t>());
-  ndp::launch_flag_wait(f + i, f + seen, f + err, timeout_us, cur_stream());
+  unsigned* h = nullptr;
+  if (host_err.has_value() && host_err->defined()) {
+    TORCH_CHECK(!host_err->is_cuda() && host_err->is_pinned() && host_err->scalar_type() == torch::kInt32,
+                "flag_wait: host_err must be a pinned int32 host tensor");
+    void* dp = nullptr;
+    TORCH_CHECK(hipHostGetDevicePointer(&dp, host_err->data_ptr(), 0) == hipSuccess,
+                "flag_wait: host_err is not device-mapped pinned memory");
+    h = static_cast<unsigned*>(dp);
+  }
+  ndp::launch_flag_wait(f + i, f + seen, f + err, timeout_us, cur_stream(), h);
   check_launch("launch_flag_wait");
 }
 
@@ -963,7 +975,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("checksum", &checksum);
   m.def("flag_signal", &flag_signal);
-  m.def("flag_wait", &flag_wait);
+  m.def("flag_wait", &flag_wait, py::arg("flags"), py::arg("i"), py::arg("seen"), py::arg("err"),
+        py::arg("timeout_us"), py::arg("host_err") = c10::optional<torch::Tensor>());
   m.def("toeplitz_expand", &toeplitz_expand);
   m.def("toeplitz_fold", &toeplitz_fold);
   m.def("toeplitz_expand_many", &toeplitz_expand_many);

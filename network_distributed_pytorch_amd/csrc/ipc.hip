@@ -18,10 +18,17 @@
 //        0..N-1 — every rank performs the identical fp32 additions, so the results are
 //        bitwise identical across ranks (replica consistency);
 //     4. write `done = e` into every peer's flag array.
-// Spins are wall-clock bounded (s_memrealtime): a timeout sets a sticky error word, later
-// collectives skip, and the host check (Communicator.check) fails the run — never a hang.
-// Works between processes sharing one GPU (the multi-process test of the captured overlap
-// path on a one-GPU box) and between GPUs over xGMI.
+// Spins are wall-clock bounded (s_memrealtime): a timeout sets a sticky error word and the
+// workgroup returns at once (no staging, no sum, no flag writes), later collectives skip,
+// and the host check (Communicator.check) fails the run on every rank — never a hang.
+// The buffer (data + flags) is allocated UNCACHED (hipDeviceMallocUncached): flags written
+// by peers and data a peer rewrites between uses must never be served from a stale cache
+// line on the reading side.  If the allocator or IPC export refuses uncached memory the
+// buffer falls back to plain hipMalloc and `uncached` is false; then the Python data plane
+// only pairs ranks that share one device (parallel/comm.py IpcDataPlane).  Exercised so far
+// between processes sharing one GPU (tests/test_ipc_gpu.py); the xGMI case is untested.
+// all_reduce_many packs a list of tensors into ONE launch: chunk w covers floats
+// [w*4096, (w+1)*4096) of the tensors' concatenation (a segment table in the arguments).
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
 #include <torch/extension.h>
@@ -43,12 +50,17 @@ constexpr int kIpcThreads = 256;
     TORCH_CHECK(_e == hipSuccess, "HIP error in ", #expr, ": ", hipGetErrorString(_e));     \
   } while (0)
 
+constexpr int kIpcMaxSegs = 48;  // tensors per launch (kernel-argument table)
+
 struct IpcArgs {
   float* data[kIpcMaxRanks];        // every rank's buffer, mapped into this process
   unsigned* ready[kIpcMaxRanks];    // rank j's ready flags [src rank][chunk]
   unsigned* done[kIpcMaxRanks];     // rank j's done flags  [src rank][chunk]
-  float* t;                         // in/out (this launch's segment)
-  int64_t n;                        // floats in this segment
+  unsigned* poison[kIpcMaxRanks];   // rank j's "a peer timed out" word
+  float* seg[kIpcMaxSegs];          // in/out tensors (or tensor pieces) of this launch
+  int64_t end[kIpcMaxSegs];         // prefix sums of their lengths (buffer offsets)
+  int nseg;
+  int64_t n;                        // floats in this launch = end[nseg - 1]
   unsigned* ctr;                    // per-chunk use counters (local)
   unsigned* err;                    // sticky error word (local)
   uint64_t max_ticks;               // spin bound, 100 MHz ticks
@@ -69,13 +81,30 @@ __device__ __forceinline__ bool spin_until(const unsigned* p, unsigned want, uns
   return true;
 }
 
+// a wait of this rank timed out: tell every peer (their next collective skips and their host
+// check fails too, instead of a peer silently reading half-published chunks)
+__device__ __forceinline__ void poison_peers(const IpcArgs& a) {
+  for (int j = 0; j < a.nranks; ++j)
+    __hip_atomic_fetch_or(a.poison[j], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// buffer offset i (< a.n) -> address inside the launch's tensors; `k` is the caller's
+// running segment index (offsets only grow within a thread's loop)
+__device__ __forceinline__ float* seg_addr(const IpcArgs& a, int64_t i, int& k) {
+  while (i >= a.end[k]) ++k;
+  return a.seg[k] + (i - (k ? a.end[k - 1] : 0));
+}
+
 __global__ __launch_bounds__(kIpcThreads) void ipc_allreduce_kernel(IpcArgs a) {
   __shared__ unsigned s_e;
   __shared__ int s_skip;
+  __shared__ int s_fail;
   const int w = blockIdx.x, tid = threadIdx.x;
   if (tid == 0) {
     s_e = a.ctr[w] + 1u;
-    s_skip = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+    s_skip = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
+             __hip_atomic_load(a.poison[a.rank], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+    s_fail = 0;
   }
   __syncthreads();
   if (s_skip) return;  // sticky error: the host check reports it
@@ -85,24 +114,32 @@ __global__ __launch_bounds__(kIpcThreads) void ipc_allreduce_kernel(IpcArgs a) {
   const int cnt = (int)min((int64_t)kIpcChunk, a.n - base);
 
   // 1. peers are done reading my chunk w of the previous use
-  if (tid < N && tid != R && e > 1u) spin_until(a.done[R] + tid * a.gmax + w, e - 1u, a.err, a.max_ticks);
+  if (tid < N && tid != R && e > 1u && !spin_until(a.done[R] + tid * a.gmax + w, e - 1u, a.err, a.max_ticks)) {
+    s_fail = 1;
+    poison_peers(a);
+  }
   __syncthreads();
+  if (s_fail) return;  // a peer may still read the old chunk: do not overwrite it
   // 2. stage my contribution, publish it
   float* mine = a.data[R] + base;
-  const float* src = a.t + base;
-  for (int i = tid; i < cnt; i += kIpcThreads) mine[i] = src[i];
+  int k = 0;
+  for (int i = tid; i < cnt; i += kIpcThreads) mine[i] = *seg_addr(a, base + i, k);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // every wave: its stores reach memory (system scope)
   __syncthreads();
   if (tid < N) __hip_atomic_store(a.ready[tid] + R * a.gmax + w, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   // 3. every contribution is there: fixed-order sum
-  if (tid < N) spin_until(a.ready[R] + tid * a.gmax + w, e, a.err, a.max_ticks);
+  if (tid < N && !spin_until(a.ready[R] + tid * a.gmax + w, e, a.err, a.max_ticks)) {
+    s_fail = 1;
+    poison_peers(a);
+  }
   __syncthreads();
+  if (s_fail) return;  // partial data: leave the caller's tensor and every flag untouched
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-  float* dst = a.t + base;
+  k = 0;
   for (int i = tid; i < cnt; i += kIpcThreads) {
     float acc = a.data[0][base + i];
     for (int j = 1; j < N; ++j) acc += a.data[j][base + i];
-    dst[i] = a.scale == 1.f ? acc : acc * a.scale;
+    *seg_addr(a, base + i, k) = a.scale == 1.f ? acc : acc * a.scale;
   }
   __syncthreads();
   // 4. I am done reading everyone's chunk w
@@ -117,10 +154,21 @@ class IpcComm {
     TORCH_CHECK(nranks >= 1 && nranks <= kIpcMaxRanks && rank >= 0 && rank < nranks, "IpcComm: bad rank/nranks");
     gmax_ = (int)std::max<int64_t>(1, capacity_bytes / (kIpcChunk * (int64_t)sizeof(float)));
     cap_floats_ = (int64_t)gmax_ * kIpcChunk;
-    const size_t flags = 2 * (size_t)kIpcMaxRanks * gmax_ * sizeof(unsigned);
+    const size_t flags = (2 * (size_t)kIpcMaxRanks * gmax_ + 1) * sizeof(unsigned);  // ready, done, poison
     bytes_ = cap_floats_ * sizeof(float) + flags;
     NDP_IPC_CHECK(hipSetDevice(device));
-    NDP_IPC_CHECK(hipMalloc(&base_, bytes_));
+    // uncached first (see the header); plain device memory if either step refuses it
+    if (std::getenv("NDP_IPC_CACHED") == nullptr && hipExtMallocWithFlags(&base_, bytes_, hipDeviceMallocUncached) == hipSuccess) {
+      hipIpcMemHandle_t h;
+      if (hipIpcGetMemHandle(&h, base_) == hipSuccess) {
+        uncached_ = true;
+      } else {
+        (void)hipFree(base_);
+        base_ = nullptr;
+      }
+    }
+    (void)hipGetLastError();  // clear a refused attempt
+    if (base_ == nullptr) NDP_IPC_CHECK(hipMalloc(&base_, bytes_));
     NDP_IPC_CHECK(hipMemset(base_, 0, bytes_));
     NDP_IPC_CHECK(hipMalloc(&local_, (gmax_ + 1) * sizeof(unsigned)));
     NDP_IPC_CHECK(hipMemset(local_, 0, (gmax_ + 1) * sizeof(unsigned)));
@@ -153,11 +201,17 @@ class IpcComm {
     opened_ = true;
   }
 
-  void all_reduce(torch::Tensor t, const std::string& op, int64_t stream) {
+  void all_reduce(torch::Tensor t, const std::string& op, int64_t stream) { all_reduce_many({t}, op, stream); }
+
+  // every tensor of the list in as few launches as the buffer capacity and the segment
+  // table allow (one for the PowerSGD payloads)
+  void all_reduce_many(const std::vector<torch::Tensor>& ts, const std::string& op, int64_t stream) {
     TORCH_CHECK(opened_, "IpcComm: open() the peer handles first");
-    TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == torch::kFloat32 && t.get_device() == device_,
-                "IpcComm: contiguous float32 tensors on the communicator's device");
     TORCH_CHECK(op == "sum" || op == "avg", "IpcComm: sum / avg only");
+    for (const auto& t : ts)
+      TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == torch::kFloat32 &&
+                      t.get_device() == device_,
+                  "IpcComm: contiguous float32 tensors on the communicator's device");
     hipStream_t s = stream == 0 ? at::hip::getCurrentHIPStream().stream() : reinterpret_cast<hipStream_t>(stream);
     IpcArgs a{};
     for (int j = 0; j < nranks_; ++j) {
@@ -165,6 +219,7 @@ class IpcComm {
       a.data[j] = reinterpret_cast<float*>(b);
       a.ready[j] = reinterpret_cast<unsigned*>(b + cap_floats_ * sizeof(float));
       a.done[j] = a.ready[j] + (size_t)kIpcMaxRanks * gmax_;
+      a.poison[j] = a.done[j] + (size_t)kIpcMaxRanks * gmax_;
     }
     a.ctr = static_cast<unsigned*>(local_);
     a.err = a.ctr + gmax_;
@@ -173,29 +228,55 @@ class IpcComm {
     a.rank = rank_;
     a.nranks = nranks_;
     a.gmax = gmax_;
-    float* p = t.data_ptr<float>();
-    for (int64_t off = 0; off < t.numel(); off += cap_floats_) {  // segments of the buffer capacity
-      a.t = p + off;
-      a.n = std::min<int64_t>(cap_floats_, t.numel() - off);
+    auto flush = [&]() {
+      if (a.nseg == 0) return;
+      a.n = a.end[a.nseg - 1];
       const int g = (int)((a.n + kIpcChunk - 1) / kIpcChunk);
       hipLaunchKernelGGL(ipc_allreduce_kernel, dim3(g), dim3(kIpcThreads), 0, s, a);
+      a.nseg = 0;
+      ++launches_;
+    };
+    for (const auto& t : ts) {
+      float* p = t.data_ptr<float>();
+      int64_t left = t.numel(), off = 0;
+      while (left > 0) {  // a tensor may straddle launches (buffer capacity)
+        const int64_t used = a.nseg ? a.end[a.nseg - 1] : 0;
+        if (used == cap_floats_ || a.nseg == kIpcMaxSegs) {
+          flush();
+          continue;
+        }
+        const int64_t take = std::min<int64_t>(left, cap_floats_ - (a.nseg ? a.end[a.nseg - 1] : 0));
+        a.seg[a.nseg] = p + off;
+        a.end[a.nseg] = (a.nseg ? a.end[a.nseg - 1] : 0) + take;
+        ++a.nseg;
+        off += take;
+        left -= take;
+      }
     }
+    flush();
     NDP_IPC_CHECK(hipGetLastError());
   }
 
-  void all_reduce_many(const std::vector<torch::Tensor>& ts, const std::string& op, int64_t stream) {
-    for (const auto& t : ts) all_reduce(t, op, stream);
+  // PCI bus id of the communicator's device (peers compare them: same device or not)
+  std::string bus_id() const {
+    char buf[64] = {0};
+    NDP_IPC_CHECK(hipDeviceGetPCIBusId(buf, sizeof(buf), device_));
+    return std::string(buf);
   }
 
-  // host-synchronising: 0 or the sticky error word
+  // host-synchronising: 0, or 1 = a wait of this rank timed out, 2 = a peer's did
   int64_t error() const {
-    unsigned v = 0;
+    unsigned v = 0, pv = 0;
     NDP_IPC_CHECK(hipMemcpy(&v, static_cast<unsigned*>(local_) + gmax_, sizeof(unsigned), hipMemcpyDeviceToHost));
-    return v;
+    const unsigned* poison = reinterpret_cast<const unsigned*>(static_cast<char*>(base_) + cap_floats_ * sizeof(float)) +
+                             2 * (size_t)kIpcMaxRanks * gmax_;
+    NDP_IPC_CHECK(hipMemcpy(&pv, poison, sizeof(unsigned), hipMemcpyDeviceToHost));
+    return (v ? 1 : 0) | (pv ? 2 : 0);
   }
   void check() const {
-    TORCH_CHECK(error() == 0, "IPC all-reduce: a peer wait timed out after ", timeout_us_ / 1e6,
-                " s (a stalled or diverged peer); the results since are invalid");
+    const int64_t e = error();
+    TORCH_CHECK(e == 0, "IPC all-reduce: ", (e & 1) ? "a peer wait of this rank" : "a peer's wait",
+                " timed out after ", timeout_us_ / 1e6, " s (a stalled or diverged rank); the results since are invalid");
   }
   void destroy() {
     if (base_ == nullptr) return;
@@ -211,6 +292,8 @@ class IpcComm {
   int device() const { return device_; }
   int64_t capacity() const { return cap_floats_ * sizeof(float); }
   bool alive() const { return base_ != nullptr; }
+  bool uncached() const { return uncached_; }
+  int64_t launches() const { return launches_; }
 
  private:
   int rank_, nranks_, device_;
@@ -221,6 +304,8 @@ class IpcComm {
   void* base_ = nullptr;
   void* local_ = nullptr;
   bool opened_ = false;
+  bool uncached_ = false;
+  int64_t launches_ = 0;
   std::vector<void*> peers_;
 };
 
@@ -241,5 +326,8 @@ void register_ipc(py::module& m) {
       .def_property_readonly("nranks", &IpcComm::nranks)
       .def_property_readonly("device", &IpcComm::device)
       .def_property_readonly("capacity", &IpcComm::capacity)
-      .def_property_readonly("alive", &IpcComm::alive);
+      .def_property_readonly("alive", &IpcComm::alive)
+      .def_property_readonly("uncached", &IpcComm::uncached)
+      .def_property_readonly("launches", &IpcComm::launches)
+      .def("bus_id", &IpcComm::bus_id);
 }

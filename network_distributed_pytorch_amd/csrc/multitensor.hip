@@ -164,8 +164,10 @@ __global__ void delay_kernel(int64_t ticks) {
 // the error word and proceeds.  The error is STICKY — once set, every later wait proceeds at
 // once (a broken ordering costs one timeout, not one per wait) — and it is fatal on the
 // host: Communicator.check() raises, the bench's health checks fail the attempt and the
-// supervisor falls back (bench.py), the engine checks it at its logging cadence.  Results
-// of a step run after a timed-out wait are never reported.
+// supervisor falls back (bench.py).  A set error word is also mirrored into a pinned host
+// word (host_err), which StepRunner reads before every replay: the run stops at the next
+// step, not at the next health-check cadence.  Results of a step run after a timed-out
+// wait are never reported.
 __global__ void flag_signal_kernel(unsigned* ctr) {
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -173,7 +175,8 @@ __global__ void flag_signal_kernel(unsigned* ctr) {
   }
 }
 
-__global__ void flag_wait_kernel(unsigned* ctr, unsigned* seen, unsigned* err, uint64_t max_ticks) {
+__global__ void flag_wait_kernel(unsigned* ctr, unsigned* seen, unsigned* err, uint64_t max_ticks,
+                                 unsigned* host_err) {
   if (threadIdx.x == 0) {
     const unsigned want = __hip_atomic_load(seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -186,6 +189,8 @@ __global__ void flag_wait_kernel(unsigned* ctr, unsigned* seen, unsigned* err, u
       }
     }
     __hip_atomic_store(seen, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (host_err != nullptr && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)
+      __hip_atomic_store(host_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
 }
@@ -194,9 +199,10 @@ void launch_flag_signal(unsigned* ctr, hipStream_t s) {
   hipLaunchKernelGGL(flag_signal_kernel, dim3(1), dim3(64), 0, s, ctr);
 }
 
-void launch_flag_wait(unsigned* ctr, unsigned* seen, unsigned* err, int64_t timeout_us, hipStream_t s) {
+void launch_flag_wait(unsigned* ctr, unsigned* seen, unsigned* err, int64_t timeout_us, hipStream_t s,
+                      unsigned* host_err) {
   const uint64_t ticks = (uint64_t)(timeout_us > 0 ? timeout_us : 0) * 100u;  // 100 MHz clock
-  hipLaunchKernelGGL(flag_wait_kernel, dim3(1), dim3(64), 0, s, ctr, seen, err, ticks);
+  hipLaunchKernelGGL(flag_wait_kernel, dim3(1), dim3(64), 0, s, ctr, seen, err, ticks, host_err);
 }
 
 constexpr int kCkBlocks = 256;

@@ -110,7 +110,8 @@ void launch_delay_ns(int64_t ns, hipStream_t s);
 // device-flag ordering between two queues: signal bumps *ctr; wait spins until *ctr has
 // been bumped once more than *seen records (then records it); err |= 1 on spin timeout
 void launch_flag_signal(unsigned* ctr, hipStream_t s);
-void launch_flag_wait(unsigned* ctr, unsigned* seen, unsigned* err, int64_t timeout_us, hipStream_t s);
+void launch_flag_wait(unsigned* ctr, unsigned* seen, unsigned* err, int64_t timeout_us, hipStream_t s,
+                      unsigned* host_err = nullptr);
 // deterministic fp64-accumulated checksum of a flat buffer (replica divergence detector)
 void launch_checksum(const float* x, int64_t n, double* out, hipStream_t s);
 

@@ -20,9 +20,21 @@ from typing import Iterable
 
 import torch
 
-__all__ = ["register", "unregister", "grad_buffer", "registered"]
+__all__ = ["register", "unregister", "grad_buffer", "registered", "release"]
 
 _VIEWS: dict = {}
+# id(param) -> autograd graph task that received the param's arena slice.  A parameter used
+# twice in one forward (tied / shared weights) gets a second gradient in the SAME backward
+# before AccumulateGrad adopted the first: that one must not alias the slice (autograd would
+# add the two aliased tensors, 2 x g2 instead of g1 + g2).  ADVICE r3.
+_HANDED: dict = {}
+
+
+def _task_id() -> int:
+    try:
+        return int(torch._C._current_graph_task_id())
+    except Exception:  # pragma: no cover - older torch: no task ids, one handout per release
+        return -2
 _ON = os.environ.get("NDP_GRAD_ARENA", "1") != "0"
 
 
@@ -33,6 +45,13 @@ def register(param: torch.Tensor, arena: torch.Tensor, offset: int) -> None:
 def unregister(params: Iterable[torch.Tensor]) -> None:
     for p in params:
         _VIEWS.pop(id(p), None)
+        _HANDED.pop(id(p), None)
+
+
+def release(params: Iterable[torch.Tensor]) -> None:
+    """The parameters' ``.grad`` were dropped (zero_grad): their slices may be handed out again."""
+    for p in params:
+        _HANDED.pop(id(p), None)
 
 
 def registered(param: torch.Tensor) -> bool:
@@ -46,6 +65,8 @@ def grad_buffer(param: torch.Tensor, like: torch.Tensor = None) -> torch.Tensor:
     e = _VIEWS.get(id(param)) if _ON else None
     if e is not None and param.grad is None and not torch.is_grad_enabled():
         ref, arena, off = e
-        if ref() is param:
+        task = _task_id()
+        if ref() is param and _HANDED.get(id(param)) != task:
+            _HANDED[id(param)] = task
             return arena[off: off + param.numel()].view_as(param)
     return torch.empty_like(param if like is None else like)

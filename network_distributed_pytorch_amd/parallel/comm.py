@@ -216,6 +216,15 @@ class IpcDataPlane:
         store = dist.distributed_c10d._get_default_store()
         IpcDataPlane._n = getattr(IpcDataPlane, "_n", 0) + 1
         key = "ndp_ipc/{}/{}".format("-".join(map(str, ranks)), IpcDataPlane._n)
+        # peers on another device need the uncached buffer (csrc/ipc.hip header): every rank
+        # publishes its device's PCI bus id and whether its buffer is uncached; a cached
+        # buffer is only paired with ranks on the same device (all ranks decide alike)
+        store.set(f"{key}/dev/{self.rank_in_group}", f"{self._c.bus_id()}|{int(self._c.uncached)}")
+        devs = [store.get(f"{key}/dev/{r}").decode().split("|") for r in range(len(ranks))]
+        if len({d for d, _ in devs}) > 1 and not all(u == "1" for _, u in devs):
+            self._c.destroy()
+            raise RuntimeError("IPC data plane: ranks on different GPUs need the uncached peer buffer, which this "
+                               "allocator/IPC export refused; use NDP_COMM=rccl")
         store.set(f"{key}/{self.rank_in_group}", self._c.handle())
         handles = [store.get(f"{key}/{r}") for r in range(len(ranks))]
         self._c.open(handles)
@@ -229,7 +238,15 @@ class IpcDataPlane:
         self._c.all_reduce(t, op)
 
     def all_reduce_many(self, ts):
-        self._c.all_reduce_many(list(ts))
+        self._c.all_reduce_many(list(ts))  # one launch (segment table, csrc/ipc.hip)
+
+    @property
+    def uncached(self) -> bool:
+        return bool(self._c.uncached)
+
+    @property
+    def launches(self) -> int:
+        return int(self._c.launches)
 
     def broadcast(self, t: torch.Tensor, src: int = 0):
         torch.cuda.current_stream().synchronize()
@@ -428,15 +445,28 @@ class Communicator:
             assert not torch.cuda.is_current_stream_capturing(), "flag buffer must exist before capture"
             dev = self._device or torch.device("cuda", torch.cuda.current_device())
             self._flags = torch.zeros(2 * _MAX_FLAGS + 3, dtype=torch.int32, device=dev)
+            # pinned host mirror of the error word (set by a timed-out wait kernel; read by
+            # StepRunner before every replay without a device sync)
+            self._host_err = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         return self._flags
 
     def graph_prologue(self):
         """First node of the compute graph: wait until the previous step's comm graph is done."""
-        self._flag_ext().flag_wait(self._flag_buf(), _DONE, _DONE + 1, _ERR, _WAIT_US)
+        self._flag_ext().flag_wait(self._flag_buf(), _DONE, _DONE + 1, _ERR, _WAIT_US, self._host_err)
 
     def graph_wait(self, i: int):
         """Comm graph: wait for the compute graph's i-th signal."""
-        self._flag_ext().flag_wait(self._flag_buf(), i, _MAX_FLAGS + i, _ERR, _WAIT_US)
+        self._flag_ext().flag_wait(self._flag_buf(), i, _MAX_FLAGS + i, _ERR, _WAIT_US, self._host_err)
+
+    def host_flag_error(self) -> int:
+        """The error word as last mirrored to host memory by a wait kernel (no device sync)."""
+        h = getattr(self, "_host_err", None)
+        return int(h[0]) if h is not None else 0
+
+    def raise_flag_error(self):
+        raise FlagTimeout("compute/comm graph ordering: a device-flag wait timed out after "
+                          f"{_WAIT_US / 1e6:.3g} s (a stalled peer, or the two streams share a hardware "
+                          "queue); the steps since are unordered and must not be used")
 
     def graph_epilogue(self):
         """Last node of the comm graph: release the next step's compute graph."""
@@ -447,6 +477,7 @@ class Communicator:
         f = self._flag_buf()
         f.zero_()
         f[_DONE] = 1
+        self._host_err.zero_()
 
     def flag_error(self) -> int:
         return int(self._flags[_ERR].item()) if self._flags is not None else 0
@@ -542,9 +573,7 @@ class Communicator:
         if self._native is not None:
             self._native.check()
         if self.flag_error():
-            raise FlagTimeout("compute/comm graph ordering: a device-flag wait timed out after "
-                              f"{_WAIT_US / 1e6:.3g} s (a stalled peer, or the two streams share a hardware "
-                              "queue); the steps since are unordered and must not be used")
+            self.raise_flag_error()
 
     def close(self):
         """Destroy the native communicator — unless a captured graph contains its

@@ -116,10 +116,13 @@ class BucketedDataParallel:
         self._works = [None] * len(self.buckets)
         self._launched = [False] * len(self.buckets)
         self._next = 0
-        # stream mode: flatten + collective on the side stream (native RCCL / world 1, device)
-        self.stream_mode = self.device.type == "cuda" and self.comm.stream_ordered
         if overlap is None:  # default: overlap only when a step has wire time to hide
             overlap = self.comm.has_traffic
+        # stream mode (overlap on a stream-ordered data plane: native RCCL / IPC / world 1):
+        # flatten + collective + SGD on the side stream.  Without overlap everything stays on
+        # the compute stream — at N = 1 the captured step is ONE serial graph, no side stream,
+        # no device-flag waits
+        self.stream_mode = self.device.type == "cuda" and self.comm.stream_ordered and bool(overlap)
         self.overlap = overlap and (self.comm.active or self.stream_mode)
         self._hooks = []
         if overlap:
@@ -226,6 +229,7 @@ class BucketedDataParallel:
     def zero_grad(self, set_to_none: bool = True):
         for p in self.params:
             p.grad = None
+        gradarena.release(self.params)
         self._reset()
 
     @torch.no_grad()

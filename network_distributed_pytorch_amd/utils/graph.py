@@ -233,6 +233,8 @@ class StepRunner:
         # an eager step since capture may have re-bound a table the graph reads
         self._upload_gen = _UPLOADS.ensure(self._uploads, self._upload_gen)
         if self.side_graphs:
+            if self._comm.host_flag_error():  # a wait of an earlier replay timed out: stop now
+                self._comm.raise_flag_error()
             # comm graph FIRST: the command processor serves the queues roughly in doorbell
             # order, so a comm graph submitted after the compute graph is dispatched only
             # when the compute queue's kernel train has (nearly) drained — measured with

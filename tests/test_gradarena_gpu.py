@@ -36,3 +36,41 @@ def test_dense_arena_gradients_in_place(device, monkeypatch):
     opt.step()
     for (n, a), (_, b) in zip(ours.named_parameters(), ref.named_parameters()):
         assert torch.allclose(a, b, rtol=1e-6, atol=1e-7), n  # fused SGD vs torch.optim.SGD
+
+
+def test_tied_weight_not_aliased(device):
+    """a parameter used twice in one forward (a shared BN here) gets two gradient
+    contributions in the same backward; the second must not alias the arena slice handed
+    to the first (that would give 2 x g2 instead of g1 + g2)."""
+    from network_distributed_pytorch_amd.ops.batchnorm import BatchNormAct2d
+    from network_distributed_pytorch_amd.parallel.ddp import BucketedDataParallel
+
+    class Tied(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.bn = BatchNormAct2d(8)
+            self.head = torch.nn.Linear(8 * 16, 3)
+
+        def forward(self, x):
+            h = self.bn(x, relu=True)
+            h = self.bn(h * 1.5 - 0.25, relu=True)  # the same weight / bias again
+            return self.head(h.flatten(1))
+
+    torch.manual_seed(0)
+    ours = Tied().to(device)
+    ref = Tied().to(device)
+    ref.load_state_dict(ours.state_dict())
+    with torch.no_grad():
+        ours.bn.weight.uniform_(0.5, 1.5)
+        ref.bn.weight.copy_(ours.bn.weight)
+    ddp = BucketedDataParallel(ours, lr=0.1, momentum=0.9)
+    x = torch.randn(16, 8, 4, 4, device=device)
+    y = torch.randint(0, 3, (16,), device=device)
+    for _ in range(2):  # the second step re-hands the slices after zero_grad
+        ddp.zero_grad()
+        for p in ref.parameters():
+            p.grad = None
+        F.cross_entropy(ours(x), y).backward()
+        F.cross_entropy(ref(x), y).backward()  # not registered: plain autograd accumulation
+        for (n, a), (_, b) in zip(ours.named_parameters(), ref.named_parameters()):
+            assert torch.allclose(a.grad, b.grad, rtol=1e-5, atol=1e-6), n

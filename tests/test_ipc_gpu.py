@@ -59,6 +59,16 @@ for k in range(5):
     want = sum(r + k for r in range(world))
     ok &= bool((x == want).all())
 out["graph_ok"] = ok
+# 3. all_reduce_many: a list of tensors is ONE launch (segment table), exact in each tensor
+dp = comm._native
+sizes = (3, 4095, 4097, 123457, 7)
+ts = [torch.full((n,), float(rank + 1 + i), device="cuda") for i, n in enumerate(sizes)]
+before = dp.launches
+dp.all_reduce_many(ts)
+torch.cuda.synchronize()
+out["many_launches"] = dp.launches - before
+out["many_ok"] = all(bool((t == sum(r + 1 + i for r in range(world))).all()) for i, t in enumerate(ts))
+out["uncached"] = dp.uncached
 comm.check()
 out["rank"] = rank
 print("RESULT " + json.dumps(out), flush=True)
@@ -101,6 +111,7 @@ def test_ipc_allreduce_multi_process_one_gpu(device, world):
             if k.startswith("err_"):
                 assert v < 1e-5, (k, v)
         assert r["graph_ok"], r
+        assert r["many_launches"] == 1 and r["many_ok"], r
     assert all(r["sums"] == res[0]["sums"] for r in res), "ranks disagree bitwise"
 
 
@@ -134,3 +145,44 @@ def test_captured_overlapped_powersgd_multi_process(device, world):
     serial = _bench(common + ["--overlap", "off"], env)
     assert serial["config"]["overlap"] is False and serial["fallback"] is None
     assert ov["param_checksum"] == serial["param_checksum"], (ov["param_checksum"], serial["param_checksum"])
+
+
+STALL = r'''
+import os, sys, json, time
+sys.path.insert(0, ROOT)
+import torch, torch.distributed as dist
+os.environ["NDP_COMM"] = "ipc"
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+torch.cuda.set_device(0)
+dist.init_process_group("gloo")
+from network_distributed_pytorch_amd.parallel.comm import Communicator
+comm = Communicator(device=torch.device("cuda", 0))
+t = torch.ones(10000, device="cuda")
+comm.all_reduce(t)  # one healthy collective first
+torch.cuda.synchronize()
+comm.check()
+dist.barrier()
+if rank == world - 1:
+    time.sleep(2.0)  # stall past the 0.3 s flag-wait bound of the others
+comm.all_reduce(t)
+torch.cuda.synchronize()
+err = None
+try:
+    comm.check()
+except RuntimeError as e:
+    err = str(e)
+print("RESULT " + json.dumps({"rank": rank, "err": err}), flush=True)
+dist.barrier()
+dist.destroy_process_group()
+'''
+
+
+@pytest.mark.timeout(300)
+def test_ipc_timeout_fails_every_rank(device):
+    """ADVICE r3: a stalled rank makes the others' waits time out; they return without
+    touching data or flags and poison every peer, so the check raises on EVERY rank (the
+    stalled one included, whose later collective would otherwise read half-published
+    chunks) instead of producing a silently wrong sum."""
+    res = _spawn(2, STALL, extra_env={"NDP_FLAG_WAIT_US": "300000"})
+    for r in res:
+        assert r["err"] is not None and "timed out" in r["err"], r
