@@ -167,6 +167,11 @@ def _loss_fn(config, model, crit):
     return f
 
 
+def _batch_len(batch) -> int:
+    first = next(iter(batch.values())) if isinstance(batch, dict) else batch[0]
+    return int(first.shape[0])
+
+
 def run_task(config) -> Dict[str, Any]:
     """The reference's training loop for the configured task (returns a summary)."""
     validate_config(config, strict=False)  # typed schema: types, choices, cross-field rules
@@ -294,7 +299,7 @@ def run_task(config) -> Dict[str, Any]:
                 sync.step()
             i += 1
             step += 1
-            samples += bsz * world
+            samples += _batch_len(batch) * world  # the ragged last batch counts what it holds
             if checker is not None:
                 if runner is not None and step % checker.every == 0:
                     runner.join()
@@ -345,7 +350,7 @@ def run_task(config) -> Dict[str, Any]:
         flat = getattr(getattr(sync, "ddp", None), "x", None)
     if flat is None:
         flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
-    summary = {"epoch_losses": losses, "steps": step, "elapsed_s": elapsed,
+    summary = {"epoch_losses": losses, "steps": step, "elapsed_s": elapsed, "samples": samples,
                "samples_per_s": samples / elapsed if elapsed > 0 else None,
                "bytes_per_step": getattr(sync, "bytes_per_step", None), "comm": comm.stats.as_dict(),
                "comm_backend": comm.backend, "world_size": world, "per_rank_batch": bsz, "graph_mode": graph_mode,

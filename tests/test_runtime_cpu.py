@@ -180,6 +180,7 @@ def test_engine_ragged_last_batch_and_reference_mean(tmp_path):
     steps = [r for r in recs if r["kind"] == "step"]
     assert ep["steps"] == ep["num_batches"] == 4  # 32 + 32 + 32 + 4
     assert len(steps) == 4 and out["steps"] == 4
+    assert out["samples"] == 100  # the ragged batch counts its 4 samples, not 32
     assert abs(ep["mean_loss"] - sum(r["loss"] for r in steps) / 4) < 1e-5
 
 
