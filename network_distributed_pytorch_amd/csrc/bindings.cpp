@@ -936,7 +936,118 @@ void attn_bwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, c10::optional<t
 }  // namespace
 
 void register_comm(py::module& m);  // comm.cpp
-void register_ipc(py::module& m);   // ipc.hip
+// ---- small-map convolutions (smallconv.hip) --------------------------------------------------
+// (class, fwd slabs, grad-x slabs, grad-W slabs) for batch B, or class -1
+py::tuple sm_plan(const std::vector<int64_t>& geom, int64_t B) {
+  const ndp::ConvGeom g = conv_geom(geom);
+  const int cls = ndp::sm_class(g);
+  const int64_t ny = B * g.Co * g.OH * g.OW, nx = B * g.C * g.H * g.W, nw = (int64_t)g.Co * g.C * g.KH * g.KW;
+  if (cls < 0 || B <= 0 || ny % 4 || nx % 4 || nw % 4) return py::make_tuple(-1, 1, 1, 1);
+  // 32-bit buffer offsets (raw buffer descriptors)
+  if (std::max(std::max(ny, nx), nw) * 4 >= (1LL << 31)) return py::make_tuple(-1, 1, 1, 1);
+  return py::make_tuple(cls, ndp::sm_splits(g, (int)B, 0), ndp::sm_splits(g, (int)B, 1), ndp::sm_splits(g, (int)B, 2));
+}
+
+static int sm_batch(const torch::Tensor& t, const ndp::ConvGeom& g, const char* who) {
+  TORCH_CHECK(ndp::sm_class(g) >= 0, who, ": no small-map kernel for this geometry");
+  return (int)t.size(0);
+}
+
+int64_t sm_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, const std::vector<int64_t>& geom,
+               c10::optional<torch::Tensor> part, bool defer) {
+  const ndp::ConvGeom g = conv_geom(geom);
+  const int B = sm_batch(x, g, "sm_fwd");
+  conv_check(x, "x", B, g.C, g.H, g.W);
+  conv_check(w, "w", g.Co, g.C, g.KH, g.KW);
+  conv_check(y, "y", B, g.Co, g.OH, g.OW);
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(y.data_ptr()) & 15) == 0, "sm_fwd: 16-B aligned y");
+  float* pp = tg_part(part, ndp::sm_splits(g, B, 0), y.numel(), "sm_fwd");
+  const int left = ndp::launch_sm_fwd(x.data_ptr<float>(), w.data_ptr<float>(), y.data_ptr<float>(), B, g, pp,
+                                      cur_stream(), defer);
+  check_launch("launch_sm_fwd");
+  return left;
+}
+
+int64_t sm_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, const std::vector<int64_t>& geom,
+                 c10::optional<torch::Tensor> part, c10::optional<torch::Tensor> addend, bool defer) {
+  const ndp::ConvGeom g = conv_geom(geom);
+  const int B = sm_batch(dy, g, "sm_dgrad");
+  conv_check(dy, "dy", B, g.Co, g.OH, g.OW);
+  conv_check(w, "w", g.Co, g.C, g.KH, g.KW);
+  conv_check(dx, "dx", B, g.C, g.H, g.W);
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(dx.data_ptr()) & 15) == 0, "sm_dgrad: 16-B aligned dx");
+  float* pp = tg_part(part, ndp::sm_splits(g, B, 1), dx.numel(), "sm_dgrad");
+  const float* ap = nullptr;
+  if (addend.has_value()) {
+    conv_check(*addend, "addend", B, g.C, g.H, g.W);
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(addend->data_ptr()) & 15) == 0, "sm_dgrad: 16-B aligned addend");
+    ap = addend->data_ptr<float>();
+  }
+  const int left = ndp::launch_sm_dgrad(dy.data_ptr<float>(), w.data_ptr<float>(), dx.data_ptr<float>(), B, g, pp,
+                                        cur_stream(), ap, defer);
+  check_launch("launch_sm_dgrad");
+  return left;
+}
+
+// out: sm_splits(g, B, 2) * numel(W) floats; returns the number of slabs written (1 = dW)
+int64_t sm_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor out, const std::vector<int64_t>& geom) {
+  const ndp::ConvGeom g = conv_geom(geom);
+  const int B = sm_batch(x, g, "sm_wgrad");
+  conv_check(x, "x", B, g.C, g.H, g.W);
+  conv_check(dy, "dy", B, g.Co, g.OH, g.OW);
+  check_f32(out, "out");
+  const int z = ndp::sm_splits(g, B, 2);
+  TORCH_CHECK(out.numel() >= (int64_t)z * g.Co * g.C * g.KH * g.KW, "sm_wgrad: out must hold ", z, " slabs of dW");
+  const int got = ndp::launch_sm_wgrad(x.data_ptr<float>(), dy.data_ptr<float>(), out.data_ptr<float>(), B, g,
+                                       cur_stream());
+  check_launch("launch_sm_wgrad");
+  return got;
+}
+
+// ---- HIP-IPC one-shot all-reduce (ipc.hip; registered here so pybind11 stays g++-only) ----
+namespace ndp {
+void* ipc_new(int rank, int nranks, int device, int64_t capacity_bytes);
+void ipc_delete(void* c);
+std::string ipc_handle(void* c);
+void ipc_open(void* c, const std::vector<std::string>& h);
+void ipc_all_reduce_many(void* c, const std::vector<at::Tensor>& ts, const std::string& op, int64_t stream);
+int64_t ipc_error(void* c);
+void ipc_check(void* c);
+void ipc_destroy(void* c);
+std::string ipc_bus_id(void* c);
+int64_t ipc_info(void* c, int what);
+}  // namespace ndp
+
+struct IpcCommPy {
+  void* c;
+  IpcCommPy(int rank, int nranks, int device, int64_t cap) : c(ndp::ipc_new(rank, nranks, device, cap)) {}
+  ~IpcCommPy() { ndp::ipc_delete(c); }  // buffers are released by destroy() (graphs may still use them)
+};
+
+void register_ipc(py::module& m) {
+  py::class_<IpcCommPy, std::shared_ptr<IpcCommPy>>(m, "IpcComm")
+      .def(py::init<int, int, int, int64_t>(), py::arg("rank"), py::arg("nranks"), py::arg("device"),
+           py::arg("capacity_bytes") = 8 << 20)
+      .def("handle", [](IpcCommPy& s) { return py::bytes(ndp::ipc_handle(s.c)); })
+      .def("open", [](IpcCommPy& s, const std::vector<std::string>& h) { ndp::ipc_open(s.c, h); })
+      .def("all_reduce", [](IpcCommPy& s, torch::Tensor t, const std::string& op, int64_t stream) {
+            ndp::ipc_all_reduce_many(s.c, {t}, op, stream);
+          }, py::arg("t"), py::arg("op") = "sum", py::arg("stream") = 0)
+      .def("all_reduce_many", [](IpcCommPy& s, const std::vector<torch::Tensor>& ts, const std::string& op,
+                                 int64_t stream) { ndp::ipc_all_reduce_many(s.c, ts, op, stream); },
+           py::arg("ts"), py::arg("op") = "sum", py::arg("stream") = 0)
+      .def("error", [](IpcCommPy& s) { return ndp::ipc_error(s.c); })
+      .def("check", [](IpcCommPy& s) { ndp::ipc_check(s.c); })
+      .def("destroy", [](IpcCommPy& s) { ndp::ipc_destroy(s.c); })
+      .def("bus_id", [](IpcCommPy& s) { return ndp::ipc_bus_id(s.c); })
+      .def_property_readonly("rank", [](IpcCommPy& s) { return ndp::ipc_info(s.c, 0); })
+      .def_property_readonly("nranks", [](IpcCommPy& s) { return ndp::ipc_info(s.c, 1); })
+      .def_property_readonly("device", [](IpcCommPy& s) { return ndp::ipc_info(s.c, 2); })
+      .def_property_readonly("capacity", [](IpcCommPy& s) { return ndp::ipc_info(s.c, 3); })
+      .def_property_readonly("alive", [](IpcCommPy& s) { return ndp::ipc_info(s.c, 4) != 0; })
+      .def_property_readonly("uncached", [](IpcCommPy& s) { return ndp::ipc_info(s.c, 5) != 0; })
+      .def_property_readonly("launches", [](IpcCommPy& s) { return ndp::ipc_info(s.c, 6); });
+}
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "network_distributed_pytorch_amd native gfx950 kernels + plan builder";
@@ -989,6 +1100,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("part") = py::none(), py::arg("addend") = py::none(), py::arg("defer") = false);
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("part"), py::arg("dw"), py::arg("geom"));
   m.def("tg_plan", &tg_plan);
+  m.def("sm_plan", &sm_plan, py::arg("geom"), py::arg("batch"));
+  m.def("sm_fwd", &sm_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("geom"), py::arg("part"),
+        py::arg("defer"));
+  m.def("sm_dgrad", &sm_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("geom"), py::arg("part"),
+        py::arg("addend"), py::arg("defer"));
+  m.def("sm_wgrad", &sm_wgrad, py::arg("x"), py::arg("dy"), py::arg("out"), py::arg("geom"));
   m.def("tg_describe", &tg_describe);
   m.def("tg_fwd", &tg_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("geom"), py::arg("part") = py::none(),
         py::arg("defer") = false);

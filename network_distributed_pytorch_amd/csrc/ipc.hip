@@ -31,7 +31,7 @@
 // [w*4096, (w+1)*4096) of the tensors' concatenation (a segment table in the arguments).
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
-#include <torch/extension.h>
+#include <ATen/ATen.h>
 
 #include <cstring>
 #include <memory>
@@ -180,10 +180,10 @@ class IpcComm {
   }
   ~IpcComm() = default;  // released by destroy() (captured graphs may still reference the buffers)
 
-  py::bytes handle() const {
+  std::string handle() const {
     hipIpcMemHandle_t h;
     NDP_IPC_CHECK(hipIpcGetMemHandle(&h, base_));
-    return py::bytes(h.reserved, HIP_IPC_HANDLE_SIZE);
+    return std::string(h.reserved, HIP_IPC_HANDLE_SIZE);
   }
 
   void open(const std::vector<std::string>& handles) {
@@ -201,15 +201,15 @@ class IpcComm {
     opened_ = true;
   }
 
-  void all_reduce(torch::Tensor t, const std::string& op, int64_t stream) { all_reduce_many({t}, op, stream); }
+  void all_reduce(at::Tensor t, const std::string& op, int64_t stream) { all_reduce_many({t}, op, stream); }
 
   // every tensor of the list in as few launches as the buffer capacity and the segment
   // table allow (one for the PowerSGD payloads)
-  void all_reduce_many(const std::vector<torch::Tensor>& ts, const std::string& op, int64_t stream) {
+  void all_reduce_many(const std::vector<at::Tensor>& ts, const std::string& op, int64_t stream) {
     TORCH_CHECK(opened_, "IpcComm: open() the peer handles first");
     TORCH_CHECK(op == "sum" || op == "avg", "IpcComm: sum / avg only");
     for (const auto& t : ts)
-      TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == torch::kFloat32 &&
+      TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == at::kFloat &&
                       t.get_device() == device_,
                   "IpcComm: contiguous float32 tensors on the communicator's device");
     hipStream_t s = stream == 0 ? at::hip::getCurrentHIPStream().stream() : reinterpret_cast<hipStream_t>(stream);
@@ -311,23 +311,33 @@ class IpcComm {
 
 }  // namespace
 
-void register_ipc(py::module& m) {
-  py::class_<IpcComm, std::shared_ptr<IpcComm>>(m, "IpcComm")
-      .def(py::init<int, int, int, int64_t>(), py::arg("rank"), py::arg("nranks"), py::arg("device"),
-           py::arg("capacity_bytes") = 8 << 20)
-      .def("handle", &IpcComm::handle)
-      .def("open", &IpcComm::open)
-      .def("all_reduce", &IpcComm::all_reduce, py::arg("t"), py::arg("op") = "sum", py::arg("stream") = 0)
-      .def("all_reduce_many", &IpcComm::all_reduce_many, py::arg("ts"), py::arg("op") = "sum", py::arg("stream") = 0)
-      .def("error", &IpcComm::error)
-      .def("check", &IpcComm::check)
-      .def("destroy", &IpcComm::destroy)
-      .def_property_readonly("rank", &IpcComm::rank)
-      .def_property_readonly("nranks", &IpcComm::nranks)
-      .def_property_readonly("device", &IpcComm::device)
-      .def_property_readonly("capacity", &IpcComm::capacity)
-      .def_property_readonly("alive", &IpcComm::alive)
-      .def_property_readonly("uncached", &IpcComm::uncached)
-      .def_property_readonly("launches", &IpcComm::launches)
-      .def("bus_id", &IpcComm::bus_id);
+// C++ surface for the pybind11 registration in bindings.cpp (pybind11 stays out of the
+// hipcc-compiled translation units: its inline internals compiled by two compilers in one
+// module corrupted the registry at import)
+namespace ndp {
+void* ipc_new(int rank, int nranks, int device, int64_t capacity_bytes) {
+  return new IpcComm(rank, nranks, device, capacity_bytes);
 }
+void ipc_delete(void* c) { delete static_cast<IpcComm*>(c); }
+std::string ipc_handle(void* c) { return static_cast<IpcComm*>(c)->handle(); }
+void ipc_open(void* c, const std::vector<std::string>& h) { static_cast<IpcComm*>(c)->open(h); }
+void ipc_all_reduce_many(void* c, const std::vector<at::Tensor>& ts, const std::string& op, int64_t stream) {
+  static_cast<IpcComm*>(c)->all_reduce_many(ts, op, stream);
+}
+int64_t ipc_error(void* c) { return static_cast<IpcComm*>(c)->error(); }
+void ipc_check(void* c) { static_cast<IpcComm*>(c)->check(); }
+void ipc_destroy(void* c) { static_cast<IpcComm*>(c)->destroy(); }
+std::string ipc_bus_id(void* c) { return static_cast<IpcComm*>(c)->bus_id(); }
+int64_t ipc_info(void* c, int what) {
+  const IpcComm* p = static_cast<IpcComm*>(c);
+  switch (what) {
+    case 0: return p->rank();
+    case 1: return p->nranks();
+    case 2: return p->device();
+    case 3: return p->capacity();
+    case 4: return p->alive() ? 1 : 0;
+    case 5: return p->uncached() ? 1 : 0;
+    default: return p->launches();
+  }
+}
+}  // namespace ndp

@@ -279,6 +279,23 @@ int launch_tg_wgrad(const float* x, const float* dy, float* out, int B, const Co
                     hipStream_t s, bool defer = false);
 }  // namespace ndp
 
+// ---- small-map convolutions on 16x16x4 f32 MFMA (smallconv.hip) ---------------------------
+namespace ndp {
+// geometry id (input <= 4x4, output <= 2x2, ResNet layer3 / layer4), -1 = not covered
+int sm_class(const ConvGeom& g);
+// split factor of direction dir (0 fwd / 1 grad-x: channel splits, slabs of numel(out) floats;
+// 2 grad-W: batch splits, slabs of numel(W) floats) at batch B; 1 = no scratch
+int sm_splits(const ConvGeom& g, int B, int dir);
+// defer: leave the split-K slabs in part, return their count (1 = y / dx final)
+int launch_sm_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s,
+                  bool defer = false);
+// addend (nullable, may alias dx): dx = grad-x + addend (never deferred)
+int launch_sm_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, float* part, hipStream_t s,
+                    const float* addend = nullptr, bool defer = false);
+// out: sm_splits(g, B, 2) slabs of numel(W) floats (slab 0 = dW when 1); returns the count
+int launch_sm_wgrad(const float* x, const float* dy, float* out, int B, const ConvGeom& g, hipStream_t s);
+}  // namespace ndp
+
 // ---- fused fp32 attention, q/k/v/o [B, S, H, 64] (attention.hip) ------------------------
 namespace ndp {
 // mask: [B, S] int32 (nonzero = attend) or null; lse: [B, H, S]; p_drop in [0, 1);

@@ -1,0 +1,705 @@
+// Small-map convolutions (input <= 4x4, output <= 2x2: ResNet layer3 / layer4 on 32x32
+// inputs) on v_mfma_f32_16x16x4_f32 — exact f32, NCHW, no W_big, no fold, no vendor GEMM.
+//
+// On a 2x2 or 1x1 map a convolution is a sum over a handful of (input pixel p, output
+// pixel q) pairs, each joined by ONE kernel tap t(p, q) (models/conv_gemm.py has the
+// Toeplitz view).  With the geometry a template parameter the pair list is a compile-time
+// constant, so each direction is a set of small GEMMs over channels, one per pair, all
+// accumulating in registers:
+//   forward  Y[b, co, q]  = sum_(p,q) sum_ci X[b, ci, p]  W[co, ci, t(p, q)]
+//   grad-x   dX[b, ci, p] = sum_(p,q) sum_co dY[b, co, q] W[co, ci, t(p, q)]
+//   grad-W   dW[co, ci, t] = sum_b sum_((p,q): t) dY[b, co, q] X[b, ci, p]
+// The weight tile is staged from W's own [co][ci][tap] rows (16-B loads of whole rows when
+// every tap is used, the used taps only otherwise), the activation tile from the [b][c][pix]
+// rows; the tap gather is LDS index arithmetic folded at compile time.  grad-W lands in W's
+// layout directly (every KH*KW tap, structural zeros written): no Toeplitz expand / fold.
+//
+// Row kernel (forward and grad-x): workgroup tile = TM images x TN output channels x every
+// output pixel; the 4 waves split the reduction channels of each LDS chunk (wave w owns
+// k-steps w*S .. w*S+S-1 of 4 channels) and add their partial tiles through LDS in wave order
+// at the end — the whole reduction of a tile inside one workgroup, deterministic, so the
+// epilogue sees final values.  Small batches that cannot fill the 256 CUs split the channels
+// over gridDim.z instead, as partial slabs summed in z order by the consumer (the fused BN
+// kernel, ops/slablink.py, or conv_slab_sum).
+// grad-W kernel: tile = TMC out x TNC in channels x every tap; the waves split the images,
+// gridDim.z splits the batch into slabs (summed by ops/gradfinish.py, batched).
+//
+// LDS images are padded so that every ds_read_b32 of an MFMA operand is conflict-free: a
+// half-wave reads 16 lanes along one index and 2 along another; either the 16-lane stride
+// is = 2 (mod 32) and the 2-lane stride odd, or the 16-lane stride odd and the 2-lane stride
+// = 16 (mod 32) — both put the 32 lanes on 32 distinct banks.
+#include <hip/hip_runtime.h>
+
+#include <stdlib.h>
+
+#include <type_traits>
+
+#include "ndp_kernels.h"
+
+namespace ndp {
+
+namespace {
+
+typedef float f32x4s __attribute__((ext_vector_type(4)));
+
+template <int HI_, int WI_, int KH_, int KW_, int ST_, int PD_>
+struct Geo {
+  static constexpr int HI = HI_, WI = WI_, KH = KH_, KW = KW_, ST = ST_, PD = PD_;
+  static constexpr int OH = (HI + 2 * PD - KH) / ST + 1, OW = (WI + 2 * PD - KW) / ST + 1;
+  static constexpr int PI = HI * WI, PO = OH * OW, T = KH * KW;
+  static constexpr int tap(int i, int o) {
+    const int ih = i / WI, iw = i % WI, oh = o / OW, ow = o % OW;
+    const int kh = ih - oh * ST + PD, kw = iw - ow * ST + PD;
+    return (kh >= 0 && kh < KH && kw >= 0 && kw < KW) ? kh * KW + kw : -1;
+  }
+  static constexpr bool used(int t) {
+    for (int i = 0; i < PI; ++i)
+      for (int o = 0; o < PO; ++o)
+        if (tap(i, o) == t) return true;
+    return false;
+  }
+  static constexpr int n_used() {
+    int n = 0;
+    for (int t = 0; t < T; ++t) n += used(t) ? 1 : 0;
+    return n;
+  }
+  static constexpr int slot(int t) {  // compact index of tap t among the used taps (-1: unused)
+    if (t < 0 || !used(t)) return -1;
+    int n = 0;
+    for (int u = 0; u < t; ++u) n += used(u) ? 1 : 0;
+    return n;
+  }
+  static constexpr int utap(int s) {  // the s-th used tap
+    for (int t = 0; t < T; ++t)
+      if (used(t) && slot(t) == s) return t;
+    return -1;
+  }
+  static constexpr int NU = n_used();
+  static constexpr bool ALL = NU == T;
+};
+
+// the ResNet small-map geometries (CIFAR inputs; any channel counts)
+using G_3x3_2 = Geo<2, 2, 3, 3, 1, 1>;    // 3x3 on 2x2 (layer3)
+using G_3x3_4s2 = Geo<4, 4, 3, 3, 2, 1>;  // 3x3 / 2, 4x4 -> 2x2 (layer3 entry)
+using G_1x1_4s2 = Geo<4, 4, 1, 1, 2, 0>;  // 1x1 / 2, 4x4 -> 2x2 (layer3 downsample)
+using G_3x3_2s2 = Geo<2, 2, 3, 3, 2, 1>;  // 3x3 / 2, 2x2 -> 1x1 (layer4 entry)
+using G_3x3_1 = Geo<1, 1, 3, 3, 1, 1>;    // 3x3 on 1x1: the centre tap (layer4)
+using G_1x1_2s2 = Geo<2, 2, 1, 1, 2, 0>;  // 1x1 / 2, 2x2 -> 1x1 (layer4 downsample)
+using G_1x1_2 = Geo<2, 2, 1, 1, 1, 0>;    // 1x1 on 2x2 (bottleneck conv1 / conv3, layer3)
+using G_1x1_1 = Geo<1, 1, 1, 1, 1, 0>;    // 1x1 on 1x1 (bottleneck, layer4)
+
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+constexpr int cpad(int need, int mod) {  // smallest v >= need with v % 32 == mod
+  int v = need;
+  while (v % 32 != mod) ++v;
+  return v;
+}
+
+__device__ __forceinline__ f32x4s mfma16(float a, float b, f32x4s c) {
+  // D(16x16) += A(16x4) B(4x16); lane l: A[l&15][l>>4], B[l>>4][l&15]; D: col l&15, row 4*(l>>4)+r
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, 0x7fffffff, 0x00020000);
+}
+constexpr uint32_t kOOB = 0xffffffffu;  // past the descriptor's range: the load returns 0
+__device__ __forceinline__ f32x4s bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(f32x4s, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+
+// ---- row kernel: forward (DIR 0) / grad-x (DIR 1) ------------------------------------------
+// operand "act": [B][K][PP] (X for the forward, dY for grad-x), K = reduction channels;
+// W [Co][C][T]: forward n = co, k = ci; grad-x n = ci, k = co.  out [B][N][PQ].
+template <class G, int DIR, int TM, int TN, int S>
+struct RowCfg {
+  static constexpr int PP = DIR == 0 ? G::PI : G::PO;
+  static constexpr int PQ = DIR == 0 ? G::PO : G::PI;
+  static constexpr int tapq(int p, int q) { return DIR == 0 ? G::tap(p, q) : G::tap(q, p); }
+  static constexpr int TK = 16 * S;  // channels per LDS chunk: 4 waves x S k-steps x 4
+  static constexpr int MB = TM / 16, NB = TN / 16;
+  // act image [b][k][p]: 16 lanes along b (RS = 2 mod 32), 2 along k (KS odd)
+  static constexpr int KS = PP | 1;
+  static constexpr int RS = cpad(TK * KS, 2);
+  static constexpr int A_SZ = TM * RS;
+  // weight image of the used taps (U, compact slot order); KSW = U | 1 (odd; = T when every
+  // tap is used, T in {1, 9}, so a W row stays contiguous in LDS)
+  //  forward [n][k][u]: 16 lanes along n (RSW = 2 mod 32), 2 along k (stride KSW, odd)
+  //  grad-x  [k][n][u]: 16 lanes along n (stride KSW, odd), 2 along k (RSW = 16 mod 32)
+  static constexpr int U = G::NU;
+  static constexpr int KSW = U | 1;
+  static constexpr int RSW = DIR == 0 ? cpad(TK * KSW, 2) : cpad(TN * KSW, 16);
+  static constexpr int W_SZ = DIR == 0 ? TN * RSW : TK * RSW;
+  static constexpr int STAGE = (A_SZ + W_SZ + 3) / 4 * 4;
+  static constexpr int NACC = MB * NB * PQ;  // f32x4 accumulators per wave
+  static constexpr int RED = 4 * NACC * 4 * 64;
+  static constexpr int LDS_FLOATS = (2 * STAGE > RED ? 2 * STAGE : RED);
+  static constexpr size_t LDS_BYTES = (size_t)LDS_FLOATS * 4;
+  // global loads per chunk: act = TM rows of TK*PP contiguous floats (16-B vectors)
+  static constexpr int AV = TM * TK * PP / 4, A_PER = (AV + 255) / 256;
+  // weights: whole rows (every tap used) as 16-B vectors, else one float per used tap
+  static constexpr int WCH = DIR == 0 ? TK : TN;    // channels along a tile row of W
+  static constexpr int WROWS = DIR == 0 ? TN : TK;  // rows (co) of the tile
+  static constexpr int WV = G::ALL ? WROWS * WCH * G::T / 4 : WROWS * WCH * U;
+  static constexpr int W_PER = (WV + 255) / 256;
+  static_assert(TM % 16 == 0 && TN % 16 == 0, "tile");
+  static_assert((TK * PP) % 4 == 0 && (!G::ALL || (WCH * G::T) % 4 == 0), "16-B rows");
+  static_assert(!G::ALL || KSW == G::T, "contiguous W rows");
+  static_assert(PP >= 4 || PP == 1, "act vectors");
+};
+
+struct SmRowArgs {
+  const float* act;     // [B][K][PP]
+  const float* w;       // [Co][C][KH][KW]
+  float* out;           // [B][N][PQ]
+  float* part;          // split-K slabs [z][B][N][PQ] (gridDim.z > 1)
+  const float* addend;  // nullable, no split: out = result + addend (may alias out)
+  int B, K, N, C, cps;  // cps: reduction channels per split
+  int64_t slab;
+};
+
+template <class G, int DIR, int TM, int TN, int S>
+__global__ __launch_bounds__(256) void sm_row_kernel(SmRowArgs a) {
+  using R = RowCfg<G, DIR, TM, TN, S>;
+  constexpr int PP = R::PP, PQ = R::PQ, TK = R::TK, U = R::U, MB = R::MB, NB = R::NB;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l16 = lane & 15, l4 = lane >> 4;
+  const int n0 = blockIdx.x * TN, b0 = blockIdx.y * TM;
+  const int kbeg = blockIdx.z * a.cps;
+  const int nchunks = (min(a.K, kbeg + a.cps) - kbeg) / TK;
+
+  const __amdgpu_buffer_rsrc_t ra = rsrc(a.act), rw = rsrc(a.w);
+  // fixed per-thread load coordinates (only a uniform chunk offset moves)
+  uint32_t aoff[R::A_PER];
+  int adst[R::A_PER];
+#pragma unroll
+  for (int v = 0; v < R::A_PER; ++v) {
+    const int e = tid + 256 * v;  // vector index in [TM][TK*PP / 4]
+    const int row = e / (TK * PP / 4), j = 4 * (e - row * (TK * PP / 4));
+    const int b = b0 + row;
+    aoff[v] = (e < R::AV && b < a.B) ? (uint32_t)((((int64_t)b * a.K + kbeg) * PP + j) * 4) : kOOB;
+    adst[v] = e < R::AV ? row * R::RS + (j / PP) * R::KS + (j % PP) : -1;
+  }
+  uint32_t woff[R::W_PER];
+  int wdst[R::W_PER];
+#pragma unroll
+  for (int v = 0; v < R::W_PER; ++v) {
+    const int e = tid + 256 * v;
+    const bool ok = e < R::WV;
+    int row, ch, tsrc, dcol;  // tile row, channel along the row, source tap / float, dest column
+    if constexpr (G::ALL) {
+      row = e / (R::WCH * G::T / 4);
+      const int j = 4 * (e - row * (R::WCH * G::T / 4));  // float in the row (contiguous in LDS too)
+      ch = 0;
+      tsrc = j;
+      dcol = j;
+    } else {
+      row = e / (R::WCH * U);
+      const int r2 = e - row * (R::WCH * U);
+      ch = r2 / U;
+      const int s = r2 - ch * U;
+      tsrc = ch * G::T + G::utap(s);
+      dcol = ch * R::KSW + s;
+    }
+    // forward rows: co = n0 + row, floats from ci = kbeg; grad-x rows: co = kbeg + row, from ci = n0
+    const int64_t g = DIR == 0 ? ((int64_t)(n0 + row) * a.C + kbeg) * G::T + tsrc
+                               : ((int64_t)(kbeg + row) * a.C + n0) * G::T + tsrc;
+    woff[v] = ok ? (uint32_t)(g * 4) : kOOB;
+    wdst[v] = ok ? row * R::RSW + dcol : -1;
+  }
+  // per-chunk advance: act TK channels; weights TK reduction channels (forward: along a row,
+  // grad-x: TK rows down)
+  const uint32_t astep = TK * PP * 4;
+  const uint32_t wstep = DIR == 0 ? TK * G::T * 4 : (uint32_t)(TK * a.C * G::T * 4);
+
+  typedef typename std::conditional<G::ALL, f32x4s, float>::type WVec;
+  f32x4s rA[R::A_PER];
+  WVec rW[R::W_PER];
+  auto load = [&](int c) {
+#pragma unroll
+    for (int v = 0; v < R::A_PER; ++v) rA[v] = bload4(ra, aoff[v] == kOOB ? kOOB : aoff[v] + c * astep);
+#pragma unroll
+    for (int v = 0; v < R::W_PER; ++v) {
+      const uint32_t o = woff[v] == kOOB ? kOOB : woff[v] + c * wstep;
+      if constexpr (G::ALL) rW[v] = bload4(rw, o);
+      else rW[v] = bload1(rw, o);
+    }
+  };
+  auto store = [&](int buf) {
+    float* As = smem + buf * R::STAGE;
+    float* Ws = As + R::A_SZ;
+#pragma unroll
+    for (int v = 0; v < R::A_PER; ++v) {
+      if (adst[v] < 0) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) As[adst[v] + (PP >= 4 ? q : q * R::KS)] = rA[v][q];
+    }
+#pragma unroll
+    for (int v = 0; v < R::W_PER; ++v) {
+      if (wdst[v] < 0) continue;
+      if constexpr (G::ALL) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Ws[wdst[v] + q] = rW[v][q];
+      } else {
+        Ws[wdst[v]] = rW[v];
+      }
+    }
+  };
+
+  f32x4s acc[MB][NB][PQ];
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int q = 0; q < PQ; ++q) acc[i][j][q] = f32x4s{0.f, 0.f, 0.f, 0.f};
+
+  if (nchunks > 0) {
+    load(0);
+    store(0);
+    __syncthreads();
+  }
+  for (int c = 0; c < nchunks; ++c) {
+    const int cur = c & 1;
+    if (c + 1 < nchunks) load(c + 1);  // in flight during this chunk's MFMAs
+    const float* As = smem + cur * R::STAGE;
+    const float* Ws = As + R::A_SZ;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int kk = (wave * S + s) * 4 + l4;  // the reduction channel this lane feeds
+      float af[MB][PP], bf[NB][U];
+#pragma unroll
+      for (int i = 0; i < MB; ++i)
+#pragma unroll
+        for (int p = 0; p < PP; ++p) af[i][p] = As[(i * 16 + l16) * R::RS + kk * R::KS + p];
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          bf[j][u] = DIR == 0 ? Ws[(j * 16 + l16) * R::RSW + kk * R::KSW + u]
+                              : Ws[kk * R::RSW + (j * 16 + l16) * R::KSW + u];
+      static_for<0, PP * PQ>([&](auto idx) {
+        constexpr int p = decltype(idx)::value / PQ, q = decltype(idx)::value % PQ;
+        constexpr int u = G::slot(R::tapq(p, q));
+        if constexpr (u >= 0) {
+#pragma unroll
+          for (int i = 0; i < MB; ++i)
+#pragma unroll
+            for (int j = 0; j < NB; ++j) acc[i][j][q] = mfma16(af[i][p], bf[j][u], acc[i][j][q]);
+        }
+      });
+    }
+    if (c + 1 < nchunks) store(cur ^ 1);  // the other buffer was released by the last barrier
+    __syncthreads();
+  }
+
+  // the 4 waves' partial tiles -> LDS -> wave w finishes register w (rows 4*l4 + w of each
+  // 16-row block), adding the waves in order 0..3
+  float* red = smem;
+  if (nchunks == 0) __syncthreads();
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int q = 0; q < PQ; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[(((wave * MB + i) * NB + j) * PQ + q) * 256 + r * 64 + lane] = acc[i][j][q][r];
+  __syncthreads();
+  const bool split = gridDim.z > 1;
+  float* dst = split ? a.part + (int64_t)blockIdx.z * a.slab : a.out;
+#pragma unroll
+  for (int i = 0; i < MB; ++i) {
+    const int b = b0 + i * 16 + 4 * l4 + wave;
+    if (b >= a.B) continue;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int n = n0 + j * 16 + l16;
+      float v[PQ];
+#pragma unroll
+      for (int q = 0; q < PQ; ++q) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) t += red[(((w * MB + i) * NB + j) * PQ + q) * 256 + wave * 64 + lane];
+        v[q] = t;
+      }
+      const int64_t o = ((int64_t)b * a.N + n) * PQ;
+      if (!split && a.addend != nullptr) {
+#pragma unroll
+        for (int q = 0; q < PQ; ++q) v[q] += a.addend[o + q];
+      }
+      if constexpr (PQ % 4 == 0) {
+#pragma unroll
+        for (int q = 0; q < PQ; q += 4)
+          *reinterpret_cast<f32x4s*>(dst + o + q) = f32x4s{v[q], v[q + 1], v[q + 2], v[q + 3]};
+      } else {
+#pragma unroll
+        for (int q = 0; q < PQ; ++q) dst[o + q] = v[q];
+      }
+    }
+  }
+}
+
+// ---- grad-W kernel ---------------------------------------------------------------------------
+// dW[co][ci][t] (+ slab z) = sum over this split's images b and the pairs (p, q) with tap t of
+// dY[b][co][q] X[b][ci][p].  MFMA: M = co (16 lanes), N = ci (16 lanes), K = 4 images.
+template <class G, int TMC, int TNC, int S>
+struct WgCfg {
+  static constexpr int PI = G::PI, PO = G::PO, U = G::NU;
+  static constexpr int TB = 16 * S;  // images per LDS chunk
+  static constexpr int MB = TMC / 16, NB = TNC / 16;
+  // dY image [b][co][q]: 16 lanes along co (KSG = PO | 1, odd), 2 along b (RSG = 16 mod 32)
+  static constexpr int KSG = PO | 1, RSG = cpad(TMC * KSG, 16), G_SZ = TB * RSG;
+  // X image [b][ci][p]: 16 lanes along ci (KSX = PI | 1), 2 along b (RSX = 16 mod 32)
+  static constexpr int KSX = PI | 1, RSX = cpad(TNC * KSX, 16), X_SZ = TB * RSX;
+  static constexpr int STAGE = (G_SZ + X_SZ + 3) / 4 * 4;
+  static constexpr int NACC = MB * NB * U;
+  static constexpr int RED = 4 * NACC * 4 * 64;
+  static constexpr int LDS_FLOATS = (2 * STAGE > RED ? 2 * STAGE : RED);
+  static constexpr size_t LDS_BYTES = (size_t)LDS_FLOATS * 4;
+  static constexpr int GV = TB * TMC * PO / 4, G_PER = (GV + 255) / 256;
+  static constexpr int XV = TB * TNC * PI / 4, X_PER = (XV + 255) / 256;
+  static_assert((TMC * PO) % 4 == 0 && (TNC * PI) % 4 == 0, "16-B rows");
+  static_assert(PO >= 4 || PO == 1, "dY vectors");
+  static_assert(PI >= 4 || PI == 1, "X vectors");
+};
+
+struct SmWgArgs {
+  const float* x;   // [B][C][PI]
+  const float* dy;  // [B][Co][PO]
+  float* out;       // dW [Co][C][T] (or slab base when gridDim.z > 1)
+  int B, C, Co, ips;  // ips: images per split
+  int64_t slab;
+};
+
+template <class G, int TMC, int TNC, int S>
+__global__ __launch_bounds__(256) void sm_wgrad_kernel(SmWgArgs a) {
+  using R = WgCfg<G, TMC, TNC, S>;
+  constexpr int PI = R::PI, PO = R::PO, U = R::U, TB = R::TB, MB = R::MB, NB = R::NB;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l16 = lane & 15, l4 = lane >> 4;
+  const int ci0 = blockIdx.x * TNC, co0 = blockIdx.y * TMC;
+  const int bbeg = blockIdx.z * a.ips;
+  const int bend = min(a.B, bbeg + a.ips);
+  const int nchunks = (bend - bbeg + TB - 1) / TB;
+
+  const __amdgpu_buffer_rsrc_t rg = rsrc(a.dy), rx = rsrc(a.x);
+  uint32_t goff[R::G_PER], xoff[R::X_PER];
+  int gdst[R::G_PER], xdst[R::X_PER], gimg[R::G_PER], ximg[R::X_PER];
+#pragma unroll
+  for (int v = 0; v < R::G_PER; ++v) {
+    const int e = tid + 256 * v;
+    const int bi = e / (TMC * PO / 4), j = 4 * (e - bi * (TMC * PO / 4));
+    const bool ok = e < R::GV;
+    gimg[v] = ok ? bi : (1 << 20);
+    goff[v] = ok ? (uint32_t)((((int64_t)(bbeg + bi) * a.Co + co0) * PO + j) * 4) : kOOB;
+    gdst[v] = ok ? bi * R::RSG + (j / PO) * R::KSG + (j % PO) : -1;
+  }
+#pragma unroll
+  for (int v = 0; v < R::X_PER; ++v) {
+    const int e = tid + 256 * v;
+    const int bi = e / (TNC * PI / 4), j = 4 * (e - bi * (TNC * PI / 4));
+    const bool ok = e < R::XV;
+    ximg[v] = ok ? bi : (1 << 20);
+    xoff[v] = ok ? (uint32_t)((((int64_t)(bbeg + bi) * a.C + ci0) * PI + j) * 4) : kOOB;
+    xdst[v] = ok ? bi * R::RSX + (j / PI) * R::KSX + (j % PI) : -1;
+  }
+  const uint32_t gstep = (uint32_t)((int64_t)TB * a.Co * PO * 4), xstep = (uint32_t)((int64_t)TB * a.C * PI * 4);
+
+  f32x4s rG[R::G_PER], rX[R::X_PER];
+  auto load = [&](int c) {
+    const int left = bend - bbeg - c * TB;  // images of this chunk inside the split
+#pragma unroll
+    for (int v = 0; v < R::G_PER; ++v)
+      rG[v] = bload4(rg, (goff[v] == kOOB || gimg[v] >= left) ? kOOB : goff[v] + c * gstep);
+#pragma unroll
+    for (int v = 0; v < R::X_PER; ++v)
+      rX[v] = bload4(rx, (xoff[v] == kOOB || ximg[v] >= left) ? kOOB : xoff[v] + c * xstep);
+  };
+  auto store = [&](int buf) {
+    float* Gs = smem + buf * R::STAGE;
+    float* Xs = Gs + R::G_SZ;
+#pragma unroll
+    for (int v = 0; v < R::G_PER; ++v) {
+      if (gdst[v] < 0) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Gs[gdst[v] + (PO >= 4 ? q : q * R::KSG)] = rG[v][q];
+    }
+#pragma unroll
+    for (int v = 0; v < R::X_PER; ++v) {
+      if (xdst[v] < 0) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Xs[xdst[v] + (PI >= 4 ? q : q * R::KSX)] = rX[v][q];
+    }
+  };
+
+  f32x4s acc[MB][NB][U];
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[i][j][u] = f32x4s{0.f, 0.f, 0.f, 0.f};
+
+  if (nchunks > 0) {
+    load(0);
+    store(0);
+    __syncthreads();
+  }
+  for (int c = 0; c < nchunks; ++c) {
+    const int cur = c & 1;
+    if (c + 1 < nchunks) load(c + 1);
+    const float* Gs = smem + cur * R::STAGE;
+    const float* Xs = Gs + R::G_SZ;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int bb = (wave * S + s) * 4 + l4;  // the image this lane feeds (zero rows past B)
+      float gf[MB][PO], xf[NB][PI];
+#pragma unroll
+      for (int i = 0; i < MB; ++i)
+#pragma unroll
+        for (int q = 0; q < PO; ++q) gf[i][q] = Gs[bb * R::RSG + (i * 16 + l16) * R::KSG + q];
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int p = 0; p < PI; ++p) xf[j][p] = Xs[bb * R::RSX + (j * 16 + l16) * R::KSX + p];
+      static_for<0, PI * PO>([&](auto idx) {
+        constexpr int p = decltype(idx)::value / PO, q = decltype(idx)::value % PO;
+        constexpr int u = G::slot(G::tap(p, q));
+        if constexpr (u >= 0) {
+#pragma unroll
+          for (int i = 0; i < MB; ++i)
+#pragma unroll
+            for (int j = 0; j < NB; ++j) acc[i][j][u] = mfma16(gf[i][q], xf[j][p], acc[i][j][u]);
+        }
+      });
+    }
+    if (c + 1 < nchunks) store(cur ^ 1);
+    __syncthreads();
+  }
+
+  float* red = smem;
+  if (nchunks == 0) __syncthreads();
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[(((wave * MB + i) * NB + j) * U + u) * 256 + r * 64 + lane] = acc[i][j][u][r];
+  __syncthreads();
+  float* dst = a.out + (int64_t)blockIdx.z * a.slab;
+#pragma unroll
+  for (int i = 0; i < MB; ++i) {
+    const int co = co0 + i * 16 + 4 * l4 + wave;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int ci = ci0 + j * 16 + l16;
+      float v[G::T];
+#pragma unroll
+      for (int t = 0; t < G::T; ++t) v[t] = 0.f;
+      static_for<0, U>([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        float s = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) s += red[(((w * MB + i) * NB + j) * U + u) * 256 + wave * 64 + lane];
+        v[G::utap(u)] = s;
+      });
+      float* o = dst + ((int64_t)co * a.C + ci) * G::T;
+#pragma unroll
+      for (int t = 0; t < G::T; ++t) o[t] = v[t];
+    }
+  }
+}
+
+// ---- dispatch ----------------------------------------------------------------------------------
+template <typename K>
+void set_lds_once(K k, size_t bytes) {
+  hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+constexpr int kSmFill = 256;  // workgroups for one per CU
+constexpr int kSmMaxSplit = 4;  // forward / grad-x slabs: the fused BN kernel sums <= 4 (kMaxFusedSlabs)
+
+int pow2_split(int base, int chunks, int cap) {
+  int ks = 1;
+  while (ks * 2 <= cap && base * ks < kSmFill && chunks % (ks * 2) == 0 && chunks / (ks * 2) >= 1) ks *= 2;
+  return ks;
+}
+
+// images per row tile: 32 when the grid still fills the chip (and the accumulators fit), else 16
+template <class G, int DIR>
+int row_tm(int B, int N) {
+  constexpr int PQ = DIR == 0 ? G::PO : G::PI;
+  if (PQ > 4) return 16;
+  return ((B + 31) / 32) * (N / 16) >= kSmFill ? 32 : 16;
+}
+
+template <class G, int DIR, int TM>
+int run_row(const float* act, const float* w, float* out, float* part, const float* addend, int B, int K, int N,
+            int C, int ks, hipStream_t s) {
+  using R = RowCfg<G, DIR, TM, 16, 1>;
+  auto k = sm_row_kernel<G, DIR, TM, 16, 1>;
+  static bool attr = false;
+  if (!attr) {
+    set_lds_once(k, R::LDS_BYTES);
+    attr = true;
+  }
+  SmRowArgs a{};
+  a.act = act;
+  a.w = w;
+  a.out = out;
+  a.part = part;
+  a.addend = ks > 1 ? nullptr : addend;
+  a.B = B;
+  a.K = K;
+  a.N = N;
+  a.C = C;
+  a.cps = K / ks;
+  a.slab = (int64_t)B * N * (DIR == 0 ? G::PO : G::PI);
+  hipLaunchKernelGGL(k, dim3(N / 16, (B + TM - 1) / TM, ks), dim3(256), R::LDS_BYTES, s, a);
+  return ks;
+}
+
+template <class G, int DIR>
+int row_splits(int B, int K, int N) {
+  const int tm = row_tm<G, DIR>(B, N);
+  return pow2_split(((B + tm - 1) / tm) * (N / 16), K / 16, kSmMaxSplit);
+}
+
+template <class G, int DIR>
+int run_row_any(const float* act, const float* w, float* out, float* part, const float* addend, int B, int K, int N,
+                int C, hipStream_t s) {
+  const int ks = part != nullptr ? row_splits<G, DIR>(B, K, N) : 1;
+  if (row_tm<G, DIR>(B, N) == 32) return run_row<G, DIR, 32>(act, w, out, part, addend, B, K, N, C, ks, s);
+  return run_row<G, DIR, 16>(act, w, out, part, addend, B, K, N, C, ks, s);
+}
+
+template <class G>
+int wg_splits(int B, int C, int Co) {
+  const int base = (C / 32) * (Co / 16);
+  int z = 1;
+  while (base * z < kSmFill && B / (z * 2) >= 32 && z < 16) z *= 2;
+  return z;
+}
+
+template <class G>
+void run_wgrad(const float* x, const float* dy, float* out, int B, int C, int Co, int splits, hipStream_t s) {
+  using R = WgCfg<G, 16, 32, 1>;
+  auto k = sm_wgrad_kernel<G, 16, 32, 1>;
+  static bool attr = false;
+  if (!attr) {
+    set_lds_once(k, R::LDS_BYTES);
+    attr = true;
+  }
+  SmWgArgs a{};
+  a.x = x;
+  a.dy = dy;
+  a.out = out;
+  a.B = B;
+  a.C = C;
+  a.Co = Co;
+  a.ips = (B + splits - 1) / splits;
+  a.slab = (int64_t)Co * C * G::T;
+  hipLaunchKernelGGL(k, dim3(C / 32, Co / 16, splits), dim3(256), R::LDS_BYTES, s, a);
+}
+
+// geometry id of a conv (-1: not a small-map geometry this file covers)
+int sm_geo(const ConvGeom& g) {
+  auto is = [&](int h, int w, int kh, int kw, int st, int pd) {
+    return g.H == h && g.W == w && g.KH == kh && g.KW == kw && g.stride == st && g.pad == pd;
+  };
+  if (is(2, 2, 3, 3, 1, 1)) return 0;
+  if (is(4, 4, 3, 3, 2, 1)) return 1;
+  if (is(4, 4, 1, 1, 2, 0)) return 2;
+  if (is(2, 2, 3, 3, 2, 1)) return 3;
+  if (is(1, 1, 3, 3, 1, 1)) return 4;
+  if (is(2, 2, 1, 1, 2, 0)) return 5;
+  if (is(2, 2, 1, 1, 1, 0)) return 6;
+  if (is(1, 1, 1, 1, 1, 0)) return 7;
+  return -1;
+}
+
+#define NDP_SM_SWITCH(ID, ...)                     \
+  switch (ID) {                                    \
+    case 0: { using G = G_3x3_2; __VA_ARGS__; }    \
+    case 1: { using G = G_3x3_4s2; __VA_ARGS__; }  \
+    case 2: { using G = G_1x1_4s2; __VA_ARGS__; }  \
+    case 3: { using G = G_3x3_2s2; __VA_ARGS__; }  \
+    case 4: { using G = G_3x3_1; __VA_ARGS__; }    \
+    case 5: { using G = G_1x1_2s2; __VA_ARGS__; }  \
+    case 6: { using G = G_1x1_2; __VA_ARGS__; }    \
+    case 7: { using G = G_1x1_1; __VA_ARGS__; }    \
+    default: break;                                \
+  }
+
+}  // namespace
+
+int sm_class(const ConvGeom& g) {
+  const int id = sm_geo(g);
+  if (id < 0) return -1;
+  // channel tiles of 16 (row kernels, chunks) and 32 (grad-W in-channel tile)
+  if (g.C % 32 || g.Co % 32) return -1;
+  return id;
+}
+
+int sm_splits(const ConvGeom& g, int B, int dir) {
+  const int id = sm_class(g);
+  if (id < 0) return 1;
+  NDP_SM_SWITCH(id, {
+    if (dir == 0) return row_splits<G, 0>(B, g.C, g.Co);
+    if (dir == 1) return row_splits<G, 1>(B, g.Co, g.C);
+    return wg_splits<G>(B, g.C, g.Co);
+  })
+  return 1;
+}
+
+int launch_sm_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s,
+                  bool defer) {
+  const int id = sm_class(g);
+  int ks = 1;
+  NDP_SM_SWITCH(id, { ks = run_row_any<G, 0>(x, w, y, part, nullptr, B, g.C, g.Co, g.C, s); break; })
+  if (ks <= 1) return 1;
+  if (defer) return ks;  // the consuming fused BN kernel sums the slabs
+  launch_slab_sum(part, y, (int64_t)B * g.Co * g.OH * g.OW, ks, s);
+  return 1;
+}
+
+int launch_sm_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, float* part, hipStream_t s,
+                    const float* addend, bool defer) {
+  const int id = sm_class(g);
+  int ks = 1;
+  NDP_SM_SWITCH(id, { ks = run_row_any<G, 1>(dy, w, dx, part, addend, B, g.Co, g.C, g.C, s); break; })
+  if (ks <= 1) return 1;
+  if (defer && addend == nullptr) return ks;
+  launch_slab_sum(part, dx, (int64_t)B * g.C * g.H * g.W, ks, s, addend);
+  return 1;
+}
+
+int launch_sm_wgrad(const float* x, const float* dy, float* out, int B, const ConvGeom& g, hipStream_t s) {
+  const int id = sm_class(g);
+  int z = 1;
+  NDP_SM_SWITCH(id, {
+    z = wg_splits<G>(B, g.C, g.Co);
+    run_wgrad<G>(x, dy, out, B, g.C, g.Co, z, s);
+    break;
+  })
+  return z;
+}
+
+#undef NDP_SM_SWITCH
+
+}  // namespace ndp

@@ -18,11 +18,14 @@ the input is subsampled first.
 input geometry, the fastest native path:
   1. a direct fp32-MFMA kernel (csrc/conv.hip via ops/conv.py) for the ResNet CIFAR shapes
      it covers (stem 7x7/2 on 32x32, 3x3 on 8x8 and 4x4, 3x3/2 8x8->4x4);
-  2. the strided / tabled MFMA GEMM kernel (csrc/tgemm.hip via ops/tgconv.py): 1x1 stride-1
-     convs on any power-of-two map, and the small-map Toeplitz product (input H*W <= 16,
-     output OH*OW <= 4) with the weight gathered in-kernel (no W_big);
-  3. the hipBLASLt Toeplitz GEMM form (``NDP_TG=0``), and the CPU path;
-  4. MIOpen otherwise.
+  2. the small-map kernels (csrc/smallconv.hip via ops/smconv.py) for the layer3 / layer4
+     geometries (3x3 on 2x2 / 1x1, the stride-2 entry convs and 1x1 downsamples, 1x1 on
+     2x2 / 1x1): compile-time (input pixel, output pixel, tap) pair lists on 16x16x4 MFMA,
+     grad-W written in W's own layout;
+  3. the strided / tabled MFMA GEMM kernel (csrc/tgemm.hip via ops/tgconv.py): 1x1 stride-1
+     convs on any power-of-two map (and, opt-in, the tabled small-map Toeplitz product);
+  4. the hipBLASLt Toeplitz GEMM form (``NDP_SM=0 NDP_TG=0``), and the CPU path;
+  5. MIOpen otherwise.
 """
 from __future__ import annotations
 
@@ -38,6 +41,7 @@ from ..ops import conv as _conv
 from ..ops.conv import DirectConvFn, direct_plan, side_stream
 from ..ops.gradarena import grad_buffer
 from ..ops.gradlink import InjectGrad
+from ..ops.smconv import SmConvFn, sm_plan
 from ..ops.tgconv import TgConvFn, tg_plan
 
 __all__ = ["GemmConv2d", "ToeplitzBank", "toeplitz_maps", "eligible"]
@@ -242,6 +246,9 @@ class GemmConv2d(nn.Conv2d):
             plan = direct_plan(x, self.weight, s, p)
             if plan is not None:
                 return DirectConvFn.apply(x, self.weight, plan, link, slab_out, grad_slab)
+            splan = sm_plan(x, self.weight, s, p)
+            if splan is not None:  # 2x2 / 1x1 maps: compile-time pair-list MFMA kernels (csrc/smallconv.hip)
+                return SmConvFn.apply(x, self.weight, splan, link, branch, slab_out, grad_slab)
             tplan = tg_plan(x, self.weight, s, p)
             if tplan is not None:  # pointwise 1x1 / small-map tabled GEMM (csrc/tgemm.hip)
                 return TgConvFn.apply(x, self.weight, tplan, link, branch, slab_out, grad_slab)
