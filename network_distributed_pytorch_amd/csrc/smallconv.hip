@@ -118,6 +118,112 @@ __device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, uint32_t off) 
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
 }
 
+// ---- fused BatchNorm: coefficient finalization (ndp_kernels.h SmBnF / SmBnB) ---------------
+// Forward: mean / invstd from the per-row-tile partial sums (fp64, fixed row order: every
+// consumer computes bitwise the same value) or the saved statistics; scale = gamma * invstd,
+// shift = beta - mean * scale — the same fp32 formulas as csrc/batchnorm.hip, so a mask or an
+// activation recomputed in backward from the saved statistics is bitwise the forward's.
+__device__ __forceinline__ void bn_fwd_coef(const SmBnF& f, int k, int C, bool writer, float& s, float& h,
+                                            float& mean, float& invstd) {
+  if (f.part != nullptr) {
+    double sum = 0.0, sq = 0.0;
+    for (int r = 0; r < f.R; ++r) {
+      sum += f.part[((int64_t)r * C + k) * 2];
+      sq += f.part[((int64_t)r * C + k) * 2 + 1];
+    }
+    const double M = f.count;
+    const double mu = sum / M;
+    double var = sq / M - mu * mu;
+    if (var < 0.0) var = 0.0;
+    mean = (float)mu;
+    invstd = (float)(1.0 / sqrt(var + (double)f.eps));
+    if (writer) {
+      f.save_mean[k] = mean;
+      f.save_invstd[k] = invstd;
+      if (f.rmean != nullptr) {
+        const double unb = M > 1.0 ? var * M / (M - 1.0) : var;
+        f.rmean[k] = (float)((1.0 - f.momentum) * (double)f.rmean[k] + f.momentum * mu);
+        f.rvar[k] = (float)((1.0 - f.momentum) * (double)f.rvar[k] + f.momentum * unb);
+      }
+      if (f.nbt != nullptr && k == 0) f.nbt[0] += 1;
+    }
+  } else {
+    mean = f.save_mean[k];
+    invstd = f.save_invstd[k];
+  }
+  s = (f.gamma ? f.gamma[k] : 1.f) * invstd;
+  h = (f.beta ? f.beta[k] : 0.f) - mean * s;
+}
+
+// Backward: k1 = gamma * invstd, mean dz, mean dz * xhat (dx = k1 (dz - mdz - xhat mdzx))
+__device__ __forceinline__ void bn_bwd_coef(const SmBnB& b, int k, int C, bool writer, float& k1, float& mdz,
+                                            float& mdzx) {
+  double sdz = 0.0, sdzx = 0.0;
+  for (int r = 0; r < b.R; ++r) {
+    sdz += b.part[((int64_t)r * C + k) * 4];
+    sdzx += b.part[((int64_t)r * C + k) * 4 + b.j];
+  }
+  if (writer) {
+    if (b.dgamma) b.dgamma[k] = (float)sdzx;
+    if (b.dbeta) b.dbeta[k] = (float)sdz;
+  }
+  k1 = (b.gamma ? b.gamma[k] : 1.f) * b.invstd[k];
+  mdz = (float)(sdz / b.count);
+  mdzx = (float)(sdzx / b.count);
+}
+
+// coefficient table rows per operand transform (LDS, [row][channel])
+__host__ __device__ constexpr int coef_rows(int amode, int amask) {
+  return amode == 0 ? 0 : amode <= 2 ? 2 : amode == 3 ? 4 : (amask == 2 ? 7 : 5);
+}
+
+// fill coef[row * nch + i] for channels k0 + i, i < nch (the operand's transform)
+__device__ __forceinline__ void fill_coefs(const SmOps& o, float* coef, int k0, int nch, int C, bool writer) {
+  for (int i = threadIdx.x; i < nch; i += blockDim.x) {
+    const int k = k0 + i;
+    float s, h, mean, invstd;
+    if (o.amode >= 1 && o.amode <= 3) {
+      bn_fwd_coef(o.af, k, C, writer, s, h, mean, invstd);
+      coef[i] = s;
+      coef[nch + i] = h;
+      if (o.amode == 3) {
+        bn_fwd_coef(o.afd, k, C, writer, s, h, mean, invstd);
+        coef[2 * nch + i] = s;
+        coef[3 * nch + i] = h;
+      }
+    } else if (o.amode == 4) {
+      float k1, mdz, mdzx;
+      bn_bwd_coef(o.ab, k, C, writer, k1, mdz, mdzx);
+      coef[i] = k1;
+      coef[nch + i] = mdz;
+      coef[2 * nch + i] = mdzx;
+      coef[3 * nch + i] = o.ab.mean[k];
+      coef[4 * nch + i] = o.ab.invstd[k];
+      if (o.amask == 2) {
+        bn_fwd_coef(o.af, k, C, false, s, h, mean, invstd);
+        coef[5 * nch + i] = s;
+        coef[6 * nch + i] = h;
+      }
+    }
+  }
+}
+
+// one operand element through the transform: x (the raw operand), e1 / e2 (the extra tensors:
+// amode 2-3 e1 = residual; amode 4 e1 = BN input c, e2 = mask tensor), channel i of the table
+__device__ __forceinline__ float xform(const SmOps& o, const float* coef, int nch, int i, float x, float e1,
+                                       float e2) {
+  if (o.amode == 1) return fmaxf(fmaf(x, coef[i], coef[nch + i]), 0.f);
+  if (o.amode == 2) return fmaxf(fmaf(x, coef[i], coef[nch + i]) + e1, 0.f);
+  if (o.amode == 3) return fmaxf(fmaf(x, coef[i], coef[nch + i]) + fmaf(e1, coef[2 * nch + i], coef[3 * nch + i]), 0.f);
+  // amode 4
+  bool m = true;
+  if (o.amask == 1) m = e2 > 0.f;
+  else if (o.amask == 2) m = fmaf(e1, coef[5 * nch + i], coef[6 * nch + i]) > 0.f;
+  const float dz = m ? x : 0.f;
+  const float xh = (e1 - coef[3 * nch + i]) * coef[4 * nch + i];
+  return coef[i] * (dz - coef[nch + i] - xh * coef[2 * nch + i]);
+}
+
 // ---- row kernel: forward (DIR 0) / grad-x (DIR 1) ------------------------------------------
 // operand "act": [B][K][PP] (X for the forward, dY for grad-x), K = reduction channels;
 // W [Co][C][T]: forward n = co, k = ci; grad-x n = ci, k = co.  out [B][N][PQ].
@@ -143,8 +249,12 @@ struct RowCfg {
   static constexpr int STAGE = (A_SZ + W_SZ + 3) / 4 * 4;
   static constexpr int NACC = MB * NB * PQ;  // f32x4 accumulators per wave
   static constexpr int RED = 4 * NACC * 4 * 64;
-  static constexpr int LDS_FLOATS = (2 * STAGE > RED ? 2 * STAGE : RED);
-  static constexpr size_t LDS_BYTES = (size_t)LDS_FLOATS * 4;
+  static constexpr int BASE = ((2 * STAGE > RED ? 2 * STAGE : RED) + 3) / 4 * 4;  // floats
+  static constexpr int ESTAT = 16 * TN * 4;  // doubles: (wave, l4) x column x 4 sums
+  // dynamic LDS: BASE floats | coefficient table (runtime rows x K) | ESTAT doubles
+  static size_t lds_bytes(int ncoef_floats) {
+    return (size_t)(BASE + (ncoef_floats + 3) / 4 * 4) * 4 + (size_t)ESTAT * 8;
+  }
   // global loads per chunk: act = TM rows of TK*PP contiguous floats (16-B vectors)
   static constexpr int AV = TM * TK * PP / 4, A_PER = (AV + 255) / 256;
   // weights: whole rows (every tap used) as 16-B vectors, else one float per used tap
@@ -163,9 +273,9 @@ struct SmRowArgs {
   const float* w;       // [Co][C][KH][KW]
   float* out;           // [B][N][PQ]
   float* part;          // split-K slabs [z][B][N][PQ] (gridDim.z > 1)
-  const float* addend;  // nullable, no split: out = result + addend (may alias out)
   int B, K, N, C, cps;  // cps: reduction channels per split
   int64_t slab;
+  SmOps ops;            // fused BN operand transform / epilogue (all modes 0: plain)
 };
 
 template <class G, int DIR, int TM, int TN, int S>
@@ -173,16 +283,29 @@ __global__ __launch_bounds__(256) void sm_row_kernel(SmRowArgs a) {
   using R = RowCfg<G, DIR, TM, TN, S>;
   constexpr int PP = R::PP, PQ = R::PQ, TK = R::TK, U = R::U, MB = R::MB, NB = R::NB;
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  const SmOps& ops = a.ops;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l16 = lane & 15, l4 = lane >> 4;
   const int n0 = blockIdx.x * TN, b0 = blockIdx.y * TM;
   const int kbeg = blockIdx.z * a.cps;
   const int nchunks = (min(a.K, kbeg + a.cps) - kbeg) / TK;
+  const int amode = ops.amode;
+  const bool origin = blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0;
+
+  // operand transform coefficients for every reduction channel (finalized here)
+  float* coef = smem + R::BASE;
+  if (amode != 0) {
+    fill_coefs(ops, coef, 0, a.K, a.K, origin);
+    __syncthreads();
+  }
 
   const __amdgpu_buffer_rsrc_t ra = rsrc(a.act), rw = rsrc(a.w);
+  const __amdgpu_buffer_rsrc_t re1 = rsrc(amode == 4 ? ops.c : ops.res), re2 = rsrc(ops.mtensor);
+  const bool ld1 = amode >= 2, ld2 = amode == 4 && ops.amask == 1;
+  const bool wmat = ops.mat != nullptr && amode >= 1 && amode <= 3 && blockIdx.x == 0 && gridDim.z == 1;
   // fixed per-thread load coordinates (only a uniform chunk offset moves)
   uint32_t aoff[R::A_PER];
-  int adst[R::A_PER];
+  int adst[R::A_PER], ach[R::A_PER];
 #pragma unroll
   for (int v = 0; v < R::A_PER; ++v) {
     const int e = tid + 256 * v;  // vector index in [TM][TK*PP / 4]
@@ -190,6 +313,7 @@ __global__ __launch_bounds__(256) void sm_row_kernel(SmRowArgs a) {
     const int b = b0 + row;
     aoff[v] = (e < R::AV && b < a.B) ? (uint32_t)((((int64_t)b * a.K + kbeg) * PP + j) * 4) : kOOB;
     adst[v] = e < R::AV ? row * R::RS + (j / PP) * R::KS + (j % PP) : -1;
+    ach[v] = j / PP;  // channel in the chunk (PP == 1: the first of 4)
   }
   uint32_t woff[R::W_PER];
   int wdst[R::W_PER];
@@ -197,18 +321,16 @@ __global__ __launch_bounds__(256) void sm_row_kernel(SmRowArgs a) {
   for (int v = 0; v < R::W_PER; ++v) {
     const int e = tid + 256 * v;
     const bool ok = e < R::WV;
-    int row, ch, tsrc, dcol;  // tile row, channel along the row, source tap / float, dest column
+    int row, tsrc, dcol;  // tile row, source float along the W row, destination column
     if constexpr (G::ALL) {
       row = e / (R::WCH * G::T / 4);
       const int j = 4 * (e - row * (R::WCH * G::T / 4));  // float in the row (contiguous in LDS too)
-      ch = 0;
       tsrc = j;
       dcol = j;
     } else {
       row = e / (R::WCH * U);
       const int r2 = e - row * (R::WCH * U);
-      ch = r2 / U;
-      const int s = r2 - ch * U;
+      const int ch = r2 / U, s = r2 - ch * U;
       tsrc = ch * G::T + G::utap(s);
       dcol = ch * R::KSW + s;
     }
@@ -224,11 +346,16 @@ __global__ __launch_bounds__(256) void sm_row_kernel(SmRowArgs a) {
   const uint32_t wstep = DIR == 0 ? TK * G::T * 4 : (uint32_t)(TK * a.C * G::T * 4);
 
   typedef typename std::conditional<G::ALL, f32x4s, float>::type WVec;
-  f32x4s rA[R::A_PER];
+  f32x4s rA[R::A_PER], rE1[R::A_PER], rE2[R::A_PER];
   WVec rW[R::W_PER];
   auto load = [&](int c) {
 #pragma unroll
-    for (int v = 0; v < R::A_PER; ++v) rA[v] = bload4(ra, aoff[v] == kOOB ? kOOB : aoff[v] + c * astep);
+    for (int v = 0; v < R::A_PER; ++v) {
+      const uint32_t o = aoff[v] == kOOB ? kOOB : aoff[v] + c * astep;
+      rA[v] = bload4(ra, o);
+      if (ld1) rE1[v] = bload4(re1, o);
+      if (ld2) rE2[v] = bload4(re2, o);
+    }
 #pragma unroll
     for (int v = 0; v < R::W_PER; ++v) {
       const uint32_t o = woff[v] == kOOB ? kOOB : woff[v] + c * wstep;
@@ -236,14 +363,22 @@ __global__ __launch_bounds__(256) void sm_row_kernel(SmRowArgs a) {
       else rW[v] = bload1(rw, o);
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, int c) {
     float* As = smem + buf * R::STAGE;
     float* Ws = As + R::A_SZ;
 #pragma unroll
     for (int v = 0; v < R::A_PER; ++v) {
       if (adst[v] < 0) continue;
+      f32x4s x = rA[v];
+      if (amode != 0) {
+        const int k = kbeg + c * TK + ach[v];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) As[adst[v] + (PP >= 4 ? q : q * R::KS)] = rA[v][q];
+        for (int q = 0; q < 4; ++q) x[q] = xform(ops, coef, a.K, k + (PP >= 4 ? 0 : q), x[q], rE1[v][q], rE2[v][q]);
+        if (wmat && aoff[v] != kOOB)
+          *reinterpret_cast<f32x4s*>(reinterpret_cast<char*>(ops.mat) + aoff[v] + c * astep) = x;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) As[adst[v] + (PP >= 4 ? q : q * R::KS)] = x[q];
     }
 #pragma unroll
     for (int v = 0; v < R::W_PER; ++v) {
@@ -267,7 +402,7 @@ __global__ __launch_bounds__(256) void sm_row_kernel(SmRowArgs a) {
 
   if (nchunks > 0) {
     load(0);
-    store(0);
+    store(0, 0);
     __syncthreads();
   }
   for (int c = 0; c < nchunks; ++c) {
@@ -300,7 +435,7 @@ __global__ __launch_bounds__(256) void sm_row_kernel(SmRowArgs a) {
         }
       });
     }
-    if (c + 1 < nchunks) store(cur ^ 1);  // the other buffer was released by the last barrier
+    if (c + 1 < nchunks) store(cur ^ 1, c + 1);  // the other buffer was released by the last barrier
     __syncthreads();
   }
 
@@ -319,6 +454,21 @@ __global__ __launch_bounds__(256) void sm_row_kernel(SmRowArgs a) {
   __syncthreads();
   const bool split = gridDim.z > 1;
   float* dst = split ? a.part + (int64_t)blockIdx.z * a.slab : a.out;
+  const int emode = split ? 0 : ops.emode;
+  double es[NB][3];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) es[j][0] = es[j][1] = es[j][2] = 0.0;
+  // epilogue BN statistics of the previous layer (emode 2): its saved forward coefficients
+  float em[NB], ei[NB], emd[NB], eid[NB], esc[NB], esh[NB];
+  if (emode == 2) {
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int n = n0 + j * 16 + l16;
+      float t0, t1;
+      bn_fwd_coef(ops.ef, n, a.N, false, esc[j], esh[j], em[j], ei[j]);
+      if (ops.eds) bn_fwd_coef(ops.efd, n, a.N, false, t0, t1, emd[j], eid[j]);
+    }
+  }
 #pragma unroll
   for (int i = 0; i < MB; ++i) {
     const int b = b0 + i * 16 + 4 * l4 + wave;
@@ -335,9 +485,12 @@ __global__ __launch_bounds__(256) void sm_row_kernel(SmRowArgs a) {
         v[q] = t;
       }
       const int64_t o = ((int64_t)b * a.N + n) * PQ;
-      if (!split && a.addend != nullptr) {
+      if (!split && ops.eadd != 0) {
 #pragma unroll
-        for (int q = 0; q < PQ; ++q) v[q] += a.addend[o + q];
+        for (int q = 0; q < PQ; ++q) {
+          const float ad = ops.addend[o + q];
+          v[q] += (ops.eadd == 2) ? ((ops.addmask[o + q] > 0.f) ? ad : 0.f) : ad;
+        }
       }
       if constexpr (PQ % 4 == 0) {
 #pragma unroll
@@ -347,13 +500,59 @@ __global__ __launch_bounds__(256) void sm_row_kernel(SmRowArgs a) {
 #pragma unroll
         for (int q = 0; q < PQ; ++q) dst[o + q] = v[q];
       }
+      if (emode == 1) {
+#pragma unroll
+        for (int q = 0; q < PQ; ++q) {
+          es[j][0] += (double)v[q];
+          es[j][1] += (double)v[q] * (double)v[q];
+        }
+      } else if (emode == 2) {
+#pragma unroll
+        for (int q = 0; q < PQ; ++q) {
+          const float cv = ops.ec[o + q];
+          bool m = true;
+          if (ops.emask == 1) m = ops.emtensor[o + q] > 0.f;
+          else if (ops.emask == 2) m = fmaf(cv, esc[j], esh[j]) > 0.f;
+          const float dz = m ? v[q] : 0.f;
+          es[j][0] += (double)dz;
+          es[j][1] += (double)dz * (double)((cv - em[j]) * ei[j]);
+          if (ops.eds) es[j][2] += (double)dz * (double)((ops.ecd[o + q] - emd[j]) * eid[j]);
+        }
+      }
+    }
+  }
+  if (emode != 0) {
+    // column sums over this tile's rows: (wave, l4) partials through LDS, fixed order
+    double* est = reinterpret_cast<double*>(smem + R::BASE + (coef_rows(amode, ops.amask) * a.K + 3) / 4 * 4);
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int e = 0; e < 3; ++e) est[((wave * 4 + l4) * TN + j * 16 + l16) * 4 + e] = es[j][e];
+    __syncthreads();
+    if (tid < TN) {
+      double t[3] = {0.0, 0.0, 0.0};
+      for (int g = 0; g < 16; ++g)
+#pragma unroll
+        for (int e = 0; e < 3; ++e) t[e] += est[(g * TN + tid) * 4 + e];
+      const int n = n0 + tid;
+      if (emode == 1) {
+        ops.epart[((int64_t)blockIdx.y * a.N + n) * 2] = t[0];
+        ops.epart[((int64_t)blockIdx.y * a.N + n) * 2 + 1] = t[1];
+      } else {
+        double* pp = ops.epart + ((int64_t)blockIdx.y * a.N + n) * 4;
+        pp[0] = t[0];
+        pp[1] = t[1];
+        pp[2] = t[2];
+        pp[3] = 0.0;
+      }
     }
   }
 }
 
 // ---- grad-W kernel ---------------------------------------------------------------------------
 // dW[co][ci][t] (+ slab z) = sum over this split's images b and the pairs (p, q) with tap t of
-// dY[b][co][q] X[b][ci][p].  MFMA: M = co (16 lanes), N = ci (16 lanes), K = 4 images.
+// G[b][co][q] A[b][ci][p], G = dY (or its BN-backward transform), A = X (or relu(bn(X))).
+// MFMA: M = co (16 lanes), N = ci (16 lanes), K = 4 images.
 template <class G, int TMC, int TNC, int S>
 struct WgCfg {
   static constexpr int PI = G::PI, PO = G::PO, U = G::NU;
@@ -366,8 +565,9 @@ struct WgCfg {
   static constexpr int STAGE = (G_SZ + X_SZ + 3) / 4 * 4;
   static constexpr int NACC = MB * NB * U;
   static constexpr int RED = 4 * NACC * 4 * 64;
-  static constexpr int LDS_FLOATS = (2 * STAGE > RED ? 2 * STAGE : RED);
-  static constexpr size_t LDS_BYTES = (size_t)LDS_FLOATS * 4;
+  static constexpr int BASE = ((2 * STAGE > RED ? 2 * STAGE : RED) + 3) / 4 * 4;
+  static constexpr int COEF = 7 * TMC + 2 * TNC;  // dY transform rows x TMC | X transform rows x TNC
+  static constexpr size_t LDS_BYTES = (size_t)(BASE + COEF) * 4;
   static constexpr int GV = TB * TMC * PO / 4, G_PER = (GV + 255) / 256;
   static constexpr int XV = TB * TNC * PI / 4, X_PER = (XV + 255) / 256;
   static_assert((TMC * PO) % 4 == 0 && (TNC * PI) % 4 == 0, "16-B rows");
@@ -381,6 +581,8 @@ struct SmWgArgs {
   float* out;       // dW [Co][C][T] (or slab base when gridDim.z > 1)
   int B, C, Co, ips;  // ips: images per split
   int64_t slab;
+  SmOps xops;       // X transform (amode 0 / 1; saved statistics)
+  SmOps gops;       // dY transform (amode 0 / 4)
 };
 
 template <class G, int TMC, int TNC, int S>
@@ -394,10 +596,23 @@ __global__ __launch_bounds__(256) void sm_wgrad_kernel(SmWgArgs a) {
   const int bbeg = blockIdx.z * a.ips;
   const int bend = min(a.B, bbeg + a.ips);
   const int nchunks = (bend - bbeg + TB - 1) / TB;
+  const int gm = a.gops.amode, xm = a.xops.amode;
+
+  // transform coefficients of this tile's channels (never the writer: statistics, dgamma /
+  // dbeta belong to the forward consumer / the grad-x kernel)
+  float* gcoef = smem + R::BASE;
+  float* xcoef = gcoef + 7 * TMC;
+  if (gm != 0 || xm != 0) {
+    if (gm != 0) fill_coefs(a.gops, gcoef, co0, TMC, a.Co, false);
+    if (xm != 0) fill_coefs(a.xops, xcoef, ci0, TNC, a.C, false);
+    __syncthreads();
+  }
 
   const __amdgpu_buffer_rsrc_t rg = rsrc(a.dy), rx = rsrc(a.x);
+  const __amdgpu_buffer_rsrc_t rc = rsrc(a.gops.c), rm = rsrc(a.gops.mtensor);
+  const bool ldc = gm == 4, ldm = gm == 4 && a.gops.amask == 1;
   uint32_t goff[R::G_PER], xoff[R::X_PER];
-  int gdst[R::G_PER], xdst[R::X_PER], gimg[R::G_PER], ximg[R::X_PER];
+  int gdst[R::G_PER], xdst[R::X_PER], gimg[R::G_PER], ximg[R::X_PER], gch[R::G_PER], xch[R::X_PER];
 #pragma unroll
   for (int v = 0; v < R::G_PER; ++v) {
     const int e = tid + 256 * v;
@@ -406,6 +621,7 @@ __global__ __launch_bounds__(256) void sm_wgrad_kernel(SmWgArgs a) {
     gimg[v] = ok ? bi : (1 << 20);
     goff[v] = ok ? (uint32_t)((((int64_t)(bbeg + bi) * a.Co + co0) * PO + j) * 4) : kOOB;
     gdst[v] = ok ? bi * R::RSG + (j / PO) * R::KSG + (j % PO) : -1;
+    gch[v] = j / PO;
   }
 #pragma unroll
   for (int v = 0; v < R::X_PER; ++v) {
@@ -415,33 +631,49 @@ __global__ __launch_bounds__(256) void sm_wgrad_kernel(SmWgArgs a) {
     ximg[v] = ok ? bi : (1 << 20);
     xoff[v] = ok ? (uint32_t)((((int64_t)(bbeg + bi) * a.C + ci0) * PI + j) * 4) : kOOB;
     xdst[v] = ok ? bi * R::RSX + (j / PI) * R::KSX + (j % PI) : -1;
+    xch[v] = j / PI;
   }
   const uint32_t gstep = (uint32_t)((int64_t)TB * a.Co * PO * 4), xstep = (uint32_t)((int64_t)TB * a.C * PI * 4);
 
-  f32x4s rG[R::G_PER], rX[R::X_PER];
+  f32x4s rG[R::G_PER], rC[R::G_PER], rM[R::G_PER], rX[R::X_PER];
   auto load = [&](int c) {
     const int left = bend - bbeg - c * TB;  // images of this chunk inside the split
 #pragma unroll
-    for (int v = 0; v < R::G_PER; ++v)
-      rG[v] = bload4(rg, (goff[v] == kOOB || gimg[v] >= left) ? kOOB : goff[v] + c * gstep);
+    for (int v = 0; v < R::G_PER; ++v) {
+      const uint32_t o = (goff[v] == kOOB || gimg[v] >= left) ? kOOB : goff[v] + c * gstep;
+      rG[v] = bload4(rg, o);
+      if (ldc) rC[v] = bload4(rc, o);
+      if (ldm) rM[v] = bload4(rm, o);
+    }
 #pragma unroll
     for (int v = 0; v < R::X_PER; ++v)
       rX[v] = bload4(rx, (xoff[v] == kOOB || ximg[v] >= left) ? kOOB : xoff[v] + c * xstep);
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, int c) {
     float* Gs = smem + buf * R::STAGE;
     float* Xs = Gs + R::G_SZ;
+    const int left = bend - bbeg - c * TB;
 #pragma unroll
     for (int v = 0; v < R::G_PER; ++v) {
       if (gdst[v] < 0) continue;
+      f32x4s g = rG[v];
+      if (gm != 0 && gimg[v] < left) {  // images past the split stay exact zeros
 #pragma unroll
-      for (int q = 0; q < 4; ++q) Gs[gdst[v] + (PO >= 4 ? q : q * R::KSG)] = rG[v][q];
+        for (int q = 0; q < 4; ++q) g[q] = xform(a.gops, gcoef, TMC, gch[v] + (PO >= 4 ? 0 : q), g[q], rC[v][q], rM[v][q]);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Gs[gdst[v] + (PO >= 4 ? q : q * R::KSG)] = g[q];
     }
 #pragma unroll
     for (int v = 0; v < R::X_PER; ++v) {
       if (xdst[v] < 0) continue;
+      f32x4s x = rX[v];
+      if (xm != 0 && ximg[v] < left) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) Xs[xdst[v] + (PI >= 4 ? q : q * R::KSX)] = rX[v][q];
+        for (int q = 0; q < 4; ++q) x[q] = xform(a.xops, xcoef, TNC, xch[v] + (PI >= 4 ? 0 : q), x[q], 0.f, 0.f);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Xs[xdst[v] + (PI >= 4 ? q : q * R::KSX)] = x[q];
     }
   };
 
@@ -455,7 +687,7 @@ __global__ __launch_bounds__(256) void sm_wgrad_kernel(SmWgArgs a) {
 
   if (nchunks > 0) {
     load(0);
-    store(0);
+    store(0, 0);
     __syncthreads();
   }
   for (int c = 0; c < nchunks; ++c) {
@@ -486,7 +718,7 @@ __global__ __launch_bounds__(256) void sm_wgrad_kernel(SmWgArgs a) {
         }
       });
     }
-    if (c + 1 < nchunks) store(cur ^ 1);
+    if (c + 1 < nchunks) store(cur ^ 1, c + 1);
     __syncthreads();
   }
 
@@ -525,18 +757,83 @@ __global__ __launch_bounds__(256) void sm_wgrad_kernel(SmWgArgs a) {
   }
 }
 
+// ---- stage-end BN apply / BN-backward statistics ------------------------------------------------
+// [B][C][P] tensors; workgroup = 16 channels x 64 images
+constexpr int kBnRows = 64;
+
+__global__ __launch_bounds__(256) void sm_bn_apply_kernel(const float* __restrict__ x, float* __restrict__ y, int B,
+                                                          int C, int P, SmOps ops) {
+  __shared__ float coef[4 * 16];
+  const int c0 = blockIdx.x * 16, b0 = blockIdx.y * kBnRows;
+  fill_coefs(ops, coef, c0, 16, C, blockIdx.y == 0);  // row block 0 writes the statistics
+  __syncthreads();
+  const int per = 16 * P;  // floats of one image in this channel block (contiguous)
+  for (int e = threadIdx.x; e < kBnRows * per; e += 256) {
+    const int r = e / per, f = e - r * per;
+    const int b = b0 + r;
+    if (b >= B) break;
+    const int i = f / P;
+    const int64_t o = ((int64_t)b * C + c0) * P + f;
+    const float e1 = ops.res != nullptr ? ops.res[o] : 0.f;
+    y[o] = xform(ops, coef, 16, i, x[o], e1, 0.f);
+  }
+}
+
+__global__ __launch_bounds__(256) void sm_bn_bstats_kernel(const float* __restrict__ dy, int B, int C, int P,
+                                                           SmOps ops) {
+  __shared__ double red[256][3];
+  const int c0 = blockIdx.x * 16, b0 = blockIdx.y * kBnRows;
+  // thread = (channel i = tid & 15, row group g = tid >> 4): rows b0 + g, b0 + g + 16, ...
+  const int i = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int c = c0 + i;
+  float sc, sh, m, is, md = 0.f, idd = 0.f, t0, t1;
+  bn_fwd_coef(ops.ef, c, C, false, sc, sh, m, is);
+  if (ops.eds) bn_fwd_coef(ops.efd, c, C, false, t0, t1, md, idd);
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+  for (int r = g; r < kBnRows; r += 16) {
+    const int b = b0 + r;
+    if (b >= B) break;
+    for (int p = 0; p < P; ++p) {
+      const int64_t o = ((int64_t)b * C + c) * P + p;
+      const float cv = ops.ec[o];
+      bool mk = true;
+      if (ops.emask == 1) mk = ops.emtensor[o] > 0.f;
+      else if (ops.emask == 2) mk = fmaf(cv, sc, sh) > 0.f;
+      const float dz = mk ? dy[o] : 0.f;
+      s0 += (double)dz;
+      s1 += (double)dz * (double)((cv - m) * is);
+      if (ops.eds) s2 += (double)dz * (double)((ops.ecd[o] - md) * idd);
+    }
+  }
+  red[threadIdx.x][0] = s0;
+  red[threadIdx.x][1] = s1;
+  red[threadIdx.x][2] = s2;
+  __syncthreads();
+  if (threadIdx.x < 16) {
+    double t[3] = {0.0, 0.0, 0.0};
+    for (int gg = 0; gg < 16; ++gg)
+      for (int e = 0; e < 3; ++e) t[e] += red[gg * 16 + threadIdx.x][e];
+    double* pp = ops.epart + ((int64_t)blockIdx.y * C + c0 + threadIdx.x) * 4;
+    pp[0] = t[0];
+    pp[1] = t[1];
+    pp[2] = t[2];
+    pp[3] = 0.0;
+  }
+}
+
 // ---- dispatch ----------------------------------------------------------------------------------
 template <typename K>
 void set_lds_once(K k, size_t bytes) {
-  hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
-constexpr int kSmFill = 256;  // workgroups for one per CU
+constexpr int kSmFill = 256;    // workgroups for one per CU
 constexpr int kSmMaxSplit = 4;  // forward / grad-x slabs: the fused BN kernel sums <= 4 (kMaxFusedSlabs)
+constexpr size_t kSmMaxLds = 160 * 1024;
 
 int pow2_split(int base, int chunks, int cap) {
   int ks = 1;
-  while (ks * 2 <= cap && base * ks < kSmFill && chunks % (ks * 2) == 0 && chunks / (ks * 2) >= 1) ks *= 2;
+  while (ks * 2 <= cap && base * ks < kSmFill && chunks % (ks * 2) == 0) ks *= 2;
   return ks;
 }
 
@@ -549,13 +846,13 @@ int row_tm(int B, int N) {
 }
 
 template <class G, int DIR, int TM>
-int run_row(const float* act, const float* w, float* out, float* part, const float* addend, int B, int K, int N,
-            int C, int ks, hipStream_t s) {
+void run_row(const float* act, const float* w, float* out, float* part, int B, int K, int N, int C, int ks,
+             const SmOps& ops, hipStream_t s) {
   using R = RowCfg<G, DIR, TM, 16, 1>;
   auto k = sm_row_kernel<G, DIR, TM, 16, 1>;
   static bool attr = false;
   if (!attr) {
-    set_lds_once(k, R::LDS_BYTES);
+    set_lds_once(k, kSmMaxLds);
     attr = true;
   }
   SmRowArgs a{};
@@ -563,15 +860,15 @@ int run_row(const float* act, const float* w, float* out, float* part, const flo
   a.w = w;
   a.out = out;
   a.part = part;
-  a.addend = ks > 1 ? nullptr : addend;
   a.B = B;
   a.K = K;
   a.N = N;
   a.C = C;
   a.cps = K / ks;
   a.slab = (int64_t)B * N * (DIR == 0 ? G::PO : G::PI);
-  hipLaunchKernelGGL(k, dim3(N / 16, (B + TM - 1) / TM, ks), dim3(256), R::LDS_BYTES, s, a);
-  return ks;
+  a.ops = ops;
+  const size_t lds = R::lds_bytes(coef_rows(ops.amode, ops.amask) * K);
+  hipLaunchKernelGGL(k, dim3(N / 16, (B + TM - 1) / TM, ks), dim3(256), lds, s, a);
 }
 
 template <class G, int DIR>
@@ -581,11 +878,12 @@ int row_splits(int B, int K, int N) {
 }
 
 template <class G, int DIR>
-int run_row_any(const float* act, const float* w, float* out, float* part, const float* addend, int B, int K, int N,
-                int C, hipStream_t s) {
+int run_row_any(const float* act, const float* w, float* out, float* part, int B, int K, int N, int C,
+                const SmOps& ops, hipStream_t s) {
   const int ks = part != nullptr ? row_splits<G, DIR>(B, K, N) : 1;
-  if (row_tm<G, DIR>(B, N) == 32) return run_row<G, DIR, 32>(act, w, out, part, addend, B, K, N, C, ks, s);
-  return run_row<G, DIR, 16>(act, w, out, part, addend, B, K, N, C, ks, s);
+  if (row_tm<G, DIR>(B, N) == 32) run_row<G, DIR, 32>(act, w, out, part, B, K, N, C, ks, ops, s);
+  else run_row<G, DIR, 16>(act, w, out, part, B, K, N, C, ks, ops, s);
+  return ks;
 }
 
 template <class G>
@@ -597,7 +895,8 @@ int wg_splits(int B, int C, int Co) {
 }
 
 template <class G>
-void run_wgrad(const float* x, const float* dy, float* out, int B, int C, int Co, int splits, hipStream_t s) {
+void run_wgrad(const float* x, const float* dy, float* out, int B, int C, int Co, int splits, const SmOps& xops,
+               const SmOps& gops, hipStream_t s) {
   using R = WgCfg<G, 16, 32, 1>;
   auto k = sm_wgrad_kernel<G, 16, 32, 1>;
   static bool attr = false;
@@ -614,6 +913,8 @@ void run_wgrad(const float* x, const float* dy, float* out, int B, int C, int Co
   a.Co = Co;
   a.ips = (B + splits - 1) / splits;
   a.slab = (int64_t)Co * C * G::T;
+  a.xops = xops;
+  a.gops = gops;
   hipLaunchKernelGGL(k, dim3(C / 32, Co / 16, splits), dim3(256), R::LDS_BYTES, s, a);
 }
 
@@ -646,6 +947,8 @@ int sm_geo(const ConvGeom& g) {
     default: break;                                \
   }
 
+const SmOps kPlain{};
+
 }  // namespace
 
 int sm_class(const ConvGeom& g) {
@@ -667,11 +970,17 @@ int sm_splits(const ConvGeom& g, int B, int dir) {
   return 1;
 }
 
+int sm_rowtile(const ConvGeom& g, int B, int dir) {
+  const int id = sm_class(g);
+  NDP_SM_SWITCH(id, { return dir == 0 ? row_tm<G, 0>(B, g.Co) : row_tm<G, 1>(B, g.C); })
+  return 16;
+}
+
 int launch_sm_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s,
                   bool defer) {
   const int id = sm_class(g);
   int ks = 1;
-  NDP_SM_SWITCH(id, { ks = run_row_any<G, 0>(x, w, y, part, nullptr, B, g.C, g.Co, g.C, s); break; })
+  NDP_SM_SWITCH(id, { ks = run_row_any<G, 0>(x, w, y, part, B, g.C, g.Co, g.C, kPlain, s); break; })
   if (ks <= 1) return 1;
   if (defer) return ks;  // the consuming fused BN kernel sums the slabs
   launch_slab_sum(part, y, (int64_t)B * g.Co * g.OH * g.OW, ks, s);
@@ -682,7 +991,12 @@ int launch_sm_dgrad(const float* dy, const float* w, float* dx, int B, const Con
                     const float* addend, bool defer) {
   const int id = sm_class(g);
   int ks = 1;
-  NDP_SM_SWITCH(id, { ks = run_row_any<G, 1>(dy, w, dx, part, addend, B, g.Co, g.C, g.C, s); break; })
+  SmOps ops{};
+  if (addend != nullptr) {  // applied in the epilogue when unsplit, by the slab sum otherwise
+    ops.eadd = 1;
+    ops.addend = addend;
+  }
+  NDP_SM_SWITCH(id, { ks = run_row_any<G, 1>(dy, w, dx, part, B, g.Co, g.C, g.C, ops, s); break; })
   if (ks <= 1) return 1;
   if (defer && addend == nullptr) return ks;
   launch_slab_sum(part, dx, (int64_t)B * g.C * g.H * g.W, ks, s, addend);
@@ -690,14 +1004,43 @@ int launch_sm_dgrad(const float* dy, const float* w, float* dx, int B, const Con
 }
 
 int launch_sm_wgrad(const float* x, const float* dy, float* out, int B, const ConvGeom& g, hipStream_t s) {
+  return launch_sm_wgrad_ops(x, dy, out, B, g, kPlain, kPlain, s);
+}
+
+void launch_sm_fwd_ops(const float* x, const float* w, float* y, int B, const ConvGeom& g, const SmOps& ops,
+                       hipStream_t s) {
+  const int id = sm_class(g);
+  NDP_SM_SWITCH(id, { run_row_any<G, 0>(x, w, y, nullptr, B, g.C, g.Co, g.C, ops, s); break; })
+}
+
+void launch_sm_dgrad_ops(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, const SmOps& ops,
+                         hipStream_t s) {
+  const int id = sm_class(g);
+  NDP_SM_SWITCH(id, { run_row_any<G, 1>(dy, w, dx, nullptr, B, g.Co, g.C, g.C, ops, s); break; })
+}
+
+int launch_sm_wgrad_ops(const float* x, const float* dy, float* out, int B, const ConvGeom& g, const SmOps& xops,
+                        const SmOps& gops, hipStream_t s) {
   const int id = sm_class(g);
   int z = 1;
   NDP_SM_SWITCH(id, {
     z = wg_splits<G>(B, g.C, g.Co);
-    run_wgrad<G>(x, dy, out, B, g.C, g.Co, z, s);
+    run_wgrad<G>(x, dy, out, B, g.C, g.Co, z, xops, gops, s);
     break;
   })
   return z;
+}
+
+int sm_bstats_rows(int B) { return (B + kBnRows - 1) / kBnRows; }
+
+void launch_sm_bn_apply(const float* x, float* y, int B, int C, int P, const SmOps& ops, hipStream_t s) {
+  hipLaunchKernelGGL(sm_bn_apply_kernel, dim3(C / 16, (B + kBnRows - 1) / kBnRows), dim3(256), 0, s, x, y, B, C, P,
+                     ops);
+}
+
+void launch_sm_bn_bstats(const float* dy, int B, int C, int P, const SmOps& ops, hipStream_t s) {
+  hipLaunchKernelGGL(sm_bn_bstats_kernel, dim3(C / 16, (B + kBnRows - 1) / kBnRows), dim3(256), 0, s, dy, B, C, P,
+                     ops);
 }
 
 #undef NDP_SM_SWITCH

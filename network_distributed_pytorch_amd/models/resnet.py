@@ -26,6 +26,7 @@ from typing import List, Optional, Type, Union
 import torch
 import torch.nn as nn
 
+from ..ops import smstage
 from ..ops.batchnorm import BatchNormAct2d
 from ..ops.gradlink import BranchLink, GradLink
 from ..ops.linear import Linear
@@ -192,7 +193,12 @@ class ResNet(nn.Module):
             x = self.maxpool(self.bn1(self.conv1(x), relu=True))
         else:
             x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
-        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        x = self.layer2(self.layer1(x))
+        blocks = smstage.stage_blocks(self, x) if (self.fused and self.training) else None
+        if blocks is not None:  # layer3 + layer4 as one node, BatchNorm fused into the convs (ops/smstage.py)
+            x = smstage.run_stage(blocks, x)
+        else:
+            x = self.layer4(self.layer3(x))
         # 1x1 feature map (32x32 inputs): the average is the value itself; flatten skips a
         # mean kernel forward and its broadcast-divide backward (bitwise identical)
         x = torch.flatten(x if x.shape[-2:] == (1, 1) else self.avgpool(x), 1)

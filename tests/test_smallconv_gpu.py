@@ -112,8 +112,9 @@ def test_smallconv_slab_defer_and_addend(device):
 def test_resnet18_layer34_on_smallconv_matches_toeplitz(device, monkeypatch):
     """ResNet-18 step: the small-map kernels against the hipBLASLt Toeplitz path (NDP_SM off)."""
     from network_distributed_pytorch_amd.models import build_model
-    from network_distributed_pytorch_amd.ops import smconv
+    from network_distributed_pytorch_amd.ops import smconv, smstage
 
+    monkeypatch.setattr(smstage, "_ON", False)  # per-module path: conv kernels vs hipBLASLt only
     torch.manual_seed(0)
     m = build_model("resnet18", 10).to(device)
     x = torch.randn(64, 3, 32, 32, device=device)
@@ -135,3 +136,45 @@ def test_resnet18_layer34_on_smallconv_matches_toeplitz(device, monkeypatch):
         a, b = g1[n].flatten().double(), g0[n].flatten().double()
         cos = (a @ b / (a.norm() * b.norm() + 1e-30)).item()
         assert cos > 0.9999, (n, cos)
+
+
+@pytest.mark.parametrize("B", [64, 512, 24])
+def test_fused_stage_matches_module_path(device, monkeypatch, B):
+    """layer3 + layer4 as one fused-BN node (ops/smstage.py) against the per-module path (small-map
+    convs + the BatchNorm kernels): output, loss, every gradient, running statistics."""
+    from network_distributed_pytorch_amd.models import build_model
+    from network_distributed_pytorch_amd.ops import smstage
+
+    torch.manual_seed(1)
+    m = build_model("resnet18", 1000).to(device)
+    with torch.no_grad():  # non-trivial BN affine parameters
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm2d):
+                mod.weight.uniform_(0.5, 1.5)
+                mod.bias.uniform_(-0.2, 0.2)
+    state = {k: v.clone() for k, v in m.state_dict().items()}
+    x = torch.randn(B, 3, 32, 32, device=device)
+    yl = torch.randint(0, 1000, (B,), device=device)
+
+    def run(on):
+        monkeypatch.setattr(smstage, "_ON", on)
+        m.load_state_dict(state)
+        m.zero_grad(set_to_none=True)
+        out = m(x)
+        loss = F.cross_entropy(out, yl)
+        loss.backward()
+        return out.detach(), {n: p.grad.clone() for n, p in m.named_parameters()}, \
+            {k: v.clone() for k, v in m.state_dict().items()}
+
+    o1, g1, s1 = run(True)
+    o0, g0, s0 = run(False)
+    assert torch.allclose(o1, o0, rtol=1e-4, atol=1e-4), (o1 - o0).abs().max()
+    for n in g0:
+        a, b = g1[n].double(), g0[n].double()
+        err = ((a - b).norm() / (b.norm() + 1e-30)).item()
+        assert err < 1e-4, (n, err)
+    for k in s0:
+        if s0[k].dtype.is_floating_point:
+            assert torch.allclose(s1[k], s0[k], rtol=1e-4, atol=1e-5), k
+        else:
+            assert torch.equal(s1[k], s0[k]), k
