@@ -61,7 +61,10 @@ def _out_hw(g):
 def stage_blocks(model, x: torch.Tensor) -> Optional[list]:
     """The BasicBlocks of layer3 + layer4 if the fused stage covers them for input ``x``
     (layer2's output), else None."""
-    if not (_ON and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and torch.is_grad_enabled()):
+    from . import smconv
+
+    if not (_ON and smconv.enabled() and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+            and torch.is_grad_enabled()):
         return None
     from ..models.resnet import BasicBlock
     from .batchnorm import BatchNormAct2d
