@@ -28,7 +28,7 @@ from ..ops.attention import attention, attention_qkv, fused_ok
 from ..ops.embedding import Embedding
 from ..ops.gradlink import GradLink
 from ..ops.layernorm import AddLayerNorm
-from ..ops.linear import Linear, linear, linear_gelu
+from ..ops.linear import Linear, linear_gelu, packed_qkv
 from ..ops.loss import cross_entropy as native_ce
 
 __all__ = ["DistilBertConfig", "DistilBertForSequenceClassification", "distilbert_base"]
@@ -62,13 +62,26 @@ class Embeddings(nn.Module):
         super().__init__()
         # native deterministic backward (graph-replayable; ops/embedding.py)
         self.word_embeddings = Embedding(c.vocab_size, c.dim, padding_idx=c.pad_token_id)
-        self.position_embeddings = nn.Embedding(c.max_position_embeddings, c.dim)
+        self.position_embeddings = Embedding(c.max_position_embeddings, c.dim)
         self.LayerNorm = AddLayerNorm(c.dim, eps=c.layer_norm_eps)
         self.LayerNorm.native = c.fused_attention  # native kernels on/off together
         self.dropout = nn.Dropout(c.dropout)
+        self._pos = {}
+
+    def _pos_ids(self, b: int, s: int, device) -> torch.Tensor:
+        # [B, S] position ids, built once per shape (no arange launch per pass)
+        key = (b, s, str(device))
+        if key not in self._pos:
+            self._pos[key] = torch.arange(s, device=device).expand(b, s).contiguous()
+        return self._pos[key]
 
     def forward(self, input_ids):
-        s = input_ids.size(1)
+        b, s = input_ids.shape
+        if input_ids.is_cuda and self.LayerNorm.native:
+            # per-token position rows: the native embedding backward sums them over the batch
+            # (no broadcast-add + ATen reduce); the word + position add rides in the fused LN
+            pos = self.position_embeddings(self._pos_ids(b, s, input_ids.device))
+            return self.dropout(self.LayerNorm(self.word_embeddings(input_ids), residual=pos))
         pos = torch.arange(s, device=input_ids.device)
         x = self.word_embeddings(input_ids) + self.position_embeddings(pos)[None]
         return self.dropout(self.LayerNorm(x))
@@ -93,12 +106,10 @@ class MultiHeadSelfAttention(nn.Module):
         h = self.n_heads
         dh = d // h
         if self.fused and PACKED_QKV and x.is_cuda and x.dtype == torch.float32 and dh == 64:
-            # one packed projection GEMM [B*S, 3D] (the three weights concatenated per pass: a
-            # 7 MB copy; their gradients come back as views of one grad-W) read in place by
-            # the fused attention kernels (ops/attention.attention_qkv)
-            w = torch.cat([self.q_lin.weight, self.k_lin.weight, self.v_lin.weight])
-            bias = torch.cat([self.q_lin.bias, self.k_lin.bias, self.v_lin.bias])
-            qkv = linear(x, w, bias, link)
+            # one packed projection GEMM [B*S, 3D] over the three weights in place (consecutive
+            # in the PowerSGD arena: no copy; ops/linear.packed_qkv), read in place by the
+            # fused attention kernels (ops/attention.attention_qkv)
+            qkv = packed_qkv(x, self.q_lin, self.k_lin, self.v_lin, link)
             ctx = attention_qkv(qkv, h, mask, self.dropout.p if self.training else 0.0)
             return self.out_lin(ctx.reshape(bs, s, d))
         q4 = self.q_lin(x, link=link).view(bs, s, h, dh)

@@ -15,10 +15,10 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ._ext import ext
-from .gradarena import grad_buffer
+from .gradarena import grad_buffer, registered
 from .gradlink import InjectGrad
 
-__all__ = ["Linear", "linear", "linear_gelu"]
+__all__ = ["Linear", "linear", "linear_gelu", "packed_qkv"]
 
 # =1: the fused native GELU-backward + bias-sum pass.  Exact (tests/test_linear_gpu.py) but
 # measured slower on 1x MI355X, DistilBERT r=8: 21.39 / 21.41 vs 21.27 ms (its column-strip
@@ -90,6 +90,77 @@ class _LinearGeluFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             dw = dh.t() @ x.reshape(-1, k)
         return dx, dw, (db if ctx.needs_input_grad[2] else None), None
+
+
+def _adjacent(ts):
+    """One [sum rows, ...] view over tensors that already sit back to back in one storage
+    (the PowerSGD parameter arena lays q / k / v out consecutively), else None."""
+    t0 = ts[0]
+    off = t0.numel()
+    for t in ts[1:]:
+        if not (t.is_contiguous() and t.dtype == t0.dtype and t.device == t0.device and t.shape[1:] == t0.shape[1:]
+                and t.untyped_storage().data_ptr() == t0.untyped_storage().data_ptr()
+                and t.data_ptr() == t0.data_ptr() + off * t0.element_size()):
+            return None
+        off += t.numel()
+    if not t0.is_contiguous():
+        return None
+    rows = sum(t.shape[0] for t in ts)
+    return torch.as_strided(t0.detach(), (rows,) + tuple(t0.shape[1:]), t0.detach().stride(), t0.storage_offset())
+
+
+class _PackedQKVFn(torch.autograd.Function):
+    """One [B*S, 3D] projection GEMM for the three attention projections whose weights stay
+    three Parameters (HF keys, the reference's PowerSGD layout and byte count): read in place
+    when they are consecutive in memory (the PowerSGD arena), concatenated otherwise; their
+    gradients come back as views of one grad-W / one bias-sum buffer (or, for parameters
+    registered in the dense arena, straight into their arena slices)."""
+
+    @staticmethod
+    def forward(ctx, x, wq, wk, wv, bq, bk, bv, link=None):
+        w = _adjacent((wq, wk, wv))
+        b = _adjacent((bq, bk, bv))
+        if w is None:
+            w = torch.cat([wq.detach(), wk.detach(), wv.detach()])
+        if b is None:
+            b = torch.cat([bq.detach(), bk.detach(), bv.detach()])
+        ctx.save_for_backward(x, w)
+        ctx.link = link
+        ctx.params = (wq, wk, wv, bq, bk, bv)
+        return F.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        n, k = w.shape
+        d = n // 3
+        g2 = g.reshape(-1, n)
+        if not g2.is_contiguous():
+            g2 = g2.contiguous()
+        x2 = x.reshape(-1, k)
+        addend = ctx.link.take() if ctx.link is not None else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = (addend.reshape(-1, k).addmm_(g2, w) if addend is not None else g2 @ w).view(x.shape)
+        elif addend is not None:
+            dx = addend.view(x.shape)
+        wq, wk, wv, bq, bk, bv = ctx.params
+        if any(registered(p) for p in (wq, wk, wv)):
+            # dense arena slices (reverse order, not adjacent): one GEMM each, written in place
+            dws = [torch.mm(g2[:, i * d:(i + 1) * d].t(), x2, out=grad_buffer(p)) for i, p in enumerate((wq, wk, wv))]
+        else:
+            dw = torch.empty(n, k, device=g.device, dtype=g.dtype)
+            torch.mm(g2.t(), x2, out=dw)
+            dws = [dw[i * d:(i + 1) * d] for i in range(3)]
+        db = torch.empty(n, device=g.device, dtype=g.dtype)
+        ext().colsum(g2, db)
+        dbs = [db[i * d:(i + 1) * d] for i in range(3)]
+        return (dx,) + tuple(dws) + tuple(dbs) + (None,)
+
+
+def packed_qkv(x: torch.Tensor, q, k, v, link=None) -> torch.Tensor:
+    """[q(x) | k(x) | v(x)] as one GEMM (Linear modules q / k / v, same shapes)."""
+    return _PackedQKVFn.apply(x, q.weight, k.weight, v.weight, q.bias, k.bias, v.bias, link)
 
 
 def linear_gelu(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, link=None) -> torch.Tensor:

@@ -48,3 +48,35 @@ def test_distilbert_fusions_match_unfused(device, monkeypatch, packed, links):
             continue
         scale = g0[n].abs().max().item() + 1e-12
         torch.testing.assert_close(g1[n], g0[n], rtol=1e-3, atol=2e-4 * scale, msg=n)
+
+
+def test_packed_qkv_in_place_in_powersgd_arena(device):
+    """In the PowerSGD parameter arena q / k / v weights (and biases) are consecutive: the
+    packed projection reads them in place (no concatenation copy) and leaves leaf-only
+    ``.grad`` views (no per-pass torch.cat, no non-leaf .grad access)."""
+    import warnings
+
+    from network_distributed_pytorch_amd.ops.linear import _adjacent
+    from network_distributed_pytorch_amd.parallel.powersgd import PowerSGDOptimizer
+
+    torch.manual_seed(0)
+    m = distilbert_base(2, dropout=0.0, attention_dropout=0.0, seq_classif_dropout=0.0).to(device).train()
+    ref = distilbert_base(2, dropout=0.0, attention_dropout=0.0, seq_classif_dropout=0.0).to(device).train()
+    ref.load_state_dict(m.state_dict())
+    PowerSGDOptimizer(m.parameters(), lr=1e-3, rank=4)  # re-points the parameters into its arena
+    att = m.distilbert.transformer.layer[0].attention
+    assert _adjacent((att.q_lin.weight, att.k_lin.weight, att.v_lin.weight)) is not None
+    assert _adjacent((att.q_lin.bias, att.k_lin.bias, att.v_lin.bias)) is not None
+    ids = torch.randint(0, 30522, (2, 128), device=device)
+    am = torch.ones(2, 128, dtype=torch.long, device=device)
+    lab = torch.randint(0, 2, (2,), device=device)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")  # a non-leaf .grad access would warn
+        l1, g1 = _grads(m, ids, am, lab)
+    l0, g0 = _grads(ref, ids, am, lab)
+    torch.testing.assert_close(l1, l0, rtol=1e-5, atol=1e-6)
+    for n in g0:
+        if n.endswith("k_lin.bias"):
+            continue
+        scale = g0[n].abs().max().item() + 1e-12
+        torch.testing.assert_close(g1[n], g0[n], rtol=1e-3, atol=2e-4 * scale, msg=n)
