@@ -804,8 +804,31 @@ void ce_bwd(torch::Tensor dl, torch::Tensor g, torch::Tensor scratch, torch::Ten
 }
 
 // fused residual add + LayerNorm (last dim D): y, s (= a + b), mean, rstd are outputs
+// LayerNorm hash dropout: mode 0 none / 1 on the input a / 2 on the output (layernorm.hip)
+static ndp::LnDrop ln_drop(int64_t mode, double p, const c10::optional<torch::Tensor>& seed,
+                           const c10::optional<torch::Tensor>& da, int64_t numel) {
+  ndp::LnDrop d{nullptr, 0u, 1.f, 0, nullptr};
+  if (mode == 0 || p <= 0.0) return d;
+  TORCH_CHECK(mode == 1 || mode == 2, "ln: dropout mode 0 / 1 / 2");
+  TORCH_CHECK(p < 1.0, "ln: dropout p < 1");
+  TORCH_CHECK(seed.has_value() && seed->is_cuda() && seed->scalar_type() == torch::kInt32 && seed->numel() >= 1,
+              "ln: dropout needs a device int32 seed");
+  d.seed = seed->data_ptr<int32_t>();
+  const double t = p * 4294967296.0;
+  d.thr = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+  d.scale = (float)(1.0 / (1.0 - p));
+  d.mode = (int)mode;
+  if (da.has_value()) {
+    check_f32(*da, "da");
+    TORCH_CHECK(da->is_contiguous() && da->numel() == numel, "ln: da [R, D]");
+    d.da = da->data_ptr<float>();
+  }
+  return d;
+}
+
 void ln_fwd(torch::Tensor a, c10::optional<torch::Tensor> b, torch::Tensor gamma, torch::Tensor beta, torch::Tensor y,
-            torch::Tensor s, torch::Tensor mean, torch::Tensor rstd, double eps) {
+            torch::Tensor s, torch::Tensor mean, torch::Tensor rstd, double eps, int64_t drop_mode, double p,
+            c10::optional<torch::Tensor> seed) {
   check_f32(a, "a"); check_f32(gamma, "gamma"); check_f32(beta, "beta"); check_f32(y, "y"); check_f32(s, "s");
   check_f32(mean, "mean"); check_f32(rstd, "rstd");
   const int D = (int)a.size(-1);
@@ -819,22 +842,25 @@ void ln_fwd(torch::Tensor a, c10::optional<torch::Tensor> b, torch::Tensor gamma
   TORCH_CHECK(mean.numel() == R && rstd.numel() == R, "ln_fwd: stats size");
   ndp::launch_ln_fwd(a.data_ptr<float>(), opt_f32(b, "b"), gamma.data_ptr<float>(), beta.data_ptr<float>(),
                      y.data_ptr<float>(), s.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(), R, D,
-                     (float)eps, cur_stream());
+                     (float)eps, cur_stream(), ln_drop(drop_mode, p, seed, c10::nullopt, R * D));
   check_launch("launch_ln_fwd");
 }
 
 void ln_bwd(torch::Tensor dy, torch::Tensor s, torch::Tensor mean, torch::Tensor rstd, torch::Tensor gamma,
-            torch::Tensor dx, torch::Tensor dgb) {
+            torch::Tensor dx, torch::Tensor dgb, int64_t drop_mode, double p, c10::optional<torch::Tensor> seed,
+            c10::optional<torch::Tensor> da) {
   check_f32(dy, "dy"); check_f32(s, "s"); check_f32(mean, "mean"); check_f32(rstd, "rstd"); check_f32(gamma, "gamma");
   check_f32(dx, "dx"); check_f32(dgb, "dgb");
   const int D = (int)s.size(-1);
   const int64_t R = s.numel() / D;
   TORCH_CHECK(ndp::ln_supported(D) && gamma.numel() == D && dgb.numel() == 2 * D, "ln_bwd: unsupported D");
   for (auto* t : {&dy, &s, &dx}) TORCH_CHECK(t->is_contiguous() && t->numel() == R * D, "ln_bwd: contiguous [R, D]");
+  const ndp::LnDrop dp = ln_drop(drop_mode, p, seed, da, R * D);
+  TORCH_CHECK(dp.mode != 1 || dp.da != nullptr, "ln_bwd: input dropout needs da");
   auto part = torch::empty({(int64_t)ndp::ln_bwd_wgs(R) * 2 * D}, s.options());
   ndp::launch_ln_bwd(dy.data_ptr<float>(), s.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                      gamma.data_ptr<float>(), dx.data_ptr<float>(), part.data_ptr<float>(), dgb.data_ptr<float>(), R, D,
-                     cur_stream());
+                     cur_stream(), dp);
   check_launch("launch_ln_bwd");
 }
 
@@ -1271,8 +1297,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("colsum", &colsum);
   m.def("gelu_bwd_colsum", &gelu_bwd_colsum);
   m.def("ce_fwd", &ce_fwd);
-  m.def("ln_fwd", &ln_fwd);
-  m.def("ln_bwd", &ln_bwd);
+  m.def("ln_fwd", &ln_fwd, py::arg("a"), py::arg("b"), py::arg("gamma"), py::arg("beta"), py::arg("y"), py::arg("s"),
+        py::arg("mean"), py::arg("rstd"), py::arg("eps"), py::arg("drop_mode") = 0, py::arg("p") = 0.0,
+        py::arg("seed") = c10::optional<torch::Tensor>());
+  m.def("ln_bwd", &ln_bwd, py::arg("dy"), py::arg("s"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"),
+        py::arg("dx"), py::arg("dgb"), py::arg("drop_mode") = 0, py::arg("p") = 0.0,
+        py::arg("seed") = c10::optional<torch::Tensor>(), py::arg("da") = c10::optional<torch::Tensor>());
   m.def("ce_bwd", &ce_bwd);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);

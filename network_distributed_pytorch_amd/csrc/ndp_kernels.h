@@ -165,13 +165,22 @@ void launch_ce_bwd(const float* dl, const float* g, const float* inv, float* dx,
 // ---- fused residual add + LayerNorm over the last dim (layernorm.hip) --------------------
 namespace ndp {
 bool ln_supported(int D);  // D in {256, 512, 768, 1024}
+// hash dropout fused into the LayerNorm: mode 0 none, 1 on a (before the residual add; the
+// backward also writes da = dropout'(dx)), 2 on the output; keep = hash >= thr (= p * 2^32)
+struct LnDrop {
+  const int32_t* seed;
+  uint32_t thr;
+  float scale;  // 1 / (1 - p)
+  int mode;
+  float* da;
+};
 // y = LN(a (+ b)) * gamma + beta; s = a (+ b), mean / rstd [R] saved for backward
 void launch_ln_fwd(const float* a, const float* b, const float* gamma, const float* beta, float* y, float* s,
-                   float* mean, float* rstd, int64_t R, int D, float eps, hipStream_t st);
+                   float* mean, float* rstd, int64_t R, int D, float eps, hipStream_t st, const LnDrop& dp);
 int ln_bwd_wgs(int64_t R);
 // dx [R, D]; part: ln_bwd_wgs(R) * 2D floats of scratch; dgb: [dgamma | dbeta] (2D floats)
 void launch_ln_bwd(const float* dy, const float* s, const float* mean, const float* rstd, const float* gamma,
-                   float* dx, float* part, float* dgb, int64_t R, int D, hipStream_t st);
+                   float* dx, float* part, float* dgb, int64_t R, int D, hipStream_t st, const LnDrop& dp);
 }  // namespace ndp
 
 // ---- convolutions, NCHW fp32 (conv.hip) -------------------------------------------------

@@ -81,7 +81,9 @@ class Embeddings(nn.Module):
             # per-token position rows: the native embedding backward sums them over the batch
             # (no broadcast-add + ATen reduce); the word + position add rides in the fused LN
             pos = self.position_embeddings(self._pos_ids(b, s, input_ids.device))
-            return self.dropout(self.LayerNorm(self.word_embeddings(input_ids), residual=pos))
+            # the dropout rides in the LayerNorm kernels (hash mask regenerated in backward)
+            return self.LayerNorm(self.word_embeddings(input_ids), residual=pos,
+                                  p_out=self.dropout.p if self.training else 0.0)
         pos = torch.arange(s, device=input_ids.device)
         x = self.word_embeddings(input_ids) + self.position_embeddings(pos)[None]
         return self.dropout(self.LayerNorm(x))
@@ -139,9 +141,12 @@ class FFN(nn.Module):
         self.lin2 = Linear(c.hidden_dim, c.dim)
         self.dropout = nn.Dropout(c.dropout)
 
-    def forward(self, x, link=None):
+    def forward(self, x, link=None, dropout: bool = True):
+        """``dropout=False``: the caller applies this dropout (fused into the block's
+        LayerNorm)."""
         # lin1 + exact GELU share one fused native backward pass (ops/linear.linear_gelu)
-        return self.dropout(self.lin2(linear_gelu(x, self.lin1.weight, self.lin1.bias, link)))
+        h = self.lin2(linear_gelu(x, self.lin1.weight, self.lin1.bias, link))
+        return self.dropout(h) if dropout else h
 
 
 class TransformerBlock(nn.Module):
@@ -160,7 +165,9 @@ class TransformerBlock(nn.Module):
         lk = self._link(self.sa_layer_norm, x)
         x = self.sa_layer_norm(self.attention(x, mask, link=lk), residual=x, link=lk)
         lk = self._link(self.output_layer_norm, x)
-        return self.output_layer_norm(self.ffn(x, link=lk), residual=x, link=lk)
+        # the FFN's output dropout rides in the LayerNorm kernels (hash mask, no mask tensor)
+        return self.output_layer_norm(self.ffn(x, link=lk, dropout=False), residual=x, link=lk,
+                                      p_in=self.ffn.dropout.p if self.training else 0.0)
 
     def _link(self, ln, x):
         if LN_LINKS and self.training and torch.is_grad_enabled() and x.requires_grad and ln.fused_ok(x, x):

@@ -78,3 +78,30 @@ def test_linear_gelu_cpu_fallback():
     w = torch.randn(12, 8)
     b = torch.randn(12)
     torch.testing.assert_close(linear_gelu(x, w, b), F.gelu(F.linear(x, w, b)))
+
+
+def test_ln_keep_mask_host_twin():
+    """Host twin of the LayerNorm hash-dropout mask: deterministic per seed, ~p dropped,
+    different seeds / rows / columns decorrelated."""
+    from network_distributed_pytorch_amd.ops.layernorm import ln_keep_mask
+
+    a = ln_keep_mask(3, 512, 768, 0.1)
+    assert torch.equal(a, ln_keep_mask(3, 512, 768, 0.1))
+    assert abs((1 - a.float().mean().item()) - 0.1) < 0.005
+    b = ln_keep_mask(4, 512, 768, 0.1)
+    assert (a != b).float().mean().item() > 0.15  # ~2 p (1 - p) for independent masks
+    assert (a[1:] != a[:-1]).float().mean().item() > 0.15
+    assert ln_keep_mask(3, 4, 256, 0.0).all()
+
+
+def test_add_layernorm_dropout_cpu_path():
+    """CPU (unfused) path of the fused-dropout LayerNorm keeps nn.Dropout semantics."""
+    torch.manual_seed(0)
+    m = AddLayerNorm(256)
+    x = torch.randn(64, 256)
+    r = torch.randn(64, 256)
+    y = m(x, residual=r, p_out=0.5)
+    zero = (y == 0).float().mean().item()
+    assert 0.4 < zero < 0.6
+    y_in = m(x, residual=r, p_in=0.0)
+    torch.testing.assert_close(y_in, F.layer_norm(x + r, (256,), m.weight, m.bias, m.eps))
