@@ -19,6 +19,9 @@ namespace ndp {
 
 typedef float f4l __attribute__((ext_vector_type(4)));
 
+// rows of a lane group in flight together (4 independent float4 loads per lane per step)
+constexpr int kColUnroll = 4;
+
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ g, int64_t M, int N,
                                                              int rows_per_chunk, float* __restrict__ part) {
   __shared__ f4l red[4][64];
@@ -30,7 +33,15 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __rest
   if (4 * c4 < N) {
     const f4l* src = reinterpret_cast<const f4l*>(g) + c4;
     const int64_t n4 = N / 4;
-    for (int64_t r = r0 + grp; r < r1; r += 4) acc += src[r * n4];
+    int64_t r = r0 + grp;
+    for (; r + 4 * (kColUnroll - 1) < r1; r += 4 * kColUnroll) {
+      f4l v[kColUnroll];
+#pragma unroll
+      for (int u = 0; u < kColUnroll; ++u) v[u] = src[(r + 4 * u) * n4];
+#pragma unroll
+      for (int u = 0; u < kColUnroll; ++u) acc += v[u];
+    }
+    for (; r < r1; r += 4) acc += src[r * n4];
   }
   red[grp][threadIdx.x & 63] = acc;
   __syncthreads();
@@ -68,7 +79,24 @@ __global__ __launch_bounds__(256) void gelu_bwd_colsum_partial_kernel(const floa
     const f4l* gs = reinterpret_cast<const f4l*>(g) + c4;
     const f4l* hs = reinterpret_cast<const f4l*>(h) + c4;
     f4l* ds = reinterpret_cast<f4l*>(dh) + c4;
-    for (int64_t r = r0 + grp; r < r1; r += 4) {
+    int64_t r = r0 + grp;
+    for (; r + 4 * (kColUnroll - 1) < r1; r += 4 * kColUnroll) {
+      f4l gv[kColUnroll], hv[kColUnroll];
+#pragma unroll
+      for (int u = 0; u < kColUnroll; ++u) {
+        gv[u] = gs[(r + 4 * u) * n4];
+        hv[u] = hs[(r + 4 * u) * n4];
+      }
+#pragma unroll
+      for (int u = 0; u < kColUnroll; ++u) {
+        f4l d;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[j] = gelu_grad(gv[u][j], hv[u][j]);
+        ds[(r + 4 * u) * n4] = d;
+        acc += d;
+      }
+    }
+    for (; r < r1; r += 4) {
       const f4l gv = gs[r * n4], hv = hs[r * n4];
       f4l d;
 #pragma unroll
@@ -97,7 +125,7 @@ void launch_gelu_bwd_colsum(const float* g, const float* h, float* dh, int64_t M
 
 int colsum_chunks(int64_t M, int N) {
   const int strips = (N / 4 + 63) / 64;
-  int chunks = (256 + strips - 1) / strips;          // ~256 workgroups in pass 1
+  int chunks = (1024 + strips - 1) / strips;         // ~1024 workgroups (4 per CU) in pass 1
   const int64_t max_chunks = (M + 31) / 32;          // >= 32 rows per chunk
   if (chunks > max_chunks) chunks = (int)max_chunks;
   return chunks < 1 ? 1 : chunks;

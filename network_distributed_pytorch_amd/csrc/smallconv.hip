@@ -119,6 +119,23 @@ __device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, uint32_t off) 
 }
 
 // ---- fused BatchNorm: coefficient finalization (ndp_kernels.h SmBnF / SmBnB) ---------------
+// sum over the R row-tile partials of channel k, field j of a [R][C][W] fp64 table: the loads
+// of 8 rows are issued together, the adds stay in row order (the same value in every consumer)
+template <int W>
+__device__ __forceinline__ double part_sum(const double* part, int R, int C, int k, int j) {
+  double t = 0.0;
+  int r = 0;
+  for (; r + 8 <= R; r += 8) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = part[((int64_t)(r + u) * C + k) * W + j];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t += v[u];
+  }
+  for (; r < R; ++r) t += part[((int64_t)r * C + k) * W + j];
+  return t;
+}
+
 // Forward: mean / invstd from the per-row-tile partial sums (fp64, fixed row order: every
 // consumer computes bitwise the same value) or the saved statistics; scale = gamma * invstd,
 // shift = beta - mean * scale — the same fp32 formulas as csrc/batchnorm.hip, so a mask or an
@@ -126,11 +143,8 @@ __device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, uint32_t off) 
 __device__ __forceinline__ void bn_fwd_coef(const SmBnF& f, int k, int C, bool writer, float& s, float& h,
                                             float& mean, float& invstd) {
   if (f.part != nullptr) {
-    double sum = 0.0, sq = 0.0;
-    for (int r = 0; r < f.R; ++r) {
-      sum += f.part[((int64_t)r * C + k) * 2];
-      sq += f.part[((int64_t)r * C + k) * 2 + 1];
-    }
+    const double sum = part_sum<2>(f.part, f.R, C, k, 0);
+    const double sq = part_sum<2>(f.part, f.R, C, k, 1);
     const double M = f.count;
     const double mu = sum / M;
     double var = sq / M - mu * mu;
@@ -158,11 +172,8 @@ __device__ __forceinline__ void bn_fwd_coef(const SmBnF& f, int k, int C, bool w
 // Backward: k1 = gamma * invstd, mean dz, mean dz * xhat (dx = k1 (dz - mdz - xhat mdzx))
 __device__ __forceinline__ void bn_bwd_coef(const SmBnB& b, int k, int C, bool writer, float& k1, float& mdz,
                                             float& mdzx) {
-  double sdz = 0.0, sdzx = 0.0;
-  for (int r = 0; r < b.R; ++r) {
-    sdz += b.part[((int64_t)r * C + k) * 4];
-    sdzx += b.part[((int64_t)r * C + k) * 4 + b.j];
-  }
+  const double sdz = part_sum<4>(b.part, b.R, C, k, 0);
+  const double sdzx = part_sum<4>(b.part, b.R, C, k, b.j);
   if (writer) {
     if (b.dgamma) b.dgamma[k] = (float)sdzx;
     if (b.dbeta) b.dbeta[k] = (float)sdz;
@@ -288,7 +299,8 @@ __global__ __launch_bounds__(256) void sm_row_kernel(SmRowArgs a) {
   const int l16 = lane & 15, l4 = lane >> 4;
   const int n0 = blockIdx.x * TN, b0 = blockIdx.y * TM;
   const int kbeg = blockIdx.z * a.cps;
-  const int nchunks = (min(a.K, kbeg + a.cps) - kbeg) / TK;
+  const int klen = min(a.K, kbeg + a.cps) - kbeg;  // a multiple of 16; the last chunk may be partial
+  const int nchunks = (klen + TK - 1) / TK;
   const int amode = ops.amode;
   const bool origin = blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0;
 
@@ -316,24 +328,27 @@ __global__ __launch_bounds__(256) void sm_row_kernel(SmRowArgs a) {
     ach[v] = j / PP;  // channel in the chunk (PP == 1: the first of 4)
   }
   uint32_t woff[R::W_PER];
-  int wdst[R::W_PER];
+  int wdst[R::W_PER], wkc[R::W_PER];
 #pragma unroll
   for (int v = 0; v < R::W_PER; ++v) {
     const int e = tid + 256 * v;
     const bool ok = e < R::WV;
-    int row, tsrc, dcol;  // tile row, source float along the W row, destination column
+    int row, tsrc, dcol, ch;  // tile row, source float along the W row, destination column, channel
     if constexpr (G::ALL) {
       row = e / (R::WCH * G::T / 4);
       const int j = 4 * (e - row * (R::WCH * G::T / 4));  // float in the row (contiguous in LDS too)
       tsrc = j;
       dcol = j;
+      ch = j / G::T;  // a 16-B vector never straddles a 16-channel boundary
     } else {
       row = e / (R::WCH * U);
       const int r2 = e - row * (R::WCH * U);
-      const int ch = r2 / U, s = r2 - ch * U;
+      ch = r2 / U;
+      const int s = r2 - ch * U;
       tsrc = ch * G::T + G::utap(s);
       dcol = ch * R::KSW + s;
     }
+    wkc[v] = DIR == 0 ? ch : row;  // reduction channel of this load inside the chunk
     // forward rows: co = n0 + row, floats from ci = kbeg; grad-x rows: co = kbeg + row, from ci = n0
     const int64_t g = DIR == 0 ? ((int64_t)(n0 + row) * a.C + kbeg) * G::T + tsrc
                                : ((int64_t)(kbeg + row) * a.C + n0) * G::T + tsrc;
@@ -348,17 +363,18 @@ __global__ __launch_bounds__(256) void sm_row_kernel(SmRowArgs a) {
   typedef typename std::conditional<G::ALL, f32x4s, float>::type WVec;
   f32x4s rA[R::A_PER], rE1[R::A_PER], rE2[R::A_PER];
   WVec rW[R::W_PER];
+  // channels past the split (a partial last chunk) load as zeros: W zero, operand zero
   auto load = [&](int c) {
 #pragma unroll
     for (int v = 0; v < R::A_PER; ++v) {
-      const uint32_t o = aoff[v] == kOOB ? kOOB : aoff[v] + c * astep;
+      const uint32_t o = (aoff[v] == kOOB || c * TK + ach[v] >= klen) ? kOOB : aoff[v] + c * astep;
       rA[v] = bload4(ra, o);
       if (ld1) rE1[v] = bload4(re1, o);
       if (ld2) rE2[v] = bload4(re2, o);
     }
 #pragma unroll
     for (int v = 0; v < R::W_PER; ++v) {
-      const uint32_t o = woff[v] == kOOB ? kOOB : woff[v] + c * wstep;
+      const uint32_t o = (woff[v] == kOOB || c * TK + wkc[v] >= klen) ? kOOB : woff[v] + c * wstep;
       if constexpr (G::ALL) rW[v] = bload4(rw, o);
       else rW[v] = bload1(rw, o);
     }
@@ -370,7 +386,7 @@ __global__ __launch_bounds__(256) void sm_row_kernel(SmRowArgs a) {
     for (int v = 0; v < R::A_PER; ++v) {
       if (adst[v] < 0) continue;
       f32x4s x = rA[v];
-      if (amode != 0) {
+      if (amode != 0 && c * TK + ach[v] < klen) {
         const int k = kbeg + c * TK + ach[v];
 #pragma unroll
         for (int q = 0; q < 4; ++q) x[q] = xform(ops, coef, a.K, k + (PP >= 4 ? 0 : q), x[q], rE1[v][q], rE2[v][q]);
@@ -827,6 +843,29 @@ void set_lds_once(K k, size_t bytes) {
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
+// LDS chunk depth: the largest S (k-steps per wave per chunk) whose double-buffered stage fits
+// 80 KB and whose staging registers stay modest — few, large chunks: each chunk costs a barrier
+// and a global round trip that its MFMAs must cover (S = 1 left the layer4 GEMMs latency-bound)
+constexpr int kSmStageFloats = 20480;
+template <class G, int DIR, int TM, int S>
+constexpr bool row_fits() {
+  using R = RowCfg<G, DIR, TM, 16, S>;
+  return 2 * R::STAGE <= kSmStageFloats && R::A_PER * 12 + R::W_PER * (G::ALL ? 4 : 1) <= 128;
+}
+template <class G, int DIR, int TM>
+constexpr int row_s() {
+  return row_fits<G, DIR, TM, 8>() ? 8 : row_fits<G, DIR, TM, 4>() ? 4 : row_fits<G, DIR, TM, 2>() ? 2 : 1;
+}
+template <class G, int S>
+constexpr bool wg_fits() {
+  using R = WgCfg<G, 16, 32, S>;
+  return 2 * R::STAGE <= kSmStageFloats && R::G_PER * 12 + R::X_PER * 4 <= 128;
+}
+template <class G>
+constexpr int wg_s() {
+  return wg_fits<G, 8>() ? 8 : wg_fits<G, 4>() ? 4 : wg_fits<G, 2>() ? 2 : 1;
+}
+
 constexpr int kSmFill = 256;    // workgroups for one per CU
 constexpr int kSmMaxSplit = 4;  // forward / grad-x slabs: the fused BN kernel sums <= 4 (kMaxFusedSlabs)
 constexpr size_t kSmMaxLds = 160 * 1024;
@@ -848,8 +887,9 @@ int row_tm(int B, int N) {
 template <class G, int DIR, int TM>
 void run_row(const float* act, const float* w, float* out, float* part, int B, int K, int N, int C, int ks,
              const SmOps& ops, hipStream_t s) {
-  using R = RowCfg<G, DIR, TM, 16, 1>;
-  auto k = sm_row_kernel<G, DIR, TM, 16, 1>;
+  constexpr int S = row_s<G, DIR, TM>();
+  using R = RowCfg<G, DIR, TM, 16, S>;
+  auto k = sm_row_kernel<G, DIR, TM, 16, S>;
   static bool attr = false;
   if (!attr) {
     set_lds_once(k, kSmMaxLds);
@@ -897,8 +937,9 @@ int wg_splits(int B, int C, int Co) {
 template <class G>
 void run_wgrad(const float* x, const float* dy, float* out, int B, int C, int Co, int splits, const SmOps& xops,
                const SmOps& gops, hipStream_t s) {
-  using R = WgCfg<G, 16, 32, 1>;
-  auto k = sm_wgrad_kernel<G, 16, 32, 1>;
+  constexpr int S = wg_s<G>();
+  using R = WgCfg<G, 16, 32, S>;
+  auto k = sm_wgrad_kernel<G, 16, 32, S>;
   static bool attr = false;
   if (!attr) {
     set_lds_once(k, R::LDS_BYTES);

@@ -20,10 +20,11 @@ from .gradlink import InjectGrad
 
 __all__ = ["Linear", "linear", "linear_gelu", "packed_qkv"]
 
-# =1: the fused native GELU-backward + bias-sum pass.  Exact (tests/test_linear_gpu.py) but
-# measured slower on 1x MI355X, DistilBERT r=8: 21.39 / 21.41 vs 21.27 ms (its column-strip
-# grid has ~250 workgroups; ATen's GELU backward streams with the whole chip) -> off.
-_FUSED_GELU = os.environ.get("NDP_FUSED_GELU", "0") != "0"
+# the fused native GELU-backward + bias-sum pass (NDP_FUSED_GELU=0: ATen GELU backward + the
+# native bias sum).  Exact (tests/test_linear_gpu.py).  Round 3 measured it slower (~250
+# column-strip workgroups, one load in flight per thread); with ~1024 workgroups and 4 rows in
+# flight per thread it is on: DistilBERT r=8, 1x MI355X, 20.70 vs 20.74 ms (profiles/r4).
+_FUSED_GELU = os.environ.get("NDP_FUSED_GELU", "1") != "0"
 
 
 class _LinearFn(torch.autograd.Function):

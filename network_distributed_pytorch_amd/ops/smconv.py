@@ -9,8 +9,13 @@ path (models/conv_gemm.py) and the tabled tgemm family for these shapes.
 
 Split-K slabs (small per-GPU batches) are summed in a fixed order — by the fused BN kernel
 that consumes the conv (``slab_out`` / ``grad_slab``, ops/slablink.py), by the kernel's own
-slab sum, or (grad-W, batch splits) by gradfinish's batched sum.  ``NDP_SM=0`` disables the
-path.
+slab sum, or (grad-W, batch splits) by gradfinish's batched sum.
+
+OFF by default (``NDP_SM=1`` turns it on for every covered geometry, ``NDP_SM=l3entry`` only for
+the two 4x4-input convs of layer3's entry block — the 3x3 / 2 and the 1x1 / 2): measured on 1x MI355X (profiles/r4/smallconv.md) the
+kernels are at parity with hipBLASLt on the 3x3 convs, faster on the layer3 entry / downsample,
+and 2.5x slower on the layer4 entry (2x2 -> 1x1, 4 of 9 taps gathered as scalars); the whole
+ResNet-18 step is slower with them (batch 512: 2.16 vs 1.93 ms, batch 64: 1.10 vs 1.00 ms).
 """
 from __future__ import annotations
 
@@ -26,11 +31,17 @@ from .gradarena import grad_buffer
 __all__ = ["sm_plan", "SmConvFn", "enabled"]
 
 _PLANS: dict = {}
-_ON = os.environ.get("NDP_SM", "1") != "0"
+_MODE = os.environ.get("NDP_SM", "0")
+_ON = _MODE != "0"
 
 
 def enabled() -> bool:
-    return _ON
+    """Every covered geometry on the small-map kernels (the fused stage needs them all)."""
+    return _ON and _MODE != "l3entry"
+
+
+def _wanted(H: int, W: int) -> bool:
+    return _MODE != "l3entry" or (H == 4 and W == 4)
 
 
 def sm_plan(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int) -> Optional[Tuple]:
@@ -39,7 +50,7 @@ def sm_plan(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int) ->
         return None
     B, C, H, W = x.shape
     Co, Ci, KH, KW = weight.shape
-    if Ci != C:
+    if Ci != C or not _wanted(H, W):
         return None
     geom = (C, H, W, Co, KH, KW, int(stride), int(padding))
     key = (geom, int(B))

@@ -25,7 +25,10 @@ backward, given dO:
 so the stage is 2-3 kernels per block in each direction instead of ~2 per conv plus ~2 per BN.
 Running statistics, saved mean / invstd, dgamma / dbeta are written by the kernels (the
 workgroup at grid origin); parameters / buffers / state_dict are the modules' own.
-``NDP_SM_STAGE=0`` keeps the per-module path (still on the small-map convs).
+``NDP_SM_STAGE=0`` keeps the per-module path (still on the small-map convs).  The stage only
+runs with the small-map convs on (``NDP_SM=1``, off by default): the fused operand transforms
+and epilogue statistics cost more than the BatchNorm launches they replace at these kernel
+speeds (profiles/r4/smallconv.md: batch 512 2.51 ms with the stage vs 2.16 without).
 """
 from __future__ import annotations
 

@@ -143,8 +143,9 @@ def test_fused_stage_matches_module_path(device, monkeypatch, B):
     """layer3 + layer4 as one fused-BN node (ops/smstage.py) against the per-module path (small-map
     convs + the BatchNorm kernels): output, loss, every gradient, running statistics."""
     from network_distributed_pytorch_amd.models import build_model
-    from network_distributed_pytorch_amd.ops import smstage
+    from network_distributed_pytorch_amd.ops import smconv, smstage
 
+    monkeypatch.setattr(smconv, "_ON", True)  # both paths on the small-map convs (off by default)
     torch.manual_seed(1)
     m = build_model("resnet18", 1000).to(device)
     with torch.no_grad():  # non-trivial BN affine parameters
