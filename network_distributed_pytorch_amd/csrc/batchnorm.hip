@@ -75,6 +75,28 @@ __device__ __forceinline__ BnSlice slice_of(int N, int S, int s) {
   return {n0, n0 + base + (s < rem ? 1 : 0)};
 }
 
+// sums of the S slice partials [c][s][2] of channel c: 8 loads in flight, adds in slice order
+__device__ __forceinline__ void slice_sums(const double* __restrict__ part, int c, int S, double& a, double& b) {
+  a = 0.0;
+  b = 0.0;
+  const double* p = part + (int64_t)c * S * 2;
+  int k = 0;
+  for (; k + 8 <= S; k += 8) {
+    double v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = p[2 * k + u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      a += v[2 * u];
+      b += v[2 * u + 1];
+    }
+  }
+  for (; k < S; ++k) {
+    a += p[2 * k];
+    b += p[2 * k + 1];
+  }
+}
+
 // ---- forward statistics -------------------------------------------------------------
 // src (nullable, VEC only): x is the sum of nslab split-K conv slabs (slab order, bitwise equal
 // to conv_slab_sum); the kernel adds them, writes x and takes its statistics in one pass.
@@ -128,11 +150,8 @@ __global__ __launch_bounds__(256) void bn_fwd_apply_kernel(
   const int s = blockIdx.x, c = blockIdx.y;
   float mean, invstd;
   if (training) {
-    double sum = 0.0, sq = 0.0;
-    for (int k = 0; k < S; ++k) {
-      sum += part[((int64_t)c * S + k) * 2];
-      sq += part[((int64_t)c * S + k) * 2 + 1];
-    }
+    double sum, sq;
+    slice_sums(part, c, S, sum, sq);
     const double M = (double)N * HW;
     const double mu = sum / M;
     double var = sq / M - mu * mu;
@@ -238,11 +257,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     float* __restrict__ dx, float* __restrict__ dres, float* __restrict__ dgamma, float* __restrict__ dbeta,
     const double* __restrict__ part, int N, int C, int HW, int S, int relu) {
   const int s = blockIdx.x, c = blockIdx.y;
-  double sdz = 0.0, sdzx = 0.0;
-  for (int k = 0; k < S; ++k) {
-    sdz += part[((int64_t)c * S + k) * 2];
-    sdzx += part[((int64_t)c * S + k) * 2 + 1];
-  }
+  double sdz, sdzx;
+  slice_sums(part, c, S, sdz, sdzx);
   if (s == 0 && threadIdx.x == 0) {
     if (dgamma) dgamma[c] = (float)sdzx;
     if (dbeta) dbeta[c] = (float)sdz;
@@ -461,6 +477,14 @@ constexpr int kFusedMaxN = 512;
 // (bitwise-equal values); the forward also stores the sum to x (BN's saved input).
 // MAXN: largest batch the register arrays hold (512 for HW <= 16; 128 for the 8x8 maps of
 // layer1 at the strong-scaling per-GPU batches 64 / 128, CW = HW = 64).
+// Workgroups are dealt to the 8 XCDs round-robin (XCD = blockIdx % 8), each XCD with its own L2.
+// Column blocks narrower than a 128-B line (CW = 4 / 8 floats) share lines with their neighbours:
+// remap so that consecutive column blocks run on the same XCD (one L2 fetches the line once).
+__device__ __forceinline__ int xcd_block(int bid, int nblk) {
+  const int xcd = bid & 7, idx = bid >> 3, per = nblk >> 3, rem = nblk & 7;
+  return xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
+}
+
 template <int HW, int BWD, int CW, int MAXN = kFusedMaxN>
 __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
     const float* __restrict__ x, const float* __restrict__ res, const float* __restrict__ dy,
@@ -476,7 +500,7 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
   __shared__ double red[2][NW][CW];
   const int CHW = C * HW;
   const int col = threadIdx.x % CW, g = threadIdx.x / CW;
-  const int j = blockIdx.x * CW + col;
+  const int j = xcd_block((int)blockIdx.x, (int)gridDim.x) * CW + col;
   const bool ok_col = j < CHW;
   const int c = ok_col ? j / HW : 0;
   float v[NP], d[NP], m[NP];

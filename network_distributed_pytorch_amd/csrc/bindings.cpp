@@ -745,19 +745,36 @@ int64_t tg_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor out, const std
 }
 
 // db = g.sum(0) for g [M, N] contiguous fp32, N % 4 == 0 (deterministic, graph-safe)
-void colsum(torch::Tensor g, torch::Tensor out) {
+// part (optional, >= colsum_chunks(M, N) * N floats): write the per-chunk partials there and
+// leave the final fixed-order sum to the caller (ops/gradfinish.py batches it); returns the
+// chunk count (0: summed into out here)
+static float* deferred_part(const c10::optional<torch::Tensor>& part, int64_t need, const char* what) {
+  if (!part.has_value()) return nullptr;
+  check_f32(*part, what);
+  TORCH_CHECK(part->is_contiguous() && part->numel() >= need, what, ": partial buffer too small");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(part->data_ptr()) & 15) == 0, what, ": 16-B aligned partials");
+  return part->data_ptr<float>();
+}
+
+int64_t colsum(torch::Tensor g, torch::Tensor out, c10::optional<torch::Tensor> part_out) {
   check_f32(g, "g"); check_f32(out, "out");
   TORCH_CHECK(g.dim() == 2 && g.size(1) % 4 == 0 && out.numel() == g.size(1), "colsum: g [M, N] with N % 4 == 0");
   TORCH_CHECK((reinterpret_cast<uintptr_t>(g.data_ptr()) & 15) == 0, "colsum: 16-B aligned input");
   const int64_t M = g.size(0);
   const int N = (int)g.size(1);
-  auto part = torch::empty({(int64_t)ndp::colsum_chunks(M, N) * N}, g.options());
-  ndp::launch_colsum(g.data_ptr<float>(), M, N, part.data_ptr<float>(), out.data_ptr<float>(), cur_stream());
+  const int chunks = ndp::colsum_chunks(M, N);
+  float* dp = deferred_part(part_out, (int64_t)chunks * N, "colsum");
+  torch::Tensor part;
+  if (dp == nullptr) part = torch::empty({(int64_t)chunks * N}, g.options());
+  ndp::launch_colsum(g.data_ptr<float>(), M, N, dp ? dp : part.data_ptr<float>(), dp ? nullptr : out.data_ptr<float>(),
+                     cur_stream());
   check_launch("launch_colsum");
+  return dp ? chunks : 0;
 }
 
 // DistilBERT FFN: dh = g * gelu'(h) and db = column sums of dh in one pass
-void gelu_bwd_colsum(torch::Tensor g, torch::Tensor h, torch::Tensor dh, torch::Tensor db) {
+int64_t gelu_bwd_colsum(torch::Tensor g, torch::Tensor h, torch::Tensor dh, torch::Tensor db,
+                        c10::optional<torch::Tensor> part_out) {
   check_f32(g, "g"); check_f32(h, "h"); check_f32(dh, "dh"); check_f32(db, "db");
   TORCH_CHECK(g.dim() == 2 && g.size(1) % 4 == 0 && h.sizes() == g.sizes() && dh.sizes() == g.sizes() &&
                   db.numel() == g.size(1),
@@ -766,10 +783,14 @@ void gelu_bwd_colsum(torch::Tensor g, torch::Tensor h, torch::Tensor dh, torch::
     TORCH_CHECK((reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0, "gelu_bwd_colsum: 16-B aligned tensors");
   const int64_t M = g.size(0);
   const int N = (int)g.size(1);
-  auto part = torch::empty({(int64_t)ndp::colsum_chunks(M, N) * N}, g.options());
+  const int chunks = ndp::colsum_chunks(M, N);
+  float* dp = deferred_part(part_out, (int64_t)chunks * N, "gelu_bwd_colsum");
+  torch::Tensor part;
+  if (dp == nullptr) part = torch::empty({(int64_t)chunks * N}, g.options());
   ndp::launch_gelu_bwd_colsum(g.data_ptr<float>(), h.data_ptr<float>(), dh.data_ptr<float>(), M, N,
-                              part.data_ptr<float>(), db.data_ptr<float>(), cur_stream());
+                              dp ? dp : part.data_ptr<float>(), dp ? nullptr : db.data_ptr<float>(), cur_stream());
   check_launch("launch_gelu_bwd_colsum");
+  return dp ? chunks : 0;
 }
 
 // fused cross-entropy forward: loss (0-d), dl [B, K] saved gradient; scratch = rowloss [B] + inv [1]
@@ -846,9 +867,9 @@ void ln_fwd(torch::Tensor a, c10::optional<torch::Tensor> b, torch::Tensor gamma
   check_launch("launch_ln_fwd");
 }
 
-void ln_bwd(torch::Tensor dy, torch::Tensor s, torch::Tensor mean, torch::Tensor rstd, torch::Tensor gamma,
-            torch::Tensor dx, torch::Tensor dgb, int64_t drop_mode, double p, c10::optional<torch::Tensor> seed,
-            c10::optional<torch::Tensor> da) {
+int64_t ln_bwd(torch::Tensor dy, torch::Tensor s, torch::Tensor mean, torch::Tensor rstd, torch::Tensor gamma,
+               torch::Tensor dx, torch::Tensor dgb, int64_t drop_mode, double p, c10::optional<torch::Tensor> seed,
+               c10::optional<torch::Tensor> da, c10::optional<torch::Tensor> part_out) {
   check_f32(dy, "dy"); check_f32(s, "s"); check_f32(mean, "mean"); check_f32(rstd, "rstd"); check_f32(gamma, "gamma");
   check_f32(dx, "dx"); check_f32(dgb, "dgb");
   const int D = (int)s.size(-1);
@@ -857,11 +878,15 @@ void ln_bwd(torch::Tensor dy, torch::Tensor s, torch::Tensor mean, torch::Tensor
   for (auto* t : {&dy, &s, &dx}) TORCH_CHECK(t->is_contiguous() && t->numel() == R * D, "ln_bwd: contiguous [R, D]");
   const ndp::LnDrop dp = ln_drop(drop_mode, p, seed, da, R * D);
   TORCH_CHECK(dp.mode != 1 || dp.da != nullptr, "ln_bwd: input dropout needs da");
-  auto part = torch::empty({(int64_t)ndp::ln_bwd_wgs(R) * 2 * D}, s.options());
+  const int wgs = ndp::ln_bwd_wgs(R);
+  float* pp = deferred_part(part_out, (int64_t)wgs * 2 * D, "ln_bwd");
+  torch::Tensor part;
+  if (pp == nullptr) part = torch::empty({(int64_t)wgs * 2 * D}, s.options());
   ndp::launch_ln_bwd(dy.data_ptr<float>(), s.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
-                     gamma.data_ptr<float>(), dx.data_ptr<float>(), part.data_ptr<float>(), dgb.data_ptr<float>(), R, D,
-                     cur_stream(), dp);
+                     gamma.data_ptr<float>(), dx.data_ptr<float>(), pp ? pp : part.data_ptr<float>(),
+                     pp ? nullptr : dgb.data_ptr<float>(), R, D, cur_stream(), dp);
   check_launch("launch_ln_bwd");
+  return pp ? wgs : 0;
 }
 
 void embedding_backward(torch::Tensor ids, torch::Tensor gout, torch::Tensor gw, int64_t pad, torch::Tensor perm,
@@ -1294,15 +1319,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("tg_wgrad", &tg_wgrad, py::arg("x"), py::arg("dy"), py::arg("out"), py::arg("geom"),
         py::arg("part") = py::none(), py::arg("defer") = false);
   m.def("embedding_backward", &embedding_backward);
-  m.def("colsum", &colsum);
-  m.def("gelu_bwd_colsum", &gelu_bwd_colsum);
+  m.def("colsum", &colsum, py::arg("g"), py::arg("out"), py::arg("part") = c10::optional<torch::Tensor>());
+  m.def("gelu_bwd_colsum", &gelu_bwd_colsum, py::arg("g"), py::arg("h"), py::arg("dh"), py::arg("db"),
+        py::arg("part") = c10::optional<torch::Tensor>());
   m.def("ce_fwd", &ce_fwd);
   m.def("ln_fwd", &ln_fwd, py::arg("a"), py::arg("b"), py::arg("gamma"), py::arg("beta"), py::arg("y"), py::arg("s"),
         py::arg("mean"), py::arg("rstd"), py::arg("eps"), py::arg("drop_mode") = 0, py::arg("p") = 0.0,
         py::arg("seed") = c10::optional<torch::Tensor>());
   m.def("ln_bwd", &ln_bwd, py::arg("dy"), py::arg("s"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"),
         py::arg("dx"), py::arg("dgb"), py::arg("drop_mode") = 0, py::arg("p") = 0.0,
-        py::arg("seed") = c10::optional<torch::Tensor>(), py::arg("da") = c10::optional<torch::Tensor>());
+        py::arg("seed") = c10::optional<torch::Tensor>(), py::arg("da") = c10::optional<torch::Tensor>(),
+        py::arg("part") = c10::optional<torch::Tensor>());
+  m.def("ln_bwd_wgs", [](int64_t R) { return (int64_t)ndp::ln_bwd_wgs(R); });
+  m.def("colsum_chunks", [](int64_t M, int64_t N) { return (int64_t)ndp::colsum_chunks(M, (int)N); });
   m.def("ce_bwd", &ce_bwd);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);

@@ -207,7 +207,7 @@ void launch_ln_bwd(const float* dy, const float* s, const float* mean, const flo
   const int wgs = ln_bwd_wgs(R);
   const int rpw = (int)((R + 4LL * wgs - 1) / (4LL * wgs));
   LN_SWITCH(D, dp.mode, ln_bwd_go, (dim3(wgs), st, dy, s, mean, rstd, gamma, dx, part, R, rpw, dp))
-  launch_slab_sum(part, dgb, 2LL * D, wgs, st);
+  if (dgb != nullptr) launch_slab_sum(part, dgb, 2LL * D, wgs, st);  // else: the caller sums (deferred)
 }
 
 }  // namespace ndp

@@ -120,7 +120,7 @@ void launch_gelu_bwd_colsum(const float* g, const float* h, float* dh, int64_t M
   const int rpc = (int)((M + chunks - 1) / chunks);
   const int strips = (N / 4 + 63) / 64;
   hipLaunchKernelGGL(gelu_bwd_colsum_partial_kernel, dim3(strips, chunks), dim3(256), 0, s, g, h, dh, M, N, rpc, part);
-  launch_slab_sum(part, out, N, chunks, s);
+  if (out != nullptr) launch_slab_sum(part, out, N, chunks, s);  // else: the caller sums (deferred)
 }
 
 int colsum_chunks(int64_t M, int N) {
@@ -136,7 +136,7 @@ void launch_colsum(const float* g, int64_t M, int N, float* part, float* out, hi
   const int rpc = (int)((M + chunks - 1) / chunks);
   const int strips = (N / 4 + 63) / 64;
   hipLaunchKernelGGL(colsum_partial_kernel, dim3(strips, chunks), dim3(256), 0, s, g, M, N, rpc, part);
-  launch_slab_sum(part, out, N, chunks, s);
+  if (out != nullptr) launch_slab_sum(part, out, N, chunks, s);  // else: the caller sums (deferred)
 }
 
 }  // namespace ndp

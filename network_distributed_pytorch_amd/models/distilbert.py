@@ -75,7 +75,7 @@ class Embeddings(nn.Module):
             self._pos[key] = torch.arange(s, device=device).expand(b, s).contiguous()
         return self._pos[key]
 
-    def forward(self, input_ids):
+    def forward(self, input_ids, seed=None):
         b, s = input_ids.shape
         if input_ids.is_cuda and self.LayerNorm.native:
             # per-token position rows: the native embedding backward sums them over the batch
@@ -83,7 +83,7 @@ class Embeddings(nn.Module):
             pos = self.position_embeddings(self._pos_ids(b, s, input_ids.device))
             # the dropout rides in the LayerNorm kernels (hash mask regenerated in backward)
             return self.LayerNorm(self.word_embeddings(input_ids), residual=pos,
-                                  p_out=self.dropout.p if self.training else 0.0)
+                                  p_out=self.dropout.p if self.training else 0.0, seed=seed)
         pos = torch.arange(s, device=input_ids.device)
         x = self.word_embeddings(input_ids) + self.position_embeddings(pos)[None]
         return self.dropout(self.LayerNorm(x))
@@ -101,9 +101,10 @@ class MultiHeadSelfAttention(nn.Module):
         self.dropout = nn.Dropout(c.attention_dropout)
         self.fused = c.fused_attention
 
-    def forward(self, x, mask: Optional[torch.Tensor], link=None):
+    def forward(self, x, mask: Optional[torch.Tensor], link=None, seed=None):
         """``link`` (ops/gradlink.GradLink): the block's residual gradient, folded into the
-        first projection's grad-x GEMM."""
+        first projection's grad-x GEMM.  ``seed``: the fused kernels' dropout seed (device
+        int32; None draws one)."""
         bs, s, d = x.shape
         h = self.n_heads
         dh = d // h
@@ -112,12 +113,12 @@ class MultiHeadSelfAttention(nn.Module):
             # in the PowerSGD arena: no copy; ops/linear.packed_qkv), read in place by the
             # fused attention kernels (ops/attention.attention_qkv)
             qkv = packed_qkv(x, self.q_lin, self.k_lin, self.v_lin, link)
-            ctx = attention_qkv(qkv, h, mask, self.dropout.p if self.training else 0.0)
+            ctx = attention_qkv(qkv, h, mask, self.dropout.p if self.training else 0.0, seed=seed)
             return self.out_lin(ctx.reshape(bs, s, d))
         q4 = self.q_lin(x, link=link).view(bs, s, h, dh)
         if self.fused and fused_ok(q4):
             ctx = attention(q4, self.k_lin(x).view(bs, s, h, dh), self.v_lin(x).view(bs, s, h, dh), mask,
-                            self.dropout.p if self.training else 0.0)
+                            self.dropout.p if self.training else 0.0, seed=seed)
             return self.out_lin(ctx.reshape(bs, s, d))
 
         def split(t):
@@ -159,15 +160,17 @@ class TransformerBlock(nn.Module):
         self.output_layer_norm = AddLayerNorm(c.dim, eps=c.layer_norm_eps)
         self.sa_layer_norm.native = self.output_layer_norm.native = c.fused_attention
 
-    def forward(self, x, mask):
+    def forward(self, x, mask, seeds=None):
+        """``seeds``: [2] device int32 dropout seeds (attention, FFN) or None (drawn per call)."""
+        s0, s1 = (seeds[0:1], seeds[1:2]) if seeds is not None else (None, None)
         # residual gradients: deposited by the fused LayerNorm backward, added in place by the
         # sublayer's first GEMM (ops/gradlink.GradLink) instead of an autograd add
         lk = self._link(self.sa_layer_norm, x)
-        x = self.sa_layer_norm(self.attention(x, mask, link=lk), residual=x, link=lk)
+        x = self.sa_layer_norm(self.attention(x, mask, link=lk, seed=s0), residual=x, link=lk)
         lk = self._link(self.output_layer_norm, x)
         # the FFN's output dropout rides in the LayerNorm kernels (hash mask, no mask tensor)
         return self.output_layer_norm(self.ffn(x, link=lk, dropout=False), residual=x, link=lk,
-                                      p_in=self.ffn.dropout.p if self.training else 0.0)
+                                      p_in=self.ffn.dropout.p if self.training else 0.0, seed=s1)
 
     def _link(self, ln, x):
         if LN_LINKS and self.training and torch.is_grad_enabled() and x.requires_grad and ln.fused_ok(x, x):
@@ -180,11 +183,11 @@ class Transformer(nn.Module):
         super().__init__()
         self.layer = nn.ModuleList([TransformerBlock(c) for _ in range(c.n_layers)])
 
-    def forward(self, x, mask):
+    def forward(self, x, mask, seeds=None):
         if mask is not None and x.is_cuda:
             mask = mask.to(torch.int32).contiguous()   # once per pass, not per layer
-        for blk in self.layer:
-            x = blk(x, mask)
+        for i, blk in enumerate(self.layer):
+            x = blk(x, mask, seeds[2 * i: 2 * i + 2] if seeds is not None else None)
         return x
 
 
@@ -195,7 +198,14 @@ class DistilBertModel(nn.Module):
         self.transformer = Transformer(c)
 
     def forward(self, input_ids, attention_mask=None):
-        return self.transformer(self.embeddings(input_ids), attention_mask)
+        seeds = None
+        if self.training and input_ids.is_cuda and self.embeddings.LayerNorm.native:
+            # every fused dropout site's seed in ONE draw (13 for 6 layers) instead of one
+            # generator launch per site
+            n = 2 * len(self.transformer.layer) + 1
+            seeds = torch.randint(0, 2 ** 31 - 1, (n,), device=input_ids.device, dtype=torch.int32)
+        x = self.embeddings(input_ids, seeds[-1:] if seeds is not None else None)
+        return self.transformer(x, attention_mask, seeds)
 
 
 class SequenceClassifierOutput(tuple):

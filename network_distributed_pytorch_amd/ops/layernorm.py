@@ -25,6 +25,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import gradfinish
 from ._ext import ext
 
 __all__ = ["AddLayerNorm", "add_layer_norm", "ln_keep_mask"]
@@ -66,6 +67,7 @@ class _AddLayerNormFn(torch.autograd.Function):
         ctx.has_res = r is not None
         ctx.link = link  # ops/gradlink.GradLink: the residual's gradient goes there instead
         ctx.mode, ctx.p = mode, p
+        ctx.params = (weight, bias)
         ctx.save_for_backward(s, mean, rstd, weight, seed)
         return y
 
@@ -77,7 +79,13 @@ class _AddLayerNormFn(torch.autograd.Function):
         dgb = torch.empty(2 * D, device=s.device, dtype=torch.float32)
         # input dropout: the sublayer's gradient is the masked copy written by the same pass
         da = torch.empty_like(s) if ctx.mode == 1 else None
-        ext().ln_bwd(dy.contiguous(), s, mean, rstd, weight, dx, dgb, ctx.mode, ctx.p, seed, da)
+        part = None
+        if gradfinish.enabled() and all(gradfinish.can_defer(p) for p in ctx.params):
+            # the [dgamma | dbeta] partial sum waits for gradfinish's one batched launch
+            part = torch.empty(ext().ln_bwd_wgs(s.numel() // D) * 2 * D, device=s.device, dtype=s.dtype)
+        left = ext().ln_bwd(dy.contiguous(), s, mean, rstd, weight, dx, dgb, ctx.mode, ctx.p, seed, da, part)
+        if part is not None:
+            gradfinish.defer_slab(part, dgb, left)
         # d(x + residual) reaches both inputs unchanged; with a link the residual's copy is
         # added by the sublayer's first GEMM (after every reader of dx for x has run)
         dres = dx if ctx.has_res else None
@@ -127,11 +135,12 @@ class AddLayerNorm(nn.LayerNorm):
                 and (residual is None or (residual.dtype == torch.float32 and residual.shape == x.shape)))
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, link=None, p_in: float = 0.0,
-                p_out: float = 0.0) -> torch.Tensor:
-        """``LN(dropout(x, p_in) + residual)``, then ``dropout(., p_out)`` (dropouts fused on device)."""
+                p_out: float = 0.0, seed: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """``LN(dropout(x, p_in) + residual)``, then ``dropout(., p_out)`` (dropouts fused on device;
+        ``seed`` a device int32 for their mask, None draws one)."""
         if self.native and len(self.normalized_shape) == 1 and self.elementwise_affine:
             return add_layer_norm(x, residual, self.weight, self.bias, self.eps,
-                                  link if self.fused_ok(x, residual) else None, p_in, p_out)
+                                  link if self.fused_ok(x, residual) else None, p_in, p_out, seed)
         if p_in > 0:
             x = F.dropout(x, p_in)
         y = super().forward(x if residual is None else x + residual)

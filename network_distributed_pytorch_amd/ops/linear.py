@@ -14,6 +14,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import gradfinish
 from ._ext import ext
 from .gradarena import grad_buffer, registered
 from .gradlink import InjectGrad
@@ -25,6 +26,23 @@ __all__ = ["Linear", "linear", "linear_gelu", "packed_qkv"]
 # column-strip workgroups, one load in flight per thread); with ~1024 workgroups and 4 rows in
 # flight per thread it is on: DistilBERT r=8, 1x MI355X, 20.70 vs 20.74 ms (profiles/r4).
 _FUSED_GELU = os.environ.get("NDP_FUSED_GELU", "1") != "0"
+
+
+def _deferrable(out: torch.Tensor, params) -> bool:
+    """The final fixed-order sum of a bias gradient may wait for gradfinish's batched launch
+    (one ``slab_sum_many`` for every deferred gradient of the backward pass)."""
+    return (gradfinish.enabled() and out.data_ptr() % 16 == 0 and out.is_contiguous()
+            and all(p is not None and gradfinish.can_defer(p) for p in params))
+
+
+def _bias_sum(g2: torch.Tensor, db: torch.Tensor, params) -> None:
+    """db = g2.sum(0) (csrc/linear.hip colsum), its last pass deferred when allowed."""
+    if _deferrable(db, params):
+        M, N = g2.shape
+        part = torch.empty(ext().colsum_chunks(M, N) * N, device=g2.device, dtype=g2.dtype)
+        gradfinish.defer_slab(part, db, ext().colsum(g2, db, part))
+    else:
+        ext().colsum(g2, db)
 
 
 class _LinearFn(torch.autograd.Function):
@@ -55,7 +73,7 @@ class _LinearFn(torch.autograd.Function):
             dw = torch.mm(g2.t(), x.reshape(-1, k), out=grad_buffer(ctx.params[0]))
         if ctx.needs_input_grad[2]:
             db = grad_buffer(ctx.params[1])
-            ext().colsum(g2, db)
+            _bias_sum(g2, db, (ctx.params[1],))
         return dx, dw, db, None
 
 
@@ -69,6 +87,7 @@ class _LinearGeluFn(torch.autograd.Function):
         h = F.linear(x, weight, bias)
         ctx.save_for_backward(x, weight, h)
         ctx.link = link
+        ctx.bias = bias
         return F.gelu(h)
 
     @staticmethod
@@ -81,7 +100,12 @@ class _LinearGeluFn(torch.autograd.Function):
         h2 = h.reshape(-1, n)
         dh = torch.empty_like(h2)
         db = torch.empty(n, device=da.device, dtype=da.dtype)
-        ext().gelu_bwd_colsum(g2, h2, dh, db)
+        if ctx.needs_input_grad[2] and _deferrable(db, (ctx.bias,)):
+            M = g2.shape[0]
+            part = torch.empty(ext().colsum_chunks(M, n) * n, device=da.device, dtype=da.dtype)
+            gradfinish.defer_slab(part, db, ext().gelu_bwd_colsum(g2, h2, dh, db, part))
+        else:
+            ext().gelu_bwd_colsum(g2, h2, dh, db)
         addend = ctx.link.take() if ctx.link is not None else None
         dx = dw = None
         if ctx.needs_input_grad[0]:
@@ -154,7 +178,7 @@ class _PackedQKVFn(torch.autograd.Function):
             torch.mm(g2.t(), x2, out=dw)
             dws = [dw[i * d:(i + 1) * d] for i in range(3)]
         db = torch.empty(n, device=g.device, dtype=g.dtype)
-        ext().colsum(g2, db)
+        _bias_sum(g2, db, (bq, bk, bv))
         dbs = [db[i * d:(i + 1) * d] for i in range(3)]
         return (dx,) + tuple(dws) + tuple(dbs) + (None,)
 
