@@ -485,23 +485,54 @@ __device__ __forceinline__ int xcd_block(int bid, int nblk) {
   return xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
 }
 
-template <int HW, int BWD, int CW, int MAXN = kFusedMaxN>
+// RS > 1 (row splits): the RS workgroups of a column block (consecutive logical blocks, so the
+// same XCD) each take 1 / RS of the images and exchange their per-column sums through global
+// memory behind a counter barrier — the cdna_hip_programming.md §6 Guideline 16 protocol
+// csrc/orth.hip uses (plain stores, vmcnt drain, release fence, relaxed agent counter; poller:
+// relaxed loads, one acquire fence).  Counters live in the module's zero-initialised scratch
+// (BnSync) and are never reset: every launch adds exactly kBnSyncPeriod to the counter of each
+// column block it runs (each workgroup kBnSyncPeriod / RS), so a launch starts on a multiple of
+// the period.  Grids are <= 256 workgroups of one CU each: always co-resident.  A spin past
+// kBnMaxSpins poisons the block's statistics with NaN and sets the error word instead of
+// hanging.  Every workgroup of a block then adds the RS partials in split order: the same
+// value everywhere (deterministic), so RS = 2 / 4 lets 256 workgroups work where the column
+// blocks alone give 64-128 (ResNet layer2-4 maps).  Opt-in (NDP_BN_ROWSPLIT, bn_row_splits).
+constexpr int kBnSyncPeriod = 4;       // = the largest RS
+constexpr int kBnSyncBlocks = 4096;    // column blocks with a counter
+constexpr unsigned kBnMaxSpins = 1u << 22;
+struct BnSync {
+  unsigned long long* ctr;  // [kBnSyncBlocks]
+  unsigned* err;            // [1]
+  double* xch;              // [blocks][RS][CW][2]
+};
+
+template <int HW, int BWD, int CW, int MAXN = kFusedMaxN, int RS = 1>
 __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
     const float* __restrict__ x, const float* __restrict__ res, const float* __restrict__ dy,
     const float* __restrict__ yin, const float* __restrict__ gamma, const float* __restrict__ beta,
     float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt, float* __restrict__ save_mean,
     float* __restrict__ save_invstd, float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ out,
     float* __restrict__ dres, int N, int C, float eps, float momentum, int relu, const float* __restrict__ src,
-    int nslab) {
+    int nslab, BnSync sy) {
   constexpr int RG = kFusedThreads / CW;
-  constexpr int NP = MAXN / RG;
+  constexpr int NP = MAXN / RG / RS;  // rows per thread in this workgroup's split
   constexpr int NW = kFusedThreads / 64;
   static_assert(CW % HW == 0 && 64 % CW == 0, "bad column block");
+  static_assert(NP >= 1 && kBnSyncPeriod % RS == 0, "bad row split");
   __shared__ double red[2][NW][CW];
+  __shared__ unsigned long long base_s;
+  __shared__ int bad_s;
   const int CHW = C * HW;
   const int col = threadIdx.x % CW, g = threadIdx.x / CW;
-  const int j = xcd_block((int)blockIdx.x, (int)gridDim.x) * CW + col;
+  const int lb = xcd_block((int)blockIdx.x, (int)gridDim.x);
+  const int cb = lb / RS, rs = lb - cb * RS;
+  const int j = cb * CW + col;
   const bool ok_col = j < CHW;
+  if (RS > 1 && threadIdx.x == 0) {  // this launch's barrier cannot complete before we arrive
+    const unsigned long long c0 = __hip_atomic_load(sy.ctr + cb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    base_s = c0 - c0 % kBnSyncPeriod;
+    bad_s = 0;
+  }
   const int c = ok_col ? j / HW : 0;
   float v[NP], d[NP], m[NP];
   float mean_s = 0.f, invstd_s = 0.f;
@@ -511,7 +542,7 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
   }
 #pragma unroll
   for (int k = 0; k < NP; ++k) {  // every load in flight before any use
-    const int n = g + k * RG;
+    const int n = g + (rs * NP + k) * RG;
     const bool ok = ok_col && n < N;
     const int64_t o = (int64_t)n * CHW + j;
     float sum = 0.f;
@@ -532,14 +563,14 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
   if (!BWD && src != nullptr) {  // BN's saved input = the conv output
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
-      const int n = g + k * RG;
+      const int n = g + (rs * NP + k) * RG;
       if (ok_col && n < N) const_cast<float*>(x)[(int64_t)n * CHW + j] = v[k];
     }
   }
   double a = 0.0, b = 0.0;
 #pragma unroll
   for (int k = 0; k < NP; ++k) {
-    if (ok_col && g + k * RG < N) {
+    if (ok_col && g + (rs * NP + k) * RG < N) {
       if (!BWD) {
         a += (double)v[k];
         b += (double)v[k] * (double)v[k];
@@ -572,9 +603,45 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
     A += red[0][k][col];
     B += red[1][k][col];
   }
+  if constexpr (RS > 1) {  // the RS splits' partials, added in split order (module header)
+    double* xb = sy.xch + (int64_t)cb * RS * CW * 2;
+    if (g == 0) {
+      xb[(rs * CW + col) * 2] = A;
+      xb[(rs * CW + col) * 2 + 1] = B;
+    }
+    if (threadIdx.x < 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(sy.ctr + cb, (unsigned long long)(kBnSyncPeriod / RS), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long target = base_s + kBnSyncPeriod;
+      unsigned spins = 0;
+      while ((long long)(__hip_atomic_load(sy.ctr + cb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > kBnMaxSpins) {  // report and poison instead of hanging
+          __hip_atomic_fetch_or(sy.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          bad_s = 1;
+          break;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    A = 0.0;
+    B = 0.0;
+#pragma unroll
+    for (int r = 0; r < RS; ++r) {
+      A += xb[(r * CW + col) * 2];
+      B += xb[(r * CW + col) * 2 + 1];
+    }
+    if (bad_s) A = B = __builtin_nan("");
+  }
   if (!ok_col) return;
   const double M = (double)N * HW;
-  const bool writer = g == 0 && (j % HW) == 0;
+  const bool writer = g == 0 && (j % HW) == 0 && rs == 0;
   if (!BWD) {
     const double mu = A / M;
     double var = B / M - mu * mu;
@@ -594,7 +661,7 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
     }
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
-      const int n = g + k * RG;
+      const int n = g + (rs * NP + k) * RG;
       if (n < N) {
         const float z = fmaf(v[k], scale, shift) + d[k];
         out[(int64_t)n * CHW + j] = relu ? fmaxf(z, 0.f) : z;
@@ -609,7 +676,7 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
     const float mdz = (float)(A / M), mdzx = (float)(B / M);
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
-      const int n = g + k * RG;
+      const int n = g + (rs * NP + k) * RG;
       if (n < N) {
         const float dz = (m[k] > 0.f) ? d[k] : 0.f;
         const float xh = (v[k] - mean_s) * invstd_s;
@@ -680,17 +747,36 @@ static int bn_colw_for(int HW, int C, int N) {
   return HW > lo ? HW : lo;
 }
 
-template <int BWD, int CW>
-static void launch_small_fused_cw(int HW, const float* x, const float* res, const float* dy, const float* yin,
+// row splits of the single-launch kernel: the smallest RS (1 / 2 / 4) that gives the launch
+// >= 256 workgroups, only while every thread keeps >= 2 rows
+static int bn_row_splits(int nblk, int N, int CW) {
+  // NDP_BN_ROWSPLIT: largest RS (1 / 2 / 4).  Default 1: measured slower on 1x MI355X (ResNet-18
+  // r=4 batch 512: RS <= 1 1.908 ms, <= 2 1.960, <= 4 1.966; profiles/r4/bench_bn_rowsplit.jsonl)
+  // — the barrier round trip costs more than the extra CUs bring at these 1-4 MB tensors.
+  static int cap = -1;
+  if (cap < 0) {
+    const char* e = getenv("NDP_BN_ROWSPLIT");
+    cap = e ? atoi(e) : 1;
+    if (cap < 1) cap = 1;
+  }
+  const int rg = kFusedThreads / CW;
+  int rs = 1;
+  while (rs < kBnSyncPeriod && rs < cap && nblk * rs < 256 && N >= 2 * rg * rs * 2 && nblk <= kBnSyncBlocks) rs *= 2;
+  return rs;
+}
+
+template <int BWD, int CW, int RS>
+static void launch_small_fused_rs(int HW, const float* x, const float* res, const float* dy, const float* yin,
                                   const float* gamma, const float* beta, float* rmean, float* rvar, int64_t* nbt,
                                   float* sm, float* si, float* dgamma, float* dbeta, float* out, float* dres, int N,
                                   int C, float eps, float momentum, int relu, hipStream_t s, const float* src,
-                                  int nslab) {
-  const dim3 grid((unsigned)(((int64_t)C * HW + CW - 1) / CW));
+                                  int nslab, const BnSync& sy, int nblk) {
+  const dim3 grid((unsigned)(nblk * RS));
 #define NDP_BN_FUSED(HWV)                                                                                            \
   if constexpr (CW % HWV == 0)                                                                                       \
-    hipLaunchKernelGGL((bn_small_fused_kernel<HWV, BWD, CW>), grid, dim3(kFusedThreads), 0, s, x, res, dy, yin, gamma, \
-                       beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out, dres, N, C, eps, momentum, relu, src, nslab)
+    hipLaunchKernelGGL((bn_small_fused_kernel<HWV, BWD, CW, kFusedMaxN, RS>), grid, dim3(kFusedThreads), 0, s, x,    \
+                       res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out, dres, N, C, eps,     \
+                       momentum, relu, src, nslab, sy)
   switch (HW) {  // the caller picks CW >= HW
     case 1: NDP_BN_FUSED(1); break;
     case 2: NDP_BN_FUSED(2); break;
@@ -701,32 +787,55 @@ static void launch_small_fused_cw(int HW, const float* x, const float* res, cons
 #undef NDP_BN_FUSED
 }
 
+template <int BWD, int CW>
+static void launch_small_fused_cw(int HW, const float* x, const float* res, const float* dy, const float* yin,
+                                  const float* gamma, const float* beta, float* rmean, float* rvar, int64_t* nbt,
+                                  float* sm, float* si, float* dgamma, float* dbeta, float* out, float* dres, int N,
+                                  int C, float eps, float momentum, int relu, hipStream_t s, const float* src,
+                                  int nslab, const BnSync& sy) {
+  const int nblk = (int)(((int64_t)C * HW + CW - 1) / CW);
+  switch (sy.ctr != nullptr ? bn_row_splits(nblk, N, CW) : 1) {
+    case 4:
+      launch_small_fused_rs<BWD, CW, 4>(HW, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta,
+                                        out, dres, N, C, eps, momentum, relu, s, src, nslab, sy, nblk);
+      break;
+    case 2:
+      launch_small_fused_rs<BWD, CW, 2>(HW, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta,
+                                        out, dres, N, C, eps, momentum, relu, s, src, nslab, sy, nblk);
+      break;
+    default:
+      launch_small_fused_rs<BWD, CW, 1>(HW, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta,
+                                        out, dres, N, C, eps, momentum, relu, s, src, nslab, sy, nblk);
+  }
+}
+
 template <int BWD>
 static void launch_small_fused(int HW, const float* x, const float* res, const float* dy, const float* yin,
                                const float* gamma, const float* beta, float* rmean, float* rvar, int64_t* nbt,
                                float* sm, float* si, float* dgamma, float* dbeta, float* out, float* dres, int N,
                                int C, float eps, float momentum, int relu, hipStream_t s, const float* src,
-                               int nslab) {
+                               int nslab, const BnSync& sy) {
   if (HW == 64) {  // one workgroup per channel: 64 lanes x 8 row groups, <= 128 images
     hipLaunchKernelGGL((bn_small_fused_kernel<64, BWD, 64, kFused64MaxN>), dim3((unsigned)C), dim3(kFusedThreads), 0,
                        s, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out, dres, N, C, eps,
-                       momentum, relu, src, nslab);
+                       momentum, relu, src, nslab, sy);
     return;
   }
   switch (bn_colw_for(HW, C, N)) {
     case 16:
       launch_small_fused_cw<BWD, 16>(HW, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out,
-                                     dres, N, C, eps, momentum, relu, s, src, nslab);
-      break;
-    default:
-      launch_small_fused_cw<BWD, 8>(HW, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out,
-                                    dres, N, C, eps, momentum, relu, s, src, nslab);
+                                     dres, N, C, eps, momentum, relu, s, src, nslab, sy);
       break;
     case 4:
       launch_small_fused_cw<BWD, 4>(HW, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out,
-                                    dres, N, C, eps, momentum, relu, s, src, nslab);
+                                    dres, N, C, eps, momentum, relu, s, src, nslab, sy);
+      break;
+    default:
+      launch_small_fused_cw<BWD, 8>(HW, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out,
+                                    dres, N, C, eps, momentum, relu, s, src, nslab, sy);
   }
 }
+
 
 template <int HW>
 static void small_stats(const float* x, const float* dy, const float* y, const float* sm, const float* si,
@@ -761,10 +870,24 @@ bool bn_small_path(int N, int C, int HW) {
          (int64_t)N * C * HW < (1LL << 30);
 }
 
+// scratch layout (fp64 slots, zero-initialised once by the module): [kBnSyncBlocks counters |
+// error word | padding to 16 slots] then the per-launch region (slice partials, coefficients,
+// or the row-split exchange of the single-launch kernel: <= 8 doubles per column)
+constexpr int64_t kBnSyncSlots = kBnSyncBlocks + 16;
+
+static BnSync bn_sync(double* part, int single_ok) {
+  if (!single_ok) return BnSync{nullptr, nullptr, nullptr};
+  return BnSync{reinterpret_cast<unsigned long long*>(part), reinterpret_cast<unsigned*>(part + kBnSyncBlocks),
+                part + kBnSyncSlots};
+}
+
 int64_t bn_part_numel(int N, int C, int HW) {
   const int64_t big = (int64_t)C * bn_slices(N, C, HW) * 2;
   const int64_t small = (int64_t)C * bn_small_slices(N, C, HW) * 2 + 3 * (int64_t)C;
-  return big > small ? big : small;
+  const int64_t xch = 8 * (int64_t)C * HW;
+  int64_t m = big > small ? big : small;
+  if (xch > m) m = xch;
+  return kBnSyncSlots + m;
 }
 
 // ----------------------------------- launchers -------------------------------------------
@@ -798,6 +921,8 @@ void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamm
                    float* rmean, float* rvar, int64_t* nbt, float* save_mean, float* save_invstd,
                    double* part, int N, int C, int HW, int S, float eps, float momentum, int relu,
                    int training, int single, hipStream_t s, const float* xpart, int nslab) {
+  const BnSync sy = bn_sync(part, 1);
+  part += kBnSyncSlots;
   if (xpart != nullptr && nslab < 2) xpart = nullptr;
   if (xpart != nullptr && nslab > kMaxFusedSlabs) {  // many slabs: the wide sum kernel first
     launch_slab_sum(xpart, const_cast<float*>(x), (int64_t)N * C * HW, nslab, s);
@@ -805,7 +930,7 @@ void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamm
   }
   if (training && single && bn_fused_ok(N, C, HW)) {
     launch_small_fused<0>(HW, x, res, nullptr, nullptr, gamma, beta, rmean, rvar, nbt, save_mean, save_invstd,
-                          nullptr, nullptr, y, nullptr, N, C, eps, momentum, relu, s, xpart, nslab);
+                          nullptr, nullptr, y, nullptr, N, C, eps, momentum, relu, s, xpart, nslab, sy);
     return;
   }
   const bool vec_ok = (HW % 4) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 &&
@@ -845,6 +970,8 @@ void launch_bn_bwd(const float* dy, const float* y, const float* x, const float*
                    const float* save_invstd, float* dx, float* dres, float* dgamma, float* dbeta, double* part,
                    int N, int C, int HW, int S, int relu, int single, hipStream_t s, const float* dypart,
                    int nslab) {
+  const BnSync sy = bn_sync(part, 1);
+  part += kBnSyncSlots;
   if (dypart != nullptr && nslab < 2) dypart = nullptr;
   if (dypart != nullptr && nslab > kMaxFusedSlabs) {
     launch_slab_sum(dypart, const_cast<float*>(dy), (int64_t)N * C * HW, nslab, s);
@@ -853,7 +980,7 @@ void launch_bn_bwd(const float* dy, const float* y, const float* x, const float*
   if (single && bn_fused_ok(N, C, HW)) {
     launch_small_fused<1>(HW, x, nullptr, dy, y, gamma, nullptr, nullptr, nullptr, nullptr,
                           const_cast<float*>(save_mean), const_cast<float*>(save_invstd), dgamma, dbeta, dx, dres, N, C,
-                          0.f, 0.f, relu, s, dypart, nslab);
+                          0.f, 0.f, relu, s, dypart, nslab, sy);
     return;
   }
   const bool vec_ok = (HW % 4) == 0 && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)x & 15) == 0 &&

@@ -110,3 +110,23 @@ def test_bn_single_launch_small_path(device, shape):
     for t0, t1, t2 in zip(*outs):
         assert torch.equal(t0, t2)              # deterministic
         torch.testing.assert_close(t0, t1, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("shape", [(512, 512, 1, 1), (512, 256, 2, 2), (512, 128, 4, 4), (256, 64, 2, 2)])
+def test_bn_single_launch_row_splits_running_stats(device, shape):
+    """(Run with NDP_BN_ROWSPLIT=4 to exercise the opt-in row splits.)  Row-split single-launch BN (workgroups of a column block exchanging partial sums behind
+    a counter barrier): running statistics written once per channel, equal to the 3-kernel
+    path; repeated launches (counters never reset) stay exact."""
+    torch.manual_seed(3)
+    C = shape[1]
+    a = BatchNormAct2d(C).to(device)
+    b = BatchNormAct2d(C).to(device)
+    b.fused_small = False
+    b.load_state_dict(a.state_dict())
+    for it in range(3):
+        x = torch.randn(shape, device=device) * (1.0 + it) + 0.3
+        ya, yb = a(x, relu=False), b(x, relu=False)
+        torch.testing.assert_close(ya, yb, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(a.running_mean, b.running_mean, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(a.running_var, b.running_var, rtol=1e-6, atol=1e-6)
+    assert a.num_batches_tracked.item() == b.num_batches_tracked.item() == 3
