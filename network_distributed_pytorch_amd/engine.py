@@ -78,6 +78,11 @@ def setup(config) -> None:
     device = device_for(config)
     if device.type == "cuda":
         torch.cuda.set_device(device)
+        # a library conv left on a path the native kernels do not cover runs MIOpen's
+        # deterministic solution (no find-database / benchmark choice): a resumed run then
+        # reproduces the uninterrupted one bitwise
+        torch.backends.cudnn.deterministic = True
+        torch.backends.cudnn.benchmark = False
     if not dist.is_available():
         print("[Failure] Distributed Environment Failed")
         return

@@ -38,7 +38,7 @@ import torch.nn.functional as F
 from ..ops import gradfinish
 from ..ops._ext import ext
 from ..ops import conv as _conv
-from ..ops.conv import DirectConvFn, direct_plan, side_stream
+from ..ops.conv import DirectConvFn, direct_plan, direct_plan_padded, side_stream
 from ..ops.gradarena import grad_buffer
 from ..ops.gradlink import InjectGrad
 from ..ops.smconv import SmConvFn, sm_plan
@@ -246,6 +246,13 @@ class GemmConv2d(nn.Conv2d):
             plan = direct_plan(x, self.weight, s, p)
             if plan is not None:
                 return DirectConvFn.apply(x, self.weight, plan, link, slab_out, grad_slab)
+            padded = direct_plan_padded(x, self.weight, s, p)
+            if padded is not None:  # ragged batch: zero-padded images, same kernels (links left empty)
+                plan, Bp = padded
+                B = x.shape[0]
+                xi = InjectGrad.apply(x, link) if link is not None else x
+                xp = torch.cat([xi, xi.new_zeros((Bp - B,) + tuple(x.shape[1:]))])
+                return DirectConvFn.apply(xp, self.weight, plan, None, None, None)[:B]
             splan = sm_plan(x, self.weight, s, p)
             if splan is not None:  # 2x2 / 1x1 maps: compile-time pair-list MFMA kernels (csrc/smallconv.hip)
                 return SmConvFn.apply(x, self.weight, splan, link, branch, slab_out, grad_slab)

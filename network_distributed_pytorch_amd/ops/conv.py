@@ -69,6 +69,24 @@ def direct_plan(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int
     return plan
 
 
+# batch quantum of the direct kernels: images per forward / grad-x workgroup (1 / 2 / 4) and
+# per grad-W slice (2 .. 16) always divide 16
+_BATCH_QUANT = 16
+
+
+def direct_plan_padded(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int) -> Optional[Tuple]:
+    """(plan, padded batch) for a batch the direct kernels cannot tile (a ragged last batch:
+    B not a multiple of their images per workgroup / slice): the conv then runs on the batch
+    zero-padded to a multiple of 16 instead of falling back to another library path (MIOpen's
+    algorithm choice is not deterministic run to run).  None if the geometry is not covered."""
+    B = x.shape[0]
+    Bp = -(-B // _BATCH_QUANT) * _BATCH_QUANT
+    if Bp == B or not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4):
+        return None
+    plan = direct_plan(x.new_empty((Bp,) + tuple(x.shape[1:])), weight, stride, padding)
+    return (plan, Bp) if plan is not None else None
+
+
 class DirectConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, plan, link=None, slab_out=None, grad_slab=None):
