@@ -163,14 +163,20 @@ py::tuple make_orth_geom(const std::vector<std::tuple<int64_t, int64_t, int64_t>
 int64_t n_of(const torch::Tensor& bytes, size_t sz) { return bytes.numel() / (int64_t)sz; }
 
 void psgd_p(torch::Tensor geom, torch::Tensor ptrs, torch::Tensor items, torch::Tensor q_warm,
-            torch::Tensor p_part, bool fuse_ef, int max_rank) {
+            torch::Tensor p_part, bool fuse_ef, int max_rank, c10::optional<torch::Tensor> p_prev) {
   check_dev(geom, "geom"); check_dev(ptrs, "ptrs"); check_dev(items, "items");
   check_f32(q_warm, "q_warm"); check_f32(p_part, "p_part");
+  const float* pp = nullptr;
+  if (p_prev.has_value()) {
+    check_f32(*p_prev, "p_prev");
+    TORCH_CHECK(fuse_ef && max_rank <= ndp::kUWideMaxRank, "psgd_p: lazy error feedback needs fuse_ef, rank <= 16");
+    pp = p_prev->data_ptr<float>();
+  }
   ndp::launch_psgd_p(reinterpret_cast<const MatGeom*>(geom.data_ptr()),
                      reinterpret_cast<const MatPtrs*>(ptrs.data_ptr()),
                      reinterpret_cast<const PItem*>(items.data_ptr()),
                      (int)n_of(items, sizeof(PItem)), q_warm.data_ptr<float>(),
-                     p_part.data_ptr<float>(), fuse_ef ? 1 : 0, max_rank, cur_stream());
+                     p_part.data_ptr<float>(), fuse_ef ? 1 : 0, max_rank, cur_stream(), pp);
   check_launch("launch_psgd_p");
 }
 
@@ -214,17 +220,22 @@ void psgd_orth(torch::Tensor geom, torch::Tensor items, torch::Tensor p, double 
 
 void psgd_update(torch::Tensor geom, torch::Tensor ptrs, torch::Tensor items, torch::Tensor p_hat,
                  torch::Tensor q_sum, double q_div, c10::optional<torch::Tensor> q_warm, int mode,
-                 double lr, double momentum, int max_rank) {
+                 double lr, double momentum, int max_rank, c10::optional<torch::Tensor> p_prev) {
   check_dev(geom, "geom"); check_dev(ptrs, "ptrs"); check_dev(items, "items");
   check_f32(p_hat, "p_hat"); check_f32(q_sum, "q_sum");
+  TORCH_CHECK(mode >= 0 && mode <= 3, "psgd_update: mode 0..3");
+  TORCH_CHECK((mode != 3 && !p_prev.has_value()) || max_rank <= ndp::kUWideMaxRank,
+              "psgd_update: lazy error feedback / materialise need rank <= 16");
   float* qw = nullptr;
   if (q_warm.has_value()) { check_f32(*q_warm, "q_warm"); qw = q_warm->data_ptr<float>(); }
+  float* pp = nullptr;
+  if (p_prev.has_value()) { check_f32(*p_prev, "p_prev"); pp = p_prev->data_ptr<float>(); }
   ndp::launch_psgd_update(reinterpret_cast<const MatGeom*>(geom.data_ptr()),
                           reinterpret_cast<const MatPtrs*>(ptrs.data_ptr()),
                           reinterpret_cast<const UItem*>(items.data_ptr()),
                           (int)n_of(items, sizeof(UItem)), p_hat.data_ptr<float>(),
                           q_sum.data_ptr<float>(), (float)q_div, qw, mode, (float)lr,
-                          (float)momentum, max_rank, cur_stream());
+                          (float)momentum, max_rank, cur_stream(), pp);
   check_launch("launch_psgd_update");
 }
 
@@ -1258,13 +1269,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("make_mat_ptrs", &make_mat_ptrs);
   m.def("make_seg_table", &make_seg_table);
   m.def("make_orth_geom", &make_orth_geom);
-  m.def("psgd_p", &psgd_p);
+  m.def("psgd_p", &psgd_p, py::arg("geom"), py::arg("ptrs"), py::arg("items"), py::arg("q_warm"), py::arg("p_part"),
+        py::arg("fuse_ef"), py::arg("max_rank"), py::arg("p_prev") = c10::optional<torch::Tensor>());
   m.def("psgd_q", &psgd_q);
   m.def("psgd_orth", &psgd_orth, py::arg("geom"), py::arg("items"), py::arg("p"), py::arg("p_div"),
         py::arg("eps"), py::arg("max_rank"), py::arg("scratch"), py::arg("ctr"), py::arg("n_items_total") = -1,
         py::arg("max_spins") = -1);
   m.def("orth_coresident_cap", &ndp::orth_coresident_cap);
-  m.def("psgd_update", &psgd_update);
+  m.def("psgd_update", &psgd_update, py::arg("geom"), py::arg("ptrs"), py::arg("items"), py::arg("p_hat"),
+        py::arg("q_sum"), py::arg("q_div"), py::arg("q_warm"), py::arg("mode"), py::arg("lr"), py::arg("momentum"),
+        py::arg("max_rank"), py::arg("p_prev") = c10::optional<torch::Tensor>());
   m.def("rank1_step", &rank1_step);
   m.def("seg_reduce", &seg_reduce);
   m.def("sgd_momentum", &sgd_momentum);

@@ -75,8 +75,10 @@ constexpr int kMaxRank = 64;
 constexpr int kSegBlockElems = 2048;  // elements per workgroup in seg_reduce
 
 // ---- launchers (powersgd.hip) --------------------------------------------------
+// p_prev (rank <= kUWideMaxRank only): lazy error feedback, e = M_prev - P_prev Qs^T formed here
 void launch_psgd_p(const MatGeom* geom, const MatPtrs* ptrs, const PItem* items, int n_items,
-                   const float* q_warm, float* p_part, int fuse_ef, int max_rank, hipStream_t s);
+                   const float* q_warm, float* p_part, int fuse_ef, int max_rank, hipStream_t s,
+                   const float* p_prev = nullptr);
 void launch_psgd_q(const MatGeom* geom, const MatPtrs* ptrs, const QItem* items, int n_items,
                    const float* p_hat, float* q_part, int max_rank, hipStream_t s);
 // partial: 2 * n_items_total * kMaxRank floats; counters: n_mats uint64 (zeroed once, never reset);
@@ -88,11 +90,14 @@ int orth_rows_per_thread(int max_rank);
 // workgroups of ONE matrix the MGS barrier may span: occupancy x CUs / 2 (-1: no device)
 int orth_coresident_cap(int max_rank);
 constexpr unsigned kOrthMaxSpins = 1u << 25;  // ~seconds of s_sleep 2
-// mode 0 = api (out/mem), 1 = engine (EF + momentum + SGD), 2 = engine + write grad
+// mode 0 = api (out/mem), 1 = engine (EF + momentum + SGD), 2 = engine + write grad,
+// 3 = e -= p_hat q_sum^T / q_div only (materialise the lazy error, rank <= kUWideMaxRank);
+// p_prev (modes 1 / 2, rank <= kUWideMaxRank): lazy error feedback — e is not written, the
+// P-hat rows are kept in p_prev for the next P pass
 void launch_psgd_update(const MatGeom* geom, const MatPtrs* ptrs, const UItem* items,
                         int n_items, const float* p_hat, const float* q_sum, float q_div,
                         float* q_warm, int mode, float lr, float momentum, int max_rank,
-                        hipStream_t s);
+                        hipStream_t s, float* p_prev = nullptr);
 // rank-1 (<=1-D) group of the fused engine: out = buf/div; m = lam*m + out; x -= lr*(out+m)
 void launch_rank1_step(const float* buf, float div, float* mom, float* x, float* g,
                        int64_t n, float lr, float momentum, hipStream_t s);

@@ -196,12 +196,19 @@ __device__ __forceinline__ bool spread_writer(int lane) {
   return (lane & (64 / V - 1)) == 0;  // the low 6 - log2(V) lane bits were plain butterflies
 }
 
+// Lazy error feedback (p_prev != nullptr): the update pass no longer writes e = M - P Q^T
+// (reading M back just for that store is 2 of its 6 HBM passes); e keeps M, p_prev keeps the
+// step's P-hat rows, and this pass forms e = M_prev - P_prev Qs^T element by element with the
+// update's exact arithmetic (Qs = the warm-start Q it reads anyway, the same fmaf chain over
+// c), so M = g + e is bitwise the eager formula's.  p_prev = 0 (first step, after a
+// checkpoint materialised e) makes the correction an exact zero.
 template <int RQ>
 __global__ __launch_bounds__(256) void psgd_p_wide_kernel(const MatGeom* __restrict__ geom,
                                                           const MatPtrs* __restrict__ ptrs,
                                                           const PItem* __restrict__ items,
                                                           const float* __restrict__ q_warm,
-                                                          float* __restrict__ p_part, int fuse_ef) {
+                                                          float* __restrict__ p_part, int fuse_ef,
+                                                          const float* __restrict__ p_prev) {
   constexpr int NS = kPKW / 256;          // 256-column slices per item
   constexpr int SB = RQ <= 8 ? NS : 2;    // slices whose loads are in flight together
   constexpr int V = 4 * RQ;
@@ -222,10 +229,10 @@ __global__ __launch_bounds__(256) void psgd_p_wide_kernel(const MatGeom* __restr
 
 #pragma unroll
   for (int s0 = 0; s0 < NS; s0 += SB) {
-    // the HBM stream of SB slices first: M = g [+ e] of the wave's 4 rows
-    f32x4 mv[4][SB];
+    // the HBM stream of SB slices first: g and e of the wave's 4 rows (combined below, once
+    // the lane's Q rows are in registers: the lazy correction needs them)
+    f32x4 mv[4][SB], ev[4][SB];
     if (g.vec) {
-      f32x4 ev[4][SB];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -236,37 +243,24 @@ __global__ __launch_bounds__(256) void psgd_p_wide_kernel(const MatGeom* __restr
           mv[i][sb] = ok ? ld4(pt.min + o) : f32x4{0.f, 0.f, 0.f, 0.f};
           ev[i][sb] = (ok && fuse_ef) ? ld4(pt.e + o) : f32x4{0.f, 0.f, 0.f, 0.f};
         }
-      if (fuse_ef) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int sb = 0; sb < SB; ++sb) {
-            const int b = it.k0 + 256 * (s0 + sb) + 4 * lane;
-            mv[i][sb] = mv[i][sb] + ev[i][sb];  // send = g + e   (ddp_init.py:156-157)
-            if (arow0 + i < n && b < it.k1) st4(pt.e + (int64_t)(arow0 + i) * m + b, mv[i][sb]);
-          }
-      }
     } else {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int sb = 0; sb < SB; ++sb) {
           const int b = it.k0 + 256 * (s0 + sb) + 4 * lane;
-          float t[4];
+          float t[4], u[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            float v = 0.f;
+            t[j] = u[j] = 0.f;
             if (arow0 + i < n && b + j < it.k1) {
               const int64_t o = (int64_t)(arow0 + i) * m + b + j;
-              v = pt.min[o];
-              if (fuse_ef) {
-                v = v + pt.e[o];
-                pt.e[o] = v;
-              }
+              t[j] = pt.min[o];
+              if (fuse_ef) u[j] = pt.e[o];
             }
-            t[j] = v;
           }
           mv[i][sb] = f32x4{t[0], t[1], t[2], t[3]};
+          ev[i][sb] = f32x4{u[0], u[1], u[2], u[3]};
         }
     }
     // Q rows of this lane's columns (L2-resident: m x r floats per matrix)
@@ -287,6 +281,36 @@ __global__ __launch_bounds__(256) void psgd_p_wide_kernel(const MatGeom* __restr
         } else {
 #pragma unroll
           for (int c = 0; c < RQ; ++c) qv[j][c] = (okj && c < r) ? Q[(int64_t)(b + j) * r + c] : 0.f;
+        }
+      }
+      if (fuse_ef) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          f32x4 e4 = ev[i][sb];
+          if (p_prev != nullptr) {  // e = M_prev - P_prev Qs^T, psgd_update_wide's arithmetic
+            const bool rok = arow0 + i < n;
+            const float* pp = p_prev + g.p_off + (int64_t)(rok ? arow0 + i : 0) * r;
+            f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int c = 0; c < RQ; ++c) {
+              if (c >= r) break;
+              const float pv = rok ? pp[c] : 0.f;
+#pragma unroll
+              for (int j = 0; j < 4; ++j) o[j] = fmaf(pv, qv[j][c], o[j]);
+            }
+            e4 = e4 - o;
+          }
+          mv[i][sb] = mv[i][sb] + e4;  // send = g + e   (ddp_init.py:156-157)
+          if (arow0 + i < n) {
+            const int64_t o = (int64_t)(arow0 + i) * m + b;
+            if (g.vec) {
+              if (b < it.k1) st4(pt.e + o, mv[i][sb]);
+            } else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j)
+                if (b + j < it.k1) pt.e[o + j] = mv[i][sb][j];
+            }
+          }
         }
       }
 #pragma unroll
@@ -520,12 +544,15 @@ __global__ __launch_bounds__(256) void psgd_update_kernel(
 // ----------------------------------------------------------------------------------
 constexpr int kURowsPerWave = kUWideRows / 4;
 
+// p_prev != nullptr (lazy error feedback, modes 1 / 2): e is not written — M is not even read —
+// and the column-block-0 workgroup of each row block keeps its P-hat rows in p_prev for the
+// next P pass.  mode 3: e -= p_hat Qs^T only (the lazy state materialised: checkpoint, API).
 template <int RQ>
 __global__ __launch_bounds__(256) void psgd_update_wide_kernel(
     const MatGeom* __restrict__ geom, const MatPtrs* __restrict__ ptrs,
     const UItem* __restrict__ items, const float* __restrict__ p_hat,
     const float* __restrict__ q_sum, float q_div, float* __restrict__ q_warm, int mode,
-    float lr, float momentum) {
+    float lr, float momentum, float* __restrict__ p_prev) {
   const UItem it = items[blockIdx.x];
   const MatGeom g = geom[it.mat];
   const MatPtrs pt = ptrs[it.mat];
@@ -544,6 +571,12 @@ __global__ __launch_bounds__(256) void psgd_update_wide_kernel(
 
   const int arow0 = it.row0 + wave * kURowsPerWave;
   if (arow0 >= n) return;
+  const bool lazy = p_prev != nullptr && (mode == 1 || mode == 2);
+  if (lazy && it.col0 == 0 && lane < r) {  // this row block's P-hat for the next P pass
+#pragma unroll
+    for (int i = 0; i < kURowsPerWave; ++i)
+      if (arow0 + i < n) p_prev[g.p_off + (int64_t)(arow0 + i) * r + lane] = P[(int64_t)(arow0 + i) * r + lane];
+  }
   const int b = it.col0 + 4 * lane;
   const int nb = max(0, min(4, m - b));  // valid columns of this lane (vec: 0 or 4)
   // the HBM stream first: M (= g + e), momentum, parameters of every row of the wave
@@ -553,8 +586,8 @@ __global__ __launch_bounds__(256) void psgd_update_wide_kernel(
     for (int i = 0; i < kURowsPerWave; ++i) {
       const bool ok = nb == 4 && arow0 + i < n;
       const int64_t o = (int64_t)(arow0 + i) * m + b;
-      Mv[i] = ok ? ld4(pt.mread + o) : f32x4{0.f, 0.f, 0.f, 0.f};
-      if (mode != 0) {
+      Mv[i] = (ok && !lazy) ? ld4(pt.mread + o) : f32x4{0.f, 0.f, 0.f, 0.f};
+      if (mode == 1 || mode == 2) {
         Mm[i] = ok ? ld4(pt.mom + o) : f32x4{0.f, 0.f, 0.f, 0.f};
         Xv[i] = ok ? ld4(pt.x + o) : f32x4{0.f, 0.f, 0.f, 0.f};
       }
@@ -597,10 +630,12 @@ __global__ __launch_bounds__(256) void psgd_update_wide_kernel(
       if (mode == 0) {
         st4(pt.out + ro + b, o);
         st4(pt.mem + ro + b, M - o);
+      } else if (mode == 3) {
+        st4(pt.e + ro + b, M - o);
       } else {
         f32x4 mm = Mm[i];
         f32x4 xx = Xv[i];
-        st4(pt.e + ro + b, M - o);
+        if (!lazy) st4(pt.e + ro + b, M - o);
 #pragma unroll
         for (int j = 0; j < 4; ++j) mm[j] = __fadd_rn(__fmul_rn(mm[j], momentum), o[j]);
         const f32x4 up = o + mm;
@@ -615,12 +650,14 @@ __global__ __launch_bounds__(256) void psgd_update_wide_kernel(
       for (int j = 0; j < 4; ++j) {
         if (j >= nb) break;
         const int64_t k = ro + b + j;
-        const float M = pt.mread[k];
+        const float M = lazy ? 0.f : pt.mread[k];
         if (mode == 0) {
           pt.out[k] = o[j];
           pt.mem[k] = M - o[j];
-        } else {
+        } else if (mode == 3) {
           pt.e[k] = M - o[j];
+        } else {
+          if (!lazy) pt.e[k] = M - o[j];
           const float mm = __fadd_rn(__fmul_rn(pt.mom[k], momentum), o[j]);
           pt.mom[k] = mm;
           const float up = o[j] + mm;
@@ -661,20 +698,22 @@ static inline int ncg_for(int max_rank) {
 
 void launch_psgd_p(const MatGeom* geom, const MatPtrs* ptrs, const PItem* items, int n_items,
                    const float* q_warm, float* p_part, int fuse_ef, int max_rank,
-                   hipStream_t s) {
+                   hipStream_t s, const float* p_prev) {
   if (n_items <= 0) return;
   // the item shape follows the plan's max rank (plan.cpp): wide 16 x kPKW items up to rank 16
   if (max_rank <= 4) {
-    hipLaunchKernelGGL(psgd_p_wide_kernel<4>, dim3(n_items), dim3(256), 0, s, geom, ptrs, items, q_warm, p_part, fuse_ef);
+    hipLaunchKernelGGL(psgd_p_wide_kernel<4>, dim3(n_items), dim3(256), 0, s, geom, ptrs, items, q_warm, p_part, fuse_ef,
+                       p_prev);
     return;
   }
   if (max_rank <= 8) {
-    hipLaunchKernelGGL(psgd_p_wide_kernel<8>, dim3(n_items), dim3(256), 0, s, geom, ptrs, items, q_warm, p_part, fuse_ef);
+    hipLaunchKernelGGL(psgd_p_wide_kernel<8>, dim3(n_items), dim3(256), 0, s, geom, ptrs, items, q_warm, p_part, fuse_ef,
+                       p_prev);
     return;
   }
   if (max_rank <= kUWideMaxRank) {
     hipLaunchKernelGGL(psgd_p_wide_kernel<kUWideMaxRank>, dim3(n_items), dim3(256), 0, s, geom, ptrs, items, q_warm,
-                       p_part, fuse_ef);
+                       p_part, fuse_ef, p_prev);
     return;
   }
   const int ncg = ncg_for(max_rank);
@@ -712,18 +751,18 @@ void launch_psgd_q(const MatGeom* geom, const MatPtrs* ptrs, const QItem* items,
 void launch_psgd_update(const MatGeom* geom, const MatPtrs* ptrs, const UItem* items,
                         int n_items, const float* p_hat, const float* q_sum, float q_div,
                         float* q_warm, int mode, float lr, float momentum, int max_rank,
-                        hipStream_t s) {
+                        hipStream_t s, float* p_prev) {
   if (n_items <= 0) return;
   // the item tiles follow the plan's max rank (plan.cpp): wide 16 x 256 tiles up to rank 16
   if (max_rank <= 4)
     hipLaunchKernelGGL(psgd_update_wide_kernel<4>, dim3(n_items), dim3(256), 0, s, geom, ptrs,
-                       items, p_hat, q_sum, q_div, q_warm, mode, lr, momentum);
+                       items, p_hat, q_sum, q_div, q_warm, mode, lr, momentum, p_prev);
   else if (max_rank <= 8)
     hipLaunchKernelGGL(psgd_update_wide_kernel<8>, dim3(n_items), dim3(256), 0, s, geom, ptrs,
-                       items, p_hat, q_sum, q_div, q_warm, mode, lr, momentum);
+                       items, p_hat, q_sum, q_div, q_warm, mode, lr, momentum, p_prev);
   else if (max_rank <= kUWideMaxRank)
     hipLaunchKernelGGL(psgd_update_wide_kernel<kUWideMaxRank>, dim3(n_items), dim3(256), 0, s,
-                       geom, ptrs, items, p_hat, q_sum, q_div, q_warm, mode, lr, momentum);
+                       geom, ptrs, items, p_hat, q_sum, q_div, q_warm, mode, lr, momentum, p_prev);
   else
     hipLaunchKernelGGL(psgd_update_kernel, dim3(n_items), dim3(256), 0, s, geom, ptrs, items,
                        p_hat, q_sum, q_div, q_warm, mode, lr, momentum);

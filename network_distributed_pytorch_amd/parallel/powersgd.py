@@ -378,6 +378,9 @@ class PowerSGDReducer(Reducer):
             off += o.numel()
 
 
+_LAZY_MAX_RANK = 16  # csrc/ndp_kernels.h kUWideMaxRank: the wide P / update kernels
+
+
 class _Group:
     """One overlap group: high-rank matrices [lo, hi) (contiguous in parameter order, so
     their P / Q payloads are contiguous slices of the reference-order buffers)."""
@@ -422,6 +425,13 @@ class PowerSGDOptimizer:
 
     ``write_grad=True`` also leaves ``p.grad = out + m`` exactly like the reference loop
     (ddp_init.py:172); it costs one extra write pass and is off by default.
+
+    **Lazy error feedback** (native, rank <= 16; ``NDP_PSGD_LAZY_EF=0`` turns it off): the
+    update pass does not store ``e = M - P Q^T`` — it would read ``M`` back only for that
+    store, 2 of its 6 arena passes.  The arena keeps ``M`` and ``p_prev`` keeps the step's
+    P-hat; the next P pass forms ``e`` element by element with the update kernel's exact
+    arithmetic (csrc/powersgd.hip), so every step is bitwise the eager formula's.  :attr:`e`
+    (and ``state_dict``) materialise the true error memory first.
     """
 
     def __init__(self, params, lr: float, momentum: float = 0.9, rank: int = 4,
@@ -465,7 +475,7 @@ class PowerSGDOptimizer:
         self.arena_numel = o
         f32 = dict(dtype=torch.float32, device=self.device)
         self.x = torch.zeros(o, **f32)
-        self.e = torch.zeros(o, **f32)
+        self._e = torch.zeros(o, **f32)
         self.m = torch.zeros(o, **f32)
         self.offsets = offs
         with torch.no_grad():
@@ -483,6 +493,12 @@ class PowerSGDOptimizer:
         self.r1_upd = torch.zeros(self.r1_numel if write_grad else 0, **f32)
         self.buf = _PlanBuffers(shapes, self.rank, self.r1_numel, self.device, native=native is not False)
         self.native = self.buf.native
+        # needs the warm-start Q of the next P pass to BE the update's Qs (reuse_query)
+        self.lazy_ef = (self.native and bool(shapes) and self.buf.max_rank <= _LAZY_MAX_RANK and reuse_query
+                        and os.environ.get("NDP_PSGD_LAZY_EF", "1") != "0")
+        self._lazy_pending = False  # an update ran since e was last materialised
+        # P-hat of the last update (lazy error feedback); zero = no pending correction
+        self.p_prev = torch.zeros(self.buf.p_total if self.lazy_ef else 0, **f32)
         self._p_seg = SegPlan([], self.device, capacity=len(shapes) + len(r1) + 1) if self.native else None
         self._r1_out = SegPlan([], self.device, capacity=len(r1) + 1) if self.native else None
         self._r1_pack = SegPlan([], self.device, capacity=len(r1) + 1) if self.native else None
@@ -555,7 +571,7 @@ class PowerSGDOptimizer:
         for p, gr, (n, m) in zip(g.params, grads, B.shapes[g.lo:g.hi]):
             assert gr.is_contiguous() and gr.dtype == torch.float32, "PowerSGD needs dense fp32 grads"
             s = self.offsets[id(p)]
-            e, mo, x = (t[s:].data_ptr() for t in (self.e, self.m, self.x))
+            e, mo, x = (t[s:].data_ptr() for t in (self._e, self.m, self.x))
             row = [gr.data_ptr(), e, e, 0, 0, mo, x, gr.data_ptr()]
             rows.append(row)
             vec.append(_vec_ok(m, row))
@@ -578,8 +594,10 @@ class PowerSGDOptimizer:
         q0, q1 = B.q_range(g.lo, g.hi)
         mode, lr, mom, spins = 2 if self.write_grad else 1, self.lr, self.momentum, self.orth_max_spins
 
+        pp = self.p_prev if self.lazy_ef else None
+
         def pipeline():
-            X.psgd_p(B.geom, B.ptrs, B.items("p", g.lo, g.hi), B.q_warm, B.p_part, True, B.max_rank)
+            X.psgd_p(B.geom, B.ptrs, B.items("p", g.lo, g.hi), B.q_warm, B.p_part, True, B.max_rank, pp)
             g.p_seg.run()
             self.comm.all_reduce(B.comm_buf[p0:p1])                       # reducer.py:126 (group g)
             B.orth(float(N), self.eps, B.items("orth", g.lo, g.hi), spins)
@@ -587,7 +605,7 @@ class PowerSGDOptimizer:
             g.q_seg.run()
             self.comm.all_reduce(B.q_memory[q0:q1])                       # reducer.py:145 (group g)
             X.psgd_update(B.geom, B.ptrs, B.items("u", g.lo, g.hi), B.comm_buf, B.q_memory, float(N),
-                          B.q_warm, mode, lr, mom, B.max_rank)
+                          B.q_warm, mode, lr, mom, B.max_rank, pp)
         self.comm.side_launch(pipeline)
         g.launched = True
 
@@ -669,7 +687,7 @@ class PowerSGDOptimizer:
         for p, (n, m) in zip(self.high, B.shapes):
             s = self.offsets[id(p)]
             g = gmap[id(p)].data_ptr()
-            e, mo, x = (t[s:].data_ptr() for t in (self.e, self.m, self.x))
+            e, mo, x = (t[s:].data_ptr() for t in (self._e, self.m, self.x))
             row = [g, e, e, 0, 0, mo, x, g]
             rows.append(row)
             vec.append(_vec_ok(m, row))
@@ -748,7 +766,8 @@ class PowerSGDOptimizer:
             return
         self._bind()
         if B.shapes:
-            ext().psgd_p(B.geom, B.ptrs, B.p_items, B.q_warm, B.p_part, True, B.max_rank)
+            ext().psgd_p(B.geom, B.ptrs, B.p_items, B.q_warm, B.p_part, True, B.max_rank,
+                         self.p_prev if self.lazy_ef else None)
         self._p_seg.run()                                      # P split-K sum + rank-1 pack
 
     @torch.no_grad()
@@ -778,7 +797,8 @@ class PowerSGDOptimizer:
             X = ext()
             if B.shapes:
                 X.psgd_update(B.geom, B.ptrs, B.u_items, B.comm_buf, B.q_memory, float(N), B.q_warm,
-                              2 if self.write_grad else 1, self.lr, self.momentum, B.max_rank)
+                              2 if self.write_grad else 1, self.lr, self.momentum, B.max_rank,
+                              self.p_prev if self.lazy_ef else None)
             if self.r1_numel:
                 r1 = slice(self.r1_start, self.arena_numel)
                 X.rank1_step(B.rank1_buf, float(N), self.m[r1], self.x[r1],
@@ -793,6 +813,7 @@ class PowerSGDOptimizer:
         """Host-side bookkeeping of one step (graph replays call this explicitly)."""
         if capturing():  # the capture pass is not a real step
             return
+        self._lazy_pending = self.lazy_ef
         self.step_count += 1
         self.bits_communicated += self.bits_per_step
         if not self.reuse_query:
@@ -832,7 +853,7 @@ class PowerSGDOptimizer:
         Ms = []
         for i, p in enumerate(self.high):
             n, m = B.shapes[i]
-            e = self._view(self.e, p)
+            e = self._view(self._e, p)
             e.add_(gmap[id(p)].reshape(-1))              # M = g + e (stored in e)
             M = e.view(n, m)
             Ms.append(M)
@@ -851,7 +872,7 @@ class PowerSGDOptimizer:
         B.q_warm.copy_(B.q_memory)
         for i, (p, M) in enumerate(zip(self.high, Ms)):
             out = torch.matmul(B.p_view(i), B.q_view(i).t()).view(-1)
-            self._view(self.e, p).copy_(M.reshape(-1) - out)
+            self._view(self._e, p).copy_(M.reshape(-1) - out)
             mom = self._view(self.m, p)
             mom.mul_(lam).add_(out)
             upd = out + mom
@@ -869,6 +890,24 @@ class PowerSGDOptimizer:
                     s = self.offsets[id(p)] - self.r1_start
                     gmap[id(p)].copy_(upd[s: s + p.numel()].view_as(p))
 
+    # -- lazy error feedback -------------------------------------------------------------------
+    @property
+    def e(self) -> torch.Tensor:
+        """The error-feedback memory (reducer.py ``memories``), materialised: with lazy error
+        feedback the arena holds ``M`` and the correction ``- P_prev Qs^T`` is applied here by
+        the update kernel's own arithmetic (mode 3), exactly as the next P pass would."""
+        self.materialize_error()
+        return self._e
+
+    @torch.no_grad()
+    def materialize_error(self):
+        if not (self.lazy_ef and self._lazy_pending) or capturing():
+            return
+        B = self.buf
+        ext().psgd_update(B.geom, B.ptrs, B.u_items, self.p_prev, B.q_warm, 1.0, None, 3, 0.0, 0.0, B.max_rank)
+        self.p_prev.zero_()
+        self._lazy_pending = False
+
     # -- training-state snapshot (graph warm-up must not change training) -------------------
     def prepare(self):
         """Draw the initial queries now (before a graph warm-up snapshot)."""
@@ -876,13 +915,16 @@ class PowerSGDOptimizer:
             self._ensure_queries()
 
     def snapshot(self):
-        return {"x": self.x.clone(), "e": self.e.clone(), "m": self.m.clone(), "q": self.buf.q_warm.clone(),
+        return {"x": self.x.clone(), "e": self._e.clone(), "p_prev": self.p_prev.clone(),
+                "lazy_pending": self._lazy_pending, "m": self.m.clone(), "q": self.buf.q_warm.clone(),
                 "step_count": self.step_count, "bits": self.bits_communicated, "q_ready": self._q_ready,
                 "rng": self.rng.get_state()}
 
     def restore(self, snap):
         self.x.copy_(snap["x"])
-        self.e.copy_(snap["e"])
+        self._e.copy_(snap["e"])
+        self.p_prev.copy_(snap["p_prev"])
+        self._lazy_pending = snap["lazy_pending"]
         self.m.copy_(snap["m"])
         self.buf.q_warm.copy_(snap["q"])
         self.step_count = snap["step_count"]
@@ -895,7 +937,7 @@ class PowerSGDOptimizer:
         return {
             "step_count": self.step_count,
             "bits_communicated": self.bits_communicated,
-            "error": self.e.detach().cpu().clone(),
+            "error": self.e.detach().cpu().clone(),  # materialised (lazy error feedback)
             "momentum": self.m.detach().cpu().clone(),
             "q_warm": self.buf.q_warm.detach().cpu().clone(),
             "q_ready": self._q_ready,
@@ -909,7 +951,9 @@ class PowerSGDOptimizer:
         assert sd["rank"] == self.rank, "checkpoint compression rank differs"
         self.step_count = int(sd["step_count"])
         self.bits_communicated = int(sd["bits_communicated"])
-        self.e.copy_(sd["error"])
+        self._e.copy_(sd["error"])
+        self.p_prev.zero_()  # e is the true error memory: no pending correction
+        self._lazy_pending = False
         self.m.copy_(sd["momentum"])
         self.buf.q_warm.copy_(sd["q_warm"])
         self._q_ready = bool(sd.get("q_ready", self.step_count > 0)) and self.reuse_query

@@ -204,3 +204,29 @@ def test_checksum_and_delay(device):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     assert 0.015 < dt < 0.5, dt
+
+
+def test_lazy_error_feedback_bitwise(device):
+    """Lazy error feedback (the update pass skips e = M - P Q^T; the next P pass forms it with
+    the same arithmetic) is bitwise the eager formula: parameters, momentum and the
+    materialised error memory after every step, and the checkpoint state."""
+    _native_loaded()
+    ma, mb = _make_model(device), _make_model(device)
+    mb.load_state_dict(ma.state_dict())
+    oa = PowerSGDOptimizer(ma.parameters(), lr=0.1, momentum=0.9, rank=4)
+    ob = PowerSGDOptimizer(mb.parameters(), lr=0.1, momentum=0.9, rank=4)
+    assert oa.lazy_ef
+    ob.lazy_ef = False
+    torch.manual_seed(6)
+    for step in range(5):
+        x = torch.randn(64, 3, 8, 8, device=device)
+        y = torch.randint(0, 10, (64,), device=device)
+        for m, o in ((ma, oa), (mb, ob)):
+            o.zero_grad()
+            torch.nn.functional.cross_entropy(m(x), y).backward()
+            o.step()
+        assert torch.equal(oa.x, ob.x) and torch.equal(oa.m, ob.m), step
+        if step % 2 == 1:  # materialising mid-run must not change the trajectory
+            assert torch.equal(oa.e, ob.e), step
+    sa, sb = oa.state_dict(), ob.state_dict()
+    assert torch.equal(sa["error"], sb["error"]) and torch.equal(sa["q_warm"], sb["q_warm"])
