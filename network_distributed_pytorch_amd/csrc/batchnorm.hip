@@ -815,10 +815,20 @@ static void launch_small_fused(int HW, const float* x, const float* res, const f
                                float* sm, float* si, float* dgamma, float* dbeta, float* out, float* dres, int N,
                                int C, float eps, float momentum, int relu, hipStream_t s, const float* src,
                                int nslab, const BnSync& sy) {
-  if (HW == 64) {  // one workgroup per channel: 64 lanes x 8 row groups, <= 128 images
-    hipLaunchKernelGGL((bn_small_fused_kernel<64, BWD, 64, kFused64MaxN>), dim3((unsigned)C), dim3(kFusedThreads), 0,
-                       s, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out, dres, N, C, eps,
-                       momentum, relu, src, nslab, sy);
+  if (HW == 64) {  // one workgroup per channel (x RS row splits): 64 lanes x 8 row groups, <= 128 images
+    const int rs = sy.ctr != nullptr ? bn_row_splits(C, N, 64) : 1;
+    if (rs == 4)
+      hipLaunchKernelGGL((bn_small_fused_kernel<64, BWD, 64, kFused64MaxN, 4>), dim3((unsigned)(4 * C)),
+                         dim3(kFusedThreads), 0, s, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma,
+                         dbeta, out, dres, N, C, eps, momentum, relu, src, nslab, sy);
+    else if (rs == 2)
+      hipLaunchKernelGGL((bn_small_fused_kernel<64, BWD, 64, kFused64MaxN, 2>), dim3((unsigned)(2 * C)),
+                         dim3(kFusedThreads), 0, s, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma,
+                         dbeta, out, dres, N, C, eps, momentum, relu, src, nslab, sy);
+    else
+      hipLaunchKernelGGL((bn_small_fused_kernel<64, BWD, 64, kFused64MaxN>), dim3((unsigned)C), dim3(kFusedThreads),
+                         0, s, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out, dres, N, C,
+                         eps, momentum, relu, src, nslab, sy);
     return;
   }
   switch (bn_colw_for(HW, C, N)) {
