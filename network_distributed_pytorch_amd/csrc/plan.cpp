@@ -10,12 +10,26 @@
 //   * Q items  : (matrix, 256-col block, row chunk)          -> split-K over n;
 //   * U items  : (matrix, 16x256 tile; 64x64 above rank 16)  -> fused decompress/update;
 //   * split-K slab offsets for the deterministic seg_reduce.
+#include <cstdlib>
 #include "plan.h"
 
 #include <algorithm>
 #include <stdexcept>
 
 namespace ndp {
+
+// columns per wide P item: kPKW, or NDP_PSGD_PKW = 256 / 512 (A/B: smaller items, more of them;
+// the kernel masks the slices past an item's k1)
+static int64_t p_item_cols() {
+  static int64_t v = -1;
+  if (v < 0) {
+    const char* e = getenv("NDP_PSGD_PKW");
+    v = e ? atoll(e) : kPKW;
+    if (v != 256 && v != 512) v = kPKW;
+  }
+  return v;
+}
+
 
 static int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
@@ -41,7 +55,7 @@ Plan build_plan(const std::vector<std::pair<int64_t, int64_t>>& shapes, int rank
     g.vec = 0;
     g.p_off = (int32_t)p_off;
     g.q_off = (int32_t)q_off;
-    const int64_t p_rows = wide ? kPWRows : kPRows, p_k = wide ? kPKW : kPK;
+    const int64_t p_rows = wide ? kPWRows : kPRows, p_k = wide ? p_item_cols() : kPK;
     g.p_chunks = (int32_t)cdiv(m, p_k);
     // Q split over n: 64-row chunks, but at most 64 chunks (cap the slab scratch), and
     // never more rows than the LDS tile holds.
