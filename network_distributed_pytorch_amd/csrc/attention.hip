@@ -18,6 +18,13 @@
 //             deterministic.
 //   dropout : counter-based hash of (seed, b*H+h, q, key) — the same mask is regenerated
 //             in backward; kept probabilities are scaled by 1/(1-p) like nn.Dropout.
+//   LDS     : tiles are staged ONCE, row-major [token][d] (b128 writes, conflict-free).  The
+//             operands that need the transposed view (V^T / dO^T / Q^T / K^T rows d as the A
+//             operand) are read as 4 ds_read_b32 from the row layout: lane (g, c16) reads
+//             row 4g + r, column c16, and with the 68-float row stride rows 4g and 4(g+1)
+//             land 16 banks apart, so each 32-lane half covers the 32 banks.  Same LDS bytes
+//             as one b128 from a transposed copy, but no transposing scalar stores (8-way
+//             bank conflicts: ~60 % of LDS cycles before, PMC round 4) and half the LDS.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "ndp_kernels.h"
@@ -90,7 +97,7 @@ struct AttnArgs {
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   const uint32_t seed = (a.drop_thr && a.seedp) ? (uint32_t)*a.seedp : 0u;
   __shared__ __attribute__((aligned(16))) float Ks[kBK * kLD];   // K[key][d]
-  __shared__ __attribute__((aligned(16))) float Vt[kD * kLD];    // V^T[d][key]
+  __shared__ __attribute__((aligned(16))) float Vs[kBK * kLD];   // V[key][d]
   __shared__ float Mk[kBK];                                      // key mask (1 / 0)
   __shared__ int blkv[kMaxBlk];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
@@ -130,8 +137,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
         vv = *reinterpret_cast<const f32x4*>(a.v + qbase + (int64_t)key * qrs + dq);
       }
       *reinterpret_cast<f32x4*>(&Ks[kr * kLD + dq]) = kv;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) Vt[(dq + t) * kLD + kr] = vv[t];
+      *reinterpret_cast<f32x4*>(&Vs[kr * kLD + dq]) = vv;
     }
     if (threadIdx.x < kBK) {
       const int key = k0 + threadIdx.x;
@@ -195,9 +201,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
       f32x4 acc = O[dt] * alpha;
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
-        const f32x4 vf = *reinterpret_cast<const f32x4*>(&Vt[(16 * dt + c16) * kLD + 16 * kt + 4 * g]);
+        const float* vr = &Vs[(16 * kt + 4 * g) * kLD + 16 * dt + c16];  // V^T[d][key] = V[key][d]
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc = mfma16(vf[r], P[kt][r], acc);
+        for (int r = 0; r < 4; ++r) acc = mfma16(vr[r * kLD], P[kt][r], acc);
       }
       O[dt] = acc;
     }
@@ -252,8 +258,6 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
   const uint32_t seed = (a.drop_thr && a.seedp) ? (uint32_t)*a.seedp : 0u;
   __shared__ __attribute__((aligned(16))) float Qs[64 * kLD];    // Q[q][d] (scaled)
   __shared__ __attribute__((aligned(16))) float dOs[64 * kLD];   // dO[q][d]
-  __shared__ __attribute__((aligned(16))) float Qt[kD * kLD];    // Q^T[d][q] (scaled)
-  __shared__ __attribute__((aligned(16))) float dOt[kD * kLD];   // dO^T[d][q]
   __shared__ float Ls[64], LLs[64], Ds[64];
   __shared__ int blkv[kMaxBlk];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
@@ -310,11 +314,6 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
       }
       *reinterpret_cast<f32x4*>(&Qs[qr * kLD + dq]) = qv;
       *reinterpret_cast<f32x4*>(&dOs[qr * kLD + dq]) = gv;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        Qt[(dq + t) * kLD + qr] = qv[t];
-        dOt[(dq + t) * kLD + qr] = gv[t];
-      }
     }
     if (threadIdx.x < 64) {
       const int qq = q0 + threadIdx.x;
@@ -355,12 +354,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
       // B = Pd (k = query 4g + r, col = key lane).  dK^T likewise with Q and dS.
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        const f32x4 gq = *reinterpret_cast<const f32x4*>(&dOt[(16 * dt + c16) * kLD + 16 * qt + 4 * g]);
-        const f32x4 qq4 = *reinterpret_cast<const f32x4*>(&Qt[(16 * dt + c16) * kLD + 16 * qt + 4 * g]);
+        const float* gr = &dOs[(16 * qt + 4 * g) * kLD + 16 * dt + c16];  // dO^T[d][q] = dO[q][d]
+        const float* qp = &Qs[(16 * qt + 4 * g) * kLD + 16 * dt + c16];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          dV[dt] = mfma16(gq[r], Pd[r], dV[dt]);
-          dK[dt] = mfma16(qq4[r], dS[r], dK[dt]);
+          dV[dt] = mfma16(gr[r * kLD], Pd[r], dV[dt]);
+          dK[dt] = mfma16(qp[r * kLD], dS[r], dK[dt]);
         }
       }
       (void)P;
@@ -380,7 +379,6 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   const uint32_t seed = (a.drop_thr && a.seedp) ? (uint32_t)*a.seedp : 0u;
   __shared__ __attribute__((aligned(16))) float Ks[kBK * kLD];   // K[key][d]
   __shared__ __attribute__((aligned(16))) float Vs[kBK * kLD];   // V[key][d]
-  __shared__ __attribute__((aligned(16))) float Kt[kD * kLD];    // K^T[d][key]
   __shared__ float Mk[kBK];
   __shared__ int blkv[kMaxBlk];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
@@ -426,8 +424,6 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
       }
       *reinterpret_cast<f32x4*>(&Ks[kr * kLD + dq]) = kv;
       *reinterpret_cast<f32x4*>(&Vs[kr * kLD + dq]) = vv;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) Kt[(dq + t) * kLD + kr] = kv[t];
     }
     if (threadIdx.x < kBK) {
       const int key = k0 + threadIdx.x;
@@ -464,9 +460,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
       // dQ^T[d][q] += K^T[d][key] dS^T[key][q]: A = K^T rows d, B = dS (k = key 4g + r)
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        const f32x4 kd = *reinterpret_cast<const f32x4*>(&Kt[(16 * dt + c16) * kLD + 16 * kt + 4 * g]);
+        const float* kp = &Ks[(16 * kt + 4 * g) * kLD + 16 * dt + c16];  // K^T[d][key] = K[key][d]
 #pragma unroll
-        for (int r = 0; r < 4; ++r) dQ[dt] = mfma16(kd[r], dS[r], dQ[dt]);
+        for (int r = 0; r < 4; ++r) dQ[dt] = mfma16(kp[r * kLD], dS[r], dQ[dt]);
       }
     }
   }
