@@ -94,7 +94,7 @@ struct AttnArgs {
 // ---------------------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void attn_fwd_kernel(AttnArgs a) {
   const uint32_t seed = (a.drop_thr && a.seedp) ? (uint32_t)*a.seedp : 0u;
   __shared__ __attribute__((aligned(16))) float Ks[kBK * kLD];   // K[key][d]
   __shared__ __attribute__((aligned(16))) float Vs[kBK * kLD];   // V[key][d]
@@ -254,7 +254,7 @@ struct AttnBwdArgs {
 // Recompute one 16(query) x 64(key) probability tile in the S^T layout used by the forward:
 // lane (g, c16): query = q (lane), keys 16kt + 4g + r.
 // dK, dV: one wave owns 16 keys (rows = d on MFMA outputs), loops over all queries.
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
   const uint32_t seed = (a.drop_thr && a.seedp) ? (uint32_t)*a.seedp : 0u;
   __shared__ __attribute__((aligned(16))) float Qs[64 * kLD];    // Q[q][d] (scaled)
   __shared__ __attribute__((aligned(16))) float dOs[64 * kLD];   // dO[q][d]
@@ -374,8 +374,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
   }
 }
 
-// dQ: one wave owns 16 queries, loops over keys (recomputes P and dP).
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
+// dQ: one wave owns 16 queries, loops over keys (recomputes P and dP).  4 waves per SIMD: its
+// registers fit 128 VGPRs without spilling (160 with AGPRs by default -> 3 waves).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   const uint32_t seed = (a.drop_thr && a.seedp) ? (uint32_t)*a.seedp : 0u;
   __shared__ __attribute__((aligned(16))) float Ks[kBK * kLD];   // K[key][d]
   __shared__ __attribute__((aligned(16))) float Vs[kBK * kLD];   // V[key][d]
