@@ -29,6 +29,7 @@ input geometry, the fastest native path:
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Tuple
 
 import torch
@@ -113,10 +114,26 @@ class ToeplitzBank:
         return self.members[i][2]
 
 
+# grad-W of a Toeplitz conv on the small-map grad-W kernel (csrc/smallconv.hip: dW in W's own
+# layout, no dW_big GEMM, no fold) where it covers the geometry.  Opt-in (NDP_TOEP_SMWGRAD=1):
+# measured slower than the hipBLASLt GEMM + batched fold on 1x MI355X (ResNet-18 r=4 b512
+# 1.904 -> 1.967 ms, b64 0.989 -> 1.019, ResNet-50 6.076 -> 6.112; profiles/r4/bench_toep_smwgrad.jsonl)
+_SM_WGRAD = os.environ.get("NDP_TOEP_SMWGRAD", "0") != "0"
+
+
+def _sm_wgrad_splits(geom, B: int) -> int:
+    """grad-W batch splits of the small-map kernel for this conv (0: not covered)."""
+    if not _SM_WGRAD:
+        return 0
+    cls, _, _, ws = ext().sm_plan(list(geom), int(B))
+    return int(ws) if cls >= 0 else 0
+
+
 class _ToeplitzConv(torch.autograd.Function):
     """Device tensors: W_big built / grad-W folded by csrc/conv.hip (index arithmetic, one
     launch each, or one expand launch for a whole :class:`ToeplitzBank`); CPU tensors (fp64
-    tests): the same maps as index tensors."""
+    tests): the same maps as index tensors.  Where the small-map kernels cover the geometry,
+    grad-W comes straight from csrc/smallconv.hip instead of the dW_big GEMM and the fold."""
 
     @staticmethod
     def forward(ctx, x, weight, src, dst, oh, ow, geom=None, bank=None, layer=None, link=None, branch=None):
@@ -137,6 +154,7 @@ class _ToeplitzConv(torch.autograd.Function):
             out = X @ w_big
         ctx.save_for_backward(X, w_big, dst)
         ctx.geom = geom
+        ctx.smw = _sm_wgrad_splits(geom, B) if (x.is_cuda and geom is not None) else 0
         ctx.weight = weight  # the Parameter: a deferred fold writes its adopted .grad
         ctx.link = link      # ops/gradlink.py: residual-branch gradient, folded in by addmm
         ctx.branch = branch if (branch is not None and x.is_cuda and geom is not None) else None
@@ -155,7 +173,21 @@ class _ToeplitzConv(torch.autograd.Function):
         if dev:  # grad-W (GEMM + fold) on the side stream, grad-x on the current one
             main = torch.cuda.current_stream()
             fork = _conv.FORK_WGRAD and ctx.needs_input_grad[0] and ctx.needs_input_grad[1]
-            if ctx.needs_input_grad[1]:
+            if ctx.needs_input_grad[1] and ctx.smw:
+                dw = grad_buffer(ctx.weight)  # the dense arm's arena slice when registered
+                xs = X.view(ctx.x_shape)
+                gs = G.view(g.shape)
+                if ctx.smw > 1:  # batch-split slabs: summed in gradfinish's batched launch (or now)
+                    part = torch.empty(ctx.smw * dw.numel(), device=G.device, dtype=G.dtype)
+                    ext().sm_wgrad(xs, gs, part, list(ctx.geom))
+                    if gradfinish.can_defer(ctx.weight):
+                        gradfinish.defer_slab(part, dw, ctx.smw)
+                    else:
+                        ext().slab_sum(part, dw.view(-1), ctx.smw)
+                else:
+                    ext().sm_wgrad(xs, gs, dw, list(ctx.geom))
+                fork = False
+            elif ctx.needs_input_grad[1]:
                 dw = grad_buffer(ctx.weight)  # the dense arm's arena slice when registered
                 dwt = torch.empty(w_big.shape, device=G.device, dtype=G.dtype)
                 side = side_stream(G.device) if fork else main
