@@ -246,19 +246,32 @@ struct ConvFwdCfg {
   //  * 8x8 stride 2, 2 images per half-wave: row stride 12 (rows 24p = {0,24,16,8} mod 32,
   //    even columns -> the 16 even banks) and an image stride = 1 (mod 32): odd banks.
   // (Measured before: 34-54 % of LDS cycles were conflict cycles, profiles/r2/pmc_counters.md.)
+  //  * 32x32 stride 2 (the 7x7 stem): the even and odd columns of each padded row are stored
+  //    apart (DEINT: position (col & 1) * HALF + col / 2, row stride 2 * HALF = 40), so the 16
+  //    lanes of an output row read 16 CONSECUTIVE words instead of every other one, and the
+  //    next output row (2 input rows = 80 words = 16 mod 32) lands on the other 16 banks
+  //    (interleaved: 2-way on every B read, 47 % of LDS cycles in conflict, PMC round 4).
   static constexpr int LAYOUT = (ST == 1 && H == 8 && W == 8 && PD == 1 && IMGS == 1) ? 1
                                 : (ST == 1 && H == 4 && W == 4 && IMGS % 2 == 0)      ? 2
                                 : (ST == 2 && H == 8 && W == 8 && IMGS % 2 == 0)      ? 3
+                                : (ST == 2 && H == 32 && W == 32 && R == 7 && IMGS == 1) ? 4
                                                                                        : 0;
+  static constexpr bool DEINT = LAYOUT == 4;
+  static constexpr int HALF = (W + 2 * PD + 2) / 2;  // >= every padded column's half position
   static constexpr int Hp = H + 2 * PD;
-  static constexpr int Wp = LAYOUT == 1 ? 12 : LAYOUT == 2 ? 8 : LAYOUT == 3 ? 12 : W + 2 * PD;
+  static constexpr int Wp = LAYOUT == 1 ? 12 : LAYOUT == 2 ? 8 : LAYOUT == 3 ? 12 : DEINT ? 2 * HALF : W + 2 * PD;
+  // LDS column of padded input column `col` within a row
+  __device__ static __forceinline__ constexpr int cpos(int col) {
+    return DEINT ? (col & 1) * HALF + (col >> 1) : col;
+  }
   // channel stride odd: the B staging stores (float4 per lane -> 4 scalar ds_write_b32, a
   // 32-lane group spanning 2-8 channels) land on disjoint bank sets per channel (<= 2-way,
   // which a b32 store absorbs); the reads of a half-wave stay inside one channel
   static constexpr int HWp = (Hp * Wp) | 1, HW = H * W;
   static constexpr int IPAD0 = LAYOUT == 2 ? 4 : LAYOUT == 3 ? 1 : 0;  // target image stride mod 32
   static constexpr int IMGSTR = LAYOUT >= 2 ? (CK * HWp + 31) / 32 * 32 + IPAD0 : CK * HWp;
-  static_assert(Wp >= W + 2 * PD, "row stride holds the zero border");
+  static_assert(Wp >= W + 2 * PD && (!DEINT || (ST == 2 && HALF * 2 == Wp && (ST * Wp) % 32 == 16)),
+                "row stride holds the zero border");
   // output pixel n of the tile -> (image, row, column)
   __device__ static __forceinline__ void pix(int n, int& img, int& p, int& q) {
     if constexpr (LAYOUT == 1) {
@@ -345,7 +358,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
     const int n = (wn * G::TN + tn) * 32 + l32;
     int img, p, q;
     G::pix(n, img, p, q);
-    b_base[tn] = img * G::IMGSTR + h * (CK / 2) * G::HWp + p * ST * G::Wp + q * ST;
+    b_base[tn] = img * G::IMGSTR + h * (CK / 2) * G::HWp + p * ST * G::Wp + (G::DEINT ? q : q * ST);
   }
 
   // B staging: float4 of the (possibly half-size, IUPS) input planes
@@ -437,8 +450,14 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
         const int img = e / (CK * IHW / 4), rem = 4 * (e - img * (CK * IHW / 4));
         const int c = rem / IHW, hw = rem - c * IHW;
         const int hh = hw / IW, ww = hw - hh * IW;
-        float* d = B + img * G::IMGSTR + c * G::HWp + (IUPS * hh + PD) * G::Wp + IUPS * ww + PD;
-        d[0] = rb[i].x; d[IUPS] = rb[i].y; d[2 * IUPS] = rb[i].z; d[3 * IUPS] = rb[i].w;
+        if constexpr (G::DEINT) {
+          float* d = B + img * G::IMGSTR + c * G::HWp + (hh + PD) * G::Wp;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) d[G::cpos(ww + PD + j)] = rb[i][j];
+        } else {
+          float* d = B + img * G::IMGSTR + c * G::HWp + (IUPS * hh + PD) * G::Wp + IUPS * ww + PD;
+          d[0] = rb[i].x; d[IUPS] = rb[i].y; d[2 * IUPS] = rb[i].z; d[3 * IUPS] = rb[i].w;
+        }
       }
     }
   };
@@ -467,7 +486,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
       for (int i = 0; i < KB; ++i) {
         const int t = blk * KB + i;
         const int c = t / G::RS, rs = t - c * G::RS, r = rs / S, s = rs - r * S;
-        const int offb = c * G::HWp + r * G::Wp + s;
+        const int offb = c * G::HWp + r * G::Wp + (G::DEINT ? (s & 1) * G::HALF + (s >> 1) : s);
         if constexpr (!G::AV) {
 #pragma unroll
           for (int tm = 0; tm < G::TM; ++tm) av[slot][i][tm] = A[a_base[tm] + t * G::LDA];
