@@ -97,6 +97,21 @@ __device__ __forceinline__ void slice_sums(const double* __restrict__ part, int 
   }
 }
 
+// the same sums over many partials (the S = batch-tile partials a conv epilogue emits,
+// conv_fwd_kernel `stats`): strided over the block, then the fixed-order block reduction;
+// the result is identical in every workgroup of the channel
+__device__ __forceinline__ void slice_sums_block(const double* __restrict__ part, int c, int S, double& a, double& b,
+                                                 double* red) {
+  a = 0.0;
+  b = 0.0;
+  const double* p = part + (int64_t)c * S * 2;
+  for (int k = threadIdx.x; k < S; k += blockDim.x) {
+    a += p[2 * k];
+    b += p[2 * k + 1];
+  }
+  block_sum2(a, b, red);
+}
+
 // ---- forward statistics -------------------------------------------------------------
 // src (nullable, VEC only): x is the sum of nslab split-K conv slabs (slab order, bitwise equal
 // to conv_slab_sum); the kernel adds them, writes x and takes its statistics in one pass.
@@ -146,7 +161,10 @@ __global__ __launch_bounds__(256) void bn_fwd_apply_kernel(
     const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ rmean,
     float* __restrict__ rvar, int64_t* __restrict__ nbt, float* __restrict__ save_mean,
     float* __restrict__ save_invstd, const double* __restrict__ part, int N, int C, int HW, int S,
-    float eps, float momentum, int relu, int training) {
+    float eps, float momentum, int relu, int training, int Sp = 0) {
+  // Sp > 0: `part` holds Sp partials per channel from the producing conv's epilogue (folded by
+  // the whole block) instead of this launch's S slice partials
+  __shared__ double red[16];
   const int s = blockIdx.x, c = blockIdx.y;
   // per-channel operands first: in flight with the slice partials, not a round trip after them
   const float gam = gamma ? gamma[c] : 1.f, bet = beta ? beta[c] : 0.f;
@@ -155,7 +173,8 @@ __global__ __launch_bounds__(256) void bn_fwd_apply_kernel(
   float mean, invstd;
   if (training) {
     double sum, sq;
-    slice_sums(part, c, S, sum, sq);
+    if (Sp > 0) slice_sums_block(part, c, Sp, sum, sq, red);
+    else slice_sums(part, c, S, sum, sq);
     const double M = (double)N * HW;
     const double mu = sum / M;
     double var = sq / M - mu * mu;
@@ -945,9 +964,11 @@ int bn_slices(int N, int C, int HW) {
 void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamma, const float* beta,
                    float* rmean, float* rvar, int64_t* nbt, float* save_mean, float* save_invstd,
                    double* part, int N, int C, int HW, int S, float eps, float momentum, int relu,
-                   int training, int single, hipStream_t s, const float* xpart, int nslab) {
+                   int training, int single, hipStream_t s, const float* xpart, int nslab, const double* xstats,
+                   int xS) {
   const BnSync sy = bn_sync(part, 1);
   part += kBnSyncSlots;
+  if (!training || xpart != nullptr) xstats = nullptr;
   if (xpart != nullptr && nslab < 2) xpart = nullptr;
   if (xpart != nullptr && nslab > kMaxFusedSlabs) {  // many slabs: the wide sum kernel first
     launch_slab_sum(xpart, const_cast<float*>(x), (int64_t)N * C * HW, nslab, s);
@@ -979,16 +1000,19 @@ void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamm
   const bool vec = (HW % 4) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 &&
                    (res == nullptr || ((uintptr_t)res & 15) == 0);
   const dim3 grid(S, C);
-  if (training) {  // the statistics pass also adds deferred conv slabs (xpart) and writes x
+  // statistics from the conv epilogue (xstats): no statistics pass, the apply folds xS partials
+  const double* ap = xstats != nullptr ? xstats : part;
+  const int Sp = xstats != nullptr ? xS : 0;
+  if (training && xstats == nullptr) {  // the statistics pass also adds deferred conv slabs (xpart), writes x
     if (vec) hipLaunchKernelGGL(bn_fwd_stats_kernel<true>, grid, dim3(256), 0, s, x, part, N, C, HW, S, xpart, nslab);
     else hipLaunchKernelGGL(bn_fwd_stats_kernel<false>, grid, dim3(256), 0, s, x, part, N, C, HW, S, nullptr, 0);
   }
   if (vec)
     hipLaunchKernelGGL(bn_fwd_apply_kernel<true>, grid, dim3(256), 0, s, x, res, y, gamma, beta, rmean, rvar, nbt,
-                       save_mean, save_invstd, part, N, C, HW, S, eps, momentum, relu, training);
+                       save_mean, save_invstd, ap, N, C, HW, S, eps, momentum, relu, training, Sp);
   else
     hipLaunchKernelGGL(bn_fwd_apply_kernel<false>, grid, dim3(256), 0, s, x, res, y, gamma, beta, rmean, rvar, nbt,
-                       save_mean, save_invstd, part, N, C, HW, S, eps, momentum, relu, training);
+                       save_mean, save_invstd, ap, N, C, HW, S, eps, momentum, relu, training, Sp);
 }
 
 void launch_bn_bwd(const float* dy, const float* y, const float* x, const float* gamma, const float* save_mean,

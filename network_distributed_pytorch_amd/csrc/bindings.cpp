@@ -311,7 +311,8 @@ void bn_fwd(torch::Tensor x, c10::optional<torch::Tensor> res, torch::Tensor y,
             c10::optional<torch::Tensor> rmean, c10::optional<torch::Tensor> rvar,
             c10::optional<torch::Tensor> nbt, torch::Tensor save_mean, torch::Tensor save_invstd,
             torch::Tensor part, double eps, double momentum, bool relu, bool training,
-            bool single, c10::optional<torch::Tensor> xpart, int64_t nslab) {
+            bool single, c10::optional<torch::Tensor> xpart, int64_t nslab,
+            c10::optional<torch::Tensor> xstats, int64_t xS) {
   check_f32(x, "x"); check_f32(y, "y"); check_f32(save_mean, "save_mean"); check_f32(save_invstd, "save_invstd");
   check_dev(part, "part");
   TORCH_CHECK(x.dim() >= 2 && x.sizes() == y.sizes(), "bn_fwd: bad shapes");
@@ -330,11 +331,20 @@ void bn_fwd(torch::Tensor x, c10::optional<torch::Tensor> res, torch::Tensor y,
   }
   const float* xp = slab_input(xpart, nslab, x.numel(), "bn_fwd");
   TORCH_CHECK(xp == nullptr || training, "bn_fwd: deferred conv slabs need training mode");
+  const double* xst = nullptr;
+  if (xstats.has_value()) {  // [C][xS][2] partial sums from the producing conv's epilogue
+    check_dev(*xstats, "xstats");
+    TORCH_CHECK(xstats->scalar_type() == torch::kFloat64 && xstats->is_contiguous() && xS > 0 &&
+                    xstats->numel() >= (int64_t)C * xS * 2 && training && xp == nullptr,
+                "bn_fwd: xstats must hold C * xS * 2 doubles (training, no deferred slabs)");
+    xst = xstats->data_ptr<double>();
+  }
   ndp::launch_bn_fwd(x.data_ptr<float>(), opt_f32(res, "res"), y.data_ptr<float>(), opt_f32(gamma, "gamma"),
                      opt_f32(beta, "beta"), const_cast<float*>(opt_f32(rmean, "running_mean")),
                      const_cast<float*>(opt_f32(rvar, "running_var")), nb, save_mean.data_ptr<float>(),
                      save_invstd.data_ptr<float>(), part.data_ptr<double>(), N, C, HW, S, (float)eps,
-                     (float)momentum, relu ? 1 : 0, training ? 1 : 0, single ? 1 : 0, cur_stream(), xp, (int)nslab);
+                     (float)momentum, relu ? 1 : 0, training ? 1 : 0, single ? 1 : 0, cur_stream(), xp, (int)nslab,
+                     xst, (int)xS);
   check_launch("launch_bn_fwd");
 }
 
@@ -566,6 +576,14 @@ py::tuple conv_plan(const std::vector<int64_t>& geom, int64_t B) {
                         ndp::conv_ksplit(cls, g, (int)B, true));
 }
 
+// batch-tile partials of the BatchNorm statistics the forward epilogue can emit (0 = none)
+int64_t conv_stats_slices(const std::vector<int64_t>& geom, int64_t B) {
+  const ndp::ConvGeom g = conv_geom(geom);
+  const int cls = ndp::conv_direct_class(g);
+  if (cls < 0 || B <= 0 || B % ndp::conv_fwd_imgs(cls)) return 0;
+  return ndp::conv_fwd_stats_slices(cls, g, (int)B);
+}
+
 float* conv_part(const c10::optional<torch::Tensor>& part, int ks, int64_t slab, const char* who) {
   if (ks <= 1) return nullptr;
   TORCH_CHECK(part.has_value(), who, ": split-K needs a part scratch tensor");
@@ -589,7 +607,7 @@ int conv_batch(const torch::Tensor& t, const ndp::ConvGeom& g, int imgs) {
 
 // defer: split-K slabs are left in `part` for the consumer; returns how many (1 = y final)
 int64_t conv_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, const std::vector<int64_t>& geom,
-                 c10::optional<torch::Tensor> part, bool defer) {
+                 c10::optional<torch::Tensor> part, bool defer, c10::optional<torch::Tensor> stats) {
   const ndp::ConvGeom g = conv_geom(geom);
   const int cls = ndp::conv_direct_class(g);
   const int B = conv_batch(x, g, ndp::conv_fwd_imgs(cls));
@@ -598,8 +616,18 @@ int64_t conv_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, const std::v
   conv_check(y, "y", B, g.Co, g.OH, g.OW);
   const int ks = ndp::conv_ksplit(cls, g, B, false);
   float* pp = conv_part(part, ks, y.numel(), "conv_fwd");
+  double* st = nullptr;
+  if (stats.has_value()) {  // BatchNorm partial sums from the epilogue: [Co][S][2]
+    const int S = ndp::conv_fwd_stats_slices(cls, g, B);
+    check_dev(*stats, "stats");
+    TORCH_CHECK(S > 0, "conv_fwd: no statistics epilogue for this geometry / batch (conv_stats_slices)");
+    TORCH_CHECK(stats->scalar_type() == torch::kFloat64 && stats->is_contiguous() &&
+                    stats->numel() >= (int64_t)g.Co * S * 2,
+                "conv_fwd: stats must hold Co * S * 2 doubles");
+    st = stats->data_ptr<double>();
+  }
   const int left = ndp::launch_conv_fwd(x.data_ptr<float>(), w.data_ptr<float>(), y.data_ptr<float>(), B, g, pp,
-                                        cur_stream(), defer);
+                                        cur_stream(), defer, st);
   check_launch("launch_conv_fwd");
   return left;
 }
@@ -1287,7 +1315,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_fwd", &bn_fwd, py::arg("x"), py::arg("res"), py::arg("y"), py::arg("gamma"), py::arg("beta"),
         py::arg("rmean"), py::arg("rvar"), py::arg("nbt"), py::arg("save_mean"), py::arg("save_invstd"),
         py::arg("part"), py::arg("eps"), py::arg("momentum"), py::arg("relu"), py::arg("training"),
-        py::arg("single"), py::arg("xpart") = py::none(), py::arg("nslab") = 0);
+        py::arg("single"), py::arg("xpart") = py::none(), py::arg("nslab") = 0, py::arg("xstats") = py::none(),
+        py::arg("xS") = 0);
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("gamma"), py::arg("save_mean"),
         py::arg("save_invstd"), py::arg("dx"), py::arg("dres"), py::arg("dgamma"), py::arg("dbeta"), py::arg("part"),
         py::arg("relu"), py::arg("single"), py::arg("dypart") = py::none(), py::arg("nslab") = 0);
@@ -1307,7 +1336,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("slab_sum_many", &slab_sum_many);
   m.def("conv_plan", &conv_plan, py::arg("geom"), py::arg("batch"));
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("geom"), py::arg("part") = py::none(),
-        py::arg("defer") = false);
+        py::arg("defer") = false, py::arg("stats") = py::none());
+  m.def("conv_stats_slices", &conv_stats_slices, py::arg("geom"), py::arg("batch"));
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("geom"),
         py::arg("part") = py::none(), py::arg("addend") = py::none(), py::arg("defer") = false);
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("part"), py::arg("dw"), py::arg("geom"));

@@ -311,6 +311,11 @@ struct ConvFwdCfg {
   static_assert(CK % 2 == 0 && BM % (32 * WM) == 0 && BN % (32 * WN) == 0 && TM >= 1 && TN >= 1, "tile");
   static_assert(NSTEP % KB == 0, "operand prefetch blocks");
   static_assert(W % 4 == 0 && BM % 4 == 0, "float4 staging");
+  // BatchNorm statistics epilogue (conv_fwd_kernel `stats`): the [BM][BN + 4] output tile
+  // fits in the LDS the main loop used, 256 / BM threads per channel, float4 reads
+  static constexpr int STATS_LDO = BN + 4, STATS_TPC = 256 / BM;
+  static constexpr bool STATS_OK = 256 % BM == 0 && BN % (4 * STATS_TPC) == 0 &&
+                                   (size_t)BM * STATS_LDO <= (size_t)NBUF * (A_SZ + B_SZ);
 };
 
 // A (weights) is read straight from W: forward rows W[m][c0:c0+CK][:] (CK*RS contiguous
@@ -330,7 +335,8 @@ template <int R, int S, int ST, int PD, int H, int W, int CK, int BM, int IMGS, 
 __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                        float* __restrict__ y, float* __restrict__ part, int Cin,
                                                        int Kout, int cps, int64_t slab,
-                                                       const float* __restrict__ addend) {
+                                                       const float* __restrict__ addend,
+                                                       double* __restrict__ stats) {
   using G = ConvFwdCfg<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW>;
   constexpr int AE = (BM * G::KK + 3) / 4;  // float4 slots (scalar path: 4 scalars per slot)
   constexpr int A_PER_T = (AE + 255) / 256;
@@ -601,6 +607,49 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
         }
       }
     }
+
+  // BatchNorm forward statistics of the tile (stats != nullptr: unsplit launches whose output
+  // feeds a BatchNorm): per output channel the sum and sum of squares of the tile's IMGS x PQ
+  // outputs, fp32 over 4 values then fp64, stored to stats[(c * S + s) * 2 + {0, 1}] with
+  // s = blockIdx.x of S = gridDim.x: the [c][s][2] slice-partial layout the BN apply kernel
+  // folds (fixed order), so the BN needs no statistics pass (one launch and one full read of y
+  // fewer).  The tile goes through the LDS the main loop no longer reads (its last iteration
+  // ended on a barrier): row writes of 32 consecutive pixels per half-wave, float4 row reads.
+  if constexpr (G::STATS_OK && UPS == 1) {
+    if (stats != nullptr) {
+      float* L = smem;
+#pragma unroll
+      for (int tm = 0; tm < G::TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < G::TN; ++tn) {
+          const int n = (wn * G::TN + tn) * 32 + l32;
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            L[((wm * G::TM + tm) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * G::STATS_LDO + n] = acc[tm][tn][r];
+        }
+      __syncthreads();
+      constexpr int TPC = G::STATS_TPC, NPT = G::BN / TPC;
+      const int c = tid / TPC, j = tid - c * TPC;
+      const float* src = L + c * G::STATS_LDO + j * NPT;
+      double sum = 0.0, sq = 0.0;
+#pragma unroll 4
+      for (int i = 0; i < NPT; i += 4) {
+        const f32x4c v = *reinterpret_cast<const f32x4c*>(src + i);
+        sum += (double)((v.x + v.y) + (v.z + v.w));
+        sq += (double)((v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w));
+      }
+#pragma unroll
+      for (int o = 1; o < TPC; o <<= 1) {
+        sum += __shfl_xor(sum, o, 64);
+        sq += __shfl_xor(sq, o, 64);
+      }
+      if (j == 0) {
+        double* d = stats + ((int64_t)(m0 + c) * gridDim.x + blockIdx.x) * 2;
+        d[0] = sum;
+        d[1] = sq;
+      }
+    }
+  }
 }
 
 // ---- grad-W -----------------------------------------------------------------------------
@@ -918,7 +967,7 @@ static void set_lds(KernelT k, size_t bytes) {
 template <int R, int S, int ST, int PD, int H, int W, int CK, int BM, int IMGS, int WM, int NBUF, int KB, bool TRANSW,
           bool VEC, int UPS = 1, int SCH = 0, int IUPS = 1>
 static int run_fwd(const float* x, const float* w, float* y, int B, int Cin, int Kout, int ksplit, float* part,
-                   hipStream_t s, const float* addend = nullptr, bool defer = false) {
+                   hipStream_t s, const float* addend = nullptr, bool defer = false, double* stats = nullptr) {
   using G = ConvFwdCfg<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW>;
   auto k = conv_fwd_kernel<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW, VEC, UPS, SCH, IUPS>;
   static bool attr = false;  // once per instantiation (> 64 KiB of LDS needs the opt-in)
@@ -928,8 +977,10 @@ static int run_fwd(const float* x, const float* w, float* y, int B, int Cin, int
   const int cps = (nchunks + ksplit - 1) / ksplit;
   ksplit = (nchunks + cps - 1) / cps;
   const int64_t slab = (int64_t)B * Kout * G::PQ;  // compact partial tile layout
+  // stats: only unsplit launches of statistics-capable tiles (conv_fwd_stats_slices says which)
+  if (!(G::STATS_OK && UPS == 1) || ksplit > 1) stats = nullptr;
   hipLaunchKernelGGL(k, dim3(B / IMGS, Kout / BM, ksplit), dim3(256), G::LDS_BYTES, s, x, w, y, part, Cin, Kout, cps,
-                     slab, ksplit > 1 ? nullptr : addend);
+                     slab, ksplit > 1 ? nullptr : addend, stats);
   // defer: leave the ksplit slabs for the consumer (the fused BN kernel sums them while it
   // reads its input, ops/slablink.py) — one launch fewer per conv
   if (ksplit > 1 && defer && UPS == 1 && addend == nullptr) return ksplit;
@@ -1053,6 +1104,19 @@ int conv_ksplit(int cls, const ConvGeom& g, int B, bool dgrad) {
   while (ks * 2 <= nchunks && base * ks < kFillWgs && ks * 2 <= maxks) ks *= 2;
   return pow2_floor(ks);
 }
+// BatchNorm statistics from the forward epilogue: the layer1 3x3 and stem 7x7 classes (their
+// BatchNorms take the two-kernel large-map path; layer2's single-launch BN computes its own),
+// unsplit launches only.  Returns the partial count S (= workgroups along the batch), 0 = none.
+int conv_fwd_stats_slices(int cls, const ConvGeom& g, int B) {
+  static_assert(ConvFwdCfg<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, false>::STATS_OK &&
+                    ConvFwdCfg<3, 3, 1, 1, 8, 8, 16, 64, 1, 2, 2, 4, false>::STATS_OK &&
+                    ConvFwdCfg<3, 3, 1, 1, 8, 8, 8, 64, 2, 2, 2, 4, false>::STATS_OK &&
+                    ConvFwdCfg<7, 7, 2, 3, 32, 32, 4, 64, 1, 2, 1, 7, false>::STATS_OK,
+                "statistics epilogue fits every layer1 / stem tile");
+  if (cls != 0 && cls != 3) return 0;
+  if (conv_ksplit(cls, g, B, false) != 1) return 0;
+  return B / conv_fwd_imgs(cls);
+}
 // 3x3 stride-2 grad-x on the zero-inserted dY: exact (tests/test_conv_direct.py), 4x the
 // MFMA work of the sub-pixel form; measured on 1x MI355X (ResNet-18 step, round 2) 2.006 /
 // 2.005 vs MIOpen 1.991 ms at batch 512, 1.054 / 1.047 vs 1.051 at 64.  DEFAULT since round 3:
@@ -1090,7 +1154,7 @@ static bool ck16(int cls) {
 }
 
 int launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s,
-                    bool defer) {
+                    bool defer, double* stats) {
   const int cls = conv_direct_class(g);
   const int ks = conv_ksplit(cls, g, B, false);
   const bool c16 = ck16(cls);
@@ -1099,18 +1163,18 @@ int launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvG
     case 0:
       if (sch == 1)
         return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, false, true, 1, 1>(x, w, y, B, g.C, g.Co, ks, part, s,
-                                                                               nullptr, defer);
+                                                                               nullptr, defer, stats);
       if (sch == 2)
         return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, false, true, 1, 2>(x, w, y, B, g.C, g.Co, ks, part, s,
-                                                                               nullptr, defer);
+                                                                               nullptr, defer, stats);
       if (conv_variant() == 1)
         return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 2, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s, nullptr,
-                                                                         defer);
+                                                                         defer, stats);
       if (c16)
         return run_fwd<3, 3, 1, 1, 8, 8, 16, 64, 1, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s,
-                                                                          nullptr, defer);
+                                                                          nullptr, defer, stats);
       return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s, nullptr,
-                                                                       defer);
+                                                                       defer, stats);
     case 1:
       if (sch == 1)
         return run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, false, true, 1, 1>(x, w, y, B, g.C, g.Co, ks, part, s,
@@ -1134,8 +1198,10 @@ int launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvG
                                                                        defer);
     case 3:
       if (sched_all())
-        return run_fwd<7, 7, 2, 3, 32, 32, 4, 64, 1, 2, 1, 7, false, false, 1, 2>(x, w, y, B, g.C, g.Co, 1, nullptr, s);
-      return run_fwd<7, 7, 2, 3, 32, 32, 4, 64, 1, 2, 1, 7, false, false>(x, w, y, B, g.C, g.Co, 1, nullptr, s);
+        return run_fwd<7, 7, 2, 3, 32, 32, 4, 64, 1, 2, 1, 7, false, false, 1, 2>(x, w, y, B, g.C, g.Co, 1, nullptr, s,
+                                                                                    nullptr, false, stats);
+      return run_fwd<7, 7, 2, 3, 32, 32, 4, 64, 1, 2, 1, 7, false, false>(x, w, y, B, g.C, g.Co, 1, nullptr, s, nullptr,
+                                                                          false, stats);
     case 4:
       if (sched_all())
         return run_fwd<1, 1, 2, 0, 8, 8, 8, 64, 4, 2, 2, 4, false, true, 1, 2>(x, w, y, B, g.C, g.Co, ks, part, s,

@@ -132,7 +132,10 @@ int64_t bn_part_numel(int N, int C, int HW);
 void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamma, const float* beta,
                    float* rmean, float* rvar, int64_t* nbt, float* save_mean, float* save_invstd,
                    double* part, int N, int C, int HW, int S, float eps, float momentum, int relu,
-                   int training, int single, hipStream_t s, const float* xpart = nullptr, int nslab = 0);
+                   int training, int single, hipStream_t s, const float* xpart = nullptr, int nslab = 0,
+                   const double* xstats = nullptr, int xS = 0);
+// xstats (nullable, training): [C][xS][2] fp64 partial sums of x from the producing conv's
+// epilogue (conv_fwd_stats_slices); the large-map path then skips its statistics pass
 // xpart / dypart (nullable): the input x (forward) / dy (backward) is the sum of `nslab`
 // split-K slabs of numel(x) floats (a deferred conv sum); the forward also writes the sum to x
 void launch_bn_bwd(const float* dy, const float* y, const float* x, const float* gamma, const float* save_mean,
@@ -240,8 +243,11 @@ bool conv_dgrad_direct(int cls);
 int conv_ksplit(int cls, const ConvGeom& g, int B, bool dgrad);
 // defer: with split-K, skip the slab sum and return the number of slabs left in `part`
 // (compact output layout, slab = numel(out)); returns 1 when `y` / `dx` holds the result
+// stats (nullable; only where conv_fwd_stats_slices > 0): BatchNorm partial sums of y from the
+// epilogue, [Co][S][2] fp64 (sum, sum of squares per channel and batch tile)
 int launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s,
-                    bool defer = false);
+                    bool defer = false, double* stats = nullptr);
+int conv_fwd_stats_slices(int cls, const ConvGeom& g, int B);
 // addend (nullable, stride-1 classes): dx += addend in the epilogue / split-K sum (never deferred)
 int launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, float* part,
                       hipStream_t s, const float* addend = nullptr, bool defer = false);

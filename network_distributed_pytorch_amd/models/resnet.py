@@ -189,8 +189,9 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        if self.fused:
-            x = self.maxpool(self.bn1(self.conv1(x), relu=True))
+        if self.fused:  # the stem conv's epilogue hands its BN the statistics (ops/slablink.py)
+            s0 = SlabLink() if (SLAB_LINKS and x.is_cuda and torch.is_grad_enabled() and self.training) else None
+            x = self.maxpool(self.bn1(self.conv1(x, slab_out=s0), relu=True, slab_in=s0))
         else:
             x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
         x = self.layer2(self.layer1(x))

@@ -38,8 +38,10 @@ class _BNActFn(torch.autograd.Function):
         save_mean = torch.empty(C, device=x.device, dtype=torch.float32)
         save_invstd = torch.empty(C, device=x.device, dtype=torch.float32)
         xpart, nslab = slab_in.take_fwd() if slab_in is not None else (None, 0)
+        # statistics from the producing conv's epilogue (ops/slablink.py): no statistics pass
+        xstats, xS = slab_in.take_stats() if slab_in is not None else (None, 0)
         X.bn_fwd(x, res, y, weight, bias, running_mean, running_var, nbt, save_mean, save_invstd, part,
-                 float(eps), float(momentum), bool(relu), True, bool(single), xpart, nslab)
+                 float(eps), float(momentum), bool(relu), True, bool(single), xpart, nslab, xstats, xS)
         ctx.grad_slab = grad_slab  # ops/slablink.py: dy may arrive as the next conv's grad-x slabs
         ctx.relu = bool(relu)
         ctx.single = bool(single)
@@ -77,6 +79,8 @@ def bn_act(x, weight, bias, running_mean, running_var, nbt, part, training, mome
     if slab_in is not None and slab_in.fwd is not None and not fused:  # no fused consumer: finish the sum
         sp, n = slab_in.take_fwd()
         ext().slab_sum(sp, x, n)
+    if slab_in is not None and not fused:
+        slab_in.take_stats()  # x is complete; the epilogue statistics go unused
     if x.is_cuda and (training or not needs_grad):  # eval + autograd: differentiable torch path below
         if x.dtype != torch.float32:  # bf16 autocast: normalise in fp32 (stats are fp64 anyway)
             x = x.float()
@@ -132,6 +136,8 @@ class BatchNormAct2d(nn.BatchNorm2d):
                 self.momentum is None or not self.track_running_stats):
             sp, n = slab_in.take_fwd()
             ext().slab_sum(sp, x, n)
+        if slab_in is not None and (self.momentum is None or not self.track_running_stats):
+            slab_in.take_stats()
         if self.momentum is None or not self.track_running_stats:
             y = super().forward(x)
             if residual is not None:

@@ -26,7 +26,20 @@ from .gradarena import grad_buffer
 __all__ = ["direct_plan", "conv2d_direct", "DirectConvFn", "side_stream"]
 
 _PLANS: dict = {}
+_STATS: dict = {}
 _SIDE: dict = {}
+
+# BatchNorm statistics from the forward epilogue where the consuming BN takes the large-map
+# path (stem, layer1; ops/slablink.py).  NDP_CONV_BNSTATS=0 restores the BN statistics pass.
+CONV_BN_STATS = os.environ.get("NDP_CONV_BNSTATS", "1") != "0"
+
+
+def stats_slices(geom, B: int) -> int:
+    """Batch-tile partials of the BN statistics the forward epilogue emits for this conv (0: none)."""
+    key = (tuple(geom), int(B))
+    if key not in _STATS:
+        _STATS[key] = int(ext().conv_stats_slices(list(geom), int(B))) if CONV_BN_STATS else 0
+    return _STATS[key]
 
 # grad-W on a side stream measured SLOWER on ResNet-18 (2.47 vs 2.37 ms/step: the two
 # halves contend for CUs / L2 instead of filling gaps), so it is opt-in.
@@ -104,9 +117,13 @@ class DirectConvFn(torch.autograd.Function):
         OW = (W + 2 * p - KW) // s + 1
         y = torch.empty(B, Co, OH, OW, device=x.device, dtype=x.dtype)
         part = torch.empty(ks_fwd * y.numel(), device=x.device, dtype=x.dtype) if ks_fwd > 1 else None
-        left = ext().conv_fwd(x, weight, y, list(geom), part, slab_out is not None and part is not None)
+        S = stats_slices(geom, B) if slab_out is not None else 0
+        stats = torch.empty(Co * S * 2, device=x.device, dtype=torch.float64) if S > 0 else None
+        left = ext().conv_fwd(x, weight, y, list(geom), part, slab_out is not None and part is not None, stats)
         if left > 1:
             slab_out.put_fwd(part, left)  # y is filled by the consuming BN kernel
+        if stats is not None:
+            slab_out.put_stats(stats, S)  # the consuming BN skips its statistics pass
         ctx.save_for_backward(x, weight)
         ctx.plan = plan
         ctx.weight = wparam  # the Parameter itself: its .grad is where a deferred sum lands

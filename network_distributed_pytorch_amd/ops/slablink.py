@@ -12,6 +12,11 @@ sum to the conv's output buffer (BN saves its input for backward).  Where no fus
 kernel covers the shape, ``launch_bn_fwd`` / ``launch_bn_bwd`` run the plain slab sum
 themselves first, so a deferred sum is always finished.
 
+Where the conv runs unsplit and its forward BN takes the two-kernel large-map path (the
+ResNet stem and layer1), the link carries the BN's statistics instead: the conv epilogue
+emits per-channel, per-batch-tile fp64 sums of its output (csrc/conv.hip ``stats``) and the
+BN's apply kernel folds them, so the BN skips its statistics launch and its full read of x.
+
 Only wired inside the fused ResNet blocks (models/resnet.py), where each conv output /
 grad-x has exactly that one consumer.
 """
@@ -25,11 +30,20 @@ __all__ = ["SlabLink"]
 
 
 class SlabLink:
-    __slots__ = ("fwd", "bwd")
+    __slots__ = ("fwd", "bwd", "stats")
 
     def __init__(self):
         self.fwd: Optional[Tuple[torch.Tensor, int]] = None  # conv output slabs -> BN forward
         self.bwd: Optional[Tuple[torch.Tensor, int]] = None  # conv grad-x slabs -> BN backward
+        self.stats: Optional[Tuple[torch.Tensor, int]] = None  # conv epilogue BN partial sums [C][S][2]
+
+    def put_stats(self, stats: torch.Tensor, n: int) -> None:
+        assert self.stats is None, "SlabLink: statistics deposited twice"
+        self.stats = (stats, int(n))
+
+    def take_stats(self) -> Tuple[Optional[torch.Tensor], int]:
+        v, self.stats = self.stats, None
+        return v if v is not None else (None, 0)
 
     def put_fwd(self, part: torch.Tensor, n: int) -> None:
         assert self.fwd is None, "SlabLink: forward slabs deposited twice"

@@ -30,6 +30,11 @@ def test_resnet18_slab_links_bitwise(device, batch, monkeypatch):
     must equal off: the step itself is deterministic)."""
     assert ops.native_available()
     monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
+    # the slab hand-off alone (the epilogue BN statistics change the summation order:
+    # tests/test_conv_bnstats_gpu.py)
+    from network_distributed_pytorch_amd.ops import conv as conv_mod
+    monkeypatch.setattr(conv_mod, "CONV_BN_STATS", False)
+    monkeypatch.setattr(conv_mod, "_STATS", {})
     torch.manual_seed(0)
     m = build_resnet(18, 1000).to(device)
     state = {k: v.clone() for k, v in m.state_dict().items()}
