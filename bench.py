@@ -152,6 +152,10 @@ class Workload:
         # fused gfx950 softmax cross-entropy (ops/loss.py); --stock keeps PyTorch-ROCm's
         self.crit = torch.nn.CrossEntropyLoss() if args.stock else CrossEntropyLoss()
         self.loss_acc = torch.zeros((), device=device)
+        # the fused loss kernel adds each step's loss into loss_acc itself (no add launch)
+        self.crit_acc = not args.stock and args.amp != "bf16" and not self.is_bert
+        if self.crit_acc:
+            self.crit.accumulate = self.loss_acc
         self.graph_mode = None
         self.runner = None
 
@@ -189,7 +193,7 @@ class Workload:
                 with torch.autocast("cuda", dtype=torch.bfloat16):
                     return fp32_loss_of(b).float()
 
-        sync, loss_acc = self.sync, self.loss_acc
+        sync, loss_acc, crit_acc = self.sync, self.loss_acc, self.crit_acc
         graph_mode = args.graph_mode
         if graph_mode == "auto" and "ref" in args.reducer:
             graph_mode = "none"  # reference-semantics arms are eager by definition
@@ -211,7 +215,8 @@ class Workload:
                 sync.zero_grad()
                 loss = loss_of(static)
                 loss.backward(one)
-                loss_acc.add_(loss.detach())  # one add, no copy into a static loss
+                if not crit_acc:
+                    loss_acc.add_(loss.detach())  # one add, no copy into a static loss
 
             runner = StepRunner(pre, sync, mode=graph_mode, warmup=3,
                                 state_tensors=list(model.buffers()))
@@ -231,7 +236,8 @@ class Workload:
                 loss = loss_of(pool[i % n_pool])
                 loss.backward()
                 sync.step()
-                loss_acc.add_(loss.detach())
+                if not crit_acc:
+                    loss_acc.add_(loss.detach())
         self.graph_mode = graph_mode
         return step
 

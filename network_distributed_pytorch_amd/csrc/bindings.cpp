@@ -834,8 +834,14 @@ int64_t gelu_bwd_colsum(torch::Tensor g, torch::Tensor h, torch::Tensor dh, torc
 
 // fused cross-entropy forward: loss (0-d), dl [B, K] saved gradient; scratch = rowloss [B] + inv [1]
 void ce_fwd(torch::Tensor x, torch::Tensor tgt, torch::Tensor dl, torch::Tensor scratch, torch::Tensor loss,
-            torch::Tensor ctr, int64_t ignore_index) {
+            torch::Tensor ctr, int64_t ignore_index, c10::optional<torch::Tensor> acc) {
   check_f32(x, "logits"); check_f32(dl, "dl"); check_f32(scratch, "scratch"); check_f32(loss, "loss");
+  float* ap = nullptr;
+  if (acc.has_value()) {  // running loss sum: acc += loss inside the kernel
+    check_f32(*acc, "acc");
+    TORCH_CHECK(acc->numel() == 1, "ce_fwd: acc must be a one-element fp32 tensor");
+    ap = acc->data_ptr<float>();
+  }
   check_dev(tgt, "target"); check_dev(ctr, "ctr");
   TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && dl.sizes() == x.sizes() && dl.is_contiguous(),
               "ce_fwd: logits / dl must be contiguous [B, K]");
@@ -848,7 +854,7 @@ void ce_fwd(torch::Tensor x, torch::Tensor tgt, torch::Tensor dl, torch::Tensor 
   float* sp = scratch.data_ptr<float>();
   ndp::launch_ce_fwd(x.data_ptr<float>(), tgt.data_ptr<int64_t>(), B, (int)x.size(1), ignore_index,
                      dl.data_ptr<float>(), sp, loss.data_ptr<float>(), sp + B,
-                     reinterpret_cast<unsigned*>(ctr.data_ptr<int32_t>()), cur_stream());
+                     reinterpret_cast<unsigned*>(ctr.data_ptr<int32_t>()), cur_stream(), ap);
   check_launch("launch_ce_fwd");
 }
 
@@ -1366,7 +1372,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("colsum", &colsum, py::arg("g"), py::arg("out"), py::arg("part") = c10::optional<torch::Tensor>());
   m.def("gelu_bwd_colsum", &gelu_bwd_colsum, py::arg("g"), py::arg("h"), py::arg("dh"), py::arg("db"),
         py::arg("part") = c10::optional<torch::Tensor>());
-  m.def("ce_fwd", &ce_fwd);
+  m.def("ce_fwd", &ce_fwd, py::arg("x"), py::arg("tgt"), py::arg("dl"), py::arg("scratch"), py::arg("loss"),
+        py::arg("ctr"), py::arg("ignore_index"), py::arg("acc") = py::none());
   m.def("ln_fwd", &ln_fwd, py::arg("a"), py::arg("b"), py::arg("gamma"), py::arg("beta"), py::arg("y"), py::arg("s"),
         py::arg("mean"), py::arg("rstd"), py::arg("eps"), py::arg("drop_mode") = 0, py::arg("p") = 0.0,
         py::arg("seed") = c10::optional<torch::Tensor>());

@@ -41,7 +41,8 @@ constexpr int kCeRegs = 16;  // row length held in registers: K <= 1024
 __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ x, const int64_t* __restrict__ tgt,
                                                      int B, int K, int64_t ignore, float* __restrict__ dl,
                                                      float* __restrict__ rowloss, float* __restrict__ loss,
-                                                     float* __restrict__ inv, unsigned* __restrict__ ctr) {
+                                                     float* __restrict__ inv, unsigned* __restrict__ ctr,
+                                                     float* __restrict__ acc) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int b = blockIdx.x * kCeRowsPerWg + wave;
   if (b < B) {
@@ -108,6 +109,7 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ x
     const float tot = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
     const float cnt = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
     loss[0] = tot / cnt;  // 0 / 0 = NaN when every row is ignored, like PyTorch
+    if (acc != nullptr) acc[0] += tot / cnt;  // running loss sum (logging): no separate add launch
     inv[0] = 1.f / cnt;
     __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -127,9 +129,10 @@ __global__ __launch_bounds__(256) void ce_bwd_kernel(const float* __restrict__ d
 }
 
 void launch_ce_fwd(const float* x, const int64_t* tgt, int B, int K, int64_t ignore, float* dl, float* rowloss,
-                   float* loss, float* inv, unsigned* ctr, hipStream_t s) {
+                   float* loss, float* inv, unsigned* ctr, hipStream_t s, float* acc) {
   const unsigned wgs = (unsigned)((B + kCeRowsPerWg - 1) / kCeRowsPerWg);
-  hipLaunchKernelGGL(ce_fwd_kernel, dim3(wgs), dim3(256), 0, s, x, tgt, B, K, ignore, dl, rowloss, loss, inv, ctr);
+  hipLaunchKernelGGL(ce_fwd_kernel, dim3(wgs), dim3(256), 0, s, x, tgt, B, K, ignore, dl, rowloss, loss, inv, ctr,
+                     acc);
 }
 
 void launch_ce_bwd(const float* dl, const float* g, const float* inv, float* dx, int64_t n, hipStream_t s) {

@@ -164,8 +164,9 @@ void launch_embedding_backward(const int64_t* ids, int T, const float* gout, int
 // x [B, K] logits, tgt [B] int64; dl [B, K] saved gradient (unscaled softmax - onehot),
 // rowloss [B] scratch, loss / inv device scalars, ctr: one zeroed uint32 (re-armed by the kernel)
 namespace ndp {
+// acc (nullable): acc[0] += loss (a running loss sum)
 void launch_ce_fwd(const float* x, const int64_t* tgt, int B, int K, int64_t ignore, float* dl, float* rowloss,
-                   float* loss, float* inv, unsigned* ctr, hipStream_t s);
+                   float* loss, float* inv, unsigned* ctr, hipStream_t s, float* acc = nullptr);
 // dx = dl * (g[0] * inv[0])
 void launch_ce_bwd(const float* dl, const float* g, const float* inv, float* dx, int64_t n, hipStream_t s);
 }  // namespace ndp

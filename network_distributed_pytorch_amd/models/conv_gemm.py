@@ -265,8 +265,8 @@ class GemmConv2d(nn.Conv2d):
         conv's grad-x (fused into the kernel / GEMM where the path allows).
         ``slab_out`` / ``grad_slab`` (ops/slablink.SlabLink, direct kernels only): the
         forward / grad-x split-K slabs go to the neighbouring fused BN instead of a sum
-        launch (other paths leave the links empty).  ``branch`` (ops/gradlink.BranchLink,
-        Toeplitz path only): grad-x shared with a sibling conv of the same input."""
+        launch (other paths leave the links empty).  ``branch`` (ops/gradlink.BranchLink):
+        grad-x shared with a sibling conv of the same input."""
         if not (self.gemm and x.is_cuda and self.groups == 1 and self.dilation == (1, 1) and self.bias is None
                 and self.stride[0] == self.stride[1] and self.padding[0] == self.padding[1]
                 and self.padding_mode == "zeros" and x.dtype == torch.float32):
@@ -277,7 +277,7 @@ class GemmConv2d(nn.Conv2d):
         if self.direct:
             plan = direct_plan(x, self.weight, s, p)
             if plan is not None:
-                return DirectConvFn.apply(x, self.weight, plan, link, slab_out, grad_slab)
+                return DirectConvFn.apply(x, self.weight, plan, link, slab_out, grad_slab, branch)
             padded = direct_plan_padded(x, self.weight, s, p)
             if padded is not None:  # ragged batch: zero-padded images, same kernels (links left empty)
                 plan, Bp = padded

@@ -102,12 +102,17 @@ def direct_plan_padded(x: torch.Tensor, weight: torch.Tensor, stride: int, paddi
 
 class DirectConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, plan, link=None, slab_out=None, grad_slab=None):
+    def forward(ctx, x, weight, plan, link=None, slab_out=None, grad_slab=None, branch=None):
         """``slab_out`` / ``grad_slab`` (ops/slablink.py): leave the forward / grad-x split-K
-        slabs for the fused BN kernel that consumes them instead of summing them here."""
+        slabs for the fused BN kernel that consumes them instead of summing them here.
+        ``branch`` (ops/gradlink.BranchLink): grad-x shared with a sibling conv of the same input
+        (a downsample block's conv1 and 1x1 downsample), summed in a kernel epilogue."""
         wparam = weight
         ctx.link = link  # ops/gradlink.py: residual-branch gradient folded into grad-x
         ctx.grad_slab = grad_slab
+        ctx.branch = branch
+        if branch is not None:
+            branch.join(direct=True)
         geom, _, wgrad_imgs, dgrad_direct, ks_fwd, _ = plan
         C, H, W, Co, KH, KW, s, p = geom
         x = x.contiguous()
@@ -152,29 +157,53 @@ class DirectConvFn(torch.autograd.Function):
                     ext().conv_wgrad(x, dy, part, dw, list(geom))
         addend = ctx.link.take() if ctx.link is not None else None
         if ctx.needs_input_grad[0]:
-            if dgrad_direct:
+            grad_slab = ctx.grad_slab
+
+            def dgrad(addend):
+                if not dgrad_direct:
+                    dx = torch.ops.aten.convolution_backward(dy, x, weight, None, [s, s], [p, p], [1, 1], False,
+                                                             [0, 0], 1, [True, False, False])[0]
+                    return dx if addend is None else dx + addend
                 dx = torch.empty_like(x)
                 part = None
                 if ks_dgrad > 1:  # partials in dx layout (the 1x1 stride-2 class: its compact 4x4 map)
                     ups = geom[4] == 1 and geom[6] == 2
                     slab = (dy.numel() // geom[3]) * geom[0] if ups else x.numel()
                     part = torch.empty(ks_dgrad * slab, device=x.device, dtype=x.dtype)
-                fuse = addend is not None and geom[6] == 1  # stride-1 classes take the addend in-kernel
-                defer = ctx.grad_slab is not None and part is not None and addend is None
+                fuse = addend is not None and _takes_addend(geom)
+                defer = grad_slab is not None and part is not None and addend is None
                 left = ext().conv_dgrad(dy, weight, dx, list(geom), part, addend.contiguous() if fuse else None,
                                         defer)
                 if left > 1:
-                    ctx.grad_slab.put_bwd(part, left)  # dx stays unwritten: the BN backward sums the slabs
-                if fuse:
-                    addend = None
+                    grad_slab.put_bwd(part, left)  # dx stays unwritten: the BN backward sums the slabs
+                return dx + addend if (addend is not None and not fuse) else dx
+
+            br = ctx.branch if ctx.branch is not None and ctx.branch.active() else None
+            other = br.take() if br is not None else None
+            if br is not None and other is None and br.all_direct() and addend is None and dgrad_direct \
+                    and _takes_addend(geom):
+                # first of two direct siblings, and this grad-x kernel can add the sibling's
+                # grad-x in its epilogue: run it once the sibling's exists (no add launch)
+                br.put(dgrad)
+            elif callable(other):  # the sibling waits for this grad-x as its addend
+                dx = other(dgrad(addend))
             else:
-                dx = torch.ops.aten.convolution_backward(dy, x, weight, None, [s, s], [p, p], [1, 1], False, [0, 0],
-                                                         1, [True, False, False])[0]
-            if addend is not None:
-                dx = dx + addend
+                if other is not None:
+                    addend = other if addend is None else addend + other
+                dx = dgrad(addend)
+                if br is not None and other is None:  # first of the two: the sibling adds onto it
+                    br.put(dx)
+                    dx = None
         if fork:
             main.wait_stream(side)
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None, None, None
+
+
+def _takes_addend(geom) -> bool:
+    """The grad-x kernel adds an addend in its epilogue / split-K sum: the 3x3 classes (stride 1,
+    and stride 2 run as the stride-1 kernel on the zero-inserted dY); not the 1x1 stride-2
+    class (even-pixel scatter epilogue)."""
+    return geom[4] == 3 and geom[5] == 3
 
 
 def conv2d_direct(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int, plan=None,

@@ -55,22 +55,29 @@ class BranchLink:
     second accumulates its product onto the deposit in place (``addmm_``, beta = 1) and
     returns the sum.  With fewer than two members the link is inert."""
 
-    __slots__ = ("members", "grad")
+    __slots__ = ("members", "direct", "grad")
 
     def __init__(self):
         self.members = 0
-        self.grad: Optional[torch.Tensor] = None
+        self.direct = 0  # members on the direct conv kernels (ops/conv.DirectConvFn)
+        self.grad = None  # the first member's grad-x, or (direct pair) its deferred grad-x kernel
 
-    def join(self) -> None:
+    def join(self, direct: bool = False) -> None:
         self.members += 1
+        self.direct += int(direct)
 
     def active(self) -> bool:
         return self.members == 2
 
-    def put(self, g: torch.Tensor) -> None:
+    def all_direct(self) -> bool:
+        """Both members are direct convs: the first may deposit a callable that runs its
+        grad-x kernel with the second's grad-x as the epilogue addend."""
+        return self.direct == 2
+
+    def put(self, g) -> None:
         assert self.grad is None, "BranchLink: grad-x deposited twice"
         self.grad = g
 
-    def take(self) -> Optional[torch.Tensor]:
+    def take(self):
         g, self.grad = self.grad, None
         return g

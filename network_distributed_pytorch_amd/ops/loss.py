@@ -41,13 +41,13 @@ def _counter(device: torch.device) -> torch.Tensor:
 
 class _CrossEntropyFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, logits, target, ignore_index):
+    def forward(ctx, logits, target, ignore_index, acc=None):
         x = logits.contiguous()
         t = target.contiguous()
         dl = torch.empty_like(x)
         scratch = torch.empty(x.shape[0] + 1, device=x.device, dtype=torch.float32)
         loss = torch.empty((), device=x.device, dtype=torch.float32)
-        ext().ce_fwd(x, t, dl, scratch, loss, _counter(x.device), int(ignore_index))
+        ext().ce_fwd(x, t, dl, scratch, loss, _counter(x.device), int(ignore_index), acc)
         ctx.save_for_backward(dl, scratch)
         return loss
 
@@ -56,20 +56,32 @@ class _CrossEntropyFn(torch.autograd.Function):
         dl, scratch = ctx.saved_tensors
         dx = torch.empty_like(dl)
         ext().ce_bwd(dl, g.reshape(1).contiguous().float(), scratch, dx)
-        return dx, None, None
+        return dx, None, None, None
 
 
-def cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index: int = -100) -> torch.Tensor:
+def cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index: int = -100,
+                  accumulate: "torch.Tensor | None" = None) -> torch.Tensor:
+    """``accumulate`` (optional one-element fp32 tensor): ``accumulate += loss`` as well (a
+    running loss sum for logging; inside the kernel on device, no separate add launch)."""
     if (_ENABLED and logits.is_cuda and logits.dim() == 2 and logits.dtype == torch.float32 and target.dtype == torch.int64
             and target.dim() == 1 and logits.shape[0] >= 1):
-        return _CrossEntropyFn.apply(logits, target, ignore_index)
-    return F.cross_entropy(logits, target, ignore_index=ignore_index)
+        return _CrossEntropyFn.apply(logits, target, ignore_index, accumulate)
+    loss = F.cross_entropy(logits, target, ignore_index=ignore_index)
+    if accumulate is not None:
+        accumulate.add_(loss.detach())
+    return loss
 
 
 class CrossEntropyLoss(nn.CrossEntropyLoss):
     """``nn.CrossEntropyLoss`` whose default configuration runs the fused kernel on device."""
 
+    # optional running loss sum (``cross_entropy(accumulate=)``), e.g. the trainer's epoch loss
+    accumulate: "torch.Tensor | None" = None
+
     def forward(self, input: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
         if (self.weight is None and self.reduction == "mean" and self.label_smoothing == 0.0):
-            return cross_entropy(input, target, self.ignore_index)
-        return super().forward(input, target)
+            return cross_entropy(input, target, self.ignore_index, self.accumulate)
+        loss = super().forward(input, target)
+        if self.accumulate is not None:
+            self.accumulate.add_(loss.detach())
+        return loss

@@ -57,3 +57,24 @@ def test_cross_entropy_cpu_fallback():
     x = torch.randn(8, 5, requires_grad=True)
     t = torch.randint(0, 5, (8,))
     torch.testing.assert_close(CrossEntropyLoss()(x, t), F.cross_entropy(x, t))
+
+
+def test_cross_entropy_accumulates_running_sum(device):
+    """``accumulate``: the kernel adds each loss into the running sum (no add launch); the
+    same sum as adding the returned losses, and the loss / gradient are unchanged."""
+    torch.manual_seed(5)
+    acc = torch.zeros((), device=device)
+    crit = CrossEntropyLoss()
+    crit.accumulate = acc
+    ref = torch.zeros((), device=device)
+    for i in range(3):
+        x = (torch.randn(64, 1000, device=device) * 2).requires_grad_(True)
+        t = torch.randint(0, 10, (64,), device=device)
+        loss = crit(x, t)
+        plain = cross_entropy(x.detach(), t)
+        assert torch.equal(loss.detach(), plain)
+        ref += plain
+        loss.backward()
+        assert torch.isfinite(x.grad).all()
+    torch.cuda.synchronize()
+    assert torch.equal(acc, ref)

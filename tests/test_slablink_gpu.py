@@ -110,3 +110,31 @@ def test_resnet18_branch_links_match(device, batch, monkeypatch):
     for n in g0:
         scale = g0[n].abs().max().item() + 1e-12
         torch.testing.assert_close(g1[n], g0[n], rtol=1e-4, atol=1e-5 * scale, msg=n)
+
+
+@pytest.mark.parametrize("batch", [64, 512])
+def test_direct_branch_link_bitwise(device, batch, monkeypatch):
+    """layer2's entry block on the direct kernels: conv1's (3x3/2) grad-x kernel adds the 1x1/2
+    downsample's grad-x in its epilogue / split-K sum (BranchLink, deferred first member) —
+    bitwise equal to autograd's add of the two (the same fp32 sum, addend added last)."""
+    from network_distributed_pytorch_amd.models.resnet import BasicBlock, conv1x1
+
+    torch.manual_seed(2)
+    ds = torch.nn.Sequential(conv1x1(64, 128, 2), BatchNormAct2d(128))
+    blk = BasicBlock(64, 128, 2, ds, norm=BatchNormAct2d).to(device).train()
+    state = {k: v.clone() for k, v in blk.state_dict().items()}
+    x0 = torch.randn(batch, 64, 8, 8, device=device)
+    g = torch.randn(batch, 128, 4, 4, device=device)
+    runs = []
+    for on in (False, True, True):
+        monkeypatch.setattr(resnet_mod, "BRANCH_LINKS", on)
+        blk.load_state_dict(state)
+        blk.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        blk(x).backward(g)
+        torch.cuda.synchronize()
+        runs.append((x.grad.clone(), {n: p.grad.clone() for n, p in blk.named_parameters()}))
+    for xg, pg in runs[1:]:
+        assert torch.equal(xg, runs[0][0])
+        for n in pg:
+            assert torch.equal(pg[n], runs[0][1][n]), n
