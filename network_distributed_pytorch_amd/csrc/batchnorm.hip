@@ -228,7 +228,7 @@ __global__ __launch_bounds__(256) void bn_bwd_stats_kernel(const float* __restri
                                                            const float* __restrict__ save_invstd,
                                                            double* __restrict__ part, int N, int C, int HW,
                                                            int S, int relu, const float* __restrict__ src = nullptr,
-                                                           int nslab = 0) {
+                                                           int nslab = 0, const float* __restrict__ sadd = nullptr) {
   __shared__ double red[16];
   const int s = blockIdx.x, c = blockIdx.y;
   const BnSlice sl = slice_of(N, S, s);
@@ -241,6 +241,7 @@ __global__ __launch_bounds__(256) void bn_bwd_stats_kernel(const float* __restri
       if (src != nullptr) {
         g = *reinterpret_cast<const f32x4*>(src + o);
         for (int z = 1; z < nslab; ++z) g += *reinterpret_cast<const f32x4*>(src + z * slab + o);
+        if (sadd != nullptr) g += *reinterpret_cast<const f32x4*>(sadd + o);  // deferred addend, last
         *reinterpret_cast<f32x4*>(const_cast<float*>(dy) + o) = g;
       } else {
         g = *reinterpret_cast<const f32x4*>(dy + o);
@@ -584,6 +585,7 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
       const int64_t slab = (int64_t)N * CHW;
       sum = src[o];
       for (int z = 1; z < nslab; ++z) sum += src[z * slab + o];
+      if (BWD && res != nullptr) sum += res[o];  // backward: `res` carries the deferred grad-x addend
     }
     if (!BWD) {
       v[k] = ok ? (src ? sum : x[o]) : 0.f;
@@ -1018,16 +1020,18 @@ void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamm
 void launch_bn_bwd(const float* dy, const float* y, const float* x, const float* gamma, const float* save_mean,
                    const float* save_invstd, float* dx, float* dres, float* dgamma, float* dbeta, double* part,
                    int N, int C, int HW, int S, int relu, int single, hipStream_t s, const float* dypart,
-                   int nslab) {
+                   int nslab, const float* dyadd) {
   const BnSync sy = bn_sync(part, 1);
   part += kBnSyncSlots;
   if (dypart != nullptr && nslab < 2) dypart = nullptr;
+  if (dypart == nullptr) dyadd = nullptr;
   if (dypart != nullptr && nslab > kMaxFusedSlabs) {
-    launch_slab_sum(dypart, const_cast<float*>(dy), (int64_t)N * C * HW, nslab, s);
+    launch_slab_sum(dypart, const_cast<float*>(dy), (int64_t)N * C * HW, nslab, s, dyadd);
     dypart = nullptr;
+    dyadd = nullptr;
   }
-  if (single && bn_fused_ok(N, C, HW)) {
-    launch_small_fused<1>(HW, x, nullptr, dy, y, gamma, nullptr, nullptr, nullptr, nullptr,
+  if (single && bn_fused_ok(N, C, HW)) {  // (the backward kernel's `res` slot: the slab addend)
+    launch_small_fused<1>(HW, x, dyadd, dy, y, gamma, nullptr, nullptr, nullptr, nullptr,
                           const_cast<float*>(save_mean), const_cast<float*>(save_invstd), dgamma, dbeta, dx, dres, N, C,
                           0.f, 0.f, relu, s, dypart, nslab, sy);
     return;
@@ -1035,10 +1039,12 @@ void launch_bn_bwd(const float* dy, const float* y, const float* x, const float*
   const bool vec_ok = (HW % 4) == 0 && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)x & 15) == 0 &&
                       ((uintptr_t)dx & 15) == 0 && (!relu || ((uintptr_t)y & 15) == 0) &&
                       (dres == nullptr || ((uintptr_t)dres & 15) == 0) && ((uintptr_t)dypart & 15) == 0;
-  if (dypart != nullptr && !(bn_stats_slabs() && vec_ok && !bn_small_path(N, C, HW))) {
+  if (dypart != nullptr && !(bn_stats_slabs() && vec_ok && !bn_small_path(N, C, HW) &&
+                             (dyadd == nullptr || ((uintptr_t)dyadd & 15) == 0))) {
     // no fused consumer: finish the conv's split-K grad-x sum into dy
-    launch_slab_sum(dypart, const_cast<float*>(dy), (int64_t)N * C * HW, nslab, s);
+    launch_slab_sum(dypart, const_cast<float*>(dy), (int64_t)N * C * HW, nslab, s, dyadd);
     dypart = nullptr;
+    dyadd = nullptr;
   }
   if (bn_small_path(N, C, HW)) {
     const int Ss = bn_small_slices(N, C, HW);
@@ -1058,7 +1064,7 @@ void launch_bn_bwd(const float* dy, const float* y, const float* x, const float*
   const dim3 grid(S, C);
   if (vec) {  // the statistics pass also adds deferred grad-x slabs (dypart) and writes dy
     hipLaunchKernelGGL(bn_bwd_stats_kernel<true>, grid, dim3(256), 0, s, dy, y, x, save_mean, save_invstd, part, N, C,
-                       HW, S, relu, dypart, nslab);
+                       HW, S, relu, dypart, nslab, dyadd);
     hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, grid, dim3(256), 0, s, dy, y, x, gamma, save_mean, save_invstd, dx,
                        dres, dgamma, dbeta, part, N, C, HW, S, relu);
   } else {

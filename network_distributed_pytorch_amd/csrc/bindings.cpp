@@ -351,8 +351,14 @@ void bn_fwd(torch::Tensor x, c10::optional<torch::Tensor> res, torch::Tensor y,
 void bn_bwd(torch::Tensor dy, c10::optional<torch::Tensor> y, torch::Tensor x, c10::optional<torch::Tensor> gamma,
             torch::Tensor save_mean, torch::Tensor save_invstd, torch::Tensor dx, c10::optional<torch::Tensor> dres,
             c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta, torch::Tensor part,
-            bool relu, bool single, c10::optional<torch::Tensor> dypart, int64_t nslab) {
+            bool relu, bool single, c10::optional<torch::Tensor> dypart, int64_t nslab,
+            c10::optional<torch::Tensor> dyadd) {
   check_f32(dy, "dy"); check_f32(x, "x"); check_f32(dx, "dx"); check_dev(part, "part");
+  if (dyadd.has_value()) {
+    check_f32(*dyadd, "dyadd");
+    TORCH_CHECK(dyadd->sizes() == dy.sizes() && dyadd->is_contiguous() && dypart.has_value(),
+                "bn_bwd: dyadd (the deferred grad-x addend) must match dy and come with dypart");
+  }
   TORCH_CHECK(dy.sizes() == x.sizes() && dx.sizes() == x.sizes(), "bn_bwd: bad shapes");
   TORCH_CHECK(!relu || y.has_value(), "bn_bwd: relu needs y");
   const int N = (int)x.size(0), C = (int)x.size(1);
@@ -365,7 +371,7 @@ void bn_bwd(torch::Tensor dy, c10::optional<torch::Tensor> y, torch::Tensor x, c
                      const_cast<float*>(opt_f32(dres, "dres")), const_cast<float*>(opt_f32(dgamma, "dgamma")),
                      const_cast<float*>(opt_f32(dbeta, "dbeta")), part.data_ptr<double>(), N, C, HW, S,
                      relu ? 1 : 0, single ? 1 : 0, cur_stream(), slab_input(dypart, nslab, dy.numel(), "bn_bwd"),
-                     (int)nslab);
+                     (int)nslab, opt_f32(dyadd, "dyadd"));
   check_launch("launch_bn_bwd");
 }
 
@@ -1325,7 +1331,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("xS") = 0);
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("gamma"), py::arg("save_mean"),
         py::arg("save_invstd"), py::arg("dx"), py::arg("dres"), py::arg("dgamma"), py::arg("dbeta"), py::arg("part"),
-        py::arg("relu"), py::arg("single"), py::arg("dypart") = py::none(), py::arg("nslab") = 0);
+        py::arg("relu"), py::arg("single"), py::arg("dypart") = py::none(), py::arg("nslab") = 0,
+        py::arg("dyadd") = py::none());
   m.def("bn_slices", &bn_slices);
   m.def("slab_sum", &slab_sum);
   m.def("bn_part_numel", &bn_part_numel);

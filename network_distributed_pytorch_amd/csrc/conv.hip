@@ -983,7 +983,8 @@ static int run_fwd(const float* x, const float* w, float* y, int B, int Cin, int
                      slab, ksplit > 1 ? nullptr : addend, stats);
   // defer: leave the ksplit slabs for the consumer (the fused BN kernel sums them while it
   // reads its input, ops/slablink.py) — one launch fewer per conv
-  if (ksplit > 1 && defer && UPS == 1 && addend == nullptr) return ksplit;
+  // (an addend then goes to the consumer too: it adds it after the slabs, launch_bn_bwd dyadd)
+  if (ksplit > 1 && defer && UPS == 1) return ksplit;
   if (ksplit > 1) {
     if constexpr (UPS == 1)
       hipLaunchKernelGGL(conv_slab_sum_kernel, dim3((unsigned)((slab / 4 + 15) / 16)), dim3(256), 0, s, part, y, slab,

@@ -141,7 +141,8 @@ void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamm
 void launch_bn_bwd(const float* dy, const float* y, const float* x, const float* gamma, const float* save_mean,
                    const float* save_invstd, float* dx, float* dres, float* dgamma, float* dbeta, double* part,
                    int N, int C, int HW, int S, int relu, int single, hipStream_t s, const float* dypart = nullptr,
-                   int nslab = 0);
+                   int nslab = 0, const float* dyadd = nullptr);
+// dyadd (nullable, with dypart): dy = sum of the slabs + dyadd (added last, as conv_slab_sum does)
 }  // namespace ndp
 
 // ---- embedding backward (embedding.hip) -------------------------------------------------
@@ -249,7 +250,8 @@ int conv_ksplit(int cls, const ConvGeom& g, int B, bool dgrad);
 int launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s,
                     bool defer = false, double* stats = nullptr);
 int conv_fwd_stats_slices(int cls, const ConvGeom& g, int B);
-// addend (nullable, stride-1 classes): dx += addend in the epilogue / split-K sum (never deferred)
+// addend (nullable, 3x3 classes): dx += addend in the epilogue / split-K sum; with defer the
+// slabs are left unsummed and the consumer adds the addend after them (launch_bn_bwd dyadd)
 int launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, float* part,
                       hipStream_t s, const float* addend = nullptr, bool defer = false);
 // out[i] = sum_{z < nslab} part[z * n + i] (+ addend[i]) in z order (n % 4 == 0), same order as

@@ -68,9 +68,15 @@ class BasicBlock(nn.Module):
         self.stride = stride
         self.fused = norm is BatchNormAct2d
 
-    def forward(self, x):
+    def forward(self, x, grad_in=None, grad_out=None):
+        """``grad_in`` / ``grad_out`` (ops/slablink.SlabLink, fused training only): conv1's
+        split-K grad-x slabs (+ the residual addend) go to the PREVIOUS block's BN2, whose
+        output gradient they are, and this block's BN2 takes the next block's (ResNet.forward
+        chains them): one sum launch fewer per block boundary."""
         if self.fused:  # conv -> BN+ReLU ; conv -> BN + identity + ReLU (fused kernels)
             train = x.is_cuda and torch.is_grad_enabled() and self.training
+            if not (train and SLAB_LINKS):
+                grad_in = grad_out = None
             # identity block: BN2's residual gradient is folded into conv1's grad-x
             # (ops/gradlink.py) instead of an autograd add of the two branches
             link = GradLink() if self.downsample is None and train and x.requires_grad else None
@@ -84,15 +90,20 @@ class BasicBlock(nn.Module):
             # layers; ops/gradlink.BranchLink) instead of an autograd add of the two
             br = (BranchLink() if BRANCH_LINKS and train and self.downsample is not None and x.requires_grad
                   else None)
+            if self.downsample is not None and br is None:
+                # x's gradient is autograd's sum of two grad-x tensors: conv1's cannot be left
+                # as unsummed slabs for the previous BN2
+                grad_in = None
             if self.downsample is not None:
                 ds = self.downsample
                 if train and len(ds) == 2 and isinstance(ds[0], GemmConv2d) and isinstance(ds[1], BatchNormAct2d):
                     identity = ds[1](ds[0](x, slab_out=sd, branch=br), slab_in=sd)
                 else:
                     identity = ds(x)
-            out = self.bn1(self.conv1(x, link=link, slab_out=s1, branch=br), relu=True, slab_in=s1, grad_slab=g1)
+            out = self.bn1(self.conv1(x, link=link, slab_out=s1, grad_slab=grad_in, branch=br), relu=True,
+                           slab_in=s1, grad_slab=g1)
             return self.bn2(self.conv2(out, slab_out=s2, grad_slab=g1), residual=identity, relu=True, link=link,
-                            slab_in=s2)
+                            slab_in=s2, grad_slab=grad_out)
         identity = x if self.downsample is None else self.downsample(x)
         out = self.relu(self.bn1(self.conv1(x)))
         out = self.bn2(self.conv2(out))
@@ -177,6 +188,17 @@ class ResNet(nn.Module):
                 nn.init.constant_(m.weight, 1)
                 nn.init.constant_(m.bias, 0)
 
+    @staticmethod
+    def _chain(blocks, x):
+        """Run consecutive BasicBlocks with a SlabLink at each boundary: block i+1's conv1 grad-x
+        slabs are summed by block i's BN2 backward (ops/slablink.py)."""
+        prev = None
+        for i, blk in enumerate(blocks):
+            nxt = SlabLink() if i + 1 < len(blocks) else None
+            x = blk(x, grad_in=prev, grad_out=nxt)
+            prev = nxt
+        return x
+
     def _make_layer(self, block, planes: int, blocks: int, stride: int = 1) -> nn.Sequential:
         downsample = None
         if stride != 1 or self.inplanes != planes * block.expansion:
@@ -194,10 +216,17 @@ class ResNet(nn.Module):
             x = self.maxpool(self.bn1(self.conv1(x, slab_out=s0), relu=True, slab_in=s0))
         else:
             x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
-        x = self.layer2(self.layer1(x))
+        train_links = (self.fused and SLAB_LINKS and self.training and x.is_cuda and torch.is_grad_enabled()
+                       and all(isinstance(b, BasicBlock) for b in self.layer1))
+        if train_links:  # block-boundary grad-x slab links (BasicBlock grad_in / grad_out)
+            x = self._chain(list(self.layer1) + list(self.layer2), x)
+        else:
+            x = self.layer2(self.layer1(x))
         blocks = smstage.stage_blocks(self, x) if (self.fused and self.training) else None
         if blocks is not None:  # layer3 + layer4 as one node, BatchNorm fused into the convs (ops/smstage.py)
             x = smstage.run_stage(blocks, x)
+        elif train_links:
+            x = self._chain(list(self.layer3) + list(self.layer4), x)
         else:
             x = self.layer4(self.layer3(x))
         # 1x1 feature map (32x32 inputs): the average is the value itself; flatten skips a

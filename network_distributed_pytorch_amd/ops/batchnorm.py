@@ -63,8 +63,9 @@ class _BNActFn(torch.autograd.Function):
         dgamma = grad_buffer(ctx.params[0], weight) if ctx.has_w else None
         dbeta = grad_buffer(ctx.params[1], weight) if ctx.has_w else None
         dypart, nslab = ctx.grad_slab.take_bwd() if ctx.grad_slab is not None else (None, 0)
+        dyadd = ctx.grad_slab.take_bwd_add() if ctx.grad_slab is not None else None
         ext().bn_bwd(dy, y, x, weight, save_mean, save_invstd, dx, dres, dgamma, dbeta, part, ctx.relu, ctx.single,
-                     dypart, nslab)
+                     dypart, nslab, dyadd)
         if ctx.link is not None and dres is not None:
             ctx.link.put(dres)
             dres = None

@@ -158,6 +158,8 @@ class DirectConvFn(torch.autograd.Function):
         addend = ctx.link.take() if ctx.link is not None else None
         if ctx.needs_input_grad[0]:
             grad_slab = ctx.grad_slab
+            if ctx.branch is not None and not ctx.branch.active():
+                grad_slab = None  # a sibling outside the link: autograd adds the two grad-x tensors
 
             def dgrad(addend):
                 if not dgrad_direct:
@@ -171,11 +173,13 @@ class DirectConvFn(torch.autograd.Function):
                     slab = (dy.numel() // geom[3]) * geom[0] if ups else x.numel()
                     part = torch.empty(ks_dgrad * slab, device=x.device, dtype=x.dtype)
                 fuse = addend is not None and _takes_addend(geom)
-                defer = grad_slab is not None and part is not None and addend is None
-                left = ext().conv_dgrad(dy, weight, dx, list(geom), part, addend.contiguous() if fuse else None,
-                                        defer)
-                if left > 1:
-                    grad_slab.put_bwd(part, left)  # dx stays unwritten: the BN backward sums the slabs
+                if fuse:
+                    addend = addend.contiguous()
+                # split-K slabs (and the addend, added after them) left to the consuming BN
+                defer = grad_slab is not None and part is not None and (addend is None or fuse)
+                left = ext().conv_dgrad(dy, weight, dx, list(geom), part, addend if fuse else None, defer)
+                if left > 1:  # dx stays unwritten: the BN backward sums the slabs (+ the addend)
+                    grad_slab.put_bwd(part, left, addend if fuse else None)
                 return dx + addend if (addend is not None and not fuse) else dx
 
             br = ctx.branch if ctx.branch is not None and ctx.branch.active() else None

@@ -12,6 +12,10 @@ sum to the conv's output buffer (BN saves its input for backward).  Where no fus
 kernel covers the shape, ``launch_bn_fwd`` / ``launch_bn_bwd`` run the plain slab sum
 themselves first, so a deferred sum is always finished.
 
+A grad-x addend (the residual-branch gradient of ops/gradlink.py) travels with the slabs and
+is added after them, as the conv's own split-K sum would; this also links a block's conv1
+to the PREVIOUS block's BN2 (models/resnet.py), whose output gradient that grad-x is.
+
 Where the conv runs unsplit and its forward BN takes the two-kernel large-map path (the
 ResNet stem and layer1), the link carries the BN's statistics instead: the conv epilogue
 emits per-channel, per-batch-tile fp64 sums of its output (csrc/conv.hip ``stats``) and the
@@ -30,11 +34,12 @@ __all__ = ["SlabLink"]
 
 
 class SlabLink:
-    __slots__ = ("fwd", "bwd", "stats")
+    __slots__ = ("fwd", "bwd", "bwd_add", "stats")
 
     def __init__(self):
         self.fwd: Optional[Tuple[torch.Tensor, int]] = None  # conv output slabs -> BN forward
         self.bwd: Optional[Tuple[torch.Tensor, int]] = None  # conv grad-x slabs -> BN backward
+        self.bwd_add: Optional[torch.Tensor] = None  # the grad-x addend, added after the slabs
         self.stats: Optional[Tuple[torch.Tensor, int]] = None  # conv epilogue BN partial sums [C][S][2]
 
     def put_stats(self, stats: torch.Tensor, n: int) -> None:
@@ -53,10 +58,17 @@ class SlabLink:
         v, self.fwd = self.fwd, None
         return v if v is not None else (None, 0)
 
-    def put_bwd(self, part: torch.Tensor, n: int) -> None:
+    def put_bwd(self, part: torch.Tensor, n: int, addend: Optional[torch.Tensor] = None) -> None:
         assert self.bwd is None, "SlabLink: grad-x slabs deposited twice"
         self.bwd = (part, int(n))
+        self.bwd_add = addend
 
     def take_bwd(self) -> Tuple[Optional[torch.Tensor], int]:
         v, self.bwd = self.bwd, None
         return v if v is not None else (None, 0)
+
+    def take_bwd_add(self) -> Optional[torch.Tensor]:
+        """The addend deposited with the grad-x slabs (a residual / sibling gradient the conv's
+        split-K sum would have added last), or None; take it with the slabs."""
+        a, self.bwd_add = self.bwd_add, None
+        return a
