@@ -228,11 +228,17 @@ __global__ __launch_bounds__(256) void bn_bwd_stats_kernel(const float* __restri
                                                            const float* __restrict__ save_invstd,
                                                            double* __restrict__ part, int N, int C, int HW,
                                                            int S, int relu, const float* __restrict__ src = nullptr,
-                                                           int nslab = 0, const float* __restrict__ sadd = nullptr) {
+                                                           int nslab = 0, const float* __restrict__ sadd = nullptr,
+                                                           const float* __restrict__ mgam = nullptr,
+                                                           const float* __restrict__ mbet = nullptr) {
   __shared__ double red[16];
   const int s = blockIdx.x, c = blockIdx.y;
   const BnSlice sl = slice_of(N, S, s);
   const float mean = save_mean[c], invstd = save_invstd[c];
+  // mbet != nullptr: the forward output was never stored (bn_relu_maxpool): its ReLU mask is
+  // recomputed from x with the forward's own float ops, fmaf(x, scale, shift) > 0
+  const float msc = mbet ? __fmul_rn(mgam ? mgam[c] : 1.f, invstd) : 0.f;
+  const float msh = mbet ? __fsub_rn(mbet[c], __fmul_rn(mean, msc)) : 0.f;
   double sdz = 0.0, sdzx = 0.0;
   if (VEC) {
     const int64_t slab = (int64_t)N * C * HW;
@@ -248,7 +254,12 @@ __global__ __launch_bounds__(256) void bn_bwd_stats_kernel(const float* __restri
       }
       const f32x4 xv = *reinterpret_cast<const f32x4*>(x + o);
       f32x4 yv = {1.f, 1.f, 1.f, 1.f};
-      if (relu) yv = *reinterpret_cast<const f32x4*>(y + o);
+      if (mbet) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) yv[j] = fmaf(xv[j], msc, msh);
+      } else if (relu) {
+        yv = *reinterpret_cast<const f32x4*>(y + o);
+      }
       float a = 0.f, b = 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -279,11 +290,14 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ x,
     const float* __restrict__ gamma, const float* __restrict__ save_mean, const float* __restrict__ save_invstd,
     float* __restrict__ dx, float* __restrict__ dres, float* __restrict__ dgamma, float* __restrict__ dbeta,
-    const double* __restrict__ part, int N, int C, int HW, int S, int relu) {
+    const double* __restrict__ part, int N, int C, int HW, int S, int relu, const float* __restrict__ mbet = nullptr) {
   const int s = blockIdx.x, c = blockIdx.y;
   // per-channel operands first: in flight with the slice partials
   const float mean = save_mean[c], invstd = save_invstd[c];
   const float g = gamma ? gamma[c] : 1.f;
+  // mbet: ReLU mask recomputed from x (bn_bwd_stats_kernel)
+  const float msc = mbet ? __fmul_rn(g, invstd) : 0.f;
+  const float msh = mbet ? __fsub_rn(mbet[c], __fmul_rn(mean, msc)) : 0.f;
   double sdz, sdzx;
   slice_sums(part, c, S, sdz, sdzx);
   if (s == 0 && threadIdx.x == 0) {
@@ -300,7 +314,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
       const f32x4 gy = *reinterpret_cast<const f32x4*>(dy + o);
       const f32x4 xv = *reinterpret_cast<const f32x4*>(x + o);
       f32x4 yv = {1.f, 1.f, 1.f, 1.f};
-      if (relu) yv = *reinterpret_cast<const f32x4*>(y + o);
+      if (mbet) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) yv[j] = fmaf(xv[j], msc, msh);
+      } else if (relu) {
+        yv = *reinterpret_cast<const f32x4*>(y + o);
+      }
       f32x4 dz, out;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -318,6 +337,79 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
       dx[o] = k1 * (dz - mdz - xh * mdzx);
       if (dres) dres[o] = dz;
     });
+  }
+}
+
+// ---- stem tail: BN (training) -> ReLU -> MaxPool(3, 2, 1) in one pass ----------------------
+// ResNet's stem writes the BN output (the largest activation of the network, 16x16 maps)
+// only for the max-pool to read it back.  Here the apply folds the statistics (the conv
+// epilogue's partials, Sp > 0, or this BN's statistics pass) and every thread computes
+// pooled outputs straight from x: relu(fmaf(x, scale, shift)) per window tap, the winning
+// tap stored as the pool's uint8 window offset (the same first-maximum scan as
+// pool.hip).  The BN output is never stored: the backward recomputes its ReLU mask from x
+// (bn_bwd_*_kernel `mbet`).  Grid (S, C) like bn_fwd_apply: a slice owns whole planes.
+__global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(
+    const float* __restrict__ x, float* __restrict__ y, uint8_t* __restrict__ idx, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt,
+    float* __restrict__ save_mean, float* __restrict__ save_invstd, const double* __restrict__ part, int N, int C,
+    int H, int W, int S, float eps, float momentum, int Sp) {
+  __shared__ double red[16];
+  const int s = blockIdx.x, c = blockIdx.y;
+  const float gam = gamma ? gamma[c] : 1.f, bet = beta ? beta[c] : 0.f;
+  const bool writer = s == 0 && threadIdx.x == 0 && rmean != nullptr;
+  const float rm = writer ? rmean[c] : 0.f, rv = writer ? rvar[c] : 0.f;
+  const int HW = H * W;
+  double sum, sq;
+  if (Sp > 0) slice_sums_block(part, c, Sp, sum, sq, red);
+  else slice_sums(part, c, S, sum, sq);
+  const double M = (double)N * HW;
+  const double mu = sum / M;
+  double var = sq / M - mu * mu;
+  if (var < 0.0) var = 0.0;
+  const float mean = (float)mu;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  if (s == 0 && threadIdx.x == 0) {
+    save_mean[c] = mean;
+    save_invstd[c] = invstd;
+    if (rmean != nullptr) {
+      const double unb = M > 1.0 ? var * M / (M - 1.0) : var;
+      rmean[c] = (float)((1.0 - momentum) * (double)rm + momentum * mu);
+      rvar[c] = (float)((1.0 - momentum) * (double)rv + momentum * unb);
+    }
+    if (nbt != nullptr && c == 0) nbt[0] += 1;
+  }
+  // unfused roundings (no contraction): the backward recomputes these exact values for its mask
+  const float scale = __fmul_rn(gam, invstd);
+  const float shift = __fsub_rn(bet, __fmul_rn(mean, scale));
+  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1, PQ = OH * OW;
+  const BnSlice sl = slice_of(N, S, s);
+  const int total = (int)(sl.n1 - sl.n0) * PQ;
+  for (int t = threadIdx.x; t < total; t += 256) {
+    const int ni = t / PQ, o = t - ni * PQ;
+    const int oh = o / OW, ow = o - oh * OW;
+    const int64_t plane = (sl.n0 + ni) * C + c;
+    const float* xp = x + plane * HW;
+    const int h0 = 2 * oh - 1, w0 = 2 * ow - 1;
+    const int kh0 = h0 < 0 ? 1 : 0, kw0 = w0 < 0 ? 1 : 0;
+    float best = -INFINITY;
+    int arg = kh0 * 3 + kw0;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int hh = h0 + kh;
+      if (kh < kh0 || hh >= H) continue;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int ww = w0 + kw;
+        if (kw < kw0 || ww >= W) continue;
+        const float v = fmaxf(fmaf(xp[hh * W + ww], scale, shift) + 0.f, 0.f);
+        if (v > best || isnan(v)) {
+          best = v;
+          arg = kh * 3 + kw;
+        }
+      }
+    }
+    y[plane * PQ + o] = best;
+    idx[plane * PQ + o] = (uint8_t)arg;
   }
 }
 
@@ -1017,10 +1109,33 @@ void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamm
                        save_mean, save_invstd, ap, N, C, HW, S, eps, momentum, relu, training, Sp);
 }
 
+// training-mode stem tail (bn_relu_maxpool_kernel); xstats as in launch_bn_fwd (nullable)
+void launch_bn_relu_maxpool(const float* x, float* y, uint8_t* idx, const float* gamma, const float* beta,
+                            float* rmean, float* rvar, int64_t* nbt, float* save_mean, float* save_invstd,
+                            double* part, int N, int C, int H, int W, float eps, float momentum, hipStream_t s,
+                            const double* xstats, int xS) {
+  part += kBnSyncSlots;
+  const int HW = H * W;
+  const int S = bn_slices(N, C, HW);
+  const dim3 grid(S, C);
+  if (xstats == nullptr) {
+    const bool vec = (HW % 4) == 0 && ((uintptr_t)x & 15) == 0;
+    if (vec) hipLaunchKernelGGL(bn_fwd_stats_kernel<true>, grid, dim3(256), 0, s, x, part, N, C, HW, S, nullptr, 0);
+    else hipLaunchKernelGGL(bn_fwd_stats_kernel<false>, grid, dim3(256), 0, s, x, part, N, C, HW, S, nullptr, 0);
+  }
+  hipLaunchKernelGGL(bn_relu_maxpool_kernel, grid, dim3(256), 0, s, x, y, idx, gamma, beta, rmean, rvar, nbt, save_mean,
+                     save_invstd, xstats != nullptr ? xstats : part, N, C, H, W, S, eps, momentum,
+                     xstats != nullptr ? xS : 0);
+}
+
+bool bn_two_kernel_path(int N, int C, int HW, int single) {
+  return !(single && bn_fused_ok(N, C, HW)) && !bn_small_path(N, C, HW);
+}
+
 void launch_bn_bwd(const float* dy, const float* y, const float* x, const float* gamma, const float* save_mean,
                    const float* save_invstd, float* dx, float* dres, float* dgamma, float* dbeta, double* part,
                    int N, int C, int HW, int S, int relu, int single, hipStream_t s, const float* dypart,
-                   int nslab, const float* dyadd) {
+                   int nslab, const float* dyadd, const float* mbeta) {
   const BnSync sy = bn_sync(part, 1);
   part += kBnSyncSlots;
   if (dypart != nullptr && nslab < 2) dypart = nullptr;
@@ -1064,9 +1179,9 @@ void launch_bn_bwd(const float* dy, const float* y, const float* x, const float*
   const dim3 grid(S, C);
   if (vec) {  // the statistics pass also adds deferred grad-x slabs (dypart) and writes dy
     hipLaunchKernelGGL(bn_bwd_stats_kernel<true>, grid, dim3(256), 0, s, dy, y, x, save_mean, save_invstd, part, N, C,
-                       HW, S, relu, dypart, nslab, dyadd);
+                       HW, S, relu, dypart, nslab, dyadd, gamma, mbeta);
     hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, grid, dim3(256), 0, s, dy, y, x, gamma, save_mean, save_invstd, dx,
-                       dres, dgamma, dbeta, part, N, C, HW, S, relu);
+                       dres, dgamma, dbeta, part, N, C, HW, S, relu, mbeta);
   } else {
     hipLaunchKernelGGL(bn_bwd_stats_kernel<false>, grid, dim3(256), 0, s, dy, y, x, save_mean, save_invstd, part, N,
                        C, HW, S, relu);

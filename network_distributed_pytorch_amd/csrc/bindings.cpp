@@ -348,11 +348,52 @@ void bn_fwd(torch::Tensor x, c10::optional<torch::Tensor> res, torch::Tensor y,
   check_launch("launch_bn_fwd");
 }
 
+// training BN -> ReLU -> MaxPool(3, 2, 1) without storing the BN output (the ResNet stem tail)
+void bn_relu_maxpool(torch::Tensor x, torch::Tensor y, torch::Tensor idx, c10::optional<torch::Tensor> gamma,
+                     c10::optional<torch::Tensor> beta, c10::optional<torch::Tensor> rmean,
+                     c10::optional<torch::Tensor> rvar, c10::optional<torch::Tensor> nbt, torch::Tensor save_mean,
+                     torch::Tensor save_invstd, torch::Tensor part, double eps, double momentum,
+                     c10::optional<torch::Tensor> xstats, int64_t xS) {
+  check_f32(x, "x"); check_f32(y, "y"); check_f32(save_mean, "save_mean"); check_f32(save_invstd, "save_invstd");
+  check_dev(part, "part"); check_dev(idx, "idx");
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(), "bn_relu_maxpool: contiguous NCHW x");
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  TORCH_CHECK(y.is_contiguous() && y.dim() == 4 && y.size(0) == N && y.size(1) == C && y.size(2) == OH &&
+                  y.size(3) == OW, "bn_relu_maxpool: y must be [N, C, (H-1)/2+1, (W-1)/2+1]");
+  TORCH_CHECK(idx.scalar_type() == torch::kUInt8 && idx.is_contiguous() && idx.sizes() == y.sizes(),
+              "bn_relu_maxpool: uint8 idx shaped like y");
+  TORCH_CHECK(part.scalar_type() == torch::kFloat64 && part.numel() >= ndp::bn_part_numel(N, C, H * W),
+              "bn part too small");
+  TORCH_CHECK(save_mean.numel() >= C && save_invstd.numel() >= C, "bn save buffers too small");
+  TORCH_CHECK((int64_t)N * C * H * W < (1LL << 31), "bn_relu_maxpool: tensor too large");
+  int64_t* nb = nullptr;
+  if (nbt.has_value()) {
+    check_dev(*nbt, "nbt");
+    TORCH_CHECK(nbt->scalar_type() == torch::kInt64, "num_batches_tracked must be int64");
+    nb = nbt->data_ptr<int64_t>();
+  }
+  const double* xst = nullptr;
+  if (xstats.has_value()) {
+    check_dev(*xstats, "xstats");
+    TORCH_CHECK(xstats->scalar_type() == torch::kFloat64 && xstats->is_contiguous() && xS > 0 &&
+                    xstats->numel() >= (int64_t)C * xS * 2, "bn_relu_maxpool: xstats must hold C * xS * 2 doubles");
+    xst = xstats->data_ptr<double>();
+  }
+  ndp::launch_bn_relu_maxpool(x.data_ptr<float>(), y.data_ptr<float>(), idx.data_ptr<uint8_t>(),
+                              opt_f32(gamma, "gamma"), opt_f32(beta, "beta"),
+                              const_cast<float*>(opt_f32(rmean, "running_mean")),
+                              const_cast<float*>(opt_f32(rvar, "running_var")), nb, save_mean.data_ptr<float>(),
+                              save_invstd.data_ptr<float>(), part.data_ptr<double>(), N, C, H, W, (float)eps,
+                              (float)momentum, cur_stream(), xst, (int)xS);
+  check_launch("launch_bn_relu_maxpool");
+}
+
 void bn_bwd(torch::Tensor dy, c10::optional<torch::Tensor> y, torch::Tensor x, c10::optional<torch::Tensor> gamma,
             torch::Tensor save_mean, torch::Tensor save_invstd, torch::Tensor dx, c10::optional<torch::Tensor> dres,
             c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta, torch::Tensor part,
             bool relu, bool single, c10::optional<torch::Tensor> dypart, int64_t nslab,
-            c10::optional<torch::Tensor> dyadd) {
+            c10::optional<torch::Tensor> dyadd, c10::optional<torch::Tensor> mbeta) {
   check_f32(dy, "dy"); check_f32(x, "x"); check_f32(dx, "dx"); check_dev(part, "part");
   if (dyadd.has_value()) {
     check_f32(*dyadd, "dyadd");
@@ -360,18 +401,24 @@ void bn_bwd(torch::Tensor dy, c10::optional<torch::Tensor> y, torch::Tensor x, c
                 "bn_bwd: dyadd (the deferred grad-x addend) must match dy and come with dypart");
   }
   TORCH_CHECK(dy.sizes() == x.sizes() && dx.sizes() == x.sizes(), "bn_bwd: bad shapes");
-  TORCH_CHECK(!relu || y.has_value(), "bn_bwd: relu needs y");
+  TORCH_CHECK(!relu || y.has_value() || mbeta.has_value(), "bn_bwd: relu needs y (or mbeta)");
   const int N = (int)x.size(0), C = (int)x.size(1);
   const int HW = (int)(x.numel() / ((int64_t)N * C));
   const int S = ndp::bn_slices(N, C, HW);
   TORCH_CHECK(part.scalar_type() == torch::kFloat64 && part.numel() >= ndp::bn_part_numel(N, C, HW),
               "bn part too small");
+  if (mbeta.has_value()) {  // ReLU mask recomputed from x: the vectorised two-kernel path only
+    check_f32(*mbeta, "mbeta");
+    TORCH_CHECK(relu && !y.has_value() && !dypart.has_value() && mbeta->numel() >= C && HW % 4 == 0 &&
+                    ndp::bn_two_kernel_path(N, C, HW, single ? 1 : 0),
+                "bn_bwd: mbeta needs relu, no y, no slabs, HW % 4 == 0 and the large-map path");
+  }
   ndp::launch_bn_bwd(dy.data_ptr<float>(), opt_f32(y, "y"), x.data_ptr<float>(), opt_f32(gamma, "gamma"),
                      save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(), dx.data_ptr<float>(),
                      const_cast<float*>(opt_f32(dres, "dres")), const_cast<float*>(opt_f32(dgamma, "dgamma")),
                      const_cast<float*>(opt_f32(dbeta, "dbeta")), part.data_ptr<double>(), N, C, HW, S,
                      relu ? 1 : 0, single ? 1 : 0, cur_stream(), slab_input(dypart, nslab, dy.numel(), "bn_bwd"),
-                     (int)nslab, opt_f32(dyadd, "dyadd"));
+                     (int)nslab, opt_f32(dyadd, "dyadd"), opt_f32(mbeta, "mbeta"));
   check_launch("launch_bn_bwd");
 }
 
@@ -1332,7 +1379,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("gamma"), py::arg("save_mean"),
         py::arg("save_invstd"), py::arg("dx"), py::arg("dres"), py::arg("dgamma"), py::arg("dbeta"), py::arg("part"),
         py::arg("relu"), py::arg("single"), py::arg("dypart") = py::none(), py::arg("nslab") = 0,
-        py::arg("dyadd") = py::none());
+        py::arg("dyadd") = py::none(), py::arg("mbeta") = py::none());
+  m.def("bn_relu_maxpool", &bn_relu_maxpool, py::arg("x"), py::arg("y"), py::arg("idx"), py::arg("gamma"),
+        py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("nbt"), py::arg("save_mean"),
+        py::arg("save_invstd"), py::arg("part"), py::arg("eps"), py::arg("momentum"), py::arg("xstats") = py::none(),
+        py::arg("xS") = 0);
+  m.def("bn_two_kernel_path", [](int64_t N, int64_t C, int64_t HW, bool single) {
+    return ndp::bn_two_kernel_path((int)N, (int)C, (int)HW, single ? 1 : 0);
+  });
   m.def("bn_slices", &bn_slices);
   m.def("slab_sum", &slab_sum);
   m.def("bn_part_numel", &bn_part_numel);

@@ -141,7 +141,16 @@ void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamm
 void launch_bn_bwd(const float* dy, const float* y, const float* x, const float* gamma, const float* save_mean,
                    const float* save_invstd, float* dx, float* dres, float* dgamma, float* dbeta, double* part,
                    int N, int C, int HW, int S, int relu, int single, hipStream_t s, const float* dypart = nullptr,
-                   int nslab = 0, const float* dyadd = nullptr);
+                   int nslab = 0, const float* dyadd = nullptr, const float* mbeta = nullptr);
+// mbeta (nullable, relu, two-kernel path only): y was never stored; the ReLU mask is recomputed
+// from x as fmaf(x, gamma * invstd, beta - mean * gamma * invstd) > 0 (the forward's own ops)
+bool bn_two_kernel_path(int N, int C, int HW, int single);
+// BN (training) -> ReLU -> MaxPool(3, 2, 1) in one pass without storing the BN output (the
+// ResNet stem tail); y / idx: the pooled output and its uint8 window offsets (pool.hip layout)
+void launch_bn_relu_maxpool(const float* x, float* y, uint8_t* idx, const float* gamma, const float* beta,
+                            float* rmean, float* rvar, int64_t* nbt, float* save_mean, float* save_invstd,
+                            double* part, int N, int C, int H, int W, float eps, float momentum, hipStream_t s,
+                            const double* xstats = nullptr, int xS = 0);
 // dyadd (nullable, with dypart): dy = sum of the slabs + dyadd (added last, as conv_slab_sum does)
 }  // namespace ndp
 

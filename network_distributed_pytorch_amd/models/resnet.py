@@ -213,7 +213,10 @@ class ResNet(nn.Module):
     def forward(self, x):
         if self.fused:  # the stem conv's epilogue hands its BN the statistics (ops/slablink.py)
             s0 = SlabLink() if (SLAB_LINKS and x.is_cuda and torch.is_grad_enabled() and self.training) else None
-            x = self.maxpool(self.bn1(self.conv1(x, slab_out=s0), relu=True, slab_in=s0))
+            x = self.conv1(x, slab_out=s0)
+            # BN -> ReLU -> max-pool in one pass, the BN output never stored (ops/batchnorm.py)
+            pooled = self.bn1.relu_maxpool(x, self.maxpool, slab_in=s0)
+            x = pooled if pooled is not None else self.maxpool(self.bn1(x, relu=True, slab_in=s0))
         else:
             x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
         train_links = (self.fused and SLAB_LINKS and self.training and x.is_cuda and torch.is_grad_enabled()

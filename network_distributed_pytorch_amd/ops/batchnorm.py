@@ -72,6 +72,45 @@ class _BNActFn(torch.autograd.Function):
         return dx, dres, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None
 
 
+class _BNReluPoolFn(torch.autograd.Function):
+    """Training BN -> ReLU -> MaxPool(3, 2, 1) (csrc/batchnorm.hip bn_relu_maxpool): the BN
+    output is never stored; backward = the native pool backward, then the BN backward with its
+    ReLU mask recomputed from x (``mbeta``)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, nbt, part, eps, momentum, single, slab_in=None):
+        X = ext()
+        x = x.contiguous()
+        N, C, H, W = x.shape
+        y = torch.empty(N, C, (H - 1) // 2 + 1, (W - 1) // 2 + 1, device=x.device, dtype=x.dtype)
+        idx = torch.empty(y.shape, device=x.device, dtype=torch.uint8)
+        save_mean = torch.empty(C, device=x.device, dtype=torch.float32)
+        save_invstd = torch.empty(C, device=x.device, dtype=torch.float32)
+        xstats, xS = slab_in.take_stats() if slab_in is not None else (None, 0)
+        X.bn_relu_maxpool(x, y, idx, weight, bias, running_mean, running_var, nbt, save_mean, save_invstd, part,
+                          float(eps), float(momentum), xstats, xS)
+        ctx.save_for_backward(x, weight, bias, save_mean, save_invstd, part, idx)
+        ctx.params = (weight, bias)
+        ctx.single = bool(single)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, bias, save_mean, save_invstd, part, idx = ctx.saved_tensors
+        dz = torch.empty_like(x)  # gradient of the (unstored) BN output = the pool's input
+        ext().maxpool_bwd(dy.contiguous(), idx, dz, 3, 2, 1)
+        dx = torch.empty_like(x)
+        dgamma = grad_buffer(ctx.params[0], weight)
+        dbeta = grad_buffer(ctx.params[1], weight)
+        ext().bn_bwd(dz, None, x, weight, save_mean, save_invstd, dx, None, dgamma, dbeta, part, True, ctx.single,
+                     None, 0, None, bias)
+        return dx, dgamma, dbeta, None, None, None, None, None, None, None, None
+
+
+# the stem tail BN -> ReLU -> MaxPool in one pass (NDP_STEM_POOL=0: BN kernel + pool kernel)
+STEM_POOL = os.environ.get("NDP_STEM_POOL", "1") != "0"
+
+
 def bn_act(x, weight, bias, running_mean, running_var, nbt, part, training, momentum, eps,
            residual=None, relu=False, single=False, link=None, slab_in=None, grad_slab=None):
     needs_grad = torch.is_grad_enabled() and (x.requires_grad or (weight is not None and weight.requires_grad)
@@ -126,6 +165,26 @@ class BatchNormAct2d(nn.BatchNorm2d):
             if self._part.numel() < need or self._part.device != x.device:
                 self._part = torch.zeros(need, dtype=torch.float64, device=x.device)
             self._part_key = key
+
+    def relu_maxpool(self, x: torch.Tensor, pool: nn.Module, slab_in=None) -> Optional[torch.Tensor]:
+        """``pool(relu(self(x)))`` in one pass for a training ``MaxPool2d(3, 2, 1)`` on device
+        (the ResNet stem tail; the BN output is never stored), or None where the fused kernel
+        does not apply (the caller runs the two modules)."""
+        k, st, p = pool.kernel_size, pool.stride, pool.padding
+        if not (STEM_POOL and self.training and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+                and torch.is_grad_enabled() and self.affine and self.track_running_stats
+                and self.momentum is not None and (slab_in is None or slab_in.fwd is None)
+                and isinstance(pool, nn.MaxPool2d) and k in (3, (3, 3)) and st in (2, (2, 2))
+                and p in (1, (1, 1)) and pool.dilation in (1, (1, 1)) and not pool.ceil_mode
+                and not pool.return_indices and (x.shape[2] * x.shape[3]) % 4 == 0):
+            return None
+        N, C = x.shape[:2]
+        if not ext().bn_two_kernel_path(N, C, x.shape[2] * x.shape[3], self.fused_small):
+            return None
+        self._ensure_part(x)
+        return _BNReluPoolFn.apply(x, self.weight, self.bias, self.running_mean, self.running_var,
+                                   self.num_batches_tracked, self._part, self.eps, self.momentum, self.fused_small,
+                                   slab_in)
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, relu: bool = False, link=None,
                 slab_in=None, grad_slab=None):
