@@ -114,6 +114,14 @@ class ToeplitzBank:
         return self.members[i][2]
 
 
+# grad-W GEMM of the Toeplitz layers on the side stream, concurrent with the grad-x GEMM (both are
+# small, latency-bound hipBLASLt launches at the strong-scaling batches); folds stay batched.
+# Opt-in (NDP_TOEP_FORK=1; NDP_CONV_FORK=1 forks every conv): measured SLOWER on 1x MI355X,
+# ResNet-18 r=4 batch 64 0.974 -> 1.170 ms, batch 512 1.877 -> 2.013 (the graph's fork / join
+# edges cost more than the overlap of two small GEMMs; profiles/r4/bench_toep_fork.jsonl)
+_TOEP_FORK = os.environ.get("NDP_TOEP_FORK", "0") == "1"
+
+
 # grad-W of a Toeplitz conv on the small-map grad-W kernel (csrc/smallconv.hip: dW in W's own
 # layout, no dW_big GEMM, no fold) where it covers the geometry.  Opt-in (NDP_TOEP_SMWGRAD=1):
 # measured slower than the hipBLASLt GEMM + batched fold on 1x MI355X (ResNet-18 r=4 b512
@@ -172,7 +180,7 @@ class _ToeplitzConv(torch.autograd.Function):
         dx = dw = None
         if dev:  # grad-W (GEMM + fold) on the side stream, grad-x on the current one
             main = torch.cuda.current_stream()
-            fork = _conv.FORK_WGRAD and ctx.needs_input_grad[0] and ctx.needs_input_grad[1]
+            fork = (_conv.FORK_WGRAD or _TOEP_FORK) and ctx.needs_input_grad[0] and ctx.needs_input_grad[1]
             if ctx.needs_input_grad[1] and ctx.smw:
                 dw = grad_buffer(ctx.weight)  # the dense arm's arena slice when registered
                 xs = X.view(ctx.x_shape)
@@ -194,7 +202,8 @@ class _ToeplitzConv(torch.autograd.Function):
                 side.wait_stream(main)
                 with torch.cuda.stream(side):
                     torch.mm(G.t(), X, out=dwt)                   # [N, K]
-                    if not fork and gradfinish.can_defer(ctx.weight):  # one batched fold launch later
+                    # one batched fold launch later (after this backward's join when forked)
+                    if (not fork or _TOEP_FORK) and gradfinish.can_defer(ctx.weight):
                         gradfinish.defer_fold(dwt, dw, ctx.geom)
                     else:
                         ext().toeplitz_fold(dwt, dw, list(ctx.geom))
