@@ -290,7 +290,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ x,
     const float* __restrict__ gamma, const float* __restrict__ save_mean, const float* __restrict__ save_invstd,
     float* __restrict__ dx, float* __restrict__ dres, float* __restrict__ dgamma, float* __restrict__ dbeta,
-    const double* __restrict__ part, int N, int C, int HW, int S, int relu, const float* __restrict__ mbet = nullptr) {
+    const double* __restrict__ part, int N, int C, int HW, int S, int relu, const float* __restrict__ mbet = nullptr,
+    int Sp = 0) {
+  // Sp > 0: `part` holds Sp partials per channel from the grad-x epilogue of the conv that
+  // produced dy (conv_fwd_kernel backward-mode statistics), folded by the whole block
+  __shared__ double red[16];
   const int s = blockIdx.x, c = blockIdx.y;
   // per-channel operands first: in flight with the slice partials
   const float mean = save_mean[c], invstd = save_invstd[c];
@@ -299,7 +303,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   const float msc = mbet ? __fmul_rn(g, invstd) : 0.f;
   const float msh = mbet ? __fsub_rn(mbet[c], __fmul_rn(mean, msc)) : 0.f;
   double sdz, sdzx;
-  slice_sums(part, c, S, sdz, sdzx);
+  if (Sp > 0) slice_sums_block(part, c, Sp, sdz, sdzx, red);
+  else slice_sums(part, c, S, sdz, sdzx);
   if (s == 0 && threadIdx.x == 0) {
     if (dgamma) dgamma[c] = (float)sdzx;
     if (dbeta) dbeta[c] = (float)sdz;
@@ -1135,7 +1140,7 @@ bool bn_two_kernel_path(int N, int C, int HW, int single) {
 void launch_bn_bwd(const float* dy, const float* y, const float* x, const float* gamma, const float* save_mean,
                    const float* save_invstd, float* dx, float* dres, float* dgamma, float* dbeta, double* part,
                    int N, int C, int HW, int S, int relu, int single, hipStream_t s, const float* dypart,
-                   int nslab, const float* dyadd, const float* mbeta) {
+                   int nslab, const float* dyadd, const float* mbeta, const double* dstats, int dS) {
   const BnSync sy = bn_sync(part, 1);
   part += kBnSyncSlots;
   if (dypart != nullptr && nslab < 2) dypart = nullptr;
@@ -1178,10 +1183,13 @@ void launch_bn_bwd(const float* dy, const float* y, const float* x, const float*
                    (dres == nullptr || ((uintptr_t)dres & 15) == 0);
   const dim3 grid(S, C);
   if (vec) {  // the statistics pass also adds deferred grad-x slabs (dypart) and writes dy
-    hipLaunchKernelGGL(bn_bwd_stats_kernel<true>, grid, dim3(256), 0, s, dy, y, x, save_mean, save_invstd, part, N, C,
-                       HW, S, relu, dypart, nslab, dyadd, gamma, mbeta);
+    // (dstats: the statistics came from the producing conv's grad-x epilogue, no pass)
+    if (dstats == nullptr || dypart != nullptr)
+      hipLaunchKernelGGL(bn_bwd_stats_kernel<true>, grid, dim3(256), 0, s, dy, y, x, save_mean, save_invstd, part, N,
+                         C, HW, S, relu, dypart, nslab, dyadd, gamma, mbeta);
+    const bool ext_st = dstats != nullptr && dypart == nullptr;
     hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, grid, dim3(256), 0, s, dy, y, x, gamma, save_mean, save_invstd, dx,
-                       dres, dgamma, dbeta, part, N, C, HW, S, relu, mbeta);
+                       dres, dgamma, dbeta, ext_st ? dstats : part, N, C, HW, S, relu, mbeta, ext_st ? dS : 0);
   } else {
     hipLaunchKernelGGL(bn_bwd_stats_kernel<false>, grid, dim3(256), 0, s, dy, y, x, save_mean, save_invstd, part, N,
                        C, HW, S, relu);

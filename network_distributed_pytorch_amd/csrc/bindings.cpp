@@ -393,7 +393,8 @@ void bn_bwd(torch::Tensor dy, c10::optional<torch::Tensor> y, torch::Tensor x, c
             torch::Tensor save_mean, torch::Tensor save_invstd, torch::Tensor dx, c10::optional<torch::Tensor> dres,
             c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta, torch::Tensor part,
             bool relu, bool single, c10::optional<torch::Tensor> dypart, int64_t nslab,
-            c10::optional<torch::Tensor> dyadd, c10::optional<torch::Tensor> mbeta) {
+            c10::optional<torch::Tensor> dyadd, c10::optional<torch::Tensor> mbeta,
+            c10::optional<torch::Tensor> dstats, int64_t dS) {
   check_f32(dy, "dy"); check_f32(x, "x"); check_f32(dx, "dx"); check_dev(part, "part");
   if (dyadd.has_value()) {
     check_f32(*dyadd, "dyadd");
@@ -407,6 +408,14 @@ void bn_bwd(torch::Tensor dy, c10::optional<torch::Tensor> y, torch::Tensor x, c
   const int S = ndp::bn_slices(N, C, HW);
   TORCH_CHECK(part.scalar_type() == torch::kFloat64 && part.numel() >= ndp::bn_part_numel(N, C, HW),
               "bn part too small");
+  const double* dst = nullptr;
+  if (dstats.has_value()) {  // [C][dS][2] partial sums from the producing conv's grad-x epilogue
+    check_dev(*dstats, "dstats");
+    TORCH_CHECK(dstats->scalar_type() == torch::kFloat64 && dstats->is_contiguous() && dS > 0 &&
+                    dstats->numel() >= (int64_t)C * dS * 2 && !dypart.has_value(),
+                "bn_bwd: dstats must hold C * dS * 2 doubles (no slabs)");
+    dst = dstats->data_ptr<double>();
+  }
   if (mbeta.has_value()) {  // ReLU mask recomputed from x: the vectorised two-kernel path only
     check_f32(*mbeta, "mbeta");
     TORCH_CHECK(relu && !y.has_value() && !dypart.has_value() && mbeta->numel() >= C && HW % 4 == 0 &&
@@ -418,7 +427,7 @@ void bn_bwd(torch::Tensor dy, c10::optional<torch::Tensor> y, torch::Tensor x, c
                      const_cast<float*>(opt_f32(dres, "dres")), const_cast<float*>(opt_f32(dgamma, "dgamma")),
                      const_cast<float*>(opt_f32(dbeta, "dbeta")), part.data_ptr<double>(), N, C, HW, S,
                      relu ? 1 : 0, single ? 1 : 0, cur_stream(), slab_input(dypart, nslab, dy.numel(), "bn_bwd"),
-                     (int)nslab, opt_f32(dyadd, "dyadd"), opt_f32(mbeta, "mbeta"));
+                     (int)nslab, opt_f32(dyadd, "dyadd"), opt_f32(mbeta, "mbeta"), dst, (int)dS);
   check_launch("launch_bn_bwd");
 }
 
@@ -686,7 +695,10 @@ int64_t conv_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, const std::v
 }
 
 int64_t conv_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, const std::vector<int64_t>& geom,
-                   c10::optional<torch::Tensor> part, c10::optional<torch::Tensor> addend, bool defer) {
+                   c10::optional<torch::Tensor> part, c10::optional<torch::Tensor> addend, bool defer,
+                   c10::optional<torch::Tensor> stats, c10::optional<torch::Tensor> bn_x,
+                   c10::optional<torch::Tensor> bn_y, c10::optional<torch::Tensor> bn_mean,
+                   c10::optional<torch::Tensor> bn_invstd) {
   const ndp::ConvGeom g = conv_geom(geom);
   const int cls = ndp::conv_direct_class(g);
   TORCH_CHECK(cls >= 0 && ndp::conv_dgrad_direct(cls), "conv_dgrad: no direct grad-x kernel for this geometry");
@@ -706,8 +718,24 @@ int64_t conv_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, const st
     TORCH_CHECK((reinterpret_cast<uintptr_t>(addend->data_ptr()) & 15) == 0, "conv_dgrad: 16-B aligned addend");
     ap = addend->data_ptr<float>();
   }
+  ndp::ConvBnStats bst{nullptr, nullptr, nullptr, nullptr, nullptr};
+  if (stats.has_value()) {  // backward-mode BN partial sums of dx: [C][S][2]
+    const int S = ndp::conv_dgrad_stats_slices(cls, g, B);
+    TORCH_CHECK(S > 0, "conv_dgrad: no statistics epilogue for this geometry / batch (conv_dgrad_stats_slices)");
+    check_dev(*stats, "stats");
+    TORCH_CHECK(stats->scalar_type() == torch::kFloat64 && stats->is_contiguous() &&
+                    stats->numel() >= (int64_t)g.C * S * 2, "conv_dgrad: stats must hold C * S * 2 doubles");
+    TORCH_CHECK(bn_x.has_value() && bn_y.has_value() && bn_mean.has_value() && bn_invstd.has_value(),
+                "conv_dgrad: stats need the BN's x, y, mean, invstd");
+    conv_check(*bn_x, "bn_x", B, g.C, g.H, g.W);
+    conv_check(*bn_y, "bn_y", B, g.C, g.H, g.W);
+    check_f32(*bn_mean, "bn_mean"); check_f32(*bn_invstd, "bn_invstd");
+    TORCH_CHECK(bn_mean->numel() >= g.C && bn_invstd->numel() >= g.C, "conv_dgrad: BN statistics size");
+    bst = ndp::ConvBnStats{stats->data_ptr<double>(), bn_x->data_ptr<float>(), bn_y->data_ptr<float>(),
+                           bn_mean->data_ptr<float>(), bn_invstd->data_ptr<float>()};
+  }
   const int left = ndp::launch_conv_dgrad(dy.data_ptr<float>(), w.data_ptr<float>(), dx.data_ptr<float>(), B, g, pp,
-                                          cur_stream(), ap, defer && cls != 4);
+                                          cur_stream(), ap, defer && cls != 4, bst.out ? &bst : nullptr);
   check_launch("launch_conv_dgrad");
   return left;
 }
@@ -1379,7 +1407,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("gamma"), py::arg("save_mean"),
         py::arg("save_invstd"), py::arg("dx"), py::arg("dres"), py::arg("dgamma"), py::arg("dbeta"), py::arg("part"),
         py::arg("relu"), py::arg("single"), py::arg("dypart") = py::none(), py::arg("nslab") = 0,
-        py::arg("dyadd") = py::none(), py::arg("mbeta") = py::none());
+        py::arg("dyadd") = py::none(), py::arg("mbeta") = py::none(), py::arg("dstats") = py::none(),
+        py::arg("dS") = 0);
   m.def("bn_relu_maxpool", &bn_relu_maxpool, py::arg("x"), py::arg("y"), py::arg("idx"), py::arg("gamma"),
         py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("nbt"), py::arg("save_mean"),
         py::arg("save_invstd"), py::arg("part"), py::arg("eps"), py::arg("momentum"), py::arg("xstats") = py::none(),
@@ -1406,7 +1435,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("defer") = false, py::arg("stats") = py::none());
   m.def("conv_stats_slices", &conv_stats_slices, py::arg("geom"), py::arg("batch"));
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("geom"),
-        py::arg("part") = py::none(), py::arg("addend") = py::none(), py::arg("defer") = false);
+        py::arg("part") = py::none(), py::arg("addend") = py::none(), py::arg("defer") = false,
+        py::arg("stats") = py::none(), py::arg("bn_x") = py::none(), py::arg("bn_y") = py::none(),
+        py::arg("bn_mean") = py::none(), py::arg("bn_invstd") = py::none());
+  m.def("conv_dgrad_stats_slices", [](const std::vector<int64_t>& geom, int64_t B) -> int64_t {
+    const ndp::ConvGeom g = conv_geom(geom);
+    const int cls = ndp::conv_direct_class(g);
+    if (cls < 0 || B <= 0 || B % ndp::conv_fwd_imgs(cls)) return 0;
+    return ndp::conv_dgrad_stats_slices(cls, g, (int)B);
+  }, py::arg("geom"), py::arg("batch"));
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("part"), py::arg("dw"), py::arg("geom"));
   m.def("tg_plan", &tg_plan);
   m.def("sm_plan", &sm_plan, py::arg("geom"), py::arg("batch"));

@@ -316,6 +316,8 @@ struct ConvFwdCfg {
   static constexpr int STATS_LDO = BN + 4, STATS_TPC = 256 / BM;
   static constexpr bool STATS_OK = 256 % BM == 0 && BN % (4 * STATS_TPC) == 0 &&
                                    (size_t)BM * STATS_LDO <= (size_t)NBUF * (A_SZ + B_SZ);
+  // backward mode keeps two such tiles (dz and dz * xhat)
+  static constexpr bool STATS2_OK = STATS_OK && (size_t)2 * BM * STATS_LDO <= (size_t)NBUF * (A_SZ + B_SZ);
 };
 
 // A (weights) is read straight from W: forward rows W[m][c0:c0+CK][:] (CK*RS contiguous
@@ -330,13 +332,13 @@ struct ConvFwdCfg {
 // the even pixels of the H x W LDS image (the odd ones keep the zero fill), i.e. the stride-1
 // correlation of the zero-inserted dY with the flipped weights:
 //   dX[c, h, w] = sum_{k,r,s} W[k, c, 2-r, 2-s] * Z[k, h-1+r, w-1+s],  Z[k, 2p, 2q] = dY[k, p, q]
+
 template <int R, int S, int ST, int PD, int H, int W, int CK, int BM, int IMGS, int WM, int NBUF, int KB, bool TRANSW,
           bool VEC, int UPS = 1, int SCH = 0, int IUPS = 1>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                        float* __restrict__ y, float* __restrict__ part, int Cin,
                                                        int Kout, int cps, int64_t slab,
-                                                       const float* __restrict__ addend,
-                                                       double* __restrict__ stats) {
+                                                       const float* __restrict__ addend, ConvBnStats st) {
   using G = ConvFwdCfg<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW>;
   constexpr int AE = (BM * G::KK + 3) / 4;  // float4 slots (scalar path: 4 scalars per slot)
   constexpr int A_PER_T = (AE + 255) / 256;
@@ -570,6 +572,15 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
   // UPS = 2 (grad-x of a 1x1 stride-2 conv): the result lands on the even pixels of a
   // (2P) x (2Q) plane and the three odd neighbours of each are written as zeros
   constexpr int OPQ = G::PQ * UPS * UPS;
+  // BatchNorm partial sums (st.out, see ConvBnStats): unsplit, statistics-capable tiles only.
+  // The two per-element quantities go through the LDS the main loop no longer reads (its last
+  // iteration ended on a barrier) as [BM][BN + 4] tiles: row writes of 32 consecutive pixels
+  // per half-wave, float4 row reads in the reduction below.
+  constexpr bool kStats = G::STATS_OK && UPS == 1;
+  const bool stats = kStats && st.out != nullptr;
+  const bool bstats = G::STATS2_OK && stats && st.bx != nullptr;
+  float* L = smem;
+  float* L2 = smem + BM * G::STATS_LDO;
 #pragma unroll
   for (int tm = 0; tm < G::TM; ++tm)
 #pragma unroll
@@ -595,48 +606,62 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
 #pragma unroll
         for (int r = 0; r < 16; ++r) ad[r] = 0.f;
       }
+      float bxv[16], byv[16], bmu[16], bis[16];  // backward statistics operands, same rule
+      if (kStats && bstats) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + (wm * G::TM + tm) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          bxv[r] = st.bx[yoff + (int64_t)m * OPQ];
+          byv[r] = st.by[yoff + (int64_t)m * OPQ];
+          bmu[r] = st.mean[m];
+          bis[r] = st.invstd[m];
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = m0 + (wm * G::TM + tm) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int mloc = (wm * G::TM + tm) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int m = m0 + mloc;
         float* d = yb + (int64_t)m * OPQ;
-        d[0] = acc[tm][tn][r] + ad[r];
+        const float v = acc[tm][tn][r] + ad[r];
+        d[0] = v;
         if constexpr (UPS == 2) {
           d[1] = 0.f;
           d[2 * G::Q] = 0.f;
           d[2 * G::Q + 1] = 0.f;
         }
+        if constexpr (kStats) {
+          if (bstats) {
+            const float dz = byv[r] > 0.f ? v : 0.f;
+            L[mloc * G::STATS_LDO + n] = dz;
+            L2[mloc * G::STATS_LDO + n] = dz * ((bxv[r] - bmu[r]) * bis[r]);
+          } else if (stats) {
+            L[mloc * G::STATS_LDO + n] = v;
+          }
+        }
       }
     }
 
-  // BatchNorm forward statistics of the tile (stats != nullptr: unsplit launches whose output
-  // feeds a BatchNorm): per output channel the sum and sum of squares of the tile's IMGS x PQ
-  // outputs, fp32 over 4 values then fp64, stored to stats[(c * S + s) * 2 + {0, 1}] with
-  // s = blockIdx.x of S = gridDim.x: the [c][s][2] slice-partial layout the BN apply kernel
-  // folds (fixed order), so the BN needs no statistics pass (one launch and one full read of y
-  // fewer).  The tile goes through the LDS the main loop no longer reads (its last iteration
-  // ended on a barrier): row writes of 32 consecutive pixels per half-wave, float4 row reads.
-  if constexpr (G::STATS_OK && UPS == 1) {
-    if (stats != nullptr) {
-      float* L = smem;
-#pragma unroll
-      for (int tm = 0; tm < G::TM; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < G::TN; ++tn) {
-          const int n = (wn * G::TN + tn) * 32 + l32;
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            L[((wm * G::TM + tm) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * G::STATS_LDO + n] = acc[tm][tn][r];
-        }
+  // Per output channel, fp32 over 4 values then fp64, stored to st.out[(c * S + s) * 2 + {0, 1}]
+  // with s = blockIdx.x of S = gridDim.x: the [c][s][2] slice-partial layout the BN kernels fold
+  // in a fixed order, so the BN runs no statistics pass (one launch and one full read fewer).
+  if constexpr (kStats) {
+    if (stats) {
       __syncthreads();
       constexpr int TPC = G::STATS_TPC, NPT = G::BN / TPC;
       const int c = tid / TPC, j = tid - c * TPC;
       const float* src = L + c * G::STATS_LDO + j * NPT;
+      const float* src2 = L2 + c * G::STATS_LDO + j * NPT;
       double sum = 0.0, sq = 0.0;
 #pragma unroll 4
       for (int i = 0; i < NPT; i += 4) {
         const f32x4c v = *reinterpret_cast<const f32x4c*>(src + i);
         sum += (double)((v.x + v.y) + (v.z + v.w));
-        sq += (double)((v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w));
+        if (bstats) {
+          const f32x4c u = *reinterpret_cast<const f32x4c*>(src2 + i);
+          sq += (double)((u.x + u.y) + (u.z + u.w));
+        } else {
+          sq += (double)((v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w));
+        }
       }
 #pragma unroll
       for (int o = 1; o < TPC; o <<= 1) {
@@ -644,7 +669,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
         sq += __shfl_xor(sq, o, 64);
       }
       if (j == 0) {
-        double* d = stats + ((int64_t)(m0 + c) * gridDim.x + blockIdx.x) * 2;
+        double* d = st.out + ((int64_t)(m0 + c) * gridDim.x + blockIdx.x) * 2;
         d[0] = sum;
         d[1] = sq;
       }
@@ -967,7 +992,8 @@ static void set_lds(KernelT k, size_t bytes) {
 template <int R, int S, int ST, int PD, int H, int W, int CK, int BM, int IMGS, int WM, int NBUF, int KB, bool TRANSW,
           bool VEC, int UPS = 1, int SCH = 0, int IUPS = 1>
 static int run_fwd(const float* x, const float* w, float* y, int B, int Cin, int Kout, int ksplit, float* part,
-                   hipStream_t s, const float* addend = nullptr, bool defer = false, double* stats = nullptr) {
+                   hipStream_t s, const float* addend = nullptr, bool defer = false,
+                   ConvBnStats stats = ConvBnStats{nullptr, nullptr, nullptr, nullptr, nullptr}) {
   using G = ConvFwdCfg<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW>;
   auto k = conv_fwd_kernel<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW, VEC, UPS, SCH, IUPS>;
   static bool attr = false;  // once per instantiation (> 64 KiB of LDS needs the opt-in)
@@ -978,7 +1004,7 @@ static int run_fwd(const float* x, const float* w, float* y, int B, int Cin, int
   ksplit = (nchunks + cps - 1) / cps;
   const int64_t slab = (int64_t)B * Kout * G::PQ;  // compact partial tile layout
   // stats: only unsplit launches of statistics-capable tiles (conv_fwd_stats_slices says which)
-  if (!(G::STATS_OK && UPS == 1) || ksplit > 1) stats = nullptr;
+  if (!(G::STATS_OK && UPS == 1) || ksplit > 1 || (stats.bx != nullptr && !G::STATS2_OK)) stats.out = nullptr;
   hipLaunchKernelGGL(k, dim3(B / IMGS, Kout / BM, ksplit), dim3(256), G::LDS_BYTES, s, x, w, y, part, Cin, Kout, cps,
                      slab, ksplit > 1 ? nullptr : addend, stats);
   // defer: leave the ksplit slabs for the consumer (the fused BN kernel sums them while it
@@ -1118,6 +1144,16 @@ int conv_fwd_stats_slices(int cls, const ConvGeom& g, int B) {
   if (conv_ksplit(cls, g, B, false) != 1) return 0;
   return B / conv_fwd_imgs(cls);
 }
+// backward-mode BN partial sums from the grad-x epilogue: the layer1 3x3 class (its BN takes the
+// two-kernel large-map path), unsplit grad-x launches only; 0 = none
+int conv_dgrad_stats_slices(int cls, const ConvGeom& g, int B) {
+  static_assert(ConvFwdCfg<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true>::STATS2_OK &&
+                    ConvFwdCfg<3, 3, 1, 1, 8, 8, 16, 64, 1, 2, 2, 4, true>::STATS2_OK,
+                "backward statistics epilogue fits the layer1 grad-x tiles");
+  // (the two-image tile variant, NDP_CONV_VARIANT=1, has no room for the two tiles)
+  if (cls != 0 || conv_variant() == 1 || conv_ksplit(cls, g, B, true) != 1) return 0;
+  return B / conv_fwd_imgs(cls);
+}
 // 3x3 stride-2 grad-x on the zero-inserted dY: exact (tests/test_conv_direct.py), 4x the
 // MFMA work of the sub-pixel form; measured on 1x MI355X (ResNet-18 step, round 2) 2.006 /
 // 2.005 vs MIOpen 1.991 ms at batch 512, 1.054 / 1.047 vs 1.051 at 64.  DEFAULT since round 3:
@@ -1155,7 +1191,8 @@ static bool ck16(int cls) {
 }
 
 int launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s,
-                    bool defer, double* stats) {
+                    bool defer, double* stats_out) {
+  const ConvBnStats stats{stats_out, nullptr, nullptr, nullptr, nullptr};
   const int cls = conv_direct_class(g);
   const int ks = conv_ksplit(cls, g, B, false);
   const bool c16 = ck16(cls);
@@ -1215,7 +1252,8 @@ int launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvG
 
 // dx[B, C, H, W] from dy[B, Co, OH, OW] (stride-1 classes only)
 int launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, float* part,
-                      hipStream_t s, const float* addend, bool defer) {
+                      hipStream_t s, const float* addend, bool defer, const ConvBnStats* bst) {
+  const ConvBnStats stats = bst != nullptr ? *bst : ConvBnStats{nullptr, nullptr, nullptr, nullptr, nullptr};
   const int cls = conv_direct_class(g);
   const int ks = conv_ksplit(cls, g, B, true);
   const bool c16 = ck16(cls);
@@ -1224,18 +1262,18 @@ int launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const C
     case 0:
       if (sch == 1)
         return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true, true, 1, 1>(dy, w, dx, B, g.Co, g.C, ks, part, s,
-                                                                              addend, defer);
+                                                                              addend, defer, stats);
       if (sch == 2)
         return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true, true, 1, 2>(dy, w, dx, B, g.Co, g.C, ks, part, s,
-                                                                              addend, defer);
+                                                                              addend, defer, stats);
       if (conv_variant() == 1)
         return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 2, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s, addend,
-                                                                        defer);
+                                                                        defer, stats);
       if (c16)
         return run_fwd<3, 3, 1, 1, 8, 8, 16, 64, 1, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s,
-                                                                         addend, defer);
+                                                                         addend, defer, stats);
       return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s, addend,
-                                                                      defer);
+                                                                      defer, stats);
     case 1:
       if (sch == 1)
         return run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, true, true, 1, 1>(dy, w, dx, B, g.Co, g.C, ks, part, s,

@@ -141,7 +141,10 @@ void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamm
 void launch_bn_bwd(const float* dy, const float* y, const float* x, const float* gamma, const float* save_mean,
                    const float* save_invstd, float* dx, float* dres, float* dgamma, float* dbeta, double* part,
                    int N, int C, int HW, int S, int relu, int single, hipStream_t s, const float* dypart = nullptr,
-                   int nslab = 0, const float* dyadd = nullptr, const float* mbeta = nullptr);
+                   int nslab = 0, const float* dyadd = nullptr, const float* mbeta = nullptr,
+                   const double* dstats = nullptr, int dS = 0);
+// dstats (nullable; large-map path, no slabs): [C][dS][2] partial sums of dz and dz * xhat from the
+// grad-x epilogue of the conv that produced dy (conv_dgrad bst); the statistics pass is skipped
 // mbeta (nullable, relu, two-kernel path only): y was never stored; the ReLU mask is recomputed
 // from x as fmaf(x, gamma * invstd, beta - mean * gamma * invstd) > 0 (the forward's own ops)
 bool bn_two_kernel_path(int N, int C, int HW, int single);
@@ -256,13 +259,28 @@ int conv_ksplit(int cls, const ConvGeom& g, int B, bool dgrad);
 // (compact output layout, slab = numel(out)); returns 1 when `y` / `dx` holds the result
 // stats (nullable; only where conv_fwd_stats_slices > 0): BatchNorm partial sums of y from the
 // epilogue, [Co][S][2] fp64 (sum, sum of squares per channel and batch tile)
+// BatchNorm partial sums from the epilogue (out != nullptr): forward mode (bx == nullptr) sums
+// the output v and v^2 for the BN that consumes it; backward mode sums dz = v * (by > 0) and
+// dz * (bx - mean) * invstd for the BN whose output gradient v is (bx / by: that BN's input and
+// ReLU output, mean / invstd its saved statistics) — the BN backward's statistics pass
+struct ConvBnStats {
+  double* out;
+  const float* bx;
+  const float* by;
+  const float* mean;
+  const float* invstd;
+};
 int launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s,
                     bool defer = false, double* stats = nullptr);
 int conv_fwd_stats_slices(int cls, const ConvGeom& g, int B);
 // addend (nullable, 3x3 classes): dx += addend in the epilogue / split-K sum; with defer the
 // slabs are left unsummed and the consumer adds the addend after them (launch_bn_bwd dyadd)
+// bst (nullable; the layer1 3x3 class, unsplit: conv_dgrad_stats_slices): backward-mode BN partial
+// sums of dx for the BN whose output gradient dx is
 int launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, float* part,
-                      hipStream_t s, const float* addend = nullptr, bool defer = false);
+                      hipStream_t s, const float* addend = nullptr, bool defer = false,
+                      const ConvBnStats* bst = nullptr);
+int conv_dgrad_stats_slices(int cls, const ConvGeom& g, int B);
 // out[i] = sum_{z < nslab} part[z * n + i] (+ addend[i]) in z order (n % 4 == 0), same order as
 // the split-K sums; out may alias addend
 void launch_slab_sum(const float* part, float* out, int64_t n, int nslab, hipStream_t s,

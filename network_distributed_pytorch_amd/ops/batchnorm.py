@@ -43,6 +43,10 @@ class _BNActFn(torch.autograd.Function):
         X.bn_fwd(x, res, y, weight, bias, running_mean, running_var, nbt, save_mean, save_invstd, part,
                  float(eps), float(momentum), bool(relu), True, bool(single), xpart, nslab, xstats, xS)
         ctx.grad_slab = grad_slab  # ops/slablink.py: dy may arrive as the next conv's grad-x slabs
+        if (grad_slab is not None and relu and _BWD_STATS
+                and X.bn_two_kernel_path(x.shape[0], C, x.numel() // (x.shape[0] * C), bool(single))):
+            # the conv producing dy may emit this BN's backward statistics (grad-x epilogue)
+            grad_slab.bn_saved = (x, y, save_mean, save_invstd)
         ctx.relu = bool(relu)
         ctx.single = bool(single)
         ctx.has_res = res is not None
@@ -64,8 +68,11 @@ class _BNActFn(torch.autograd.Function):
         dbeta = grad_buffer(ctx.params[1], weight) if ctx.has_w else None
         dypart, nslab = ctx.grad_slab.take_bwd() if ctx.grad_slab is not None else (None, 0)
         dyadd = ctx.grad_slab.take_bwd_add() if ctx.grad_slab is not None else None
+        dstats, dS = ctx.grad_slab.take_bwd_stats() if ctx.grad_slab is not None else (None, 0)
+        if ctx.grad_slab is not None:
+            ctx.grad_slab.bn_saved = None
         ext().bn_bwd(dy, y, x, weight, save_mean, save_invstd, dx, dres, dgamma, dbeta, part, ctx.relu, ctx.single,
-                     dypart, nslab, dyadd)
+                     dypart, nslab, dyadd, None, dstats if dypart is None else None, dS if dypart is None else 0)
         if ctx.link is not None and dres is not None:
             ctx.link.put(dres)
             dres = None
@@ -106,6 +113,10 @@ class _BNReluPoolFn(torch.autograd.Function):
                      None, 0, None, bias)
         return dx, dgamma, dbeta, None, None, None, None, None, None, None, None
 
+
+# BN backward statistics from the grad-x epilogue of the conv producing dy (ops/slablink.py;
+# NDP_BN_BWD_STATS=0: the BN's own statistics pass)
+_BWD_STATS = os.environ.get("NDP_BN_BWD_STATS", "1") != "0"
 
 # the stem tail BN -> ReLU -> MaxPool in one pass (NDP_STEM_POOL=0: BN kernel + pool kernel)
 STEM_POOL = os.environ.get("NDP_STEM_POOL", "1") != "0"

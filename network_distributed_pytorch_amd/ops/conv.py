@@ -177,6 +177,15 @@ class DirectConvFn(torch.autograd.Function):
                     addend = addend.contiguous()
                 # split-K slabs (and the addend, added after them) left to the consuming BN
                 defer = grad_slab is not None and part is not None and (addend is None or fuse)
+                # unsplit: the consuming BN's backward statistics from this epilogue (ops/slablink.py)
+                bn = grad_slab.bn_saved if (grad_slab is not None and part is None and (addend is None or fuse)) \
+                    else None
+                S = int(ext().conv_dgrad_stats_slices(list(geom), x.shape[0])) if bn is not None else 0
+                if S > 0:
+                    stats = torch.empty(x.shape[1] * S * 2, device=x.device, dtype=torch.float64)
+                    ext().conv_dgrad(dy, weight, dx, list(geom), None, addend if fuse else None, False, stats, *bn)
+                    grad_slab.put_bwd_stats(stats, S)
+                    return dx
                 left = ext().conv_dgrad(dy, weight, dx, list(geom), part, addend if fuse else None, defer)
                 if left > 1:  # dx stays unwritten: the BN backward sums the slabs (+ the addend)
                     grad_slab.put_bwd(part, left, addend if fuse else None)

@@ -21,6 +21,10 @@ ResNet stem and layer1), the link carries the BN's statistics instead: the conv 
 emits per-channel, per-batch-tile fp64 sums of its output (csrc/conv.hip ``stats``) and the
 BN's apply kernel folds them, so the BN skips its statistics launch and its full read of x.
 
+In backward the same idea runs the other way: a BN whose ReLU output is known deposits
+(x, y, mean, invstd) in its gradient link, and the direct conv producing that gradient emits
+the BN backward's per-channel partial sums of dz and dz * xhat from its grad-x epilogue.
+
 Only wired inside the fused ResNet blocks (models/resnet.py), where each conv output /
 grad-x has exactly that one consumer.
 """
@@ -34,13 +38,25 @@ __all__ = ["SlabLink"]
 
 
 class SlabLink:
-    __slots__ = ("fwd", "bwd", "bwd_add", "stats")
+    __slots__ = ("fwd", "bwd", "bwd_add", "stats", "bn_saved", "bstats")
 
     def __init__(self):
         self.fwd: Optional[Tuple[torch.Tensor, int]] = None  # conv output slabs -> BN forward
         self.bwd: Optional[Tuple[torch.Tensor, int]] = None  # conv grad-x slabs -> BN backward
         self.bwd_add: Optional[torch.Tensor] = None  # the grad-x addend, added after the slabs
         self.stats: Optional[Tuple[torch.Tensor, int]] = None  # conv epilogue BN partial sums [C][S][2]
+        # backward: the BN's (x, y, save_mean, save_invstd), deposited by its forward, so the conv
+        # producing its output gradient can emit the BN backward's partial sums (bstats)
+        self.bn_saved: Optional[tuple] = None
+        self.bstats: Optional[Tuple[torch.Tensor, int]] = None
+
+    def put_bwd_stats(self, stats: torch.Tensor, n: int) -> None:
+        assert self.bstats is None, "SlabLink: backward statistics deposited twice"
+        self.bstats = (stats, int(n))
+
+    def take_bwd_stats(self) -> Tuple[Optional[torch.Tensor], int]:
+        v, self.bstats = self.bstats, None
+        return v if v is not None else (None, 0)
 
     def put_stats(self, stats: torch.Tensor, n: int) -> None:
         assert self.stats is None, "SlabLink: statistics deposited twice"

@@ -121,3 +121,58 @@ def test_stats_link_unused_by_unfused_bn(device):
     x = torch.randn(4, 2, 4, 4, device=device)
     bn(x, slab_in=link)
     assert link.stats is None
+
+
+@pytest.mark.parametrize("B", [256, 512])
+def test_dgrad_epilogue_bwd_stats_match_fp64(device, B):
+    """Backward mode: the layer1 grad-x epilogue emits, per channel and image, the sums of
+    dz = dx * (y > 0) and dz * (x - mean) * invstd for the BN whose output gradient dx is."""
+    C, H = 64, 8
+    geom = [C, H, H, C, 3, 3, 1, 1]
+    S = int(ext().conv_dgrad_stats_slices(geom, B))
+    assert S == B
+    torch.manual_seed(B + 1)
+    dy = torch.randn(B, C, H, H, device=device)
+    w = torch.randn(C, C, 3, 3, device=device) * 0.05
+    bx = torch.randn(B, C, H, H, device=device) * 1.5 + 0.2
+    by = torch.relu(torch.randn(B, C, H, H, device=device))
+    mean = torch.randn(C, device=device) * 0.1
+    invstd = torch.rand(C, device=device) + 0.5
+    dx = torch.empty_like(bx)
+    dx_ref = torch.empty_like(bx)
+    stats = torch.full((C * S * 2,), float("nan"), device=device, dtype=torch.float64)
+    ext().conv_dgrad(dy, w, dx_ref, geom, None, None, False)
+    ext().conv_dgrad(dy, w, dx, geom, None, None, False, stats, bx, by, mean, invstd)
+    assert torch.equal(dx, dx_ref)
+    dz = dx.double() * (by > 0).double()
+    xh = (bx.double() - mean.double().view(1, C, 1, 1)) * invstd.double().view(1, C, 1, 1)
+    st = stats.view(C, S, 2)
+    ref_a = dz.sum((2, 3)).t()
+    ref_b = (dz * xh).sum((2, 3)).t()
+    tol = 1e-5 * (dz.abs().max().item() * H * H)
+    assert (st[..., 0] - ref_a).abs().max().item() < tol
+    assert (st[..., 1] - ref_b).abs().max().item() < tol * 8
+
+
+@pytest.mark.parametrize("batch", [256, 512])
+def test_resnet18_bwd_epilogue_stats_close_and_repeatable(device, batch, monkeypatch):
+    from network_distributed_pytorch_amd.ops import batchnorm as bn_mod
+
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
+    torch.manual_seed(0)
+    m = build_resnet(18, 1000).to(device)
+    state = {k: v.clone() for k, v in m.state_dict().items()}
+    x = torch.rand(batch, 3, 32, 32, device=device) * 2 - 1
+    y = torch.randint(0, 10, (batch,), device=device)
+    runs = []
+    for on in (False, True, True):
+        monkeypatch.setattr(bn_mod, "_BWD_STATS", on)
+        m.load_state_dict(state)
+        runs.append(_step(m, x, y))
+    (l0, g0, s0), (l1, g1, s1), (l2, g2, s2) = runs
+    assert torch.equal(l1, l2) and torch.equal(l0, l1)
+    for n in g1:
+        assert torch.equal(g1[n], g2[n]), n
+    for n in g0:
+        scale = g0[n].abs().max().item() + 1e-12
+        assert (g0[n] - g1[n]).abs().max().item() < 2e-3 * scale, n

@@ -35,6 +35,8 @@ def test_resnet18_slab_links_bitwise(device, batch, monkeypatch):
     from network_distributed_pytorch_amd.ops import conv as conv_mod
     monkeypatch.setattr(conv_mod, "CONV_BN_STATS", False)
     monkeypatch.setattr(conv_mod, "_STATS", {})
+    from network_distributed_pytorch_amd.ops import batchnorm as bn_mod
+    monkeypatch.setattr(bn_mod, "_BWD_STATS", False)
     torch.manual_seed(0)
     m = build_resnet(18, 1000).to(device)
     state = {k: v.clone() for k, v in m.state_dict().items()}
