@@ -1151,8 +1151,10 @@ int conv_dgrad_stats_slices(int cls, const ConvGeom& g, int B) {
                     ConvFwdCfg<3, 3, 1, 1, 8, 8, 16, 64, 1, 2, 2, 4, true>::STATS2_OK,
                 "backward statistics epilogue fits the layer1 grad-x tiles");
   // (the two-image tile variant, NDP_CONV_VARIANT=1, has no room for the two tiles)
-  if (cls != 0 || conv_variant() == 1 || conv_ksplit(cls, g, B, true) != 1) return 0;
-  return B / conv_fwd_imgs(cls);
+  // class 2 (3x3 stride 2) runs the layer1 grad-x kernel on the zero-inserted dY: one image per tile
+  if ((cls != 0 && cls != 2) || conv_variant() == 1 || conv_ksplit(cls, g, B, true) != 1) return 0;
+  if (cls == 2 && !conv_dgrad_direct(cls)) return 0;
+  return cls == 2 ? B : B / conv_fwd_imgs(cls);
 }
 // 3x3 stride-2 grad-x on the zero-inserted dY: exact (tests/test_conv_direct.py), 4x the
 // MFMA work of the sub-pixel form; measured on 1x MI355X (ResNet-18 step, round 2) 2.006 /
@@ -1288,7 +1290,7 @@ int launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const C
                                                                       defer);
     case 2:  // 3x3 stride 2: the layer1 grad-x kernel on the zero-inserted dY (staged, not stored)
       return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true, true, 1, 2, 2>(dy, w, dx, B, g.Co, g.C, ks, part, s,
-                                                                              addend, defer);
+                                                                              addend, defer, stats);
     case 4: return run_fwd<1, 1, 1, 0, 4, 4, 8, 64, 4, 2, 2, 4, true, true, 2>(dy, w, dx, B, g.Co, g.C, ks, part, s);
     default: return 1;
   }

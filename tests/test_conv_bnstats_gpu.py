@@ -124,16 +124,19 @@ def test_stats_link_unused_by_unfused_bn(device):
 
 
 @pytest.mark.parametrize("B", [256, 512])
-def test_dgrad_epilogue_bwd_stats_match_fp64(device, B):
-    """Backward mode: the layer1 grad-x epilogue emits, per channel and image, the sums of
+@pytest.mark.parametrize("Co,st", [(64, 1), (128, 2)])
+def test_dgrad_epilogue_bwd_stats_match_fp64(device, B, Co, st):
+    """Backward mode: the layer1 grad-x epilogue (and layer2's strided entry conv's, run as the
+    same kernel on the zero-inserted dY) emits, per channel and image, the sums of
     dz = dx * (y > 0) and dz * (x - mean) * invstd for the BN whose output gradient dx is."""
     C, H = 64, 8
-    geom = [C, H, H, C, 3, 3, 1, 1]
+    geom = [C, H, H, Co, 3, 3, st, 1]
     S = int(ext().conv_dgrad_stats_slices(geom, B))
     assert S == B
     torch.manual_seed(B + 1)
-    dy = torch.randn(B, C, H, H, device=device)
-    w = torch.randn(C, C, 3, 3, device=device) * 0.05
+    OH = (H - 1) // st + 1
+    dy = torch.randn(B, Co, OH, OH, device=device)
+    w = torch.randn(Co, C, 3, 3, device=device) * 0.05
     bx = torch.randn(B, C, H, H, device=device) * 1.5 + 0.2
     by = torch.relu(torch.randn(B, C, H, H, device=device))
     mean = torch.randn(C, device=device) * 0.1
