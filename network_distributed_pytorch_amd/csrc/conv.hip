@@ -96,9 +96,68 @@ __global__ __launch_bounds__(256) void toeplitz_expand_many_kernel(ExpandBatch b
   }
 }
 
+// kExpandRows consecutive W_big^T rows of one layer per workgroup, the 256 threads over the
+// rows' (row, ci) pairs: a one-row workgroup left half its threads idle at C = 128 and spent
+// its time on the layer scan and index setup for 2-8 KB of stores (21.6 µs per ResNet-18
+// forward for ~35 MB, 1.6 TB/s; profiles/r4).  Consecutive threads write consecutive H*W-float
+// segments of a row: coalesced.
+constexpr int kExpandRows = 8;
+template <int H, int W>
+__device__ __forceinline__ void expand_rows(const float* __restrict__ w, float* __restrict__ wt, const ConvGeom& g,
+                                            int n0) {
+  const int C = g.C, OHW = g.OH * g.OW;
+  const int64_t K = (int64_t)C * H * W;
+  for (int idx = threadIdx.x; idx < kExpandRows * C; idx += 256) {
+    const int rr = idx / C, ci = idx - rr * C;
+    const int n = n0 + rr;
+    const int co = n / OHW, ohw = n - co * OHW;
+    const int oh = ohw / g.OW, ow = ohw - oh * g.OW;
+    const int h0 = oh * g.stride - g.pad, w0 = ow * g.stride - g.pad;
+    const float* wc = w + ((int64_t)co * C + ci) * g.KH * g.KW;
+    float v[H * W];
+#pragma unroll
+    for (int ih = 0; ih < H; ++ih)
+#pragma unroll
+      for (int iw = 0; iw < W; ++iw) {
+        const int kh = ih - h0, kw = iw - w0;
+        v[ih * W + iw] = (kh >= 0 && kh < g.KH && kw >= 0 && kw < g.KW) ? wc[kh * g.KW + kw] : 0.f;
+      }
+    float* d = wt + (int64_t)n * K + (int64_t)ci * (H * W);
+    if constexpr ((H * W) % 4 == 0) {
+#pragma unroll
+      for (int j = 0; j < H * W; j += 4)
+        *reinterpret_cast<f32x4e*>(d + j) = f32x4e{v[j], v[j + 1], v[j + 2], v[j + 3]};
+    } else {
+#pragma unroll
+      for (int j = 0; j < H * W; ++j) d[j] = v[j];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void toeplitz_expand_rows_kernel(ExpandBatch b) {
+  const int64_t r0 = (int64_t)blockIdx.x * kExpandRows;
+  int e = 0;
+  while (e + 1 < b.n && r0 >= b.end[e]) ++e;
+  const ConvGeom& g = b.g[e];
+  const int n0 = (int)(r0 - (e ? b.end[e - 1] : 0));
+  if (g.H == 1 && g.W == 1) expand_rows<1, 1>(b.w[e], b.wt[e], g, n0);
+  else if (g.H == 2 && g.W == 2) expand_rows<2, 2>(b.w[e], b.wt[e], g, n0);
+  else expand_rows<4, 4>(b.w[e], b.wt[e], g, n0);
+}
+
 void launch_toeplitz_expand_many(const ExpandBatch& b, hipStream_t s) {
   if (b.n <= 0) return;
-  hipLaunchKernelGGL(toeplitz_expand_many_kernel, dim3((unsigned)b.end[b.n - 1]), dim3(256), 0, s, b);
+  bool rows_ok = true;  // every layer's rows split into whole groups of the covered map sizes
+  for (int e = 0; e < b.n; ++e) {
+    const ConvGeom& g = b.g[e];
+    const int64_t rows = b.end[e] - (e ? b.end[e - 1] : 0);
+    rows_ok = rows_ok && rows % kExpandRows == 0 && g.H == g.W && (g.H == 1 || g.H == 2 || g.H == 4);
+  }
+  if (rows_ok)
+    hipLaunchKernelGGL(toeplitz_expand_rows_kernel, dim3((unsigned)(b.end[b.n - 1] / kExpandRows)), dim3(256), 0, s,
+                       b);
+  else
+    hipLaunchKernelGGL(toeplitz_expand_many_kernel, dim3((unsigned)b.end[b.n - 1]), dim3(256), 0, s, b);
 }
 
 // One thread per (co, ci) weight PAIR: it reads, for every output position (oh, ow), the
@@ -132,6 +191,56 @@ __device__ __forceinline__ void fold_pair(const float* __restrict__ dwt, const C
     }
 }
 
+// The same fold with the geometry at compile time (ResNet-18/34 layer3 / layer4 Toeplitz
+// shapes): every tap test resolves statically and the <= OH*OW*H*W loads of a pair issue
+// together instead of behind a runtime-bounded loop (the generic fold ran at 1.4 TB/s).
+// Same (oh, ow, ih, iw) accumulation order per tap: bitwise equal to fold_pair.
+template <int H, int W, int OH, int OW, int ST, int PD, int KH, int KW>
+__device__ __forceinline__ void fold_pair_t(const float* __restrict__ dwt, int C, int pair,
+                                            float (&acc)[kFoldMaxTaps]) {
+  const int co = pair / C, ci = pair - co * C;
+  const int64_t K = (int64_t)C * H * W;
+#pragma unroll
+  for (int t = 0; t < kFoldMaxTaps; ++t) acc[t] = 0.f;
+  float v[OH * OW][H * W];
+#pragma unroll
+  for (int oh = 0; oh < OH; ++oh)
+#pragma unroll
+    for (int ow = 0; ow < OW; ++ow) {
+      const float* row = dwt + (int64_t)((co * OH + oh) * OW + ow) * K + (int64_t)ci * (H * W);
+#pragma unroll
+      for (int ih = 0; ih < H; ++ih)
+#pragma unroll
+        for (int iw = 0; iw < W; ++iw) {
+          const int kh = ih - oh * ST + PD, kw = iw - ow * ST + PD;
+          v[oh * OW + ow][ih * W + iw] = (kh >= 0 && kh < KH && kw >= 0 && kw < KW) ? row[ih * W + iw] : 0.f;
+        }
+    }
+#pragma unroll
+  for (int oh = 0; oh < OH; ++oh)
+#pragma unroll
+    for (int ow = 0; ow < OW; ++ow)
+#pragma unroll
+      for (int ih = 0; ih < H; ++ih)
+#pragma unroll
+        for (int iw = 0; iw < W; ++iw) {
+          const int kh = ih - oh * ST + PD, kw = iw - ow * ST + PD;
+          if (kh >= 0 && kh < KH && kw >= 0 && kw < KW) acc[kh * KW + kw] += v[oh * OW + ow][ih * W + iw];
+        }
+}
+
+__device__ __forceinline__ void fold_any(const float* __restrict__ dwt, const ConvGeom& g, int pair,
+                                         float (&acc)[kFoldMaxTaps]) {
+  const bool k3 = g.KH == 3 && g.KW == 3 && g.pad == 1, k1 = g.KH == 1 && g.KW == 1 && g.pad == 0;
+  if (k3 && g.H == 2 && g.W == 2 && g.stride == 1) fold_pair_t<2, 2, 2, 2, 1, 1, 3, 3>(dwt, g.C, pair, acc);
+  else if (k3 && g.H == 4 && g.W == 4 && g.stride == 2) fold_pair_t<4, 4, 2, 2, 2, 1, 3, 3>(dwt, g.C, pair, acc);
+  else if (k1 && g.H == 4 && g.W == 4 && g.stride == 2) fold_pair_t<4, 4, 2, 2, 2, 0, 1, 1>(dwt, g.C, pair, acc);
+  else if (k3 && g.H == 2 && g.W == 2 && g.stride == 2) fold_pair_t<2, 2, 1, 1, 2, 1, 3, 3>(dwt, g.C, pair, acc);
+  else if (k1 && g.H == 2 && g.W == 2 && g.stride == 2) fold_pair_t<2, 2, 1, 1, 2, 0, 1, 1>(dwt, g.C, pair, acc);
+  else if (k3 && g.H == 1 && g.W == 1 && g.stride == 1) fold_pair_t<1, 1, 1, 1, 1, 1, 3, 3>(dwt, g.C, pair, acc);
+  else fold_pair(dwt, g, pair, acc);
+}
+
 // Every deferred grad-W fold of a backward pass in ONE launch (ops/gradfinish.py): flat
 // grid over all layers' (co, ci) pairs, the layer found from the <= kMaxExpand prefix sums
 // in the kernel arguments.  A workgroup's 256 pairs own one contiguous run of 256 * KH*KW
@@ -150,7 +259,7 @@ __global__ __launch_bounds__(256) void toeplitz_fold_many_kernel(FoldBatch b) {
     const ConvGeom& g = b.g[e];
     const int T = g.KH * g.KW;
     float acc[kFoldMaxTaps];
-    fold_pair(b.dwt[e], g, (int)(i - e_lo), acc);
+    fold_any(b.dwt[e], g, (int)(i - e_lo), acc);
 #pragma unroll
     for (int t = 0; t < kFoldMaxTaps; ++t)
       if (t < T) stage[threadIdx.x * T + t] = acc[t];
@@ -165,7 +274,7 @@ __global__ __launch_bounds__(256) void toeplitz_fold_many_kernel(FoldBatch b) {
   const int T = g.KH * g.KW;
   const int pair = (int)(i - (e ? b.end[e - 1] : 0));
   float acc[kFoldMaxTaps];
-  fold_pair(b.dwt[e], g, pair, acc);
+  fold_any(b.dwt[e], g, pair, acc);
   float* out = b.dw[e] + (int64_t)pair * T;
 #pragma unroll
   for (int t = 0; t < kFoldMaxTaps; ++t)
