@@ -388,6 +388,65 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(
   const float shift = __fsub_rn(bet, __fmul_rn(mean, scale));
   const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1, PQ = OH * OW;
   const BnSlice sl = slice_of(N, S, s);
+  if ((W & 3) == 0 && 64 % (W >> 2) == 0 && (H & 1) == 0 && (W & 1) == 0) {
+    // pool.hip's vectorised pair scheme: one thread per output pair (oh, 2j), (oh, 2j + 1), the
+    // three input rows' columns 4j .. 4j+3 as one float4 each (normalised + ReLU in registers),
+    // column 4j - 1 from the left lane (the W/4 lanes of a row are adjacent in the wave)
+    const int W4 = W >> 2, pairs = OH * W4;
+    const int total = (int)(sl.n1 - sl.n0) * pairs;
+    for (int base = 0; base < total; base += 256) {  // uniform trip count: every lane shuffles
+      const int t = base + (int)threadIdx.x;
+      const bool live = t < total;
+      const int ni = live ? t / pairs : 0, r = live ? t - ni * pairs : 0;
+      const int oh = r / W4, j = r - oh * W4;
+      const int64_t plane = (sl.n0 + ni) * C + c;
+      const float* xp = x + plane * HW;
+      float v[3][5];
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const int hh = 2 * oh - 1 + kh;
+        f32x4 q = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        if (live && hh >= 0 && hh < H) {
+          q = *reinterpret_cast<const f32x4*>(xp + hh * W + 4 * j);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) q[u] = fmaxf(fmaf(q[u], scale, shift) + 0.f, 0.f);
+        }
+        const float left = __shfl_up(q[3], 1, 64);
+        v[kh][0] = (j > 0) ? left : -INFINITY;
+        v[kh][1] = q[0]; v[kh][2] = q[1]; v[kh][3] = q[2]; v[kh][4] = q[3];
+      }
+      if (!live) continue;
+      float out[2];
+      uint8_t arg[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {  // output column ow = 2j + u: taps at columns 4j - 1 + 2u + kw
+        const int ow = 2 * j + u;
+        const int kh0 = oh == 0 ? 1 : 0, kw0 = ow == 0 ? 1 : 0;
+        float best = -INFINITY;
+        int a0 = kh0 * 3 + kw0;
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+          if (kh < kh0 || 2 * oh - 1 + kh >= H) continue;
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw) {
+            if (kw < kw0 || 2 * ow - 1 + kw >= W) continue;
+            const float val = v[kh][2 * u + kw];
+            if (val > best || isnan(val)) {
+              best = val;
+              a0 = kh * 3 + kw;
+            }
+          }
+        }
+        out[u] = best;
+        arg[u] = (uint8_t)a0;
+      }
+      const int64_t o = plane * PQ + oh * OW + 2 * j;
+      *reinterpret_cast<float2*>(y + o) = make_float2(out[0], out[1]);
+      idx[o] = arg[0];
+      idx[o + 1] = arg[1];
+    }
+    return;
+  }
   const int total = (int)(sl.n1 - sl.n0) * PQ;
   for (int t = threadIdx.x; t < total; t += 256) {
     const int ni = t / PQ, o = t - ni * PQ;
