@@ -1119,6 +1119,22 @@ int bn_slices(int N, int C, int HW) {
   return (int)s;
 }
 
+// apply-pass slices when the statistics come from a conv epilogue: every apply workgroup folds
+// ALL the conv's per-image partials of its channel, so fewer, larger workgroups repeat that
+// fold fewer times (NDP_BN_EXT_DIV = S divisor, A/B).  Measured on 1x MI355X, ResNet-18 r=4
+// batch 512: divisor 1 / 2 / 4 / 8 = 1.862-1.874 / 1.864 / 1.884 / 1.926 ms: default 1
+// (profiles/r4/bench_bn_ext_div.jsonl)
+static int ext_apply_slices(int S) {
+  static int div = -1;
+  if (div < 0) {
+    const char* e = getenv("NDP_BN_EXT_DIV");
+    div = e ? atoi(e) : 1;
+    if (div < 1) div = 1;
+  }
+  const int a = S / div;
+  return a < 1 ? 1 : a;
+}
+
 void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamma, const float* beta,
                    float* rmean, float* rvar, int64_t* nbt, float* save_mean, float* save_invstd,
                    double* part, int N, int C, int HW, int S, float eps, float momentum, int relu,
@@ -1165,12 +1181,14 @@ void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamm
     if (vec) hipLaunchKernelGGL(bn_fwd_stats_kernel<true>, grid, dim3(256), 0, s, x, part, N, C, HW, S, xpart, nslab);
     else hipLaunchKernelGGL(bn_fwd_stats_kernel<false>, grid, dim3(256), 0, s, x, part, N, C, HW, S, nullptr, 0);
   }
+  const int Sa = Sp > 0 ? ext_apply_slices(S) : S;
+  const dim3 agrid(Sa, C);
   if (vec)
-    hipLaunchKernelGGL(bn_fwd_apply_kernel<true>, grid, dim3(256), 0, s, x, res, y, gamma, beta, rmean, rvar, nbt,
-                       save_mean, save_invstd, ap, N, C, HW, S, eps, momentum, relu, training, Sp);
+    hipLaunchKernelGGL(bn_fwd_apply_kernel<true>, agrid, dim3(256), 0, s, x, res, y, gamma, beta, rmean, rvar, nbt,
+                       save_mean, save_invstd, ap, N, C, HW, Sa, eps, momentum, relu, training, Sp);
   else
-    hipLaunchKernelGGL(bn_fwd_apply_kernel<false>, grid, dim3(256), 0, s, x, res, y, gamma, beta, rmean, rvar, nbt,
-                       save_mean, save_invstd, ap, N, C, HW, S, eps, momentum, relu, training, Sp);
+    hipLaunchKernelGGL(bn_fwd_apply_kernel<false>, agrid, dim3(256), 0, s, x, res, y, gamma, beta, rmean, rvar, nbt,
+                       save_mean, save_invstd, ap, N, C, HW, Sa, eps, momentum, relu, training, Sp);
 }
 
 // training-mode stem tail (bn_relu_maxpool_kernel); xstats as in launch_bn_fwd (nullable)
@@ -1187,8 +1205,9 @@ void launch_bn_relu_maxpool(const float* x, float* y, uint8_t* idx, const float*
     if (vec) hipLaunchKernelGGL(bn_fwd_stats_kernel<true>, grid, dim3(256), 0, s, x, part, N, C, HW, S, nullptr, 0);
     else hipLaunchKernelGGL(bn_fwd_stats_kernel<false>, grid, dim3(256), 0, s, x, part, N, C, HW, S, nullptr, 0);
   }
-  hipLaunchKernelGGL(bn_relu_maxpool_kernel, grid, dim3(256), 0, s, x, y, idx, gamma, beta, rmean, rvar, nbt, save_mean,
-                     save_invstd, xstats != nullptr ? xstats : part, N, C, H, W, S, eps, momentum,
+  const int Sa = xstats != nullptr ? ext_apply_slices(S) : S;
+  hipLaunchKernelGGL(bn_relu_maxpool_kernel, dim3(Sa, C), dim3(256), 0, s, x, y, idx, gamma, beta, rmean, rvar, nbt,
+                     save_mean, save_invstd, xstats != nullptr ? xstats : part, N, C, H, W, Sa, eps, momentum,
                      xstats != nullptr ? xS : 0);
 }
 
@@ -1247,8 +1266,10 @@ void launch_bn_bwd(const float* dy, const float* y, const float* x, const float*
       hipLaunchKernelGGL(bn_bwd_stats_kernel<true>, grid, dim3(256), 0, s, dy, y, x, save_mean, save_invstd, part, N,
                          C, HW, S, relu, dypart, nslab, dyadd, gamma, mbeta);
     const bool ext_st = dstats != nullptr && dypart == nullptr;
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, grid, dim3(256), 0, s, dy, y, x, gamma, save_mean, save_invstd, dx,
-                       dres, dgamma, dbeta, ext_st ? dstats : part, N, C, HW, S, relu, mbeta, ext_st ? dS : 0);
+    const int Sa = ext_st ? ext_apply_slices(S) : S;
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(Sa, C), dim3(256), 0, s, dy, y, x, gamma, save_mean,
+                       save_invstd, dx, dres, dgamma, dbeta, ext_st ? dstats : part, N, C, HW, Sa, relu, mbeta,
+                       ext_st ? dS : 0);
   } else {
     hipLaunchKernelGGL(bn_bwd_stats_kernel<false>, grid, dim3(256), 0, s, dy, y, x, save_mean, save_invstd, part, N,
                        C, HW, S, relu);
