@@ -100,7 +100,10 @@ __global__ __launch_bounds__(256) void toeplitz_expand_many_kernel(ExpandBatch b
 // rows' (row, ci) pairs: a one-row workgroup left half its threads idle at C = 128 and spent
 // its time on the layer scan and index setup for 2-8 KB of stores (21.6 µs per ResNet-18
 // forward for ~35 MB, 1.6 TB/s; profiles/r4).  Consecutive threads write consecutive H*W-float
-// segments of a row: coalesced.
+// segments of a row: coalesced.  What remains (~19 µs at batch 64): PMC shows 42 MB READ for
+// 37 MB written — layer4's 1x1-map layers use only the centre tap, but every cache line of
+// their [co][ci][3][3] weights is fetched to extract it; issuing 2-4 pairs' loads per thread
+// before their stores changed nothing (measured).
 constexpr int kExpandRows = 8;
 template <int H, int W>
 __device__ __forceinline__ void expand_rows(const float* __restrict__ w, float* __restrict__ wt, const ConvGeom& g,
