@@ -466,6 +466,28 @@ void maxpool_bwd(torch::Tensor dy, torch::Tensor idx, torch::Tensor dx, int64_t 
   check_launch("launch_maxpool_bwd");
 }
 
+// MaxPool(3, 2, 1) backward of the fused stem tail + its BN's backward statistics ([C][N][2])
+void maxpool_bwd_bnstats(torch::Tensor dy, torch::Tensor idx, torch::Tensor dx, torch::Tensor x,
+                         c10::optional<torch::Tensor> gamma, c10::optional<torch::Tensor> beta, torch::Tensor mean,
+                         torch::Tensor invstd, torch::Tensor stats) {
+  check_f32(dy, "dy"); check_f32(dx, "dx"); check_f32(x, "x"); check_dev(idx, "idx");
+  check_f32(mean, "mean"); check_f32(invstd, "invstd"); check_dev(stats, "stats");
+  TORCH_CHECK(idx.scalar_type() == torch::kUInt8 && idx.sizes() == dy.sizes() && idx.is_contiguous(),
+              "maxpool: idx must be contiguous uint8 shaped like dy");
+  TORCH_CHECK(x.sizes() == dx.sizes() && x.is_contiguous() && dx.dim() == 4, "maxpool_bwd_bnstats: x shaped like dx");
+  const ndp::PoolGeom g = pool_geom(dx, dy, 3, 2, 1);
+  TORCH_CHECK(ndp::maxpool_bwd_bnstats_ok(g), "maxpool_bwd_bnstats: needs the 16x16 -> 8x8 stem window");
+  const int N = (int)dx.size(0), C = (int)dx.size(1);
+  TORCH_CHECK(stats.scalar_type() == torch::kFloat64 && stats.is_contiguous() && stats.numel() >= (int64_t)C * N * 2,
+              "maxpool_bwd_bnstats: stats must hold C * N * 2 doubles");
+  TORCH_CHECK(mean.numel() >= C && invstd.numel() >= C, "maxpool_bwd_bnstats: statistics size");
+  const ndp::PoolBnStats bs{x.data_ptr<float>(), opt_f32(gamma, "gamma"), opt_f32(beta, "beta"),
+                            mean.data_ptr<float>(), invstd.data_ptr<float>(), stats.data_ptr<double>(), C, N};
+  ndp::launch_maxpool_bwd(dy.data_ptr<float>(), idx.data_ptr<uint8_t>(), dx.data_ptr<float>(), N * C, g, cur_stream(),
+                          bs);
+  check_launch("launch_maxpool_bwd");
+}
+
 int bn_slices(int N, int C, int HW) { return ndp::bn_slices(N, C, HW); }
 int64_t bn_part_numel(int N, int C, int HW) { return ndp::bn_part_numel(N, C, HW); }
 
@@ -1421,6 +1443,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_part_numel", &bn_part_numel);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("maxpool_bwd_bnstats", &maxpool_bwd_bnstats, py::arg("dy"), py::arg("idx"), py::arg("dx"), py::arg("x"),
+        py::arg("gamma"), py::arg("beta"), py::arg("mean"), py::arg("invstd"), py::arg("stats"));
   m.def("checksum", &checksum);
   m.def("flag_signal", &flag_signal);
   m.def("flag_wait", &flag_wait, py::arg("flags"), py::arg("i"), py::arg("seen"), py::arg("err"),

@@ -441,6 +441,20 @@ struct PoolGeom {
 };
 // idx: uint8 window offset (kh*KW + kw) of each output's maximum
 void launch_maxpool_fwd(const float* x, float* y, uint8_t* idx, int planes, const PoolGeom& g, hipStream_t s);
+// BatchNorm backward statistics from the pool backward (stats != nullptr; ResNet stem tail, the
+// BN output never stored): per plane (n, c) the sums of dz = dx * mask(x) and dz * xhat into
+// stats[(c * N + n) * 2], the mask recomputed from x as bn_relu_maxpool computed its output
+struct PoolBnStats {
+  const float* x;
+  const float* gamma;
+  const float* beta;
+  const float* mean;
+  const float* invstd;
+  double* stats;
+  int C, N;
+};
+bool maxpool_bwd_bnstats_ok(const PoolGeom& g);
 void launch_maxpool_bwd(const float* dy, const uint8_t* idx, float* dx, int planes, const PoolGeom& g,
-                        hipStream_t s);
+                        hipStream_t s,
+                        const PoolBnStats& bs = PoolBnStats{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0});
 }  // namespace ndp

@@ -183,7 +183,8 @@ __global__ __launch_bounds__(kPoolThreads) void maxpool_fwd_s2_kernel(const floa
 
 __global__ __launch_bounds__(kPoolThreads) void maxpool_bwd_s2_kernel(const float* __restrict__ dy,
                                                                       const uint8_t* __restrict__ idx,
-                                                                      float* __restrict__ dx, PoolArgs a) {
+                                                                      float* __restrict__ dx, PoolArgs a,
+                                                                      PoolBnStats bs) {
   const uint32_t e = blockIdx.x * kPoolThreads + threadIdx.x;  // output position
   if (e >= a.total) return;
   const int OH = a.g.OH, OW = a.g.OW, W = a.g.W;
@@ -212,6 +213,36 @@ __global__ __launch_bounds__(kPoolThreads) void maxpool_bwd_s2_kernel(const floa
   float* dxp = dx + (size_t)plane * a.in_plane.d + (size_t)(2 * i) * W + 2 * j;
   *reinterpret_cast<float2*>(dxp) = make_float2(d00, d01);
   *reinterpret_cast<float2*>(dxp + W) = make_float2(d10, d11);
+  if (bs.stats != nullptr) {
+    // the BN backward's statistics of this plane (64 outputs = this wave, launcher-checked):
+    // dz = d * mask with the ReLU mask recomputed from the BN input x exactly as the fused
+    // forward computed its output (bn_relu_maxpool), xhat = (x - mean) * invstd
+    const int ch = (int)(plane % (uint32_t)bs.C), n = (int)(plane / (uint32_t)bs.C);
+    const float mean = bs.mean[ch], invstd = bs.invstd[ch];
+    const float gam = bs.gamma ? bs.gamma[ch] : 1.f, bet = bs.beta ? bs.beta[ch] : 0.f;
+    const float sc = __fmul_rn(gam, invstd), sh = __fsub_rn(bet, __fmul_rn(mean, sc));
+    const float* xp = bs.x + (size_t)plane * a.in_plane.d + (size_t)(2 * i) * W + 2 * j;
+    const float2 x0 = *reinterpret_cast<const float2*>(xp), x1 = *reinterpret_cast<const float2*>(xp + W);
+    const float xs[4] = {x0.x, x0.y, x1.x, x1.y}, ds[4] = {d00, d01, d10, d11};
+    float sa = 0.f, sb = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float dz = fmaf(xs[k], sc, sh) > 0.f ? ds[k] : 0.f;
+      sa += dz;
+      sb += dz * ((xs[k] - mean) * invstd);
+    }
+    double da = (double)sa, db = (double)sb;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      da += __shfl_xor(da, off, 64);
+      db += __shfl_xor(db, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      double* st = bs.stats + ((int64_t)ch * bs.N + n) * 2;
+      st[0] = da;
+      st[1] = db;
+    }
+  }
 }
 
 PoolArgs pool_args(const PoolGeom& g, int64_t total) {
@@ -252,15 +283,17 @@ void launch_maxpool_fwd(const float* x, float* y, uint8_t* idx, int planes, cons
     hipLaunchKernelGGL((maxpool_fwd_kernel<0, 0, 0>), grid, dim3(kPoolThreads), 0, s, x, y, idx, a);
 }
 
+bool maxpool_bwd_bnstats_ok(const PoolGeom& g) { return s2_fast(g) && g.OH * g.OW == 64; }
+
 void launch_maxpool_bwd(const float* dy, const uint8_t* idx, float* dx, int planes, const PoolGeom& g,
-                        hipStream_t s) {
+                        hipStream_t s, const PoolBnStats& bs) {
   const int64_t total = (int64_t)planes * g.H * g.W;
   if (total <= 0) return;
   if (s2_fast(g)) {
     const int64_t outs = (int64_t)planes * g.OH * g.OW;
     const PoolArgs a = pool_args(g, outs);
     hipLaunchKernelGGL(maxpool_bwd_s2_kernel, dim3((unsigned)((outs + kPoolThreads - 1) / kPoolThreads)),
-                       dim3(kPoolThreads), 0, s, dy, idx, dx, a);
+                       dim3(kPoolThreads), 0, s, dy, idx, dx, a, bs);
     return;
   }
   const PoolArgs a = pool_args(g, total);

@@ -105,12 +105,19 @@ class _BNReluPoolFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, weight, bias, save_mean, save_invstd, part, idx = ctx.saved_tensors
         dz = torch.empty_like(x)  # gradient of the (unstored) BN output = the pool's input
-        ext().maxpool_bwd(dy.contiguous(), idx, dz, 3, 2, 1)
         dx = torch.empty_like(x)
         dgamma = grad_buffer(ctx.params[0], weight)
         dbeta = grad_buffer(ctx.params[1], weight)
-        ext().bn_bwd(dz, None, x, weight, save_mean, save_invstd, dx, None, dgamma, dbeta, part, True, ctx.single,
-                     None, 0, None, bias)
+        N, C, H, W = x.shape
+        if _BWD_STATS and H == 16 and W == 16:  # the pool backward also emits the BN's statistics
+            stats = torch.empty(C * N * 2, device=x.device, dtype=torch.float64)
+            ext().maxpool_bwd_bnstats(dy.contiguous(), idx, dz, x, weight, bias, save_mean, save_invstd, stats)
+            ext().bn_bwd(dz, None, x, weight, save_mean, save_invstd, dx, None, dgamma, dbeta, part, True, ctx.single,
+                         None, 0, None, bias, stats, N)
+        else:
+            ext().maxpool_bwd(dy.contiguous(), idx, dz, 3, 2, 1)
+            ext().bn_bwd(dz, None, x, weight, save_mean, save_invstd, dx, None, dgamma, dbeta, part, True, ctx.single,
+                         None, 0, None, bias)
         return dx, dgamma, dbeta, None, None, None, None, None, None, None, None
 
 
