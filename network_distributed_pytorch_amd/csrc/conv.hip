@@ -1239,8 +1239,17 @@ int conv_ksplit(int cls, const ConvGeom& g, int B, bool dgrad) {
     const char* e = getenv("NDP_CONV_MAXKS");
     maxks = e ? atoi(e) : 4;
   }
+  // the 1x1 stride-2 grad-x (class 4): its split-K sum is a separate even-pixel scatter launch
+  // (conv_slab_sum_ups); NDP_DS_DGRAD_MAXKS caps its split (A/B: 1x MI355X, ResNet-18 r=4, cap 1
+  // at batch 512 1.869 / 1.864 -> 1.865 / 1.863 ms (noise), at batch 64 0.960 -> 0.967: no cap)
+  static int ds_maxks = -1;
+  if (ds_maxks < 0) {
+    const char* e = getenv("NDP_DS_DGRAD_MAXKS");
+    ds_maxks = e ? atoi(e) : 0;
+  }
+  const int cap = (dgrad && cls == 4 && ds_maxks > 0) ? ds_maxks : maxks;
   int ks = 1;
-  while (ks * 2 <= nchunks && base * ks < kFillWgs && ks * 2 <= maxks) ks *= 2;
+  while (ks * 2 <= nchunks && base * ks < kFillWgs && ks * 2 <= cap) ks *= 2;
   return pow2_floor(ks);
 }
 // BatchNorm statistics from the forward epilogue: the layer1 3x3 and stem 7x7 classes (their
