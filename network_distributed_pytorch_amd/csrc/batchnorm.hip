@@ -646,8 +646,8 @@ __global__ __launch_bounds__(256) void bn_small_apply_kernel(
 // value): fp64 per thread -> xor butterfly over the HW lanes of a channel and the row
 // groups inside the wave (commutative pairings: identical on every lane) -> fixed-order
 // fold of the 8 per-wave partials through LDS.  CW trades grid size (C*HW / CW workgroups;
-// 256 CUs to fill) against row-segment width per load (CW * 4 bytes): NDP_BN_COLW picks
-// it (tuning only), default by measurement.  Used when N <= 512 (ResNet's per-GPU batch).
+// 256 CUs to fill) against row-segment width per load (CW * 4 bytes): bn_colw_for picks
+// it by measurement.  Used when N <= 512 (ResNet's per-GPU batch).
 constexpr int kFusedThreads = 512;
 constexpr int kFusedMaxN = 512;
 
@@ -666,54 +666,25 @@ __device__ __forceinline__ int xcd_block(int bid, int nblk) {
   return xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
 }
 
-// RS > 1 (row splits): the RS workgroups of a column block (consecutive logical blocks, so the
-// same XCD) each take 1 / RS of the images and exchange their per-column sums through global
-// memory behind a counter barrier — the cdna_hip_programming.md §6 Guideline 16 protocol
-// csrc/orth.hip uses (plain stores, vmcnt drain, release fence, relaxed agent counter; poller:
-// relaxed loads, one acquire fence).  Counters live in the module's zero-initialised scratch
-// (BnSync) and are never reset: every launch adds exactly kBnSyncPeriod to the counter of each
-// column block it runs (each workgroup kBnSyncPeriod / RS), so a launch starts on a multiple of
-// the period.  Grids are <= 256 workgroups of one CU each: always co-resident.  A spin past
-// kBnMaxSpins poisons the block's statistics with NaN and sets the error word instead of
-// hanging.  Every workgroup of a block then adds the RS partials in split order: the same
-// value everywhere (deterministic), so RS = 2 / 4 lets 256 workgroups work where the column
-// blocks alone give 64-128 (ResNet layer2-4 maps).  Opt-in (NDP_BN_ROWSPLIT, bn_row_splits).
-constexpr int kBnSyncPeriod = 4;       // = the largest RS
-constexpr int kBnSyncBlocks = 4096;    // column blocks with a counter
-constexpr unsigned kBnMaxSpins = 1u << 22;
-struct BnSync {
-  unsigned long long* ctr;  // [kBnSyncBlocks]
-  unsigned* err;            // [1]
-  double* xch;              // [blocks][RS][CW][2]
-};
-
-template <int HW, int BWD, int CW, int MAXN = kFusedMaxN, int RS = 1>
+template <int HW, int BWD, int CW, int MAXN = kFusedMaxN>
 __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
     const float* __restrict__ x, const float* __restrict__ res, const float* __restrict__ dy,
     const float* __restrict__ yin, const float* __restrict__ gamma, const float* __restrict__ beta,
     float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt, float* __restrict__ save_mean,
     float* __restrict__ save_invstd, float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ out,
     float* __restrict__ dres, int N, int C, float eps, float momentum, int relu, const float* __restrict__ src,
-    int nslab, BnSync sy) {
+    int nslab) {
   constexpr int RG = kFusedThreads / CW;
-  constexpr int NP = MAXN / RG / RS;  // rows per thread in this workgroup's split
+  constexpr int NP = MAXN / RG;  // rows per thread
   constexpr int NW = kFusedThreads / 64;
   static_assert(CW % HW == 0 && 64 % CW == 0, "bad column block");
-  static_assert(NP >= 1 && kBnSyncPeriod % RS == 0, "bad row split");
+  static_assert(NP >= 1, "bad row count");
   __shared__ double red[2][NW][CW];
-  __shared__ unsigned long long base_s;
-  __shared__ int bad_s;
   const int CHW = C * HW;
   const int col = threadIdx.x % CW, g = threadIdx.x / CW;
-  const int lb = xcd_block((int)blockIdx.x, (int)gridDim.x);
-  const int cb = lb / RS, rs = lb - cb * RS;
+  const int cb = xcd_block((int)blockIdx.x, (int)gridDim.x);
   const int j = cb * CW + col;
   const bool ok_col = j < CHW;
-  if (RS > 1 && threadIdx.x == 0) {  // this launch's barrier cannot complete before we arrive
-    const unsigned long long c0 = __hip_atomic_load(sy.ctr + cb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    base_s = c0 - c0 % kBnSyncPeriod;
-    bad_s = 0;
-  }
   const int c = ok_col ? j / HW : 0;
   float v[NP], d[NP], m[NP];
   // every per-channel operand is loaded up front, alongside the tensor stream: read after the
@@ -726,14 +697,14 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
     }
     if (gamma) gam = gamma[c];
     if (!BWD && beta) bet = beta[c];
-    if (!BWD && rmean != nullptr && g == 0 && (j % HW) == 0 && rs == 0) {
+    if (!BWD && rmean != nullptr && g == 0 && (j % HW) == 0) {
       rm = rmean[c];
       rv = rvar[c];
     }
   }
 #pragma unroll
   for (int k = 0; k < NP; ++k) {  // every load in flight before any use
-    const int n = g + (rs * NP + k) * RG;
+    const int n = g + k * RG;
     const bool ok = ok_col && n < N;
     const int64_t o = (int64_t)n * CHW + j;
     float sum = 0.f;
@@ -755,14 +726,14 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
   if (!BWD && src != nullptr) {  // BN's saved input = the conv output
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
-      const int n = g + (rs * NP + k) * RG;
+      const int n = g + k * RG;
       if (ok_col && n < N) const_cast<float*>(x)[(int64_t)n * CHW + j] = v[k];
     }
   }
   double a = 0.0, b = 0.0;
 #pragma unroll
   for (int k = 0; k < NP; ++k) {
-    if (ok_col && g + (rs * NP + k) * RG < N) {
+    if (ok_col && g + k * RG < N) {
       if (!BWD) {
         a += (double)v[k];
         b += (double)v[k] * (double)v[k];
@@ -795,45 +766,9 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
     A += red[0][k][col];
     B += red[1][k][col];
   }
-  if constexpr (RS > 1) {  // the RS splits' partials, added in split order (module header)
-    double* xb = sy.xch + (int64_t)cb * RS * CW * 2;
-    if (g == 0) {
-      xb[(rs * CW + col) * 2] = A;
-      xb[(rs * CW + col) * 2 + 1] = B;
-    }
-    if (threadIdx.x < 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_fetch_add(sy.ctr + cb, (unsigned long long)(kBnSyncPeriod / RS), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned long long target = base_s + kBnSyncPeriod;
-      unsigned spins = 0;
-      while ((long long)(__hip_atomic_load(sy.ctr + cb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > kBnMaxSpins) {  // report and poison instead of hanging
-          __hip_atomic_fetch_or(sy.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          bad_s = 1;
-          break;
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    A = 0.0;
-    B = 0.0;
-#pragma unroll
-    for (int r = 0; r < RS; ++r) {
-      A += xb[(r * CW + col) * 2];
-      B += xb[(r * CW + col) * 2 + 1];
-    }
-    if (bad_s) A = B = __builtin_nan("");
-  }
   if (!ok_col) return;
   const double M = (double)N * HW;
-  const bool writer = g == 0 && (j % HW) == 0 && rs == 0;
+  const bool writer = g == 0 && (j % HW) == 0;
   if (!BWD) {
     const double mu = A / M;
     double var = B / M - mu * mu;
@@ -853,7 +788,7 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
     }
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
-      const int n = g + (rs * NP + k) * RG;
+      const int n = g + k * RG;
       if (n < N) {
         const float z = fmaf(v[k], scale, shift) + d[k];
         out[(int64_t)n * CHW + j] = relu ? fmaxf(z, 0.f) : z;
@@ -868,7 +803,7 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
     const float mdz = (float)(A / M), mdzx = (float)(B / M);
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
-      const int n = g + (rs * NP + k) * RG;
+      const int n = g + k * RG;
       if (n < N) {
         const float dz = (m[k] > 0.f) ? d[k] : 0.f;
         const float xh = (v[k] - mean_s) * invstd_s;
@@ -880,58 +815,22 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
   }
 }
 
-// largest HW routed to the single-launch path (NDP_BN_SINGLE_MAX: 4 / 8 / 16, tuning only)
-static int bn_single_max() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("NDP_BN_SINGLE_MAX");
-    v = e ? atoi(e) : 16;  // ResNet-18 step: 4 -> 2.165 ms, 16 (layer2 too) -> 2.150 ms (1x MI355X)
-  }
-  return v;
-}
-
-// 8x8 maps (ResNet layer1) at per-GPU batch <= kFused64MaxN: one launch per direction, one
-// workgroup per channel.  OFF by default (NDP_BN_SINGLE64=1 to A/B): measured on 1x MI355X
-// (ResNet-18 step, graph) 1.0797 vs 1.0772 ms at batch 64 and 1.2322 vs 1.2122 at 128 — 64
-// workgroups cannot stream the 8x8 maps (or the split-K slabs they would sum) fast enough.
-constexpr int kFused64MaxN = 128;
-static bool bn_single64() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("NDP_BN_SINGLE64");
-    v = e ? atoi(e) : 0;
-  }
-  return v != 0;
-}
-
+// Single-launch small-map path: HW in {1, 2, 4, 8, 16} (ResNet-18 step on 1x MI355X: HW <= 4 ->
+// 2.165 ms, <= 16 (layer2 too) -> 2.150 ms), N <= kFusedMaxN.  The 8x8 maps of layer1 (64
+// workgroups, one per channel) measured slower than the two-kernel path at batch 64 / 128
+// (1.0797 vs 1.0772 / 1.2322 vs 1.2122 ms) and so did row splits over a cross-workgroup barrier
+// (batch 512 1.908 -> 1.960 / 1.966 ms; round 4, removed in round 5).
 static bool bn_fused_ok(int N, int C, int HW) {
-  if (HW == 64) return bn_single64() && N >= 1 && N <= kFused64MaxN;
-  return (HW == 1 || HW == 2 || HW == 4 || HW == 8 || HW == 16) && HW <= bn_single_max() && N >= 1 &&
-         N <= kFusedMaxN && (int64_t)N * C * HW < (1LL << 30);
+  return (HW == 1 || HW == 2 || HW == 4 || HW == 8 || HW == 16) && N >= 1 && N <= kFusedMaxN &&
+         (int64_t)N * C * HW < (1LL << 30);
 }
 
-// column-block width of the single-launch path (NDP_BN_COLW: 4 / 8 / 16, tuning only)
-static int bn_colw() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("NDP_BN_COLW");
-    // 0 (default): per launch shape, bn_colw_for; 4 / 8 / 16: fixed (round 2 measured 8 best
-    // as a single global value: ResNet-18 step 4 -> 2.221 ms, 8 -> 2.182, 16 -> 2.202)
-    v = e ? atoi(e) : 0;
-    if (v != 0 && v != 4 && v != 8 && v != 16) v = 0;
-  }
-  return v;
-}
-
-// column-block width for one launch: the fixed NDP_BN_COLW, or (0) the widest block that still
-// gives >= 256 workgroups (one per CU), else the narrowest allowed one — 4 columns (16-B row
-// segments) only at per-GPU batch <= 128, where grid size matters more than segment width.
-// Measured (1x MI355X, profiles/r3/bn_colw.md) against the fixed 8: ResNet-18 r=4 batch 512
-// 1.945 -> 1.943 ms, batch 64 1.012 -> 1.000 ms, ResNet-152 r=4 15.19 -> 14.78 ms, ResNet-50
-// dense 6.246 -> 6.178 ms.
+// column-block width for one launch: the widest block that still gives >= 256 workgroups (one per
+// CU), else the narrowest allowed one — 4 columns (16-B row segments) only at per-GPU batch <= 128,
+// where grid size matters more than segment width.  Measured (1x MI355X, profiles/r3/bn_colw.md)
+// against a fixed 8: ResNet-18 r=4 batch 512 1.945 -> 1.943 ms, batch 64 1.012 -> 1.000 ms,
+// ResNet-152 r=4 15.19 -> 14.78 ms, ResNet-50 dense 6.246 -> 6.178 ms.
 static int bn_colw_for(int HW, int C, int N) {
-  const int mode = bn_colw();
-  if (mode != 0) return mode > HW ? mode : HW;
   const int lo = N <= 128 ? 4 : 8;
   const int64_t cols = (int64_t)C * HW;
   for (int cw = 16; cw >= lo; cw >>= 1)
@@ -939,36 +838,18 @@ static int bn_colw_for(int HW, int C, int N) {
   return HW > lo ? HW : lo;
 }
 
-// row splits of the single-launch kernel: the smallest RS (1 / 2 / 4) that gives the launch
-// >= 256 workgroups, only while every thread keeps >= 2 rows
-static int bn_row_splits(int nblk, int N, int CW) {
-  // NDP_BN_ROWSPLIT: largest RS (1 / 2 / 4).  Default 1: measured slower on 1x MI355X (ResNet-18
-  // r=4 batch 512: RS <= 1 1.908 ms, <= 2 1.960, <= 4 1.966; profiles/r4/bench_bn_rowsplit.jsonl)
-  // — the barrier round trip costs more than the extra CUs bring at these 1-4 MB tensors.
-  static int cap = -1;
-  if (cap < 0) {
-    const char* e = getenv("NDP_BN_ROWSPLIT");
-    cap = e ? atoi(e) : 1;
-    if (cap < 1) cap = 1;
-  }
-  const int rg = kFusedThreads / CW;
-  int rs = 1;
-  while (rs < kBnSyncPeriod && rs < cap && nblk * rs < 256 && N >= 2 * rg * rs * 2 && nblk <= kBnSyncBlocks) rs *= 2;
-  return rs;
-}
-
-template <int BWD, int CW, int RS>
-static void launch_small_fused_rs(int HW, const float* x, const float* res, const float* dy, const float* yin,
+template <int BWD, int CW>
+static void launch_small_fused_cw(int HW, const float* x, const float* res, const float* dy, const float* yin,
                                   const float* gamma, const float* beta, float* rmean, float* rvar, int64_t* nbt,
                                   float* sm, float* si, float* dgamma, float* dbeta, float* out, float* dres, int N,
                                   int C, float eps, float momentum, int relu, hipStream_t s, const float* src,
-                                  int nslab, const BnSync& sy, int nblk) {
-  const dim3 grid((unsigned)(nblk * RS));
-#define NDP_BN_FUSED(HWV)                                                                                            \
-  if constexpr (CW % HWV == 0)                                                                                       \
-    hipLaunchKernelGGL((bn_small_fused_kernel<HWV, BWD, CW, kFusedMaxN, RS>), grid, dim3(kFusedThreads), 0, s, x,    \
-                       res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out, dres, N, C, eps,     \
-                       momentum, relu, src, nslab, sy)
+                                  int nslab) {
+  const int nblk = (int)(((int64_t)C * HW + CW - 1) / CW);
+#define NDP_BN_FUSED(HWV)                                                                                          \
+  if constexpr (CW % HWV == 0)                                                                                     \
+    hipLaunchKernelGGL((bn_small_fused_kernel<HWV, BWD, CW, kFusedMaxN>), dim3((unsigned)nblk), dim3(kFusedThreads), \
+                       0, s, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out, dres, N, C, \
+                       eps, momentum, relu, src, nslab)
   switch (HW) {  // the caller picks CW >= HW
     case 1: NDP_BN_FUSED(1); break;
     case 2: NDP_BN_FUSED(2); break;
@@ -979,62 +860,24 @@ static void launch_small_fused_rs(int HW, const float* x, const float* res, cons
 #undef NDP_BN_FUSED
 }
 
-template <int BWD, int CW>
-static void launch_small_fused_cw(int HW, const float* x, const float* res, const float* dy, const float* yin,
-                                  const float* gamma, const float* beta, float* rmean, float* rvar, int64_t* nbt,
-                                  float* sm, float* si, float* dgamma, float* dbeta, float* out, float* dres, int N,
-                                  int C, float eps, float momentum, int relu, hipStream_t s, const float* src,
-                                  int nslab, const BnSync& sy) {
-  const int nblk = (int)(((int64_t)C * HW + CW - 1) / CW);
-  switch (sy.ctr != nullptr ? bn_row_splits(nblk, N, CW) : 1) {
-    case 4:
-      launch_small_fused_rs<BWD, CW, 4>(HW, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta,
-                                        out, dres, N, C, eps, momentum, relu, s, src, nslab, sy, nblk);
-      break;
-    case 2:
-      launch_small_fused_rs<BWD, CW, 2>(HW, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta,
-                                        out, dres, N, C, eps, momentum, relu, s, src, nslab, sy, nblk);
-      break;
-    default:
-      launch_small_fused_rs<BWD, CW, 1>(HW, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta,
-                                        out, dres, N, C, eps, momentum, relu, s, src, nslab, sy, nblk);
-  }
-}
-
 template <int BWD>
 static void launch_small_fused(int HW, const float* x, const float* res, const float* dy, const float* yin,
                                const float* gamma, const float* beta, float* rmean, float* rvar, int64_t* nbt,
                                float* sm, float* si, float* dgamma, float* dbeta, float* out, float* dres, int N,
                                int C, float eps, float momentum, int relu, hipStream_t s, const float* src,
-                               int nslab, const BnSync& sy) {
-  if (HW == 64) {  // one workgroup per channel (x RS row splits): 64 lanes x 8 row groups, <= 128 images
-    const int rs = sy.ctr != nullptr ? bn_row_splits(C, N, 64) : 1;
-    if (rs == 4)
-      hipLaunchKernelGGL((bn_small_fused_kernel<64, BWD, 64, kFused64MaxN, 4>), dim3((unsigned)(4 * C)),
-                         dim3(kFusedThreads), 0, s, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma,
-                         dbeta, out, dres, N, C, eps, momentum, relu, src, nslab, sy);
-    else if (rs == 2)
-      hipLaunchKernelGGL((bn_small_fused_kernel<64, BWD, 64, kFused64MaxN, 2>), dim3((unsigned)(2 * C)),
-                         dim3(kFusedThreads), 0, s, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma,
-                         dbeta, out, dres, N, C, eps, momentum, relu, src, nslab, sy);
-    else
-      hipLaunchKernelGGL((bn_small_fused_kernel<64, BWD, 64, kFused64MaxN>), dim3((unsigned)C), dim3(kFusedThreads),
-                         0, s, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out, dres, N, C,
-                         eps, momentum, relu, src, nslab, sy);
-    return;
-  }
+                               int nslab) {
   switch (bn_colw_for(HW, C, N)) {
     case 16:
       launch_small_fused_cw<BWD, 16>(HW, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out,
-                                     dres, N, C, eps, momentum, relu, s, src, nslab, sy);
+                                     dres, N, C, eps, momentum, relu, s, src, nslab);
       break;
     case 4:
       launch_small_fused_cw<BWD, 4>(HW, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out,
-                                    dres, N, C, eps, momentum, relu, s, src, nslab, sy);
+                                    dres, N, C, eps, momentum, relu, s, src, nslab);
       break;
     default:
       launch_small_fused_cw<BWD, 8>(HW, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out,
-                                    dres, N, C, eps, momentum, relu, s, src, nslab, sy);
+                                    dres, N, C, eps, momentum, relu, s, src, nslab);
   }
 }
 
@@ -1057,39 +900,18 @@ static void small_stats_any(int HW, const float* x, const float* dy, const float
   }
 }
 
-// largest HW routed to the small-map kernels (NDP_BN_SMALL_MAX, tuning only; default 4)
-static int bn_small_max() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("NDP_BN_SMALL_MAX");
-    v = e ? atoi(e) : 4;  // HW = 16 measured faster on the per-channel kernels
-  }
-  return v;
-}
-
+// the three-kernel small-map path (statistics, finalize, apply) for HW <= 4 where the
+// single-launch kernel does not apply (batch > 512); HW = 16 measured faster on the
+// per-channel kernels
 bool bn_small_path(int N, int C, int HW) {
-  return (HW == 1 || HW == 2 || HW == 4 || HW == 8 || HW == 16) && HW <= bn_small_max() &&
-         (int64_t)N * C * HW < (1LL << 30);
+  return (HW == 1 || HW == 2 || HW == 4) && (int64_t)N * C * HW < (1LL << 30);
 }
 
-// scratch layout (fp64 slots, zero-initialised once by the module): [kBnSyncBlocks counters |
-// error word | padding to 16 slots] then the per-launch region (slice partials, coefficients,
-// or the row-split exchange of the single-launch kernel: <= 8 doubles per column)
-constexpr int64_t kBnSyncSlots = kBnSyncBlocks + 16;
-
-static BnSync bn_sync(double* part, int single_ok) {
-  if (!single_ok) return BnSync{nullptr, nullptr, nullptr};
-  return BnSync{reinterpret_cast<unsigned long long*>(part), reinterpret_cast<unsigned*>(part + kBnSyncBlocks),
-                part + kBnSyncSlots};
-}
-
+// scratch: the per-launch slice partials and coefficients (fp64)
 int64_t bn_part_numel(int N, int C, int HW) {
   const int64_t big = (int64_t)C * bn_slices(N, C, HW) * 2;
   const int64_t small = (int64_t)C * bn_small_slices(N, C, HW) * 2 + 3 * (int64_t)C;
-  const int64_t xch = 8 * (int64_t)C * HW;
-  int64_t m = big > small ? big : small;
-  if (xch > m) m = xch;
-  return kBnSyncSlots + m;
+  return big > small ? big : small;
 }
 
 // ----------------------------------- launchers -------------------------------------------
@@ -1099,16 +921,8 @@ int64_t bn_part_numel(int N, int C, int HW) {
 // BN's 128 workgroups read 8 slabs slower than the 256-CU sum kernel plus a launch).
 constexpr int kMaxFusedSlabs = 4;
 // Two-kernel path (8x8 maps of layer1): the statistics pass adds the deferred slabs and writes
-// the summed tensor, no separate sum launch (NDP_BN_STATS_SLABS=0 to A/B).  ResNet-18 step on
-// 1x MI355X: batch 128 1.196 / 1.198 -> 1.164 / 1.165 ms, batch 64 1.061 / 1.058 -> 1.046 / 1.053.
-static bool bn_stats_slabs() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("NDP_BN_STATS_SLABS");
-    v = e ? atoi(e) : 1;
-  }
-  return v != 0;
-}
+// the summed tensor, no separate sum launch.  ResNet-18 step on 1x MI355X: batch 128 1.196 /
+// 1.198 -> 1.164 / 1.165 ms, batch 64 1.061 / 1.058 -> 1.046 / 1.053.
 int bn_slices(int N, int C, int HW) {
   // ~4 workgroups per CU over the whole launch, >= ~2K elements per workgroup
   int64_t s = (1024 + C - 1) / C;
@@ -1120,28 +934,15 @@ int bn_slices(int N, int C, int HW) {
 }
 
 // apply-pass slices when the statistics come from a conv epilogue: every apply workgroup folds
-// ALL the conv's per-image partials of its channel, so fewer, larger workgroups repeat that
-// fold fewer times (NDP_BN_EXT_DIV = S divisor, A/B).  Measured on 1x MI355X, ResNet-18 r=4
-// batch 512: divisor 1 / 2 / 4 / 8 = 1.862-1.874 / 1.864 / 1.884 / 1.926 ms: default 1
-// (profiles/r4/bench_bn_ext_div.jsonl)
-static int ext_apply_slices(int S) {
-  static int div = -1;
-  if (div < 0) {
-    const char* e = getenv("NDP_BN_EXT_DIV");
-    div = e ? atoi(e) : 1;
-    if (div < 1) div = 1;
-  }
-  const int a = S / div;
-  return a < 1 ? 1 : a;
-}
+// ALL the conv's per-image partials of its channel (fewer, larger workgroups measured slower:
+// ResNet-18 r=4 batch 512, S / 1 / 2 / 4 / 8 = 1.862-1.874 / 1.864 / 1.884 / 1.926 ms, round 4)
+static int ext_apply_slices(int S) { return S < 1 ? 1 : S; }
 
 void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamma, const float* beta,
                    float* rmean, float* rvar, int64_t* nbt, float* save_mean, float* save_invstd,
                    double* part, int N, int C, int HW, int S, float eps, float momentum, int relu,
                    int training, int single, hipStream_t s, const float* xpart, int nslab, const double* xstats,
                    int xS) {
-  const BnSync sy = bn_sync(part, 1);
-  part += kBnSyncSlots;
   if (!training || xpart != nullptr) xstats = nullptr;
   if (xpart != nullptr && nslab < 2) xpart = nullptr;
   if (xpart != nullptr && nslab > kMaxFusedSlabs) {  // many slabs: the wide sum kernel first
@@ -1150,12 +951,12 @@ void launch_bn_fwd(const float* x, const float* res, float* y, const float* gamm
   }
   if (training && single && bn_fused_ok(N, C, HW)) {
     launch_small_fused<0>(HW, x, res, nullptr, nullptr, gamma, beta, rmean, rvar, nbt, save_mean, save_invstd,
-                          nullptr, nullptr, y, nullptr, N, C, eps, momentum, relu, s, xpart, nslab, sy);
+                          nullptr, nullptr, y, nullptr, N, C, eps, momentum, relu, s, xpart, nslab);
     return;
   }
   const bool vec_ok = (HW % 4) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 &&
                       (res == nullptr || ((uintptr_t)res & 15) == 0) && ((uintptr_t)xpart & 15) == 0;
-  if (xpart != nullptr && !(bn_stats_slabs() && training && vec_ok && !bn_small_path(N, C, HW))) {
+  if (xpart != nullptr && !(training && vec_ok && !bn_small_path(N, C, HW))) {
     // no fused consumer for this shape: finish the conv's split-K sum here
     launch_slab_sum(xpart, const_cast<float*>(x), (int64_t)N * C * HW, nslab, s);
     xpart = nullptr;
@@ -1196,7 +997,6 @@ void launch_bn_relu_maxpool(const float* x, float* y, uint8_t* idx, const float*
                             float* rmean, float* rvar, int64_t* nbt, float* save_mean, float* save_invstd,
                             double* part, int N, int C, int H, int W, float eps, float momentum, hipStream_t s,
                             const double* xstats, int xS) {
-  part += kBnSyncSlots;
   const int HW = H * W;
   const int S = bn_slices(N, C, HW);
   const dim3 grid(S, C);
@@ -1219,8 +1019,6 @@ void launch_bn_bwd(const float* dy, const float* y, const float* x, const float*
                    const float* save_invstd, float* dx, float* dres, float* dgamma, float* dbeta, double* part,
                    int N, int C, int HW, int S, int relu, int single, hipStream_t s, const float* dypart,
                    int nslab, const float* dyadd, const float* mbeta, const double* dstats, int dS) {
-  const BnSync sy = bn_sync(part, 1);
-  part += kBnSyncSlots;
   if (dypart != nullptr && nslab < 2) dypart = nullptr;
   if (dypart == nullptr) dyadd = nullptr;
   if (dypart != nullptr && nslab > kMaxFusedSlabs) {
@@ -1231,13 +1029,13 @@ void launch_bn_bwd(const float* dy, const float* y, const float* x, const float*
   if (single && bn_fused_ok(N, C, HW)) {  // (the backward kernel's `res` slot: the slab addend)
     launch_small_fused<1>(HW, x, dyadd, dy, y, gamma, nullptr, nullptr, nullptr, nullptr,
                           const_cast<float*>(save_mean), const_cast<float*>(save_invstd), dgamma, dbeta, dx, dres, N, C,
-                          0.f, 0.f, relu, s, dypart, nslab, sy);
+                          0.f, 0.f, relu, s, dypart, nslab);
     return;
   }
   const bool vec_ok = (HW % 4) == 0 && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)x & 15) == 0 &&
                       ((uintptr_t)dx & 15) == 0 && (!relu || ((uintptr_t)y & 15) == 0) &&
                       (dres == nullptr || ((uintptr_t)dres & 15) == 0) && ((uintptr_t)dypart & 15) == 0;
-  if (dypart != nullptr && !(bn_stats_slabs() && vec_ok && !bn_small_path(N, C, HW) &&
+  if (dypart != nullptr && !(vec_ok && !bn_small_path(N, C, HW) &&
                              (dyadd == nullptr || ((uintptr_t)dyadd & 15) == 0))) {
     // no fused consumer: finish the conv's split-K grad-x sum into dy
     launch_slab_sum(dypart, const_cast<float*>(dy), (int64_t)N * C * HW, nslab, s, dyadd);

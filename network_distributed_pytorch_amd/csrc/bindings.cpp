@@ -1135,221 +1135,6 @@ void attn_bwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, c10::optional<t
 }  // namespace
 
 void register_comm(py::module& m);  // comm.cpp
-// ---- small-map convolutions (smallconv.hip) --------------------------------------------------
-// (class, fwd slabs, grad-x slabs, grad-W slabs) for batch B, or class -1
-py::tuple sm_plan(const std::vector<int64_t>& geom, int64_t B) {
-  const ndp::ConvGeom g = conv_geom(geom);
-  const int cls = ndp::sm_class(g);
-  const int64_t ny = B * g.Co * g.OH * g.OW, nx = B * g.C * g.H * g.W, nw = (int64_t)g.Co * g.C * g.KH * g.KW;
-  if (cls < 0 || B <= 0 || ny % 4 || nx % 4 || nw % 4) return py::make_tuple(-1, 1, 1, 1);
-  // 32-bit buffer offsets (raw buffer descriptors)
-  if (std::max(std::max(ny, nx), nw) * 4 >= (1LL << 31)) return py::make_tuple(-1, 1, 1, 1);
-  return py::make_tuple(cls, ndp::sm_splits(g, (int)B, 0), ndp::sm_splits(g, (int)B, 1), ndp::sm_splits(g, (int)B, 2));
-}
-
-static int sm_batch(const torch::Tensor& t, const ndp::ConvGeom& g, const char* who) {
-  TORCH_CHECK(ndp::sm_class(g) >= 0, who, ": no small-map kernel for this geometry");
-  return (int)t.size(0);
-}
-
-int64_t sm_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, const std::vector<int64_t>& geom,
-               c10::optional<torch::Tensor> part, bool defer) {
-  const ndp::ConvGeom g = conv_geom(geom);
-  const int B = sm_batch(x, g, "sm_fwd");
-  conv_check(x, "x", B, g.C, g.H, g.W);
-  conv_check(w, "w", g.Co, g.C, g.KH, g.KW);
-  conv_check(y, "y", B, g.Co, g.OH, g.OW);
-  TORCH_CHECK((reinterpret_cast<uintptr_t>(y.data_ptr()) & 15) == 0, "sm_fwd: 16-B aligned y");
-  float* pp = tg_part(part, ndp::sm_splits(g, B, 0), y.numel(), "sm_fwd");
-  const int left = ndp::launch_sm_fwd(x.data_ptr<float>(), w.data_ptr<float>(), y.data_ptr<float>(), B, g, pp,
-                                      cur_stream(), defer);
-  check_launch("launch_sm_fwd");
-  return left;
-}
-
-int64_t sm_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, const std::vector<int64_t>& geom,
-                 c10::optional<torch::Tensor> part, c10::optional<torch::Tensor> addend, bool defer) {
-  const ndp::ConvGeom g = conv_geom(geom);
-  const int B = sm_batch(dy, g, "sm_dgrad");
-  conv_check(dy, "dy", B, g.Co, g.OH, g.OW);
-  conv_check(w, "w", g.Co, g.C, g.KH, g.KW);
-  conv_check(dx, "dx", B, g.C, g.H, g.W);
-  TORCH_CHECK((reinterpret_cast<uintptr_t>(dx.data_ptr()) & 15) == 0, "sm_dgrad: 16-B aligned dx");
-  float* pp = tg_part(part, ndp::sm_splits(g, B, 1), dx.numel(), "sm_dgrad");
-  const float* ap = nullptr;
-  if (addend.has_value()) {
-    conv_check(*addend, "addend", B, g.C, g.H, g.W);
-    TORCH_CHECK((reinterpret_cast<uintptr_t>(addend->data_ptr()) & 15) == 0, "sm_dgrad: 16-B aligned addend");
-    ap = addend->data_ptr<float>();
-  }
-  const int left = ndp::launch_sm_dgrad(dy.data_ptr<float>(), w.data_ptr<float>(), dx.data_ptr<float>(), B, g, pp,
-                                        cur_stream(), ap, defer);
-  check_launch("launch_sm_dgrad");
-  return left;
-}
-
-// out: sm_splits(g, B, 2) * numel(W) floats; returns the number of slabs written (1 = dW)
-int64_t sm_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor out, const std::vector<int64_t>& geom) {
-  const ndp::ConvGeom g = conv_geom(geom);
-  const int B = sm_batch(x, g, "sm_wgrad");
-  conv_check(x, "x", B, g.C, g.H, g.W);
-  conv_check(dy, "dy", B, g.Co, g.OH, g.OW);
-  check_f32(out, "out");
-  const int z = ndp::sm_splits(g, B, 2);
-  TORCH_CHECK(out.numel() >= (int64_t)z * g.Co * g.C * g.KH * g.KW, "sm_wgrad: out must hold ", z, " slabs of dW");
-  const int got = ndp::launch_sm_wgrad(x.data_ptr<float>(), dy.data_ptr<float>(), out.data_ptr<float>(), B, g,
-                                       cur_stream());
-  check_launch("launch_sm_wgrad");
-  return got;
-}
-
-// ---- fused-BN small-map stage (smallconv.hip SmOps), described by Python dicts -------------
-template <typename T>
-static T* dptr(const py::dict& d, const char* k) {
-  if (!d.contains(k)) return nullptr;
-  py::object o = d[k];
-  if (o.is_none()) return nullptr;
-  torch::Tensor t = o.cast<torch::Tensor>();
-  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "sm ops: '", k, "' must be a contiguous device tensor");
-  return static_cast<T*>(t.data_ptr());
-}
-static int64_t ival(const py::dict& d, const char* k, int64_t def = 0) {
-  return d.contains(k) && !py::object(d[k]).is_none() ? d[k].cast<int64_t>() : def;
-}
-static double fval(const py::dict& d, const char* k, double def = 0.0) {
-  return d.contains(k) && !py::object(d[k]).is_none() ? d[k].cast<double>() : def;
-}
-static ndp::SmBnF bnf_from(const py::dict& o, const char* key) {
-  ndp::SmBnF f{};
-  if (!o.contains(key) || py::object(o[key]).is_none()) return f;
-  py::dict d = o[key].cast<py::dict>();
-  f.part = dptr<const double>(d, "part");
-  f.R = (int32_t)ival(d, "R");
-  f.count = fval(d, "count");
-  f.gamma = dptr<const float>(d, "gamma");
-  f.beta = dptr<const float>(d, "beta");
-  f.eps = (float)fval(d, "eps", 1e-5);
-  f.momentum = (float)fval(d, "momentum", 0.1);
-  f.save_mean = dptr<float>(d, "save_mean");
-  f.save_invstd = dptr<float>(d, "save_invstd");
-  f.rmean = dptr<float>(d, "rmean");
-  f.rvar = dptr<float>(d, "rvar");
-  f.nbt = dptr<int64_t>(d, "nbt");
-  TORCH_CHECK(f.save_mean != nullptr && f.save_invstd != nullptr, "sm ops: BN '", key, "' needs save_mean/save_invstd");
-  return f;
-}
-static ndp::SmBnB bnb_from(const py::dict& o, const char* key) {
-  ndp::SmBnB b{};
-  if (!o.contains(key) || py::object(o[key]).is_none()) return b;
-  py::dict d = o[key].cast<py::dict>();
-  b.part = dptr<const double>(d, "part");
-  b.R = (int32_t)ival(d, "R");
-  b.j = (int32_t)ival(d, "j", 1);
-  b.count = fval(d, "count");
-  b.gamma = dptr<const float>(d, "gamma");
-  b.mean = dptr<const float>(d, "mean");
-  b.invstd = dptr<const float>(d, "invstd");
-  b.dgamma = dptr<float>(d, "dgamma");
-  b.dbeta = dptr<float>(d, "dbeta");
-  TORCH_CHECK(b.part && b.mean && b.invstd, "sm ops: BN backward '", key, "' needs part/mean/invstd");
-  return b;
-}
-static ndp::SmOps ops_from(const py::dict& d) {
-  ndp::SmOps o{};
-  o.amode = (int32_t)ival(d, "amode");
-  o.amask = (int32_t)ival(d, "amask");
-  o.af = bnf_from(d, "af");
-  o.afd = bnf_from(d, "afd");
-  o.ab = bnb_from(d, "ab");
-  o.res = dptr<const float>(d, "res");
-  o.mtensor = dptr<const float>(d, "mtensor");
-  o.c = dptr<const float>(d, "c");
-  o.mat = dptr<float>(d, "mat");
-  o.emode = (int32_t)ival(d, "emode");
-  o.eadd = (int32_t)ival(d, "eadd");
-  o.addend = dptr<const float>(d, "addend");
-  o.addmask = dptr<const float>(d, "addmask");
-  o.epart = dptr<double>(d, "epart");
-  o.emask = (int32_t)ival(d, "emask");
-  o.eds = (int32_t)ival(d, "eds");
-  o.emtensor = dptr<const float>(d, "emtensor");
-  o.ec = dptr<const float>(d, "ec");
-  o.ecd = dptr<const float>(d, "ecd");
-  o.ef = bnf_from(d, "ef");
-  o.efd = bnf_from(d, "efd");
-  TORCH_CHECK(o.amode >= 0 && o.amode <= 4 && o.emode >= 0 && o.emode <= 2 && o.eadd >= 0 && o.eadd <= 2,
-              "sm ops: bad mode");
-  TORCH_CHECK((o.amode != 2 && o.amode != 3) || o.res, "sm ops: amode 2/3 need 'res'");
-  TORCH_CHECK(o.amode != 4 || (o.c && (o.amask != 1 || o.mtensor)), "sm ops: amode 4 needs 'c' (+ 'mtensor')");
-  TORCH_CHECK(o.emode == 0 || o.epart, "sm ops: emode needs 'epart'");
-  TORCH_CHECK(o.emode != 2 || (o.ec && (o.emask != 1 || o.emtensor) && (!o.eds || o.ecd)),
-              "sm ops: emode 2 needs 'ec' (+ 'emtensor' / 'ecd')");
-  TORCH_CHECK(o.eadd == 0 || (o.addend && (o.eadd != 2 || o.addmask)), "sm ops: eadd needs 'addend' (+ 'addmask')");
-  return o;
-}
-
-int64_t sm_rowtile(const std::vector<int64_t>& geom, int64_t B, int64_t dir) {
-  return ndp::sm_rowtile(conv_geom(geom), (int)B, (int)dir);
-}
-
-void sm_fwd_ops(torch::Tensor x, torch::Tensor w, torch::Tensor y, const std::vector<int64_t>& geom, py::dict ops) {
-  const ndp::ConvGeom g = conv_geom(geom);
-  const int B = sm_batch(x, g, "sm_fwd_ops");
-  conv_check(x, "x", B, g.C, g.H, g.W);
-  conv_check(w, "w", g.Co, g.C, g.KH, g.KW);
-  conv_check(y, "y", B, g.Co, g.OH, g.OW);
-  ndp::launch_sm_fwd_ops(x.data_ptr<float>(), w.data_ptr<float>(), y.data_ptr<float>(), B, g, ops_from(ops),
-                         cur_stream());
-  check_launch("launch_sm_fwd_ops");
-}
-
-void sm_dgrad_ops(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, const std::vector<int64_t>& geom, py::dict ops) {
-  const ndp::ConvGeom g = conv_geom(geom);
-  const int B = sm_batch(dy, g, "sm_dgrad_ops");
-  conv_check(dy, "dy", B, g.Co, g.OH, g.OW);
-  conv_check(w, "w", g.Co, g.C, g.KH, g.KW);
-  conv_check(dx, "dx", B, g.C, g.H, g.W);
-  ndp::launch_sm_dgrad_ops(dy.data_ptr<float>(), w.data_ptr<float>(), dx.data_ptr<float>(), B, g, ops_from(ops),
-                           cur_stream());
-  check_launch("launch_sm_dgrad_ops");
-}
-
-int64_t sm_wgrad_ops(torch::Tensor x, torch::Tensor dy, torch::Tensor out, const std::vector<int64_t>& geom,
-                     py::dict xops, py::dict gops) {
-  const ndp::ConvGeom g = conv_geom(geom);
-  const int B = sm_batch(x, g, "sm_wgrad_ops");
-  conv_check(x, "x", B, g.C, g.H, g.W);
-  conv_check(dy, "dy", B, g.Co, g.OH, g.OW);
-  check_f32(out, "out");
-  const int z = ndp::sm_splits(g, B, 2);
-  TORCH_CHECK(out.numel() >= (int64_t)z * g.Co * g.C * g.KH * g.KW, "sm_wgrad_ops: out must hold ", z, " slabs");
-  const int got = ndp::launch_sm_wgrad_ops(x.data_ptr<float>(), dy.data_ptr<float>(), out.data_ptr<float>(), B, g,
-                                           ops_from(xops), ops_from(gops), cur_stream());
-  check_launch("launch_sm_wgrad_ops");
-  return got;
-}
-
-void sm_bn_apply(torch::Tensor x, torch::Tensor y, py::dict ops) {
-  check_f32(x, "x");
-  check_f32(y, "y");
-  TORCH_CHECK(x.dim() == 4 && x.sizes() == y.sizes() && x.size(1) % 16 == 0, "sm_bn_apply: [B, C % 16, H, W]");
-  const ndp::SmOps o = ops_from(ops);
-  TORCH_CHECK(o.amode == 2 || o.amode == 3, "sm_bn_apply: amode 2 / 3");
-  ndp::launch_sm_bn_apply(x.data_ptr<float>(), y.data_ptr<float>(), (int)x.size(0), (int)x.size(1),
-                          (int)(x.size(2) * x.size(3)), o, cur_stream());
-  check_launch("launch_sm_bn_apply");
-}
-
-void sm_bn_bstats(torch::Tensor dy, py::dict ops) {
-  check_f32(dy, "dy");
-  TORCH_CHECK(dy.dim() == 4 && dy.size(1) % 16 == 0, "sm_bn_bstats: [B, C % 16, H, W]");
-  const ndp::SmOps o = ops_from(ops);
-  TORCH_CHECK(o.epart && o.ec && (o.emask != 1 || o.emtensor) && (!o.eds || o.ecd), "sm_bn_bstats: bad ops");
-  ndp::launch_sm_bn_bstats(dy.data_ptr<float>(), (int)dy.size(0), (int)dy.size(1), (int)(dy.size(2) * dy.size(3)), o,
-                           cur_stream());
-  check_launch("launch_sm_bn_bstats");
-}
-
 // ---- HIP-IPC one-shot all-reduce (ipc.hip; registered here so pybind11 stays g++-only) ----
 namespace ndp {
 void* ipc_new(int rank, int nranks, int device, int64_t capacity_bytes);
@@ -1470,19 +1255,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   }, py::arg("geom"), py::arg("batch"));
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("part"), py::arg("dw"), py::arg("geom"));
   m.def("tg_plan", &tg_plan);
-  m.def("sm_plan", &sm_plan, py::arg("geom"), py::arg("batch"));
-  m.def("sm_fwd", &sm_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("geom"), py::arg("part"),
-        py::arg("defer"));
-  m.def("sm_dgrad", &sm_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("geom"), py::arg("part"),
-        py::arg("addend"), py::arg("defer"));
-  m.def("sm_wgrad", &sm_wgrad, py::arg("x"), py::arg("dy"), py::arg("out"), py::arg("geom"));
-  m.def("sm_rowtile", &sm_rowtile);
-  m.def("sm_bstats_rows", &ndp::sm_bstats_rows);
-  m.def("sm_fwd_ops", &sm_fwd_ops);
-  m.def("sm_dgrad_ops", &sm_dgrad_ops);
-  m.def("sm_wgrad_ops", &sm_wgrad_ops);
-  m.def("sm_bn_apply", &sm_bn_apply);
-  m.def("sm_bn_bstats", &sm_bn_bstats);
   m.def("tg_describe", &tg_describe);
   m.def("tg_fwd", &tg_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("geom"), py::arg("part") = py::none(),
         py::arg("defer") = false);

@@ -1177,21 +1177,8 @@ int conv_direct_class(const ConvGeom& g) {
   return -1;
 }
 
-// tuning variant (NDP_CONV_VARIANT, benchmarking only): 0 = default
-static int conv_variant() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("NDP_CONV_VARIANT");
-    v = e ? atoi(e) : 0;
-  }
-  return v;
-}
-
 // images per workgroup of the forward / grad-x kernels, images per grad-W slice
-int conv_fwd_imgs(int cls) {
-  if (cls == 0) return conv_variant() == 1 ? 2 : 1;
-  return cls == 3 ? 1 : 4;
-}
+int conv_fwd_imgs(int cls) { return (cls == 0 || cls == 3) ? 1 : 4; }
 
 static constexpr int kFillWgs = 256;  // one workgroup per CU: below this, split the reduction
 
@@ -1203,53 +1190,32 @@ static int pow2_floor(int v) {
 
 // images per grad-W slice: the class default, lowered (power of two dividing B) until the
 // grid has >= kFillWgs workgroups.  Workgroups per slice = (Kout / 32) * ceil(Cin / CB).
+// (Larger slices = fewer slabs to sum measured slower in round 3: batch 512 x2 1.9937, x4
+// 1.9969 vs 1.9904 / 1.9927 ms; batch 256 1.4473 / 1.4444 vs 1.441.)
 int conv_wgrad_imgs(int cls, const ConvGeom& g, int B) {
-  int def = cls == 0 ? (conv_variant() == 1 ? 2 : 4) : cls == 1 ? 16 : cls == 2 ? 8 : cls == 4 ? 8 : 2;
-  // NDP_WGRAD_IMGS_MUL (A/B only): larger slices = fewer slabs to sum; measured slower (batch
-  // 512: x2 1.9937, x4 1.9969 vs 1.9904 / 1.9927 ms; batch 256: 1.4473 / 1.4444 vs 1.441)
-  static int mul = -1;
-  if (mul < 0) {
-    const char* e = getenv("NDP_WGRAD_IMGS_MUL");
-    mul = e ? atoi(e) : 1;
-    if (mul < 1) mul = 1;
-  }
-  for (int m = mul; m > 1 && def * 2 <= B && B % (def * 2) == 0 &&
-                  (B / (def * 2)) * (g.Co / 32) * ((g.C + 31) / 32) >= kFillWgs;
-       m /= 2)
-    def *= 2;
+  int def = cls == 0 ? 4 : cls == 1 ? 16 : cls == 2 ? 8 : cls == 4 ? 8 : 2;
   const int cb = cls == 3 ? 3 : 32;
   const int per_slice = (g.Co / 32) * ((g.C + cb - 1) / cb);
   while (def > 1 && (B / def) * per_slice < kFillWgs && B % (def / 2) == 0) def /= 2;
   return def;
 }
 
+// split-K cap: 4 keeps layer2's slabs summable inside the fused BN kernel (batchnorm.hip
+// kMaxFusedSlabs) — ResNet-18 step on 1x MI355X, batch 128 1.216 / 1.197 -> 1.191 / 1.188 ms,
+// batch 64 1.050 / 1.050 -> 1.049 / 1.046 (uncapped: 8 slabs at batch 64).  The 1x1 stride-2
+// grad-x takes the same cap (a cap of 1 measured 0.960 -> 0.967 ms at batch 64).
+static constexpr int kConvMaxSplit = 4;
+
 // split-K factor of the forward (dgrad = false) / grad-x (dgrad = true) kernels: a power of
 // two <= the channel chunks, so that (B / IMGS) * (outC / 64) * ksplit >= kFillWgs
 int conv_ksplit(int cls, const ConvGeom& g, int B, bool dgrad) {
-  if (cls == 3 || (dgrad && !conv_dgrad_direct(cls))) return 1;
+  if (cls < 0 || cls == 3) return 1;
   const int inC = dgrad ? g.Co : g.C, outC = dgrad ? g.C : g.Co;
   const int imgs = (dgrad && cls == 2) ? 1 : conv_fwd_imgs(cls);  // class-2 grad-x: 8x8 tiles, 1 image
   const int base = (B / imgs) * (outC / 64);
   const int nchunks = inC / 8;
-  // split cap (NDP_CONV_MAXKS to A/B): 4 keeps layer2's slabs summable inside the fused BN
-  // kernel (batchnorm.hip kMaxFusedSlabs) — ResNet-18 step on 1x MI355X, batch 128 1.216 / 1.197 ->
-  // 1.191 / 1.188 ms, batch 64 1.050 / 1.050 -> 1.049 / 1.046 (uncapped: 8 slabs at batch 64)
-  static int maxks = -1;
-  if (maxks < 0) {
-    const char* e = getenv("NDP_CONV_MAXKS");
-    maxks = e ? atoi(e) : 4;
-  }
-  // the 1x1 stride-2 grad-x (class 4): its split-K sum is a separate even-pixel scatter launch
-  // (conv_slab_sum_ups); NDP_DS_DGRAD_MAXKS caps its split (A/B: 1x MI355X, ResNet-18 r=4, cap 1
-  // at batch 512 1.869 / 1.864 -> 1.865 / 1.863 ms (noise), at batch 64 0.960 -> 0.967: no cap)
-  static int ds_maxks = -1;
-  if (ds_maxks < 0) {
-    const char* e = getenv("NDP_DS_DGRAD_MAXKS");
-    ds_maxks = e ? atoi(e) : 0;
-  }
-  const int cap = (dgrad && cls == 4 && ds_maxks > 0) ? ds_maxks : maxks;
   int ks = 1;
-  while (ks * 2 <= nchunks && base * ks < kFillWgs && ks * 2 <= cap) ks *= 2;
+  while (ks * 2 <= nchunks && base * ks < kFillWgs && ks * 2 <= kConvMaxSplit) ks *= 2;
   return pow2_floor(ks);
 }
 // BatchNorm statistics from the forward epilogue: the layer1 3x3 and stem 7x7 classes (their
@@ -1257,8 +1223,6 @@ int conv_ksplit(int cls, const ConvGeom& g, int B, bool dgrad) {
 // unsplit launches only.  Returns the partial count S (= workgroups along the batch), 0 = none.
 int conv_fwd_stats_slices(int cls, const ConvGeom& g, int B) {
   static_assert(ConvFwdCfg<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, false>::STATS_OK &&
-                    ConvFwdCfg<3, 3, 1, 1, 8, 8, 16, 64, 1, 2, 2, 4, false>::STATS_OK &&
-                    ConvFwdCfg<3, 3, 1, 1, 8, 8, 8, 64, 2, 2, 2, 4, false>::STATS_OK &&
                     ConvFwdCfg<7, 7, 2, 3, 32, 32, 4, 64, 1, 2, 1, 7, false>::STATS_OK,
                 "statistics epilogue fits every layer1 / stem tile");
   if (cls != 0 && cls != 3) return 0;
@@ -1268,147 +1232,61 @@ int conv_fwd_stats_slices(int cls, const ConvGeom& g, int B) {
 // backward-mode BN partial sums from the grad-x epilogue: the layer1 3x3 class (its BN takes the
 // two-kernel large-map path), unsplit grad-x launches only; 0 = none
 int conv_dgrad_stats_slices(int cls, const ConvGeom& g, int B) {
-  static_assert(ConvFwdCfg<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true>::STATS2_OK &&
-                    ConvFwdCfg<3, 3, 1, 1, 8, 8, 16, 64, 1, 2, 2, 4, true>::STATS2_OK,
+  static_assert(ConvFwdCfg<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true>::STATS2_OK,
                 "backward statistics epilogue fits the layer1 grad-x tiles");
-  // (the two-image tile variant, NDP_CONV_VARIANT=1, has no room for the two tiles)
   // class 2 (3x3 stride 2) runs the layer1 grad-x kernel on the zero-inserted dY: one image per tile
-  if ((cls != 0 && cls != 2) || conv_variant() == 1 || conv_ksplit(cls, g, B, true) != 1) return 0;
-  if (cls == 2 && !conv_dgrad_direct(cls)) return 0;
+  if ((cls != 0 && cls != 2) || conv_ksplit(cls, g, B, true) != 1) return 0;
   return cls == 2 ? B : B / conv_fwd_imgs(cls);
 }
-// 3x3 stride-2 grad-x on the zero-inserted dY: exact (tests/test_conv_direct.py), 4x the
-// MFMA work of the sub-pixel form; measured on 1x MI355X (ResNet-18 step, round 2) 2.006 /
-// 2.005 vs MIOpen 1.991 ms at batch 512, 1.054 / 1.047 vs 1.051 at 64.  DEFAULT since round 3:
-// the MIOpen kernel was the last non-native call of the ResNet-18 step, and its algorithm
-// choice depends on MIOpen's on-disk find database (written by earlier processes, e.g. a
-// cudnn.benchmark run): on a box with a populated database it was non-deterministic and,
-// captured in a hipGraph, produced NaN (tools/gpu_iso.sh bisection).  NDP_CONV_DGRAD2=0
-// restores MIOpen.
-static bool dgrad2_on() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("NDP_CONV_DGRAD2");
-    v = e ? atoi(e) : 1;
-  }
-  return v != 0;
-}
-bool conv_dgrad_direct(int cls) { return cls == 0 || cls == 1 || (cls == 2 && dgrad2_on()) || cls == 4; }
-// MFMA-block schedule of the layer1 / layer2 fwd + grad-x kernels (SCH template argument):
-// default 2 (pinned MFMA / LDS-read interleave): ResNet-18 step on 1x MI355X 2.0175 / 2.0154
-// -> 1.9981 / 1.9994 ms at batch 512, 1.0582 / 1.0627 -> 1.0546 / 1.0569 at batch 64;
-// NDP_CONV_VARIANT 5 = iglp_opt(0) (2.0043 / 1.0602), 7 = the compiler's schedule.
-static int conv_sched() {
-  const int v = conv_variant();
-  return v == 5 ? 1 : (v == 0 || v == 6 || v == 8) ? 2 : 0;
-}
-// NDP_CONV_VARIANT=8: the pinned interleave also for the stem, 3x3/2 and 1x1/2 forwards (A/B)
-static bool sched_all() { return conv_variant() == 8; }
+// Every class runs its grad-x natively.  The 3x3 stride-2 grad-x runs on the zero-inserted dY
+// (exact, 4x the MFMA work of the sub-pixel form; round 2: 2.006 / 2.005 vs MIOpen 1.991 ms at
+// batch 512): MIOpen's algorithm choice depends on its on-disk find database and, captured in a
+// hipGraph, was found non-deterministic and NaN-producing (round 3 bisection).
+bool conv_dgrad_direct(int cls) { return cls >= 0 && cls <= 4 && cls != 3; }
 
-// NDP_CONV_VARIANT (benchmarking only): 1 = two images per layer1 tile; 2 = 16-channel
-// chunks (half the chunk barriers, twice the MFMA work behind each prefetch) for the 3x3
-// classes 0-2; 3 = 16-channel chunks for classes 1-2 only (already one workgroup per CU)
-static bool ck16(int cls) {
-  const int v = conv_variant();
-  return (v == 2 && cls <= 2) || (v == 3 && (cls == 1 || cls == 2));
-}
-
+// MFMA-block schedule of the layer1 / layer2 fwd + grad-x kernels: SCH = 2 (pinned MFMA /
+// LDS-read interleave): ResNet-18 step on 1x MI355X 2.0175 / 2.0154 -> 1.9981 / 1.9994 ms at
+// batch 512, 1.0582 / 1.0627 -> 1.0546 / 1.0569 at batch 64 against the compiler's schedule
+// (iglp_opt(0): 2.0043 / 1.0602; the pinned interleave on the stem / 3x3-2 / 1x1-2 forwards
+// and 16-channel chunks or two-image layer1 tiles were slower — round 3 A/Bs)
 int launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s,
                     bool defer, double* stats_out) {
   const ConvBnStats stats{stats_out, nullptr, nullptr, nullptr, nullptr};
   const int cls = conv_direct_class(g);
   const int ks = conv_ksplit(cls, g, B, false);
-  const bool c16 = ck16(cls);
-  const int sch = conv_sched();
   switch (cls) {
     case 0:
-      if (sch == 1)
-        return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, false, true, 1, 1>(x, w, y, B, g.C, g.Co, ks, part, s,
-                                                                               nullptr, defer, stats);
-      if (sch == 2)
-        return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, false, true, 1, 2>(x, w, y, B, g.C, g.Co, ks, part, s,
-                                                                               nullptr, defer, stats);
-      if (conv_variant() == 1)
-        return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 2, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s, nullptr,
-                                                                         defer, stats);
-      if (c16)
-        return run_fwd<3, 3, 1, 1, 8, 8, 16, 64, 1, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s,
-                                                                          nullptr, defer, stats);
-      return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s, nullptr,
-                                                                       defer, stats);
+      return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, false, true, 1, 2>(x, w, y, B, g.C, g.Co, ks, part, s,
+                                                                             nullptr, defer, stats);
     case 1:
-      if (sch == 1)
-        return run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, false, true, 1, 1>(x, w, y, B, g.C, g.Co, ks, part, s,
-                                                                               nullptr, defer);
-      if (sch == 2)
-        return run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, false, true, 1, 2>(x, w, y, B, g.C, g.Co, ks, part, s,
-                                                                               nullptr, defer);
-      if (c16)
-        return run_fwd<3, 3, 1, 1, 4, 4, 16, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s,
-                                                                          nullptr, defer);
-      return run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s, nullptr,
-                                                                       defer);
+      return run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, false, true, 1, 2>(x, w, y, B, g.C, g.Co, ks, part, s,
+                                                                             nullptr, defer);
     case 2:
-      if (c16)
-        return run_fwd<3, 3, 2, 1, 8, 8, 16, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s,
-                                                                          nullptr, defer);
-      if (sched_all())
-        return run_fwd<3, 3, 2, 1, 8, 8, 8, 64, 4, 2, 2, 4, false, true, 1, 2>(x, w, y, B, g.C, g.Co, ks, part, s,
-                                                                               nullptr, defer);
       return run_fwd<3, 3, 2, 1, 8, 8, 8, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s, nullptr,
                                                                        defer);
     case 3:
-      if (sched_all())
-        return run_fwd<7, 7, 2, 3, 32, 32, 4, 64, 1, 2, 1, 7, false, false, 1, 2>(x, w, y, B, g.C, g.Co, 1, nullptr, s,
-                                                                                    nullptr, false, stats);
       return run_fwd<7, 7, 2, 3, 32, 32, 4, 64, 1, 2, 1, 7, false, false>(x, w, y, B, g.C, g.Co, 1, nullptr, s, nullptr,
                                                                           false, stats);
     case 4:
-      if (sched_all())
-        return run_fwd<1, 1, 2, 0, 8, 8, 8, 64, 4, 2, 2, 4, false, true, 1, 2>(x, w, y, B, g.C, g.Co, ks, part, s,
-                                                                               nullptr, defer);
       return run_fwd<1, 1, 2, 0, 8, 8, 8, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s, nullptr,
                                                                        defer);
     default: return 1;
   }
 }
 
-// dx[B, C, H, W] from dy[B, Co, OH, OW] (stride-1 classes only)
+// dx[B, C, H, W] from dy[B, Co, OH, OW]
 int launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, float* part,
                       hipStream_t s, const float* addend, bool defer, const ConvBnStats* bst) {
   const ConvBnStats stats = bst != nullptr ? *bst : ConvBnStats{nullptr, nullptr, nullptr, nullptr, nullptr};
   const int cls = conv_direct_class(g);
   const int ks = conv_ksplit(cls, g, B, true);
-  const bool c16 = ck16(cls);
-  const int sch = conv_sched();
   switch (cls) {
     case 0:
-      if (sch == 1)
-        return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true, true, 1, 1>(dy, w, dx, B, g.Co, g.C, ks, part, s,
-                                                                              addend, defer, stats);
-      if (sch == 2)
-        return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true, true, 1, 2>(dy, w, dx, B, g.Co, g.C, ks, part, s,
-                                                                              addend, defer, stats);
-      if (conv_variant() == 1)
-        return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 2, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s, addend,
-                                                                        defer, stats);
-      if (c16)
-        return run_fwd<3, 3, 1, 1, 8, 8, 16, 64, 1, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s,
-                                                                         addend, defer, stats);
-      return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s, addend,
-                                                                      defer, stats);
+      return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true, true, 1, 2>(dy, w, dx, B, g.Co, g.C, ks, part, s,
+                                                                            addend, defer, stats);
     case 1:
-      if (sch == 1)
-        return run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, true, true, 1, 1>(dy, w, dx, B, g.Co, g.C, ks, part, s,
-                                                                              addend, defer);
-      if (sch == 2)
-        return run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, true, true, 1, 2>(dy, w, dx, B, g.Co, g.C, ks, part, s,
-                                                                              addend, defer);
-      if (c16)
-        return run_fwd<3, 3, 1, 1, 4, 4, 16, 64, 4, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s,
-                                                                         addend, defer);
-      return run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, true, true>(dy, w, dx, B, g.Co, g.C, ks, part, s, addend,
-                                                                      defer);
+      return run_fwd<3, 3, 1, 1, 4, 4, 8, 64, 4, 2, 2, 4, true, true, 1, 2>(dy, w, dx, B, g.Co, g.C, ks, part, s,
+                                                                            addend, defer);
     case 2:  // 3x3 stride 2: the layer1 grad-x kernel on the zero-inserted dY (staged, not stored)
       return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true, true, 1, 2, 2>(dy, w, dx, B, g.Co, g.C, ks, part, s,
                                                                               addend, defer, stats);

@@ -158,7 +158,7 @@ class IpcComm {
     bytes_ = cap_floats_ * sizeof(float) + flags;
     NDP_IPC_CHECK(hipSetDevice(device));
     // uncached first (see the header); plain device memory if either step refuses it
-    if (std::getenv("NDP_IPC_CACHED") == nullptr && hipExtMallocWithFlags(&base_, bytes_, hipDeviceMallocUncached) == hipSuccess) {
+    if (hipExtMallocWithFlags(&base_, bytes_, hipDeviceMallocUncached) == hipSuccess) {
       hipIpcMemHandle_t h;
       if (hipIpcGetMemHandle(&h, base_) == hipSuccess) {
         uncached_ = true;

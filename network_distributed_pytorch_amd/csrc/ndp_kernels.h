@@ -329,95 +329,6 @@ int launch_tg_wgrad(const float* x, const float* dy, float* out, int B, const Co
                     hipStream_t s, bool defer = false);
 }  // namespace ndp
 
-// ---- small-map convolutions on 16x16x4 f32 MFMA (smallconv.hip) ---------------------------
-namespace ndp {
-// Fused BatchNorm for the small-map stage (ops/smstage.py).  A BN layer's forward statistics
-// come as per-row-tile partial sums written by the epilogue of the conv that produces its
-// input, and are finalized in the prologue of every kernel that consumes the BN output
-// (the workgroup at grid origin also writes save_mean / save_invstd and the running stats).
-struct SmBnF {
-  const double* part;  // [R][C][2] (sum, sum of squares); nullptr: use save_mean / save_invstd
-  int32_t R, pad;
-  double count;        // elements per channel (batch x pixels)
-  const float* gamma;
-  const float* beta;
-  float eps, momentum;
-  float* save_mean;    // written by the finalizing workgroup when part != nullptr
-  float* save_invstd;
-  float* rmean;        // running statistics (nullable), same writer
-  float* rvar;
-  int64_t* nbt;
-};
-// backward coefficients of one BN layer from per-row-tile partial sums of dz and dz * x-hat
-struct SmBnB {
-  const double* part;  // [R][C][4]: sum dz, sum dz * xhat, sum dz * xhat_ds, 0
-  int32_t R, j;        // j: which x-hat sum this BN uses (1: its own input, 2: the downsample BN's)
-  double count;
-  const float* gamma;
-  const float* mean;   // saved forward statistics
-  const float* invstd;
-  float* dgamma;       // written by the workgroup at grid origin (nullable)
-  float* dbeta;
-};
-// operand transform + epilogue of one small-map kernel (all modes 0: the plain convolution)
-struct SmOps {
-  // operand ("act": X forward, dY grad-x / grad-W) transform while it is staged:
-  //  1 relu(bn(x)); 2 relu(bn(x) + res); 3 relu(bn(x) + bn_d(res)); 4 BN backward of dY:
-  //  k1 * (dz - mean dz - xhat * mean dz*xhat), dz = dY * mask
-  int32_t amode;
-  int32_t amask;       // amode 4: relu mask of the BN output: 0 none, 1 mtensor > 0, 2 bn(c) > 0 recomputed
-  SmBnF af;            // amode 1-3: the operand's BN; amode 4 / amask 2: its saved forward statistics
-  SmBnF afd;           // amode 3: the residual's (downsample) BN
-  SmBnB ab;            // amode 4
-  const float* res;    // amode 2: residual (operand layout); amode 3: the raw downsample conv output
-  const float* mtensor;
-  const float* c;      // amode 4: the BN's input (raw conv output, operand layout)
-  float* mat;          // amode 1-3: the transformed operand is also written here (n-tile 0)
-  // epilogue (row kernels, no channel split)
-  int32_t emode;       // 1: sum / sum sq of the output -> epart [rowtile][N][2]; 2: BN-backward sums
-                       // of the previous BN (its dz = out * mask) -> epart [rowtile][N][4]
-  int32_t eadd;        // 1: out += addend; 2: out += addend * (addmask > 0)
-  const float* addend;
-  const float* addmask;
-  double* epart;
-  int32_t emask, eds;  // emode 2: mask 0 none / 1 emtensor > 0 / 2 bn(ec) > 0; eds: also the ds x-hat sum
-  const float* emtensor;
-  const float* ec;     // previous BN's input (output layout)
-  const float* ecd;    // previous downsample BN's input
-  SmBnF ef;            // previous BN (saved statistics)
-  SmBnF efd;           // previous downsample BN (saved statistics)
-};
-
-// geometry id (input <= 4x4, output <= 2x2, ResNet layer3 / layer4), -1 = not covered
-int sm_class(const ConvGeom& g);
-// split factor of direction dir (0 fwd / 1 grad-x: channel splits, slabs of numel(out) floats;
-// 2 grad-W: batch splits, slabs of numel(W) floats) at batch B; 1 = no scratch
-int sm_splits(const ConvGeom& g, int B, int dir);
-// defer: leave the split-K slabs in part, return their count (1 = y / dx final)
-int launch_sm_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s,
-                  bool defer = false);
-// addend (nullable, may alias dx): dx = grad-x + addend (never deferred)
-int launch_sm_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, float* part, hipStream_t s,
-                    const float* addend = nullptr, bool defer = false);
-// out: sm_splits(g, B, 2) slabs of numel(W) floats (slab 0 = dW when 1); returns the count
-int launch_sm_wgrad(const float* x, const float* dy, float* out, int B, const ConvGeom& g, hipStream_t s);
-// fused-BN variants: no channel split (the epilogue sees whole sums); ops describes the
-// operand transform / epilogue (grad-W: xops transforms X, gops transforms dY; epilogue unused)
-int sm_rowtile(const ConvGeom& g, int B, int dir);  // images per row tile (rows of the epilogue partials)
-void launch_sm_fwd_ops(const float* x, const float* w, float* y, int B, const ConvGeom& g, const SmOps& ops,
-                       hipStream_t s);
-void launch_sm_dgrad_ops(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, const SmOps& ops,
-                         hipStream_t s);
-int launch_sm_wgrad_ops(const float* x, const float* dy, float* out, int B, const ConvGeom& g, const SmOps& xops,
-                        const SmOps& gops, hipStream_t s);
-// y = relu(bn(x) + res) / relu(bn(x) + bn_d(rx)) (ops.amode 2 / 3, [B][C][P]) -- the stage's last output
-void launch_sm_bn_apply(const float* x, float* y, int B, int C, int P, const SmOps& ops, hipStream_t s);
-// BN-backward partial sums of a BN whose output gradient is dy ([B][C][P]), ops.emask / ec / ecd /
-// ef / efd / eds as in the row epilogue; writes ops.epart [R][C][4], R = sm_bstats_rows(B)
-int sm_bstats_rows(int B);
-void launch_sm_bn_bstats(const float* dy, int B, int C, int P, const SmOps& ops, hipStream_t s);
-}  // namespace ndp
-
 // ---- fused fp32 attention, q/k/v/o [B, S, H, 64] (attention.hip) ------------------------
 namespace ndp {
 // mask: [B, S] int32 (nonzero = attend) or null; lse: [B, H, S]; p_drop in [0, 1);

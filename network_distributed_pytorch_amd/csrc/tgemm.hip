@@ -325,15 +325,7 @@ int ilog2_exact(int v) {
 TgIndex plain(int64_t stride) { return TgIndex{0, stride, 30, 0}; }  // i < 2^30: outer part always 0
 TgIndex comp(int sh, int64_t outer, int64_t inner) { return TgIndex{outer, inner, sh, 0}; }
 
-int tg_fill() {  // split-K until tiles x splits reaches this many workgroups (NDP_TG_FILL)
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("NDP_TG_FILL");
-    v = e ? atoi(e) : 256;  // one workgroup per CU at least
-    if (v < 1) v = 256;
-  }
-  return v;
-}
+constexpr int kTgFill = 256;  // split-K until tiles x splits reaches one workgroup per CU
 
 TgTile tg_tile(int, int) { return kTile64; }
 
@@ -343,21 +335,14 @@ int tg_pick_splits(int M, int N, int K, int cap) {
   const int tiles = ((M + t.bm - 1) / t.bm) * ((N + t.bn - 1) / t.bn);
   const int ktiles = (K + t.bk - 1) / t.bk;
   int s = 1;
-  while (s * 2 <= cap && tiles * s < tg_fill() && ktiles >= 4 * s) s *= 2;
+  while (s * 2 <= cap && tiles * s < kTgFill && ktiles >= 4 * s) s *= 2;
   return s;
 }
 
-int tg_cap() {
-  static int v = -1;
-  if (v < 0) {
-    // 4 = batchnorm.hip kMaxFusedSlabs: forward / grad-x slabs up to 4 are summed inside the
-    // fused BN kernel that consumes the conv (ops/slablink.py), i.e. at no extra launch
-    const char* e = getenv("NDP_TG_MAXSPLIT");
-    v = e ? atoi(e) : 4;
-    if (v < 1) v = 1;
-  }
-  return v;
-}
+// 4 = batchnorm.hip kMaxFusedSlabs: forward / grad-x slabs up to 4 are summed inside the fused
+// BN kernel that consumes the conv (ops/slablink.py), i.e. at no extra launch
+constexpr int kTgCap = 4;
+static int tg_cap() { return kTgCap; }
 
 // 16-B loads along `fast` are legal when its 4 consecutive indices are 4 consecutive floats
 // (unit inner stride, outer steps and every stride of `slow` multiples of 4 floats), the base
@@ -366,17 +351,6 @@ bool vec_ok(const TgIndex& fast, const TgIndex& slow, const float* base, int ext
   const bool unit = fast.si == 1 && (fast.sh == 30 || (fast.sh >= 2 && fast.so % 4 == 0));
   const bool slow4 = slow.so % 4 == 0 && (slow.sh == 0 || slow.si % 4 == 0);
   return unit && slow4 && (reinterpret_cast<uintptr_t>(base) & 15) == 0 && extent % 4 == 0;
-}
-
-bool tg_vec() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("NDP_TG_VEC");  // 0: scalar loads only (A/B)
-    // on by default since the branch-free raw-buffer k-loop: R152 r=4 16.11 -> 15.45 ms,
-    // R50 dense 6.56 -> 6.31 ms (profiles/r3/tg_bench.md); slower with the old predicated loads
-    v = e ? atoi(e) : 1;
-  }
-  return v != 0;
 }
 
 template <int BM, int BN, int BK, int DEPTH>
@@ -413,8 +387,8 @@ int run(TgArgs a, bool akf, bool bnf, int splits, float* final_out, hipStream_t 
   splits = (ktiles + per - 1) / per;
   if (splits <= 1) a.part = nullptr;
   const dim3 grid((a.N + tile.bn - 1) / tile.bn, (a.M + tile.bm - 1) / tile.bm, splits);
-  const bool va = vec_ok(akf ? a.ak : a.am, akf ? a.am : a.ak, a.a, akf ? a.K : a.M) && tg_vec();
-  const bool vb = !a.gather && vec_ok(bnf ? a.bn : a.bk, bnf ? a.bk : a.bn, a.b, bnf ? a.N : a.K) && tg_vec();
+  const bool va = vec_ok(akf ? a.ak : a.am, akf ? a.am : a.ak, a.a, akf ? a.K : a.M);
+  const bool vb = !a.gather && vec_ok(bnf ? a.bn : a.bk, bnf ? a.bk : a.bn, a.b, bnf ? a.N : a.K);
   launch_tile<kTile64.bm, kTile64.bn, kTile64.bk, 2>(a, akf, bnf, va, vb, grid, s);
   if (splits <= 1) return 1;
   if (defer && a.addend == nullptr) return splits;  // the consumer (fused BN, gradfinish) sums them

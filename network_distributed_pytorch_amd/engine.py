@@ -54,6 +54,9 @@ def default_config(**over) -> Dict[str, Any]:
         emulate_world=None, bucket_mb=None, reuse_query=True, overlap=None, psgd_groups=None,
         checkpoint_dir=None, resume=None, log_file=None, log_every=1, check_replicas_every=0,
         check_health_every=50, write_grad=False, verbose=True, trace_phases=False,
+        # MIOpen's deterministic solver for any conv the native kernels do not cover (bitwise
+        # resume); restored to the caller's setting by cleanup()
+        deterministic=True,
     )
     cfg.update(over)
     return cfg
@@ -71,6 +74,9 @@ def _log(config, *a):
         print(*a, flush=True)
 
 
+_SAVED_CUDNN: list = []
+
+
 def setup(config) -> None:
     """Seed, then ``init_process_group`` (ddp_guide_cifar10/ddp_init.py:64-99)."""
     torch.manual_seed(config["seed"] + config["rank"])
@@ -80,9 +86,12 @@ def setup(config) -> None:
         torch.cuda.set_device(device)
         # a library conv left on a path the native kernels do not cover runs MIOpen's
         # deterministic solution (no find-database / benchmark choice): a resumed run then
-        # reproduces the uninterrupted one bitwise
-        torch.backends.cudnn.deterministic = True
-        torch.backends.cudnn.benchmark = False
+        # reproduces the uninterrupted one bitwise.  Opt out with config["deterministic"] =
+        # False; cleanup() restores the previous process-wide values.
+        if config.get("deterministic", True):
+            _SAVED_CUDNN.append((torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark))
+            torch.backends.cudnn.deterministic = True
+            torch.backends.cudnn.benchmark = False
     if not dist.is_available():
         print("[Failure] Distributed Environment Failed")
         return
@@ -117,6 +126,9 @@ def cleanup(config=None) -> None:
         print(">>>>> PyTorch DDP Destroy <<<<<")
     if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()
+    if _SAVED_CUDNN:  # setup()'s determinism switch is process-wide: hand the old values back
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = _SAVED_CUDNN[0]
+        _SAVED_CUDNN.clear()
     if config is None or config.get("verbose", True):
         print("All ranks successfully destroyed")
         print("==============================\n")

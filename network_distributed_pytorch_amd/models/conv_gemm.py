@@ -18,18 +18,16 @@ the input is subsampled first.
 input geometry, the fastest native path:
   1. a direct fp32-MFMA kernel (csrc/conv.hip via ops/conv.py) for the ResNet CIFAR shapes
      it covers (stem 7x7/2 on 32x32, 3x3 on 8x8 and 4x4, 3x3/2 8x8->4x4);
-  2. the small-map kernels (csrc/smallconv.hip via ops/smconv.py) for the layer3 / layer4
-     geometries (3x3 on 2x2 / 1x1, the stride-2 entry convs and 1x1 downsamples, 1x1 on
-     2x2 / 1x1): compile-time (input pixel, output pixel, tap) pair lists on 16x16x4 MFMA,
-     grad-W written in W's own layout;
-  3. the strided / tabled MFMA GEMM kernel (csrc/tgemm.hip via ops/tgconv.py): 1x1 stride-1
-     convs on any power-of-two map (and, opt-in, the tabled small-map Toeplitz product);
-  4. the hipBLASLt Toeplitz GEMM form (``NDP_SM=0 NDP_TG=0``), and the CPU path;
-  5. MIOpen otherwise.
+  2. the strided / tabled MFMA GEMM kernel (csrc/tgemm.hip via ops/tgconv.py): 1x1 stride-1
+     convs on any power-of-two map;
+  3. the hipBLASLt Toeplitz GEMM form for the layer3 / layer4 small maps (``NDP_FUSION_OFF=tgemm``
+     sends the 1x1 convs there too), and the CPU path;
+  4. MIOpen otherwise.
+(Round 4's compile-time pair-list small-map kernels were correct but lost to the hipBLASLt
+Toeplitz GEMMs in the step — profiles/r4/smallconv.md — and were removed in round 5.)
 """
 from __future__ import annotations
 
-import os
 from typing import Dict, Tuple
 
 import torch
@@ -38,11 +36,9 @@ import torch.nn.functional as F
 
 from ..ops import gradfinish
 from ..ops._ext import ext
-from ..ops import conv as _conv
-from ..ops.conv import DirectConvFn, direct_plan, direct_plan_padded, side_stream
+from ..ops.conv import DirectConvFn, direct_plan, direct_plan_padded
 from ..ops.gradarena import grad_buffer
 from ..ops.gradlink import InjectGrad
-from ..ops.smconv import SmConvFn, sm_plan
 from ..ops.tgconv import TgConvFn, tg_plan
 
 __all__ = ["GemmConv2d", "ToeplitzBank", "toeplitz_maps", "eligible"]
@@ -114,34 +110,10 @@ class ToeplitzBank:
         return self.members[i][2]
 
 
-# grad-W GEMM of the Toeplitz layers on the side stream, concurrent with the grad-x GEMM (both are
-# small, latency-bound hipBLASLt launches at the strong-scaling batches); folds stay batched.
-# Opt-in (NDP_TOEP_FORK=1; NDP_CONV_FORK=1 forks every conv): measured SLOWER on 1x MI355X,
-# ResNet-18 r=4 batch 64 0.974 -> 1.170 ms, batch 512 1.877 -> 2.013 (the graph's fork / join
-# edges cost more than the overlap of two small GEMMs; profiles/r4/bench_toep_fork.jsonl)
-_TOEP_FORK = os.environ.get("NDP_TOEP_FORK", "0") == "1"
-
-
-# grad-W of a Toeplitz conv on the small-map grad-W kernel (csrc/smallconv.hip: dW in W's own
-# layout, no dW_big GEMM, no fold) where it covers the geometry.  Opt-in (NDP_TOEP_SMWGRAD=1):
-# measured slower than the hipBLASLt GEMM + batched fold on 1x MI355X (ResNet-18 r=4 b512
-# 1.904 -> 1.967 ms, b64 0.989 -> 1.019, ResNet-50 6.076 -> 6.112; profiles/r4/bench_toep_smwgrad.jsonl)
-_SM_WGRAD = os.environ.get("NDP_TOEP_SMWGRAD", "0") != "0"
-
-
-def _sm_wgrad_splits(geom, B: int) -> int:
-    """grad-W batch splits of the small-map kernel for this conv (0: not covered)."""
-    if not _SM_WGRAD:
-        return 0
-    cls, _, _, ws = ext().sm_plan(list(geom), int(B))
-    return int(ws) if cls >= 0 else 0
-
-
 class _ToeplitzConv(torch.autograd.Function):
     """Device tensors: W_big built / grad-W folded by csrc/conv.hip (index arithmetic, one
     launch each, or one expand launch for a whole :class:`ToeplitzBank`); CPU tensors (fp64
-    tests): the same maps as index tensors.  Where the small-map kernels cover the geometry,
-    grad-W comes straight from csrc/smallconv.hip instead of the dW_big GEMM and the fold."""
+    tests): the same maps as index tensors."""
 
     @staticmethod
     def forward(ctx, x, weight, src, dst, oh, ow, geom=None, bank=None, layer=None, link=None, branch=None):
@@ -162,7 +134,6 @@ class _ToeplitzConv(torch.autograd.Function):
             out = X @ w_big
         ctx.save_for_backward(X, w_big, dst)
         ctx.geom = geom
-        ctx.smw = _sm_wgrad_splits(geom, B) if (x.is_cuda and geom is not None) else 0
         ctx.weight = weight  # the Parameter: a deferred fold writes its adopted .grad
         ctx.link = link      # ops/gradlink.py: residual-branch gradient, folded in by addmm
         ctx.branch = branch if (branch is not None and x.is_cuda and geom is not None) else None
@@ -178,35 +149,15 @@ class _ToeplitzConv(torch.autograd.Function):
         G = g.reshape(g.shape[0], -1)
         dev = G.is_cuda and ctx.geom is not None
         dx = dw = None
-        if dev:  # grad-W (GEMM + fold) on the side stream, grad-x on the current one
-            main = torch.cuda.current_stream()
-            fork = (_conv.FORK_WGRAD or _TOEP_FORK) and ctx.needs_input_grad[0] and ctx.needs_input_grad[1]
-            if ctx.needs_input_grad[1] and ctx.smw:
-                dw = grad_buffer(ctx.weight)  # the dense arm's arena slice when registered
-                xs = X.view(ctx.x_shape)
-                gs = G.view(g.shape)
-                if ctx.smw > 1:  # batch-split slabs: summed in gradfinish's batched launch (or now)
-                    part = torch.empty(ctx.smw * dw.numel(), device=G.device, dtype=G.dtype)
-                    ext().sm_wgrad(xs, gs, part, list(ctx.geom))
-                    if gradfinish.can_defer(ctx.weight):
-                        gradfinish.defer_slab(part, dw, ctx.smw)
-                    else:
-                        ext().slab_sum(part, dw.view(-1), ctx.smw)
-                else:
-                    ext().sm_wgrad(xs, gs, dw, list(ctx.geom))
-                fork = False
-            elif ctx.needs_input_grad[1]:
+        if dev:  # grad-W: GEMM now, the fold in gradfinish's one batched launch
+            if ctx.needs_input_grad[1]:
                 dw = grad_buffer(ctx.weight)  # the dense arm's arena slice when registered
                 dwt = torch.empty(w_big.shape, device=G.device, dtype=G.dtype)
-                side = side_stream(G.device) if fork else main
-                side.wait_stream(main)
-                with torch.cuda.stream(side):
-                    torch.mm(G.t(), X, out=dwt)                   # [N, K]
-                    # one batched fold launch later (after this backward's join when forked)
-                    if (not fork or _TOEP_FORK) and gradfinish.can_defer(ctx.weight):
-                        gradfinish.defer_fold(dwt, dw, ctx.geom)
-                    else:
-                        ext().toeplitz_fold(dwt, dw, list(ctx.geom))
+                torch.mm(G.t(), X, out=dwt)                       # [N, K]
+                if gradfinish.can_defer(ctx.weight):
+                    gradfinish.defer_fold(dwt, dw, ctx.geom)
+                else:
+                    ext().toeplitz_fold(dwt, dw, list(ctx.geom))
             if ctx.needs_input_grad[0]:
                 addend = ctx.link.take() if ctx.link is not None else None
                 br = ctx.branch if ctx.branch is not None and ctx.branch.active() else None
@@ -224,8 +175,6 @@ class _ToeplitzConv(torch.autograd.Function):
                     if br is not None and other is None:  # first of the two: the sibling adds onto it
                         br.put(dx)
                         dx = None
-            if fork:
-                main.wait_stream(side)
             return dx, dw, None, None, None, None, None, None, None, None, None
         if ctx.needs_input_grad[0]:
             dx = (G @ w_big.t()).view(ctx.x_shape)
@@ -294,9 +243,6 @@ class GemmConv2d(nn.Conv2d):
                 xi = InjectGrad.apply(x, link) if link is not None else x
                 xp = torch.cat([xi, xi.new_zeros((Bp - B,) + tuple(x.shape[1:]))])
                 return DirectConvFn.apply(xp, self.weight, plan, None, None, None)[:B]
-            splan = sm_plan(x, self.weight, s, p)
-            if splan is not None:  # 2x2 / 1x1 maps: compile-time pair-list MFMA kernels (csrc/smallconv.hip)
-                return SmConvFn.apply(x, self.weight, splan, link, branch, slab_out, grad_slab)
             tplan = tg_plan(x, self.weight, s, p)
             if tplan is not None:  # pointwise 1x1 / small-map tabled GEMM (csrc/tgemm.hip)
                 return TgConvFn.apply(x, self.weight, tplan, link, branch, slab_out, grad_slab)

@@ -30,13 +30,14 @@ from ..ops.gradlink import GradLink
 from ..ops.layernorm import AddLayerNorm
 from ..ops.linear import Linear, linear_gelu, packed_qkv
 from ..ops.loss import cross_entropy as native_ce
+from ..knobs import fusion_on
 
 __all__ = ["DistilBertConfig", "DistilBertForSequenceClassification", "distilbert_base"]
 
-# one packed QKV projection read in place by the attention kernels (NDP_PACKED_QKV=0: three)
-PACKED_QKV = os.environ.get("NDP_PACKED_QKV", "1") != "0"
-# LayerNorm residual gradients folded into the next GEMM (NDP_LN_LINKS=0: autograd adds)
-LN_LINKS = os.environ.get("NDP_LN_LINKS", "1") != "0"
+# one packed QKV projection read in place by the attention kernels (NDP_FUSION_OFF=packed_qkv: three)
+PACKED_QKV = fusion_on("packed_qkv")
+# LayerNorm residual gradients folded into the next GEMM (NDP_FUSION_OFF=ln_links: autograd adds)
+LN_LINKS = fusion_on("ln_links")
 
 
 @dataclasses.dataclass

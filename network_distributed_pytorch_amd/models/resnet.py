@@ -26,22 +26,22 @@ from typing import List, Optional, Type, Union
 import torch
 import torch.nn as nn
 
-from ..ops import smstage
 from ..ops.batchnorm import BatchNormAct2d
 from ..ops.gradlink import BranchLink, GradLink
 from ..ops.linear import Linear
 from ..ops.pool import MaxPool2d
 from ..ops.slablink import SlabLink
 from .conv_gemm import GemmConv2d, ToeplitzBank
+from ..knobs import fusion_on
 
 __all__ = ["ResNet", "BasicBlock", "Bottleneck", "resnet18", "resnet34", "resnet50", "resnet101",
            "resnet152", "build_resnet"]
 
-# split-K slab hand-off between direct convs and fused BN (ops/slablink.py; NDP_SLAB_LINKS=0
+# split-K slab hand-off between direct convs and fused BN (ops/slablink.py; NDP_FUSION_OFF=slab_links
 # or tests flip it for A/B)
-SLAB_LINKS = os.environ.get("NDP_SLAB_LINKS", "1") != "0"
+SLAB_LINKS = fusion_on("slab_links")
 # downsample blocks: conv1 / downsample grad-x accumulated in place (ops/gradlink.BranchLink)
-BRANCH_LINKS = os.environ.get("NDP_BRANCH_LINKS", "1") != "0"
+BRANCH_LINKS = fusion_on("branch_links")
 
 
 def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -219,19 +219,17 @@ class ResNet(nn.Module):
             x = pooled if pooled is not None else self.maxpool(self.bn1(x, relu=True, slab_in=s0))
         else:
             x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        # the chained path calls the blocks directly: not when hooks sit on the layer modules
+        # (they would not fire)
         train_links = (self.fused and SLAB_LINKS and self.training and x.is_cuda and torch.is_grad_enabled()
-                       and all(isinstance(b, BasicBlock) for b in self.layer1))
+                       and all(isinstance(b, BasicBlock) for b in self.layer1)
+                       and not any(m._forward_hooks or m._forward_pre_hooks
+                                   for m in (self.layer1, self.layer2, self.layer3, self.layer4)))
         if train_links:  # block-boundary grad-x slab links (BasicBlock grad_in / grad_out)
             x = self._chain(list(self.layer1) + list(self.layer2), x)
-        else:
-            x = self.layer2(self.layer1(x))
-        blocks = smstage.stage_blocks(self, x) if (self.fused and self.training) else None
-        if blocks is not None:  # layer3 + layer4 as one node, BatchNorm fused into the convs (ops/smstage.py)
-            x = smstage.run_stage(blocks, x)
-        elif train_links:
             x = self._chain(list(self.layer3) + list(self.layer4), x)
         else:
-            x = self.layer4(self.layer3(x))
+            x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         # 1x1 feature map (32x32 inputs): the average is the value itself; flatten skips a
         # mean kernel forward and its broadcast-divide backward (bitwise identical)
         x = torch.flatten(x if x.shape[-2:] == (1, 1) else self.avgpool(x), 1)

@@ -21,6 +21,7 @@ import torch.nn.functional as F
 
 from ._ext import ext
 from .gradarena import grad_buffer
+from ..knobs import fusion_on
 
 __all__ = ["BatchNormAct2d", "bn_act"]
 
@@ -122,11 +123,11 @@ class _BNReluPoolFn(torch.autograd.Function):
 
 
 # BN backward statistics from the grad-x epilogue of the conv producing dy (ops/slablink.py;
-# NDP_BN_BWD_STATS=0: the BN's own statistics pass)
-_BWD_STATS = os.environ.get("NDP_BN_BWD_STATS", "1") != "0"
+# NDP_FUSION_OFF=bn_bwd_stats: the BN's own statistics pass)
+_BWD_STATS = fusion_on("bn_bwd_stats")
 
-# the stem tail BN -> ReLU -> MaxPool in one pass (NDP_STEM_POOL=0: BN kernel + pool kernel)
-STEM_POOL = os.environ.get("NDP_STEM_POOL", "1") != "0"
+# the stem tail BN -> ReLU -> MaxPool in one pass (NDP_FUSION_OFF=stem_pool: BN kernel + pool kernel)
+STEM_POOL = fusion_on("stem_pool")
 
 
 def bn_act(x, weight, bias, running_mean, running_var, nbt, part, training, momentum, eps,
@@ -171,8 +172,8 @@ class BatchNormAct2d(nn.BatchNorm2d):
         # per-(channel, slice) fp64 partials: C * S * 2 with S <= ceil(1024 / C) (bn_slices)
         self.register_buffer("_part", torch.zeros((num_features + 1024) * 2, dtype=torch.float64),
                              persistent=False)
-        # single-launch small-map kernels (HW <= 4, N <= 512); NDP_BN_SINGLE=0: 3-kernel path (A/B)
-        self.fused_small = os.environ.get("NDP_BN_SINGLE", "1") != "0"
+        # single-launch small-map kernels (HW <= 16, N <= 512); False: the 3-kernel path (tests)
+        self.fused_small = True
 
     def _ensure_part(self, x: torch.Tensor) -> None:
         """Grow the fp64 partial-sum scratch to what this input shape needs (first call for

@@ -5,8 +5,8 @@ hand-written gfx950 kernels for the shape classes the extension reports through
 ``conv_plan`` (ResNet stem 7x7/2 on 32x32, layer1 3x3 on 8x8, layer2 3x3 on 4x4, its
 strided 8x8->4x4 entry conv and its 1x1/2 downsample).  Grad-input of the strided 3x3 class
 runs natively as the layer1 grad-x kernel on the zero-inserted dY (zeros from the LDS staging;
-exact); ``NDP_CONV_DGRAD2=0`` sends it to MIOpen, whose find-database-dependent algorithm was
-found non-deterministic and NaN-producing under hipGraph capture;  the 1x1/2
+exact; MIOpen's find-database-dependent algorithm for it was found non-deterministic and
+NaN-producing under hipGraph capture);  the 1x1/2
 downsample's grad-input is the transposed 1x1 product written to the even pixels; the stem's
 input never needs a gradient.
 :func:`direct_plan` returns None for every other geometry, so callers keep their MIOpen /
@@ -22,16 +22,16 @@ import torch
 from . import gradfinish
 from ._ext import ext
 from .gradarena import grad_buffer
+from ..knobs import fusion_on
 
-__all__ = ["direct_plan", "conv2d_direct", "DirectConvFn", "side_stream"]
+__all__ = ["direct_plan", "conv2d_direct", "DirectConvFn"]
 
 _PLANS: dict = {}
 _STATS: dict = {}
-_SIDE: dict = {}
 
 # BatchNorm statistics from the forward epilogue where the consuming BN takes the large-map
-# path (stem, layer1; ops/slablink.py).  NDP_CONV_BNSTATS=0 restores the BN statistics pass.
-CONV_BN_STATS = os.environ.get("NDP_CONV_BNSTATS", "1") != "0"
+# path (stem, layer1; ops/slablink.py).  NDP_FUSION_OFF=conv_bnstats restores the BN statistics pass.
+CONV_BN_STATS = fusion_on("conv_bnstats")
 
 
 def stats_slices(geom, B: int) -> int:
@@ -40,25 +40,6 @@ def stats_slices(geom, B: int) -> int:
     if key not in _STATS:
         _STATS[key] = int(ext().conv_stats_slices(list(geom), int(B))) if CONV_BN_STATS else 0
     return _STATS[key]
-
-# grad-W on a side stream measured SLOWER on ResNet-18 (2.47 vs 2.37 ms/step: the two
-# halves contend for CUs / L2 instead of filling gaps), so it is opt-in.
-FORK_WGRAD = os.environ.get("NDP_CONV_FORK", "0") == "1"
-
-
-def side_stream(device: torch.device) -> torch.cuda.Stream:
-    """Per-device side stream for the weight-gradient half of a conv backward.
-
-    grad-x and grad-W of one convolution are independent: grad-W (and its slab sum) runs
-    on this stream while grad-x runs on the current one, joined before the backward
-    returns — concurrent kernels on the GPU, a fork/join in a captured hipGraph.  All
-    buffers are allocated on the current stream before the fork, so the caching allocator
-    never hands a block to one stream while the other still reads it.
-    """
-    idx = device.index if device.index is not None else torch.cuda.current_device()
-    if idx not in _SIDE:
-        _SIDE[idx] = torch.cuda.Stream(device=idx)
-    return _SIDE[idx]
 
 
 def direct_plan(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int) -> Optional[Tuple]:
@@ -141,25 +122,22 @@ class DirectConvFn(torch.autograd.Function):
         s, p = geom[6], geom[7]
         dy = dy.contiguous()
         dx = dw = None
-        main = torch.cuda.current_stream()
-        fork = FORK_WGRAD and ctx.needs_input_grad[0] and ctx.needs_input_grad[1]
         if ctx.needs_input_grad[1]:
             B = x.shape[0]
             dw = grad_buffer(ctx.weight, weight)  # the dense arm's arena slice when registered
             part = torch.empty((B // wgrad_imgs) * weight.numel(), device=x.device, dtype=x.dtype)
-            side = side_stream(x.device) if fork else main
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                if not fork and gradfinish.can_defer(ctx.weight):  # slabs now, one batched sum later
-                    ext().conv_wgrad(x, dy, part, None, list(geom))
-                    gradfinish.defer_slab(part, dw, B // wgrad_imgs)
-                else:
-                    ext().conv_wgrad(x, dy, part, dw, list(geom))
+            if gradfinish.can_defer(ctx.weight):  # slabs now, one batched sum later
+                ext().conv_wgrad(x, dy, part, None, list(geom))
+                gradfinish.defer_slab(part, dw, B // wgrad_imgs)
+            else:
+                ext().conv_wgrad(x, dy, part, dw, list(geom))
         addend = ctx.link.take() if ctx.link is not None else None
         if ctx.needs_input_grad[0]:
             grad_slab = ctx.grad_slab
-            if ctx.branch is not None and not ctx.branch.active():
-                grad_slab = None  # a sibling outside the link: autograd adds the two grad-x tensors
+            if ctx.branch is not None and not (ctx.branch.active() and ctx.branch.all_direct()):
+                # a sibling outside the link, or one that is not a direct kernel (its grad-x is
+                # added later): the previous BN2 must not take this grad-x alone
+                grad_slab = None
 
             def dgrad(addend):
                 if not dgrad_direct:
@@ -207,8 +185,6 @@ class DirectConvFn(torch.autograd.Function):
                 if br is not None and other is None:  # first of the two: the sibling adds onto it
                     br.put(dx)
                     dx = None
-        if fork:
-            main.wait_stream(side)
         return dx, dw, None, None, None, None, None
 
 

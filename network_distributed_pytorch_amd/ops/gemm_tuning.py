@@ -17,7 +17,7 @@ validator lines (PyTorch / HIP / hipBLASLt / rocBLAS versions, gfx arch); on any
 TunableOp rejects it and :func:`enable` switches TunableOp back off.
 
 Environment:
-  NDP_TUNED_GEMMS=0          do not load the table (library defaults)
+  NDP_FUSION_OFF=tuned_gemms do not load the table (library defaults)
   PYTORCH_TUNABLEOP_ENABLED  set by the user: TunableOp is theirs, :func:`enable` does nothing
                              (how the table is (re)measured: tools/gpu_r2_tunable.sh)
 
@@ -30,6 +30,7 @@ import os
 import warnings
 
 import torch
+from ..knobs import fusion_on
 
 __all__ = ["TABLE", "enable", "disable", "enabled", "table_shapes"]
 
@@ -57,7 +58,7 @@ def enable(path: str = TABLE) -> bool:
     """Load the measured solution table (idempotent).  Returns True when it is in use."""
     if _STATE["enabled"]:
         return True
-    if os.environ.get("NDP_TUNED_GEMMS", "1") == "0" or "PYTORCH_TUNABLEOP_ENABLED" in os.environ:
+    if not fusion_on("tuned_gemms") or "PYTORCH_TUNABLEOP_ENABLED" in os.environ:
         return False
     if not torch.cuda.is_available() or torch.version.hip is None or not os.path.exists(path):
         return False

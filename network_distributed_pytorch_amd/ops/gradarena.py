@@ -19,6 +19,7 @@ import weakref
 from typing import Iterable
 
 import torch
+from ..knobs import fusion_on
 
 __all__ = ["register", "unregister", "grad_buffer", "registered", "release"]
 
@@ -35,7 +36,7 @@ def _task_id() -> int:
         return int(torch._C._current_graph_task_id())
     except Exception:  # pragma: no cover - older torch: no task ids, one handout per release
         return -2
-_ON = os.environ.get("NDP_GRAD_ARENA", "1") != "0"
+_ON = fusion_on("grad_arena")
 
 
 def register(param: torch.Tensor, arena: torch.Tensor, offset: int) -> None:

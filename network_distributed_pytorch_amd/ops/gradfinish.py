@@ -10,7 +10,7 @@ earlier when a consumer needs them mid-backward (:func:`flush`: the overlapped g
 sync calls it before handing a group's gradients to the side stream).  Same summation
 order per element as the per-layer kernels: results are bitwise identical.
 
-Capture-safe (kernel arguments only, no table uploads).  ``NDP_DEFER_GRADW=0`` restores
+Capture-safe (kernel arguments only, no table uploads).  ``NDP_FUSION_OFF=defer_gradw`` restores
 per-layer launches.
 """
 from __future__ import annotations
@@ -20,11 +20,12 @@ import os
 import torch
 
 from ._ext import ext
+from ..knobs import fusion_on
 
 __all__ = ["enabled", "can_defer", "defer_slab", "defer_fold", "flush", "pending"]
 
 _MAX = 24  # csrc/ndp_kernels.h kMaxExpand
-_ENABLED = os.environ.get("NDP_DEFER_GRADW", "1") != "0"
+_ENABLED = fusion_on("defer_gradw")
 _slabs: list = []
 _folds: list = []
 _queued = [False]
@@ -52,11 +53,35 @@ def _end_of_backward():
     flush()
 
 
+def _task_id() -> int:
+    try:
+        return int(torch._C._current_graph_task_id())
+    except Exception:  # pragma: no cover - older torch: no task ids
+        return -2
+
+
+# id(param) -> autograd graph task in which a gradient of the param was deferred
+_CLAIMED: dict = {}
+
+
 def can_defer(param: torch.Tensor) -> bool:
     """Deferral needs the returned buffer to BE the final gradient: ``param.grad is None``
     (AccumulateGrad adopts the buffer, or ``autograd.grad`` returns it) and no
-    double-backward graph."""
-    return _ENABLED and param.grad is None and not torch.is_grad_enabled()
+    double-backward graph.
+
+    A parameter used twice in one forward (shared / tied module) gets a second gradient in
+    the SAME graph task before AccumulateGrad adopted the first; autograd then adds the two
+    buffers as soon as the second arrives.  So the first claim of a task defers, and a
+    second one finishes every pending sum right now (stream-ordered before autograd's add
+    reads the first buffer) and is computed immediately."""
+    if not (_ENABLED and param.grad is None and not torch.is_grad_enabled()):
+        return False
+    task = _task_id()
+    if _CLAIMED.get(id(param)) == task:
+        flush()
+        return False
+    _CLAIMED[id(param)] = task
+    return True
 
 
 def _alias(t: torch.Tensor) -> torch.Tensor:

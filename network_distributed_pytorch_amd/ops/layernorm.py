@@ -7,7 +7,7 @@ affine, the sum saved for backward) and the backward as one row kernel plus one 
 reduction of the [dgamma | dbeta] partials — deterministic and hipGraph-replayable — instead
 of PyTorch-ROCm's add + LayerNorm + three backward kernels.  Same parameters / ``state_dict``
 as ``nn.LayerNorm`` (HF checkpoints load unchanged).  CPU tensors, other dtypes, unsupported
-widths (last dim not 256/512/768/1024) or ``NDP_FUSED_LN=0`` run the PyTorch ops.
+widths (last dim not 256/512/768/1024) or ``NDP_FUSION_OFF=fused_ln`` run the PyTorch ops.
 
 HF DistilBERT's hidden dropouts ride in the same kernels: ``p_in`` drops the sublayer output
 before the residual add (FFN: ``LN(dropout(lin2(.)) + x)``), ``p_out`` drops the normalised
@@ -27,10 +27,11 @@ import torch.nn.functional as F
 
 from . import gradfinish
 from ._ext import ext
+from ..knobs import fusion_on
 
 __all__ = ["AddLayerNorm", "add_layer_norm", "ln_keep_mask"]
 
-_ENABLED = os.environ.get("NDP_FUSED_LN", "1") != "0"
+_ENABLED = fusion_on("fused_ln")
 _WIDTHS = (256, 512, 768, 1024)
 _M32 = 0xFFFFFFFF
 

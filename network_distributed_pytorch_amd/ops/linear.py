@@ -18,14 +18,15 @@ from . import gradfinish
 from ._ext import ext
 from .gradarena import grad_buffer, registered
 from .gradlink import InjectGrad
+from ..knobs import fusion_on
 
 __all__ = ["Linear", "linear", "linear_gelu", "packed_qkv"]
 
-# the fused native GELU-backward + bias-sum pass (NDP_FUSED_GELU=0: ATen GELU backward + the
+# the fused native GELU-backward + bias-sum pass (NDP_FUSION_OFF=fused_gelu: ATen GELU backward + the
 # native bias sum).  Exact (tests/test_linear_gpu.py).  Round 3 measured it slower (~250
 # column-strip workgroups, one load in flight per thread); with ~1024 workgroups and 4 rows in
 # flight per thread it is on: DistilBERT r=8, 1x MI355X, 20.70 vs 20.74 ms (profiles/r4).
-_FUSED_GELU = os.environ.get("NDP_FUSED_GELU", "1") != "0"
+_FUSED_GELU = fusion_on("fused_gelu")
 
 
 def _deferrable(out: torch.Tensor, params) -> bool:

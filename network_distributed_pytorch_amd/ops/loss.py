@@ -20,11 +20,12 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ._ext import ext
+from ..knobs import fusion_on
 
 __all__ = ["cross_entropy", "CrossEntropyLoss"]
 
 _CTR: dict = {}
-_ENABLED = os.environ.get("NDP_FUSED_CE", "1") != "0"  # =0: PyTorch-ROCm's loss kernels (A/B)
+_ENABLED = fusion_on("fused_ce")  # =0: PyTorch-ROCm's loss kernels (A/B)
 
 
 def _counter(device: torch.device) -> torch.Tensor:

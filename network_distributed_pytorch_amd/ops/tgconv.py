@@ -14,8 +14,9 @@ all on one hand-written gfx950 MFMA GEMM kernel:
 
 Split-K slabs are summed in a fixed order (deterministic) — by the kernel's own slab sum,
 by the fused BN kernel that consumes the conv (``slab_out`` / ``grad_slab``,
-ops/slablink.py) or by gradfinish's batched sum (grad-W).  ``NDP_TG=0`` disables the path
-(``NDP_TG_SMALL=0`` / ``NDP_TG_PW=0`` one family), restoring Toeplitz / MIOpen.
+ops/slablink.py) or by gradfinish's batched sum (grad-W).  ``NDP_FUSION_OFF=tgemm`` disables the path, restoring Toeplitz / MIOpen.  The ``small``
+family and the pointwise kernel on 1x1 maps are off (measured slower; tests switch them on
+through the module constants).
 """
 from __future__ import annotations
 
@@ -27,16 +28,17 @@ import torch
 from . import gradfinish
 from ._ext import ext
 from .gradarena import grad_buffer
+from ..knobs import fusion_on
 
 __all__ = ["tg_plan", "TgConvFn", "enabled"]
 
 _PLANS: dict = {}
-_ON = os.environ.get("NDP_TG", "1") != "0"
+_ON = fusion_on("tgemm")
 # small-map family off by default: measured 0.46-0.72x the hipBLASLt Toeplitz GEMMs on the
 # ResNet-18 layer3 / layer4 shapes at batch 64 / 512 (tools/tg_bench.py, profiles/r3/tg_bench.md)
-_SMALL = os.environ.get("NDP_TG_SMALL", "0") != "0"
-_PW = os.environ.get("NDP_TG_PW", "1") != "0"
-_PW1 = os.environ.get("NDP_TG_PW1", "0") != "0"  # pointwise on 1x1 maps (measured slower: off)
+_SMALL = False
+_PW = True
+_PW1 = False  # pointwise on 1x1 maps (measured slower: off)
 POINTWISE, SMALL = 0, 1
 
 

@@ -39,6 +39,7 @@ import torch
 
 from ..ops import SegPlan, capturing, ext, gradfinish, upload, upload_epoch
 from .comm import Communicator, n_bits
+from ..knobs import fusion_on
 
 __all__ = [
     "plan_layout",
@@ -426,7 +427,7 @@ class PowerSGDOptimizer:
     ``write_grad=True`` also leaves ``p.grad = out + m`` exactly like the reference loop
     (ddp_init.py:172); it costs one extra write pass and is off by default.
 
-    **Lazy error feedback** (native, rank <= 16; ``NDP_PSGD_LAZY_EF=0`` turns it off): the
+    **Lazy error feedback** (native, rank <= 16; ``NDP_FUSION_OFF=lazy_ef`` turns it off): the
     update pass does not store ``e = M - P Q^T`` — it would read ``M`` back only for that
     store, 2 of its 6 arena passes.  The arena keeps ``M`` and ``p_prev`` keeps the step's
     P-hat; the next P pass forms ``e`` element by element with the update kernel's exact
@@ -495,7 +496,7 @@ class PowerSGDOptimizer:
         self.native = self.buf.native
         # needs the warm-start Q of the next P pass to BE the update's Qs (reuse_query)
         self.lazy_ef = (self.native and bool(shapes) and self.buf.max_rank <= _LAZY_MAX_RANK and reuse_query
-                        and os.environ.get("NDP_PSGD_LAZY_EF", "1") != "0")
+                        and fusion_on("lazy_ef"))
         self._lazy_pending = False  # an update ran since e was last materialised
         # P-hat of the last update (lazy error feedback); zero = no pending correction
         self.p_prev = torch.zeros(self.buf.p_total if self.lazy_ef else 0, **f32)

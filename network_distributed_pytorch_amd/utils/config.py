@@ -73,6 +73,7 @@ class TrainConfig:
     verbose: bool = True
     trace_phases: bool = False
     toy_mlp_steps: int = 0
+    deterministic: bool = True  # MIOpen's deterministic solver while the run lasts (engine.setup)
 
 
 _FIELDS = {f.name: f for f in dataclasses.fields(TrainConfig)}

@@ -53,9 +53,10 @@ import torch.distributed as dist
 
 from ..ops import _UPLOADS, ext
 from ..parallel.comm import world_size
+from ..knobs import fusion_on
 
-# NDP_DEFER_UPLOADS=0: capture-time table uploads stay memcpy nodes re-run on every replay
-_DEFER_UPLOADS = os.environ.get("NDP_DEFER_UPLOADS", "1") != "0"
+# NDP_FUSION_OFF=defer_uploads: capture-time table uploads stay memcpy nodes re-run on every replay
+_DEFER_UPLOADS = fusion_on("defer_uploads")
 
 __all__ = ["StepRunner", "GraphedStep", "auto_mode"]
 

@@ -1,6 +1,5 @@
-"""Direct fp32-MFMA convolutions (csrc/conv.hip) vs an fp64 CPU oracle (F.conv2d).
-(The 3x3 stride-2 native grad-x is opt-in, NDP_CONV_DGRAD2=1: run this file with it set to
-cover that kernel, as tools/gpu_r2_dgrad2.sh did.)"""
+"""Direct fp32-MFMA convolutions (csrc/conv.hip) vs an fp64 CPU oracle (F.conv2d), every
+direction of every class, including the 3x3 stride-2 grad-x on the zero-inserted dY."""
 import pytest
 import torch
 import torch.nn.functional as F
