@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
+#include <string>
+
 #include "ndp_kernels.h"
 
 namespace ndp {
@@ -648,6 +650,19 @@ __global__ __launch_bounds__(256) void bn_small_apply_kernel(
 // fold of the 8 per-wave partials through LDS.  CW trades grid size (C*HW / CW workgroups;
 // 256 CUs to fill) against row-segment width per load (CW * 4 bytes): bn_colw_for picks
 // it by measurement.  Used when N <= 512 (ResNet's per-GPU batch).
+// NDP_FUSION_OFF=bn_vec4 (knobs.py): the scalar single-launch kernel, for A/B arms; tests flip
+// it through bn_set_vec4
+static int g_bn_vec4 = -1;
+static bool vec_off() {
+  if (g_bn_vec4 < 0) {
+    const char* e = getenv("NDP_FUSION_OFF");
+    const std::string s = std::string(",") + (e ? e : "") + ",";
+    g_bn_vec4 = (s.find(",bn_vec4,") != std::string::npos || s.find(",all,") != std::string::npos) ? 0 : 1;
+  }
+  return g_bn_vec4 == 0;
+}
+void bn_set_vec4(bool on) { g_bn_vec4 = on ? 1 : 0; }
+
 constexpr int kFusedThreads = 512;
 constexpr int kFusedMaxN = 512;
 
@@ -815,6 +830,219 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
   }
 }
 
+// The same single-launch BN with one float4 (4 consecutive columns) per thread instead of one
+// float.  The scalar kernel's loads are 64-lane dword accesses: at batch 512 its 128 workgroups
+// were bound by the texture-address rate of half the CUs (16 B/clk/CU, ~2 TB/s effective: the
+// layer2 backward took 16.5 µs for 21 MB, profiles/r4/kernels_b512_head.md).  dwordx4 moves 4x
+// the bytes per address cycle.  A float4 holds whole channels' pixel runs: one channel (HW >= 4,
+// its HW/4 float4s on adjacent lanes) or 4 / HW channels (HW = 1, 2: separate sums per
+// channel).  Same fp64 sums, same fixed-order fold: deterministic run to run.
+template <int HW, int BWD, int CW, int MAXN = kFusedMaxN>
+__global__ __launch_bounds__(kFusedThreads) void bn_small_fused_v4_kernel(
+    const float* __restrict__ x, const float* __restrict__ res, const float* __restrict__ dy,
+    const float* __restrict__ yin, const float* __restrict__ gamma, const float* __restrict__ beta,
+    float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt, float* __restrict__ save_mean,
+    float* __restrict__ save_invstd, float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ out,
+    float* __restrict__ dres, int N, int C, float eps, float momentum, int relu, const float* __restrict__ src,
+    int nslab) {
+  constexpr int CT = CW / 4;                   // threads per row
+  constexpr int RG = kFusedThreads / CT;       // row groups
+  constexpr int NP = (MAXN + RG - 1) / RG;     // rows per thread
+  constexpr int NW = kFusedThreads / 64;
+  constexpr int NCH = HW >= 4 ? 1 : 4 / HW;    // channels per float4
+  constexpr int CPC = HW >= 4 ? 4 : HW;        // components per channel inside a float4
+  constexpr int LPC = HW >= 4 ? HW / 4 : 1;    // lanes per channel
+  constexpr int CPW = CW / HW;                 // channels per workgroup
+  static_assert(CW % 4 == 0 && CW % HW == 0 && CT <= 64 && 64 % CT == 0, "bad column block");
+  __shared__ double red[2][NW][CPW];
+  const int CHW = C * HW;
+  const int ct = threadIdx.x % CT, g = threadIdx.x / CT, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int cb = xcd_block((int)blockIdx.x, (int)gridDim.x);
+  const int j0 = cb * CW + 4 * ct;
+  const bool ok_col = j0 < CHW;
+  const int c0 = ok_col ? j0 / HW : 0;  // first channel of this float4
+  float mean_s[NCH], invstd_s[NCH], gam[NCH], bet[NCH], rm[NCH], rv[NCH];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int c = c0 + i;
+    mean_s[i] = 0.f; invstd_s[i] = 0.f; gam[i] = 1.f; bet[i] = 0.f; rm[i] = 0.f; rv[i] = 0.f;
+    if (ok_col) {
+      if (BWD) {
+        mean_s[i] = save_mean[c];
+        invstd_s[i] = save_invstd[c];
+      }
+      if (gamma) gam[i] = gamma[c];
+      if (!BWD && beta) bet[i] = beta[c];
+      if (!BWD && rmean != nullptr && g == 0) {
+        rm[i] = rmean[c];
+        rv[i] = rvar[c];
+      }
+    }
+  }
+  f32x4 v[NP], d[NP], m[NP];
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f}, one = {1.f, 1.f, 1.f, 1.f};
+  const int64_t slab = (int64_t)N * CHW;
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {  // every load in flight before any use
+    const int n = g + k * RG;
+    const bool ok = ok_col && n < N;
+    const int64_t o = (int64_t)n * CHW + j0;
+    f32x4 sum = zero;
+    if (src != nullptr && ok) {  // deferred split-K sum, slab order (bitwise = conv_slab_sum)
+      sum = *reinterpret_cast<const f32x4*>(src + o);
+      for (int z = 1; z < nslab; ++z) sum += *reinterpret_cast<const f32x4*>(src + z * slab + o);
+      if (BWD && res != nullptr) sum += *reinterpret_cast<const f32x4*>(res + o);
+    }
+    if (!BWD) {
+      v[k] = ok ? (src ? sum : *reinterpret_cast<const f32x4*>(x + o)) : zero;
+      d[k] = (ok && res) ? *reinterpret_cast<const f32x4*>(res + o) : zero;
+    } else {
+      v[k] = ok ? *reinterpret_cast<const f32x4*>(x + o) : zero;
+      d[k] = ok ? (src ? sum : *reinterpret_cast<const f32x4*>(dy + o)) : zero;
+      m[k] = (ok && relu) ? *reinterpret_cast<const f32x4*>(yin + o) : one;
+    }
+  }
+  if (!BWD && src != nullptr) {  // BN's saved input = the conv output
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const int n = g + k * RG;
+      if (ok_col && n < N) *reinterpret_cast<f32x4*>(const_cast<float*>(x) + (int64_t)n * CHW + j0) = v[k];
+    }
+  }
+  double a[NCH], b[NCH];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) a[i] = b[i] = 0.0;
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    if (ok_col && g + k * RG < N) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = e / CPC;
+        if (!BWD) {
+          a[i] += (double)v[k][e];
+          b[i] += (double)v[k][e] * (double)v[k][e];
+        } else {
+          const float dz = (m[k][e] > 0.f) ? d[k][e] : 0.f;
+          a[i] += (double)dz;
+          b[i] += (double)dz * (double)((v[k][e] - mean_s[i]) * invstd_s[i]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+#pragma unroll
+    for (int o = LPC / 2; o > 0; o >>= 1) {  // the float4s of a channel are adjacent lanes
+      a[i] += __shfl_xor(a[i], o, 64);
+      b[i] += __shfl_xor(b[i], o, 64);
+    }
+#pragma unroll
+    for (int o = CT; o < 64; o <<= 1) {  // row groups inside the wave
+      a[i] += __shfl_xor(a[i], o, 64);
+      b[i] += __shfl_xor(b[i], o, 64);
+    }
+  }
+  // channel slot of this thread's first channel inside the workgroup
+  const int slot = (4 * ct) / HW;
+  const bool lead = HW >= 4 ? ((4 * ct) % HW) == 0 : true;  // one writer lane per channel
+  if (lane < CT && lead) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      red[0][wave][slot + i] = a[i];
+      red[1][wave][slot + i] = b[i];
+    }
+  }
+  __syncthreads();
+  double A[NCH], B[NCH];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    A[i] = B[i] = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      A[i] += red[0][w][slot + i];
+      B[i] += red[1][w][slot + i];
+    }
+  }
+  if (!ok_col) return;
+  const double M = (double)N * HW;
+  const bool writer = g == 0 && lead;
+  if (!BWD) {
+    f32x4 sc, sh;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const double mu = A[i] / M;
+      double var = B[i] / M - mu * mu;
+      if (var < 0.0) var = 0.0;
+      const float mean = (float)mu, invstd = (float)(1.0 / sqrt(var + (double)eps));
+      const float scale = gam[i] * invstd;
+      const float shift = bet[i] - mean * scale;
+#pragma unroll
+      for (int e = 0; e < CPC; ++e) {
+        sc[i * CPC + e] = scale;
+        sh[i * CPC + e] = shift;
+      }
+      if (writer) {
+        const int c = c0 + i;
+        save_mean[c] = mean;
+        save_invstd[c] = invstd;
+        if (rmean != nullptr) {
+          const double unb = M > 1.0 ? var * M / (M - 1.0) : var;
+          rmean[c] = (float)((1.0 - momentum) * (double)rm[i] + momentum * mu);
+          rvar[c] = (float)((1.0 - momentum) * (double)rv[i] + momentum * unb);
+        }
+        if (nbt != nullptr && c == 0) nbt[0] += 1;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const int n = g + k * RG;
+      if (n < N) {
+        f32x4 z;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float t = fmaf(v[k][e], sc[e], sh[e]) + d[k][e];
+          z[e] = relu ? fmaxf(t, 0.f) : t;
+        }
+        *reinterpret_cast<f32x4*>(out + (int64_t)n * CHW + j0) = z;
+      }
+    }
+  } else {
+    f32x4 k1, mdz, mdzx, mu, is;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      if (writer) {
+        if (dgamma) dgamma[c0 + i] = (float)B[i];
+        if (dbeta) dbeta[c0 + i] = (float)A[i];
+      }
+#pragma unroll
+      for (int e = 0; e < CPC; ++e) {
+        k1[i * CPC + e] = gam[i] * invstd_s[i];
+        mdz[i * CPC + e] = (float)(A[i] / M);
+        mdzx[i * CPC + e] = (float)(B[i] / M);
+        mu[i * CPC + e] = mean_s[i];
+        is[i * CPC + e] = invstd_s[i];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const int n = g + k * RG;
+      if (n < N) {
+        f32x4 o4, z4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float dz = (m[k][e] > 0.f) ? d[k][e] : 0.f;
+          const float xh = (v[k][e] - mu[e]) * is[e];
+          o4[e] = k1[e] * (dz - mdz[e] - xh * mdzx[e]);
+          z4[e] = dz;
+        }
+        const int64_t o = (int64_t)n * CHW + j0;
+        *reinterpret_cast<f32x4*>(out + o) = o4;
+        if (dres) *reinterpret_cast<f32x4*>(dres + o) = z4;
+      }
+    }
+  }
+}
+
 // Single-launch small-map path: HW in {1, 2, 4, 8, 16} (ResNet-18 step on 1x MI355X: HW <= 4 ->
 // 2.165 ms, <= 16 (layer2 too) -> 2.150 ms), N <= kFusedMaxN.  The 8x8 maps of layer1 (64
 // workgroups, one per channel) measured slower than the two-kernel path at batch 64 / 128
@@ -845,11 +1073,21 @@ static void launch_small_fused_cw(int HW, const float* x, const float* res, cons
                                   int C, float eps, float momentum, int relu, hipStream_t s, const float* src,
                                   int nslab) {
   const int nblk = (int)(((int64_t)C * HW + CW - 1) / CW);
+  auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  // float4 kernel: rows of whole float4s, 16-B aligned operands (every ResNet launch)
+  const bool v4 = ((int64_t)C * HW) % 4 == 0 && a16(x) && a16(res) && a16(dy) && a16(yin) && a16(out) &&
+                  a16(dres) && a16(src) && !vec_off();
 #define NDP_BN_FUSED(HWV)                                                                                          \
-  if constexpr (CW % HWV == 0)                                                                                     \
-    hipLaunchKernelGGL((bn_small_fused_kernel<HWV, BWD, CW, kFusedMaxN>), dim3((unsigned)nblk), dim3(kFusedThreads), \
-                       0, s, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out, dres, N, C, \
-                       eps, momentum, relu, src, nslab)
+  if constexpr (CW % HWV == 0) {                                                                                   \
+    if (v4)                                                                                                        \
+      hipLaunchKernelGGL((bn_small_fused_v4_kernel<HWV, BWD, CW, kFusedMaxN>), dim3((unsigned)nblk),               \
+                         dim3(kFusedThreads), 0, s, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma,  \
+                         dbeta, out, dres, N, C, eps, momentum, relu, src, nslab);                                   \
+    else                                                                                                           \
+      hipLaunchKernelGGL((bn_small_fused_kernel<HWV, BWD, CW, kFusedMaxN>), dim3((unsigned)nblk),                  \
+                         dim3(kFusedThreads), 0, s, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma,  \
+                         dbeta, out, dres, N, C, eps, momentum, relu, src, nslab);                                   \
+  }
   switch (HW) {  // the caller picks CW >= HW
     case 1: NDP_BN_FUSED(1); break;
     case 2: NDP_BN_FUSED(2); break;

@@ -1223,6 +1223,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_two_kernel_path", [](int64_t N, int64_t C, int64_t HW, bool single) {
     return ndp::bn_two_kernel_path((int)N, (int)C, (int)HW, single ? 1 : 0);
   });
+  m.def("bn_set_vec4", &ndp::bn_set_vec4);
   m.def("bn_slices", &bn_slices);
   m.def("slab_sum", &slab_sum);
   m.def("bn_part_numel", &bn_part_numel);

@@ -148,6 +148,7 @@ void launch_bn_bwd(const float* dy, const float* y, const float* x, const float*
 // mbeta (nullable, relu, two-kernel path only): y was never stored; the ReLU mask is recomputed
 // from x as fmaf(x, gamma * invstd, beta - mean * gamma * invstd) > 0 (the forward's own ops)
 bool bn_two_kernel_path(int N, int C, int HW, int single);
+void bn_set_vec4(bool on);
 // BN (training) -> ReLU -> MaxPool(3, 2, 1) in one pass without storing the BN output (the
 // ResNet stem tail); y / idx: the pooled output and its uint8 window offsets (pool.hip layout)
 void launch_bn_relu_maxpool(const float* x, float* y, uint8_t* idx, const float* gamma, const float* beta,

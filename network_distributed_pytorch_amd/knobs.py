@@ -23,6 +23,7 @@ FUSIONS = {
     "branch_links": "downsample-block grad-x of conv1 + 1x1 downsample shared in place (ops/gradlink.py)",
     "conv_bnstats": "BN forward statistics from the direct-conv epilogue (ops/conv.py)",
     "bn_bwd_stats": "BN backward statistics from the grad-x epilogue / pool backward (ops/batchnorm.py)",
+    "bn_vec4": "float4 single-launch small-map BN kernel (csrc/batchnorm.hip; off: the scalar one)",
     "stem_pool": "stem BN -> ReLU -> max-pool in one pass (ops/batchnorm.py)",
     "defer_gradw": "grad-W slab sums / folds batched at the end of backward (ops/gradfinish.py)",
     "grad_arena": "dense-arm gradients written straight into the bucket arena (ops/gradarena.py)",

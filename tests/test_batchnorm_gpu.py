@@ -130,3 +130,55 @@ def test_bn_single_launch_row_splits_running_stats(device, shape):
     torch.testing.assert_close(a.running_mean, b.running_mean, rtol=1e-6, atol=1e-6)
     torch.testing.assert_close(a.running_var, b.running_var, rtol=1e-6, atol=1e-6)
     assert a.num_batches_tracked.item() == b.num_batches_tracked.item() == 3
+
+
+@pytest.mark.parametrize("shape", [(512, 512, 1, 1), (64, 512, 1, 1), (512, 256, 2, 2), (64, 256, 2, 2),
+                                   (512, 128, 4, 4), (64, 128, 4, 4), (40, 96, 2, 1), (3, 20, 1, 1),
+                                   (100, 64, 4, 2), (33, 300, 1, 1)])
+@pytest.mark.parametrize("res,relu", [(False, True), (True, True), (False, False)])
+def test_bn_vec4_vs_fp64(device, shape, res, relu):
+    """float4 single-launch small-map BN (csrc/batchnorm.hip bn_small_fused_v4): forward output,
+    statistics and every gradient against an fp64 PyTorch reference; bitwise run-to-run."""
+    from network_distributed_pytorch_amd.ops._ext import ext
+    torch.manual_seed(4)
+    C = shape[1]
+    m = BatchNormAct2d(C).to(device)
+    with torch.no_grad():
+        m.weight.uniform_(0.5, 1.5)
+        m.bias.uniform_(-0.5, 0.5)
+    x = torch.randn(shape, device=device) * 1.7 + 0.4
+    r = torch.randn(shape, device=device) if res else None
+    g = torch.randn(shape, device=device)
+    # fp64 reference
+    xd = x.double().cpu().requires_grad_(True)
+    rd = r.double().cpu().requires_grad_(True) if res else None
+    wd = m.weight.detach().double().cpu().requires_grad_(True)
+    bd = m.bias.detach().double().cpu().requires_grad_(True)
+    yd = F.batch_norm(xd, None, None, wd, bd, True, 0.0, m.eps)
+    if res:
+        yd = yd + rd
+    if relu:
+        yd = F.relu(yd)
+    yd.backward(g.double().cpu())
+    runs = []
+    ext().bn_set_vec4(True)
+    try:
+        for _ in range(2):
+            xx = x.clone().requires_grad_(True)
+            rr = r.clone().requires_grad_(True) if res else None
+            m.weight.grad = m.bias.grad = None
+            y = m(xx, residual=rr, relu=relu)
+            y.backward(g)
+            runs.append([y.detach(), xx.grad, m.weight.grad.clone(), m.bias.grad.clone()]
+                        + ([rr.grad] if res else []))
+    finally:
+        ext().bn_set_vec4(True)
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)  # deterministic
+    y, dx, dw, db = runs[0][:4]
+    torch.testing.assert_close(y.double().cpu(), yd.detach(), rtol=1e-5, atol=2e-5)
+    torch.testing.assert_close(dx.double().cpu(), xd.grad, rtol=1e-4, atol=5e-5)
+    torch.testing.assert_close(dw.double().cpu(), wd.grad, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(db.double().cpu(), bd.grad, rtol=1e-5, atol=1e-4)
+    if res:
+        torch.testing.assert_close(runs[0][4].double().cpu(), rd.grad, rtol=0, atol=1e-6)
