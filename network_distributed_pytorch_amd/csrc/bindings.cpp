@@ -731,11 +731,10 @@ int64_t conv_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, const st
   const int ks = ndp::conv_ksplit(cls, g, B, true);
   // partial slabs are compact [B][C][OH*OW]-pixel tiles of the transposed product (for the
   // stride-2 1x1 class the 4x4 map, before the even-pixel scatter)
-  const int64_t slab = (int64_t)B * g.C * (cls == 4 ? g.OH * g.OW : g.H * g.W);
+  const int64_t slab = (int64_t)B * g.C * ((cls == 4 || cls == 5) ? g.OH * g.OW : g.H * g.W);
   float* pp = conv_part(part, ks, slab, "conv_dgrad");
   const float* ap = nullptr;
   if (addend.has_value()) {
-    TORCH_CHECK(cls != 4, "conv_dgrad: no addend for the stride-2 1x1 class");
     conv_check(*addend, "addend", B, g.C, g.H, g.W);
     TORCH_CHECK((reinterpret_cast<uintptr_t>(addend->data_ptr()) & 15) == 0, "conv_dgrad: 16-B aligned addend");
     ap = addend->data_ptr<float>();
@@ -757,7 +756,7 @@ int64_t conv_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, const st
                            bn_mean->data_ptr<float>(), bn_invstd->data_ptr<float>()};
   }
   const int left = ndp::launch_conv_dgrad(dy.data_ptr<float>(), w.data_ptr<float>(), dx.data_ptr<float>(), B, g, pp,
-                                          cur_stream(), ap, defer && cls != 4, bst.out ? &bst : nullptr);
+                                          cur_stream(), ap, defer && cls != 4 && cls != 5, bst.out ? &bst : nullptr);
   check_launch("launch_conv_dgrad");
   return left;
 }

@@ -422,7 +422,7 @@ struct ConvFwdCfg {
   static constexpr size_t LDS_BYTES = (size_t)NBUF * (A_SZ + B_SZ) * sizeof(float);
   static_assert(CK % 2 == 0 && BM % (32 * WM) == 0 && BN % (32 * WN) == 0 && TM >= 1 && TN >= 1, "tile");
   static_assert(NSTEP % KB == 0, "operand prefetch blocks");
-  static_assert(W % 4 == 0 && BM % 4 == 0, "float4 staging");
+  static_assert((W % 4 == 0 || (PD == 0 && H * W == 4)) && BM % 4 == 0, "float4 staging");
   // BatchNorm statistics epilogue (conv_fwd_kernel `stats`): the [BM][BN + 4] output tile
   // fits in the LDS the main loop used, 256 / BM threads per channel, float4 reads
   static constexpr int STATS_LDO = BN + 4, STATS_TPC = 256 / BM;
@@ -484,7 +484,9 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
   // B staging: float4 of the (possibly half-size, IUPS) input planes
   constexpr int IW = W / IUPS, IHW = (H / IUPS) * IW;
   constexpr int B4I = IMGS * CK * IHW / 4, BPT = (B4I + 255) / 256;
-  static_assert(IW % 4 == 0 && (IUPS == 1 || (ST == 1 && UPS == 1)), "input staging");
+  // a 2x2 unpadded plane is one float4 stored whole (row stride Wp = W = 2)
+  static_assert((IW % 4 == 0 || (PD == 0 && IUPS == 1 && IHW == 4)) && (IUPS == 1 || (ST == 1 && UPS == 1)),
+                "input staging");
   f32x4c ra[A_PER_T];
   f32x4c rb[BPT];
   auto load = [&](int ch) {
@@ -707,16 +709,26 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
       // block added into conv1's grad-x (no separate add launch).  All 16 addends are loaded
       // under ONE uniform branch before any store: a per-element `addend ? acc + addend[o]`
       // compiled to 16 serial load + s_waitcnt vmcnt(0) round trips.
-      float ad[16];
+      // UPS == 2: the three odd neighbours of each written pixel carry the addend alone
+      float ad[16], ad1[UPS == 2 ? 16 : 1], ad2[UPS == 2 ? 16 : 1], ad3[UPS == 2 ? 16 : 1];
       if (addend != nullptr) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int m = m0 + (wm * G::TM + tm) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          ad[r] = addend[yoff + (int64_t)m * OPQ];
+          const float* ap = addend + yoff + (int64_t)m * OPQ;
+          ad[r] = ap[0];
+          if constexpr (UPS == 2) {
+            ad1[r] = ap[1];
+            ad2[r] = ap[2 * G::Q];
+            ad3[r] = ap[2 * G::Q + 1];
+          }
         }
       } else {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) ad[r] = 0.f;
+        for (int r = 0; r < 16; ++r) {
+          ad[r] = 0.f;
+          if constexpr (UPS == 2) ad1[r] = ad2[r] = ad3[r] = 0.f;
+        }
       }
       float bxv[16], byv[16], bmu[16], bis[16];  // backward statistics operands, same rule
       if (kStats && bstats) {
@@ -737,9 +749,9 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
         const float v = acc[tm][tn][r] + ad[r];
         d[0] = v;
         if constexpr (UPS == 2) {
-          d[1] = 0.f;
-          d[2 * G::Q] = 0.f;
-          d[2 * G::Q + 1] = 0.f;
+          d[1] = ad1[r];
+          d[2 * G::Q] = ad2[r];
+          d[2 * G::Q + 1] = ad3[r];
         }
         if constexpr (kStats) {
           if (bstats) {
@@ -1068,25 +1080,31 @@ void launch_slab_sum_many(const SlabBatch& b, hipStream_t s) {
 }
 
 // split-K sum for the stride-2 1x1 grad-x: dx[b, c, 2p + i, 2q + j] = (i == j == 0) ?
-// sum_z part[z][b][c][p][q] : 0; one thread per float4 of dx (two output rows of 8 columns
-// = 4 float4; PQ = 16 compact pixels per plane)
+// sum_z part[z][b][c][p][q] : 0 (+ addend[b, c, 2p + i, 2q + j]); one thread per float4 of dx
+// (a (2P) x (2Q) plane, 2Q / 4 float4 per row; compact P x Q pixels per partial plane)
+template <int P, int Q>
 __global__ __launch_bounds__(256) void conv_slab_sum_ups_kernel(const float* __restrict__ part, float* __restrict__ dx,
-                                                                int64_t slab, int n_slices) {
+                                                                int64_t slab, int n_slices,
+                                                                const float* __restrict__ addend) {
+  constexpr int F4R = (2 * Q) / 4, F4P = 2 * P * F4R;
+  static_assert((2 * Q) % 4 == 0, "float4 rows");
   const int64_t i4 = (int64_t)blockIdx.x * 256 + threadIdx.x;  // float4 index into dx
   if (i4 * 4 >= slab * 4) return;                              // dx has 4x the compact elements
-  const int64_t plane = i4 / 16, r4 = i4 - plane * 16;         // 16 float4 per 8x8 plane
-  const int row = (int)(r4 >> 1), half = (int)(r4 & 1);        // 2 float4 per 8-wide row
+  const int64_t plane = i4 / F4P;
+  const int r4 = (int)(i4 - plane * F4P);
+  const int row = r4 / F4R, half = r4 - row * F4R;
   f32x4c v = {0.f, 0.f, 0.f, 0.f};
+  if (addend != nullptr) v = *reinterpret_cast<const f32x4c*>(addend + i4 * 4);
   if ((row & 1) == 0) {
     const int p = row >> 1, q0 = half * 2;                    // this float4 covers q = q0, q0 + 1
-    const float* src = part + plane * 16 + p * 4 + q0;
+    const float* src = part + plane * (P * Q) + p * Q + q0;
     float a = 0.f, b = 0.f;
     for (int z = 0; z < n_slices; ++z) {
       a += src[z * slab];
       b += src[z * slab + 1];
     }
-    v.x = a;
-    v.z = b;
+    v.x += a;
+    v.z += b;
   }
   *reinterpret_cast<f32x4c*>(dx + i4 * 4) = v;
 }
@@ -1128,8 +1146,8 @@ static int run_fwd(const float* x, const float* w, float* y, int B, int Cin, int
       hipLaunchKernelGGL(conv_slab_sum_kernel, dim3((unsigned)((slab / 4 + 15) / 16)), dim3(256), 0, s, part, y, slab,
                          ksplit, addend);
     else
-      hipLaunchKernelGGL(conv_slab_sum_ups_kernel, dim3((unsigned)((slab + 255) / 256)), dim3(256), 0, s, part, y, slab,
-                         ksplit);
+      hipLaunchKernelGGL((conv_slab_sum_ups_kernel<G::P, G::Q>), dim3((unsigned)((slab + 255) / 256)), dim3(256), 0, s,
+                         part, y, slab, ksplit, addend);
   }
   return 1;
 }
@@ -1163,6 +1181,9 @@ static void run_wgrad(const float* x, const float* dy, float* part, float* dw, i
 //   id 4: 1x1 s2 p0 8x8->4x4 (layer2 downsample)        C % 32 == 0, K % 64 == 0;
 //         grad-x = the 1x1 transposed product on the 4x4 map, written to the even pixels
 //         of the 8x8 plane (UPS = 2 epilogue, odd pixels zero)
+//   id 5: 1x1 s2 p0 4x4->2x2 (layer3 downsample)        the id-4 scheme one map size down: 16
+//         images per tile; the Toeplitz GEMM it replaces multiplied 15 zero rows of W_big per
+//         useful one (profiles/r5/toeplitz_layers_b512.md: 72.8 us fwd + bwd at batch 512)
 int conv_direct_class(const ConvGeom& g) {
   if (g.KH == 3 && g.KW == 3 && g.pad == 1 && g.stride == 1 && g.H == 8 && g.W == 8 && g.C % 64 == 0 && g.Co % 64 == 0)
     return 0;
@@ -1174,11 +1195,13 @@ int conv_direct_class(const ConvGeom& g) {
     return 3;
   if (g.KH == 1 && g.KW == 1 && g.pad == 0 && g.stride == 2 && g.H == 8 && g.W == 8 && g.C % 64 == 0 && g.Co % 64 == 0)
     return 4;
+  if (g.KH == 1 && g.KW == 1 && g.pad == 0 && g.stride == 2 && g.H == 4 && g.W == 4 && g.C % 64 == 0 && g.Co % 64 == 0)
+    return 5;
   return -1;
 }
 
 // images per workgroup of the forward / grad-x kernels, images per grad-W slice
-int conv_fwd_imgs(int cls) { return (cls == 0 || cls == 3) ? 1 : 4; }
+int conv_fwd_imgs(int cls) { return (cls == 0 || cls == 3) ? 1 : cls == 5 ? 16 : 4; }
 
 static constexpr int kFillWgs = 256;  // one workgroup per CU: below this, split the reduction
 
@@ -1193,7 +1216,7 @@ static int pow2_floor(int v) {
 // (Larger slices = fewer slabs to sum measured slower in round 3: batch 512 x2 1.9937, x4
 // 1.9969 vs 1.9904 / 1.9927 ms; batch 256 1.4473 / 1.4444 vs 1.441.)
 int conv_wgrad_imgs(int cls, const ConvGeom& g, int B) {
-  int def = cls == 0 ? 4 : cls == 1 ? 16 : cls == 2 ? 8 : cls == 4 ? 8 : 2;
+  int def = cls == 0 ? 4 : cls == 1 ? 16 : cls == 2 ? 8 : cls == 4 ? 8 : cls == 5 ? 16 : 2;
   const int cb = cls == 3 ? 3 : 32;
   const int per_slice = (g.Co / 32) * ((g.C + cb - 1) / cb);
   while (def > 1 && (B / def) * per_slice < kFillWgs && B % (def / 2) == 0) def /= 2;
@@ -1242,7 +1265,7 @@ int conv_dgrad_stats_slices(int cls, const ConvGeom& g, int B) {
 // (exact, 4x the MFMA work of the sub-pixel form; round 2: 2.006 / 2.005 vs MIOpen 1.991 ms at
 // batch 512): MIOpen's algorithm choice depends on its on-disk find database and, captured in a
 // hipGraph, was found non-deterministic and NaN-producing (round 3 bisection).
-bool conv_dgrad_direct(int cls) { return cls >= 0 && cls <= 4 && cls != 3; }
+bool conv_dgrad_direct(int cls) { return cls >= 0 && cls <= 5 && cls != 3; }
 
 // MFMA-block schedule of the layer1 / layer2 fwd + grad-x kernels: SCH = 2 (pinned MFMA /
 // LDS-read interleave): ResNet-18 step on 1x MI355X 2.0175 / 2.0154 -> 1.9981 / 1.9994 ms at
@@ -1270,6 +1293,9 @@ int launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvG
     case 4:
       return run_fwd<1, 1, 2, 0, 8, 8, 8, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s, nullptr,
                                                                        defer);
+    case 5:
+      return run_fwd<1, 1, 2, 0, 4, 4, 8, 64, 16, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s, nullptr,
+                                                                        defer);
     default: return 1;
   }
 }
@@ -1290,7 +1316,10 @@ int launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const C
     case 2:  // 3x3 stride 2: the layer1 grad-x kernel on the zero-inserted dY (staged, not stored)
       return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true, true, 1, 2, 2>(dy, w, dx, B, g.Co, g.C, ks, part, s,
                                                                               addend, defer, stats);
-    case 4: return run_fwd<1, 1, 1, 0, 4, 4, 8, 64, 4, 2, 2, 4, true, true, 2>(dy, w, dx, B, g.Co, g.C, ks, part, s);
+    case 4:
+      return run_fwd<1, 1, 1, 0, 4, 4, 8, 64, 4, 2, 2, 4, true, true, 2>(dy, w, dx, B, g.Co, g.C, ks, part, s, addend);
+    case 5:
+      return run_fwd<1, 1, 1, 0, 2, 2, 8, 64, 16, 2, 2, 4, true, true, 2>(dy, w, dx, B, g.Co, g.C, ks, part, s, addend);
     default: return 1;
   }
 }
@@ -1306,6 +1335,7 @@ void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, 
     case 2: run_wgrad<3, 3, 2, 1, 8, 8, 32, 32, 3, 3, 4>(x, dy, part, dw, B, g.C, g.Co, imgs, s); break;
     case 3: run_wgrad<7, 7, 2, 3, 32, 32, 3, 32, 5, 1, 4>(x, dy, part, dw, B, g.C, g.Co, imgs, s); break;
     case 4: run_wgrad<1, 1, 2, 0, 8, 8, 32, 32, 1, 1, 4>(x, dy, part, dw, B, g.C, g.Co, imgs, s); break;
+    case 5: run_wgrad<1, 1, 2, 0, 4, 4, 32, 32, 1, 1, 2>(x, dy, part, dw, B, g.C, g.Co, imgs, s); break;
     default: break;
   }
 }

@@ -189,10 +189,10 @@ class DirectConvFn(torch.autograd.Function):
 
 
 def _takes_addend(geom) -> bool:
-    """The grad-x kernel adds an addend in its epilogue / split-K sum: the 3x3 classes (stride 1,
-    and stride 2 run as the stride-1 kernel on the zero-inserted dY); not the 1x1 stride-2
-    class (even-pixel scatter epilogue)."""
-    return geom[4] == 3 and geom[5] == 3
+    """The grad-x kernel adds an addend in its epilogue / split-K sum: every direct class (the
+    3x3 ones on their stride-1 / zero-inserted maps, the 1x1 stride-2 ones in the even-pixel
+    scatter epilogue, whose odd pixels then carry the addend alone)."""
+    return (geom[4] == 3 and geom[5] == 3) or (geom[4] == 1 and geom[5] == 1 and geom[6] == 2)
 
 
 def conv2d_direct(x: torch.Tensor, weight: torch.Tensor, stride: int, padding: int, plan=None,

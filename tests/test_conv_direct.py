@@ -9,7 +9,9 @@ import torch.nn.functional as F
 CASES = [(64, 64, 3, 1, 1, 8, 8), (128, 128, 3, 1, 1, 4, 16), (64, 128, 3, 2, 1, 8, 8), (3, 64, 7, 2, 3, 32, 4),
          (128, 64, 3, 1, 1, 8, 4), (64, 192, 3, 1, 1, 4, 16), (64, 64, 3, 1, 1, 8, 64), (128, 128, 3, 1, 1, 4, 64),
          (64, 64, 3, 1, 1, 8, 6), (64, 128, 1, 2, 0, 8, 8), (64, 128, 1, 2, 0, 8, 64), (256, 512, 1, 2, 0, 8, 16),
-         (64, 128, 3, 2, 1, 8, 64), (128, 128, 3, 2, 1, 8, 32), (64, 128, 3, 2, 1, 8, 512)]
+         (64, 128, 3, 2, 1, 8, 64), (128, 128, 3, 2, 1, 8, 32), (64, 128, 3, 2, 1, 8, 512),
+         (128, 256, 1, 2, 0, 4, 16), (128, 256, 1, 2, 0, 4, 64), (128, 256, 1, 2, 0, 4, 512),
+         (512, 1024, 1, 2, 0, 4, 32)]
 
 
 @pytest.mark.gpu
@@ -76,3 +78,28 @@ def test_direct_plan_adapts_to_batch(device):
     big = direct_plan(torch.randn(512, 128, 4, 4, device=device), w, 1, 1)
     assert small[4] > 1 and small[5] > 1 and small[2] < big[2]
     assert big[4] == 1 and big[5] == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,hw,B", [(64, 128, 8, 64), (64, 128, 8, 512), (128, 256, 4, 16), (128, 256, 4, 64),
+                                           (128, 256, 4, 512)])
+def test_strided_1x1_dgrad_addend(device, cin, cout, hw, B):
+    """1x1 stride-2 grad-x with an addend (the downsample block's sibling grad-x): the even-pixel
+    scatter epilogue / split-K sum writes dx + addend, odd pixels = addend, vs fp64."""
+    from network_distributed_pytorch_amd.ops._ext import ext
+    from network_distributed_pytorch_amd.ops.conv import direct_plan
+
+    torch.manual_seed(5)
+    x = torch.randn(B, cin, hw, hw, device=device)
+    w = torch.randn(cout, cin, 1, 1, device=device) / cin ** 0.5
+    plan = direct_plan(x, w, 2, 0)
+    assert plan is not None
+    geom, ksd = plan[0], plan[5]
+    dy = torch.randn(B, cout, hw // 2, hw // 2, device=device)
+    add = torch.randn_like(x)
+    dx = torch.empty_like(x)
+    part = torch.empty(ksd * dy.numel() // cout * cin, device=device) if ksd > 1 else None
+    ext().conv_dgrad(dy, w, dx, list(geom), part, add, False)
+    ref = F.conv_transpose2d(dy.double().cpu(), w.double().cpu(), stride=2, output_padding=1) + add.double().cpu()
+    err = (dx.double().cpu() - ref).abs().max().item()
+    assert err <= 1e-5 * ref.abs().max().item(), err
