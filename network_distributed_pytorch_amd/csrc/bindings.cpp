@@ -689,9 +689,35 @@ int conv_batch(const torch::Tensor& t, const ndp::ConvGeom& g, int imgs) {
   return B;
 }
 
+// Winograd weight transforms of w (forward + grad-x layouts, 32 * Co * C floats): the caller's (built once per pass by
+// wino_weights and shared by forward and grad-x), or built here
+torch::Tensor wino_u_for(const c10::optional<torch::Tensor>& given, const torch::Tensor& w, const ndp::ConvGeom& g,
+                         bool needed) {
+  if (!needed) return torch::Tensor();
+  if (given.has_value()) {
+    check_f32(*given, "wino_u");
+    TORCH_CHECK(given->numel() == ndp::wino_u_numel(g.C, g.Co), "wino_u: 32 * Co * C floats (both layouts)");
+    return *given;
+  }
+  torch::Tensor u = torch::empty({ndp::wino_u_numel(g.C, g.Co)}, w.options());
+  ndp::launch_wino_weights(w.data_ptr<float>(), u.data_ptr<float>(), g.Co, g.C, cur_stream());
+  return u;
+}
+
+// the forward Winograd weight transform of a 3x3 weight (csrc/winograd.hip)
+void wino_weights(torch::Tensor w, torch::Tensor u) {
+  check_f32(w, "w"); check_f32(u, "u");
+  TORCH_CHECK(w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3, "wino_weights: 3x3 weight");
+  TORCH_CHECK(u.numel() == 32 * w.size(0) * w.size(1), "wino_weights: u holds 32 * Co * C floats");
+  TORCH_CHECK(w.size(0) % 16 == 0 && w.size(1) % 16 == 0, "wino_weights: channels in multiples of 16");
+  ndp::launch_wino_weights(w.data_ptr<float>(), u.data_ptr<float>(), (int)w.size(0), (int)w.size(1), cur_stream());
+  check_launch("launch_wino_weights");
+}
+
 // defer: split-K slabs are left in `part` for the consumer; returns how many (1 = y final)
 int64_t conv_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, const std::vector<int64_t>& geom,
-                 c10::optional<torch::Tensor> part, bool defer, c10::optional<torch::Tensor> stats) {
+                 c10::optional<torch::Tensor> part, bool defer, c10::optional<torch::Tensor> stats,
+                 c10::optional<torch::Tensor> wino_u) {
   const ndp::ConvGeom g = conv_geom(geom);
   const int cls = ndp::conv_direct_class(g);
   const int B = conv_batch(x, g, ndp::conv_fwd_imgs(cls));
@@ -710,8 +736,9 @@ int64_t conv_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, const std::v
                 "conv_fwd: stats must hold Co * S * 2 doubles");
     st = stats->data_ptr<double>();
   }
+  torch::Tensor wu = wino_u_for(wino_u, w, g, ndp::conv_wino(cls, g, B, false));
   const int left = ndp::launch_conv_fwd(x.data_ptr<float>(), w.data_ptr<float>(), y.data_ptr<float>(), B, g, pp,
-                                        cur_stream(), defer, st);
+                                        cur_stream(), defer, st, wu.defined() ? wu.data_ptr<float>() : nullptr);
   check_launch("launch_conv_fwd");
   return left;
 }
@@ -720,7 +747,7 @@ int64_t conv_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, const st
                    c10::optional<torch::Tensor> part, c10::optional<torch::Tensor> addend, bool defer,
                    c10::optional<torch::Tensor> stats, c10::optional<torch::Tensor> bn_x,
                    c10::optional<torch::Tensor> bn_y, c10::optional<torch::Tensor> bn_mean,
-                   c10::optional<torch::Tensor> bn_invstd) {
+                   c10::optional<torch::Tensor> bn_invstd, c10::optional<torch::Tensor> wino_u) {
   const ndp::ConvGeom g = conv_geom(geom);
   const int cls = ndp::conv_direct_class(g);
   TORCH_CHECK(cls >= 0 && ndp::conv_dgrad_direct(cls), "conv_dgrad: no direct grad-x kernel for this geometry");
@@ -755,8 +782,10 @@ int64_t conv_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, const st
     bst = ndp::ConvBnStats{stats->data_ptr<double>(), bn_x->data_ptr<float>(), bn_y->data_ptr<float>(),
                            bn_mean->data_ptr<float>(), bn_invstd->data_ptr<float>()};
   }
+  torch::Tensor wu = wino_u_for(wino_u, w, g, ndp::conv_wino(cls, g, B, true));
   const int left = ndp::launch_conv_dgrad(dy.data_ptr<float>(), w.data_ptr<float>(), dx.data_ptr<float>(), B, g, pp,
-                                          cur_stream(), ap, defer && cls != 4 && cls != 5, bst.out ? &bst : nullptr);
+                                          cur_stream(), ap, defer && cls != 4 && cls != 5, bst.out ? &bst : nullptr,
+                                          wu.defined() ? wu.data_ptr<float>() : nullptr);
   check_launch("launch_conv_dgrad");
   return left;
 }
@@ -1223,6 +1252,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return ndp::bn_two_kernel_path((int)N, (int)C, (int)HW, single ? 1 : 0);
   });
   m.def("bn_set_vec4", &ndp::bn_set_vec4);
+  m.def("wino_set_enabled", &ndp::wino_set_enabled);
   m.def("bn_slices", &bn_slices);
   m.def("slab_sum", &slab_sum);
   m.def("bn_part_numel", &bn_part_numel);
@@ -1241,12 +1271,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("slab_sum_many", &slab_sum_many);
   m.def("conv_plan", &conv_plan, py::arg("geom"), py::arg("batch"));
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("geom"), py::arg("part") = py::none(),
-        py::arg("defer") = false, py::arg("stats") = py::none());
+        py::arg("defer") = false, py::arg("stats") = py::none(), py::arg("wino_u") = py::none());
+  m.def("wino_weights", &wino_weights);
+  m.def("conv_wino", [](const std::vector<int64_t>& geom, int64_t B, bool dgrad) {
+    const ndp::ConvGeom g = conv_geom(geom);
+    const int cls = ndp::conv_direct_class(g);
+    return cls >= 0 && B > 0 && B % ndp::conv_fwd_imgs(cls) == 0 && ndp::conv_wino(cls, g, (int)B, dgrad);
+  });
   m.def("conv_stats_slices", &conv_stats_slices, py::arg("geom"), py::arg("batch"));
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("geom"),
         py::arg("part") = py::none(), py::arg("addend") = py::none(), py::arg("defer") = false,
         py::arg("stats") = py::none(), py::arg("bn_x") = py::none(), py::arg("bn_y") = py::none(),
-        py::arg("bn_mean") = py::none(), py::arg("bn_invstd") = py::none());
+        py::arg("bn_mean") = py::none(), py::arg("bn_invstd") = py::none(), py::arg("wino_u") = py::none());
   m.def("conv_dgrad_stats_slices", [](const std::vector<int64_t>& geom, int64_t B) -> int64_t {
     const ndp::ConvGeom g = conv_geom(geom);
     const int cls = ndp::conv_direct_class(g);

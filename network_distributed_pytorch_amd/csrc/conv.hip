@@ -1244,13 +1244,21 @@ int conv_ksplit(int cls, const ConvGeom& g, int B, bool dgrad) {
 // BatchNorm statistics from the forward epilogue: the layer1 3x3 and stem 7x7 classes (their
 // BatchNorms take the two-kernel large-map path; layer2's single-launch BN computes its own),
 // unsplit launches only.  Returns the partial count S (= workgroups along the batch), 0 = none.
+// Winograd F(2x2, 3x3) (winograd.hip) for the 8x8 3x3 classes: forward of class 0, grad-x of
+// class 0 and of class 2 (its zero-inserted dY), unsplit launches that tile exactly
+bool conv_wino(int cls, const ConvGeom& g, int B, bool dgrad) {
+  if (dgrad)
+    return (cls == 0 || cls == 2) && conv_ksplit(cls, g, B, true) == 1 && wino_ok(g.Co, g.C, B, 8, 8);
+  return cls == 0 && conv_ksplit(cls, g, B, false) == 1 && wino_ok(g.C, g.Co, B, 8, 8);
+}
+
 int conv_fwd_stats_slices(int cls, const ConvGeom& g, int B) {
   static_assert(ConvFwdCfg<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, false>::STATS_OK &&
                     ConvFwdCfg<7, 7, 2, 3, 32, 32, 4, 64, 1, 2, 1, 7, false>::STATS_OK,
                 "statistics epilogue fits every layer1 / stem tile");
   if (cls != 0 && cls != 3) return 0;
   if (conv_ksplit(cls, g, B, false) != 1) return 0;
-  return B / conv_fwd_imgs(cls);
+  return conv_wino(cls, g, B, false) ? B / wino_imgs() : B / conv_fwd_imgs(cls);
 }
 // backward-mode BN partial sums from the grad-x epilogue: the layer1 3x3 class (its BN takes the
 // two-kernel large-map path), unsplit grad-x launches only; 0 = none
@@ -1259,6 +1267,7 @@ int conv_dgrad_stats_slices(int cls, const ConvGeom& g, int B) {
                 "backward statistics epilogue fits the layer1 grad-x tiles");
   // class 2 (3x3 stride 2) runs the layer1 grad-x kernel on the zero-inserted dY: one image per tile
   if ((cls != 0 && cls != 2) || conv_ksplit(cls, g, B, true) != 1) return 0;
+  if (conv_wino(cls, g, B, true)) return B / wino_imgs();
   return cls == 2 ? B : B / conv_fwd_imgs(cls);
 }
 // Every class runs its grad-x natively.  The 3x3 stride-2 grad-x runs on the zero-inserted dY
@@ -1273,10 +1282,14 @@ bool conv_dgrad_direct(int cls) { return cls >= 0 && cls <= 5 && cls != 3; }
 // (iglp_opt(0): 2.0043 / 1.0602; the pinned interleave on the stem / 3x3-2 / 1x1-2 forwards
 // and 16-channel chunks or two-image layer1 tiles were slower — round 3 A/Bs)
 int launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s,
-                    bool defer, double* stats_out) {
+                    bool defer, double* stats_out, float* wino_u) {
   const ConvBnStats stats{stats_out, nullptr, nullptr, nullptr, nullptr};
   const int cls = conv_direct_class(g);
   const int ks = conv_ksplit(cls, g, B, false);
+  if (wino_u != nullptr && conv_wino(cls, g, B, false)) {
+    launch_wino_conv(x, wino_u, y, B, g.C, g.Co, false, 1, nullptr, stats, s);
+    return 1;
+  }
   switch (cls) {
     case 0:
       return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, false, true, 1, 2>(x, w, y, B, g.C, g.Co, ks, part, s,
@@ -1302,10 +1315,14 @@ int launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvG
 
 // dx[B, C, H, W] from dy[B, Co, OH, OW]
 int launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, float* part,
-                      hipStream_t s, const float* addend, bool defer, const ConvBnStats* bst) {
+                      hipStream_t s, const float* addend, bool defer, const ConvBnStats* bst, float* wino_u) {
   const ConvBnStats stats = bst != nullptr ? *bst : ConvBnStats{nullptr, nullptr, nullptr, nullptr, nullptr};
   const int cls = conv_direct_class(g);
   const int ks = conv_ksplit(cls, g, B, true);
+  if (wino_u != nullptr && conv_wino(cls, g, B, true)) {
+    launch_wino_conv(dy, wino_u, dx, B, g.Co, g.C, true, cls == 2 ? 2 : 1, addend, stats, s);
+    return 1;
+  }
   switch (cls) {
     case 0:
       return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true, true, 1, 2>(dy, w, dx, B, g.Co, g.C, ks, part, s,

@@ -271,8 +271,10 @@ struct ConvBnStats {
   const float* mean;
   const float* invstd;
 };
+// wino_u (nullable): the conv's Winograd weight transforms (launch_wino_weights: forward + grad-x
+// layouts, 32 * Co * C floats) when conv_wino(cls, g, B, dgrad) — the launch then runs the Winograd kernel
 int launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s,
-                    bool defer = false, double* stats = nullptr);
+                    bool defer = false, double* stats = nullptr, float* wino_u = nullptr);
 int conv_fwd_stats_slices(int cls, const ConvGeom& g, int B);
 // addend (nullable, 3x3 classes): dx += addend in the epilogue / split-K sum; with defer the
 // slabs are left unsummed and the consumer adds the addend after them (launch_bn_bwd dyadd)
@@ -280,8 +282,19 @@ int conv_fwd_stats_slices(int cls, const ConvGeom& g, int B);
 // sums of dx for the BN whose output gradient dx is
 int launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, float* part,
                       hipStream_t s, const float* addend = nullptr, bool defer = false,
-                      const ConvBnStats* bst = nullptr);
+                      const ConvBnStats* bst = nullptr, float* wino_u = nullptr);
 int conv_dgrad_stats_slices(int cls, const ConvGeom& g, int B);
+// Winograd F(2x2, 3x3) path of the 8x8 3x3 classes (winograd.hip): whether a launch takes it,
+// and the U scratch it needs (16 * inC * outC floats)
+bool conv_wino(int cls, const ConvGeom& g, int B, bool dgrad);
+bool wino_ok(int inC, int outC, int B, int H, int W);
+bool wino_disabled();
+void wino_set_enabled(bool on);
+int wino_imgs();
+int64_t wino_u_numel(int inC, int outC);
+void launch_wino_weights(const float* w, float* u, int Co, int C, hipStream_t s);
+void launch_wino_conv(const float* x, const float* u, float* y, int B, int inC, int outC, bool transw, int iups,
+                      const float* addend, const ConvBnStats& st, hipStream_t s);
 // out[i] = sum_{z < nslab} part[z * n + i] (+ addend[i]) in z order (n % 4 == 0), same order as
 // the split-K sums; out may alias addend
 void launch_slab_sum(const float* part, float* out, int64_t n, int nslab, hipStream_t s,

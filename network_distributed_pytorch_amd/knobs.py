@@ -24,6 +24,7 @@ FUSIONS = {
     "conv_bnstats": "BN forward statistics from the direct-conv epilogue (ops/conv.py)",
     "bn_bwd_stats": "BN backward statistics from the grad-x epilogue / pool backward (ops/batchnorm.py)",
     "bn_vec4": "float4 single-launch small-map BN kernel (csrc/batchnorm.hip; off: the scalar one)",
+    "winograd": "F(2x2,3x3) Winograd for the layer1 3x3 forward / grad-x (csrc/winograd.hip)",
     "stem_pool": "stem BN -> ReLU -> max-pool in one pass (ops/batchnorm.py)",
     "defer_gradw": "grad-W slab sums / folds batched at the end of backward (ops/gradfinish.py)",
     "grad_arena": "dense-arm gradients written straight into the bucket arena (ops/gradarena.py)",

@@ -34,6 +34,17 @@ _STATS: dict = {}
 CONV_BN_STATS = fusion_on("conv_bnstats")
 
 
+_WINO: dict = {}
+
+
+def wino_dirs(geom, B: int) -> Tuple[bool, bool]:
+    """(forward, grad-x) of this conv take the Winograd kernel (csrc/winograd.hip)."""
+    key = (tuple(geom), int(B))
+    if key not in _WINO:
+        _WINO[key] = (bool(ext().conv_wino(list(geom), int(B), False)), bool(ext().conv_wino(list(geom), int(B), True)))
+    return _WINO[key]
+
+
 def stats_slices(geom, B: int) -> int:
     """Batch-tile partials of the BN statistics the forward epilogue emits for this conv (0: none)."""
     key = (tuple(geom), int(B))
@@ -105,7 +116,16 @@ class DirectConvFn(torch.autograd.Function):
         part = torch.empty(ks_fwd * y.numel(), device=x.device, dtype=x.dtype) if ks_fwd > 1 else None
         S = stats_slices(geom, B) if slab_out is not None else 0
         stats = torch.empty(Co * S * 2, device=x.device, dtype=torch.float64) if S > 0 else None
-        left = ext().conv_fwd(x, weight, y, list(geom), part, slab_out is not None and part is not None, stats)
+        # Winograd layers (csrc/winograd.hip): the weight transform once per pass, shared by the
+        # forward and the grad-x launch (saved for backward)
+        wf, wd = wino_dirs(geom, B)
+        wu = None
+        if wf or wd:
+            wu = torch.empty(32 * weight.numel() // 9, device=x.device, dtype=x.dtype)  # fwd + grad-x layouts
+            ext().wino_weights(weight, wu)
+        left = ext().conv_fwd(x, weight, y, list(geom), part, slab_out is not None and part is not None, stats,
+                              wu if wf else None)
+        ctx.wu = wu if wd else None
         if left > 1:
             slab_out.put_fwd(part, left)  # y is filled by the consuming BN kernel
         if stats is not None:
@@ -161,10 +181,12 @@ class DirectConvFn(torch.autograd.Function):
                 S = int(ext().conv_dgrad_stats_slices(list(geom), x.shape[0])) if bn is not None else 0
                 if S > 0:
                     stats = torch.empty(x.shape[1] * S * 2, device=x.device, dtype=torch.float64)
-                    ext().conv_dgrad(dy, weight, dx, list(geom), None, addend if fuse else None, False, stats, *bn)
+                    ext().conv_dgrad(dy, weight, dx, list(geom), None, addend if fuse else None, False, stats, *bn,
+                                     wino_u=ctx.wu)
                     grad_slab.put_bwd_stats(stats, S)
                     return dx
-                left = ext().conv_dgrad(dy, weight, dx, list(geom), part, addend if fuse else None, defer)
+                left = ext().conv_dgrad(dy, weight, dx, list(geom), part, addend if fuse else None, defer,
+                                        wino_u=ctx.wu)
                 if left > 1:  # dx stays unwritten: the BN backward sums the slabs (+ the addend)
                     grad_slab.put_bwd(part, left, addend if fuse else None)
                 return dx + addend if (addend is not None and not fuse) else dx

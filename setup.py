@@ -17,7 +17,7 @@ CSRC = os.path.join("network_distributed_pytorch_amd", "csrc")
 SOURCES = [os.path.join(CSRC, f) for f in ("bindings.cpp", "plan.cpp", "comm.cpp", "powersgd.hip", "orth.hip",
                                                 "multitensor.hip", "batchnorm.hip", "attention.hip", "conv.hip",
                                                 "pool.hip", "embedding.hip", "linear.hip", "loss.hip", "layernorm.hip",
-                                                "tgemm.hip", "ipc.hip")]
+                                                "tgemm.hip", "ipc.hip", "winograd.hip")]
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
 

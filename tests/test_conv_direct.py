@@ -103,3 +103,43 @@ def test_strided_1x1_dgrad_addend(device, cin, cout, hw, B):
     ref = F.conv_transpose2d(dy.double().cpu(), w.double().cpu(), stride=2, output_padding=1) + add.double().cpu()
     err = (dx.double().cpu() - ref).abs().max().item()
     assert err <= 1e-5 * ref.abs().max().item(), err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,s,B", [(64, 64, 1, 512), (128, 64, 1, 512), (64, 128, 2, 512), (64, 64, 1, 1024)])
+def test_winograd_vs_direct_vs_fp64(device, cin, cout, s, B):
+    """Winograd F(2x2,3x3) (csrc/winograd.hip: layer1 forward / grad-x, the stride-2 class's grad-x on
+    the zero-inserted dY) against the direct MFMA kernels and an fp64 oracle: its error stays within
+    a small factor of the direct kernels' and of the fp64 tolerance; bitwise run-to-run."""
+    from network_distributed_pytorch_amd.ops._ext import ext
+    from network_distributed_pytorch_amd.ops.conv import conv2d_direct
+
+    torch.manual_seed(6)
+    x = torch.randn(B, cin, 8, 8, dtype=torch.float64)
+    w = torch.randn(cout, cin, 3, 3, dtype=torch.float64) / (cin * 9) ** 0.5
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    yr = F.conv2d(xr, wr, stride=s, padding=1)
+    g = torch.randn_like(yr)
+    yr.backward(g)
+    res = {}
+    try:
+        for wino in (True, False, True):
+            ext().wino_set_enabled(wino)
+            xd = x.float().to(device).requires_grad_(True)
+            wd = w.float().to(device).requires_grad_(True)
+            y = conv2d_direct(xd, wd, s, 1)
+            y.backward(g.float().to(device))
+            out = (y.detach().cpu().double(), xd.grad.cpu().double(), wd.grad.cpu().double())
+            if wino in res:
+                for a, b in zip(res[wino], out):
+                    assert torch.equal(a, b)  # deterministic
+            res[wino] = out
+    finally:
+        ext().wino_set_enabled(True)
+    for i, (ref, name) in enumerate(((yr, "y"), (xr.grad, "dx"), (wr.grad, "dw"))):
+        scale = ref.abs().max().item()
+        ew = (res[True][i] - ref).abs().max().item() / scale
+        ed = (res[False][i] - ref).abs().max().item() / scale
+        print(f"{name}: winograd rel err {ew:.2e}, direct {ed:.2e}")
+        assert ew <= 4e-6 * (cin * 9) ** 0.5, (name, ew, ed)
