@@ -1074,9 +1074,12 @@ static void launch_small_fused_cw(int HW, const float* x, const float* res, cons
                                   int nslab) {
   const int nblk = (int)(((int64_t)C * HW + CW - 1) / CW);
   auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-  // float4 kernel: rows of whole float4s, 16-B aligned operands (every ResNet launch)
+  // float4 kernel: rows of whole float4s, 16-B aligned operands.  Not for small maps at small
+  // batches: with HW <= 4 and N <= 128 the scalar kernel's 4-column blocks keep 4x more threads
+  // busy per row and its reduction is shorter — ResNet-18 at batch 64: HW = 1 4.8 vs 6.7 µs, HW = 4
+  // 4.8 vs 5.0 µs per launch (v4 wins everywhere at batch 512 and for HW = 16: 8.0 -> 5.3 µs at 64)
   const bool v4 = ((int64_t)C * HW) % 4 == 0 && a16(x) && a16(res) && a16(dy) && a16(yin) && a16(out) &&
-                  a16(dres) && a16(src) && !vec_off();
+                  a16(dres) && a16(src) && !vec_off() && (HW >= 8 || N > 128);
 #define NDP_BN_FUSED(HWV)                                                                                          \
   if constexpr (CW % HWV == 0) {                                                                                   \
     if (v4)                                                                                                        \

@@ -714,6 +714,30 @@ void wino_weights(torch::Tensor w, torch::Tensor u) {
   check_launch("launch_wino_weights");
 }
 
+// every Winograd layer of a model in one launch: [(w, u), ...]
+void wino_weights_many(const std::vector<std::pair<torch::Tensor, torch::Tensor>>& items) {
+  TORCH_CHECK((int)items.size() <= ndp::kMaxWino, "wino_weights_many: at most ", ndp::kMaxWino, " layers");
+  ndp::WinoBatch b{};
+  int acc = 0;
+  for (const auto& it : items) {
+    const torch::Tensor& w = it.first;
+    const torch::Tensor& u = it.second;
+    check_f32(w, "w"); check_f32(u, "u");
+    TORCH_CHECK(w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3 && w.size(0) % 16 == 0 && w.size(1) % 16 == 0,
+                "wino_weights_many: 3x3 weights, channels in multiples of 16");
+    TORCH_CHECK(u.numel() == 32 * w.size(0) * w.size(1), "wino_weights_many: u holds 32 * Co * C floats");
+    b.w[b.n] = w.data_ptr<float>();
+    b.u[b.n] = u.data_ptr<float>();
+    b.Co[b.n] = (int)w.size(0);
+    b.C[b.n] = (int)w.size(1);
+    acc += (int)(w.size(0) / 16 * (w.size(1) / 16));
+    b.end[b.n] = acc;
+    ++b.n;
+  }
+  ndp::launch_wino_weights_many(b, cur_stream());
+  check_launch("launch_wino_weights_many");
+}
+
 // defer: split-K slabs are left in `part` for the consumer; returns how many (1 = y final)
 int64_t conv_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, const std::vector<int64_t>& geom,
                  c10::optional<torch::Tensor> part, bool defer, c10::optional<torch::Tensor> stats,
@@ -1273,6 +1297,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("geom"), py::arg("part") = py::none(),
         py::arg("defer") = false, py::arg("stats") = py::none(), py::arg("wino_u") = py::none());
   m.def("wino_weights", &wino_weights);
+  m.def("wino_weights_many", &wino_weights_many);
   m.def("conv_wino", [](const std::vector<int64_t>& geom, int64_t B, bool dgrad) {
     const ndp::ConvGeom g = conv_geom(geom);
     const int cls = ndp::conv_direct_class(g);

@@ -293,6 +293,17 @@ void wino_set_enabled(bool on);
 int wino_imgs();
 int64_t wino_u_numel(int inC, int outC);
 void launch_wino_weights(const float* w, float* u, int Co, int C, hipStream_t s);
+// several layers' transforms in one launch (ops/conv.py WinoBank)
+constexpr int kMaxWino = 16;
+struct WinoBatch {
+  const float* w[kMaxWino];
+  float* u[kMaxWino];
+  int Co[kMaxWino];
+  int C[kMaxWino];
+  int end[kMaxWino];  // inclusive prefix sums of the (Co / 16) * (C / 16) block counts
+  int n;
+};
+void launch_wino_weights_many(const WinoBatch& b, hipStream_t s);
 void launch_wino_conv(const float* x, const float* u, float* y, int B, int inC, int outC, bool transw, int iups,
                       const float* addend, const ConvBnStats& st, hipStream_t s);
 // out[i] = sum_{z < nslab} part[z * n + i] (+ addend[i]) in z order (n % 4 == 0), same order as

@@ -294,11 +294,12 @@ __global__ __launch_bounds__(256, 2) void wino_fwd_kernel(const float* __restric
 //                   transposed weights' transform, k contiguous)
 // Workgroup = one transform row uu x a 16 x 16 (co, ci) block; the grad-x copy goes through an
 // LDS transpose so both outputs are written with lanes along their contiguous index.
-__global__ __launch_bounds__(256) void wino_weights_kernel(const float* __restrict__ w, float* __restrict__ u, int Co,
-                                                           int C) {
-  __shared__ float tr[4][16][17];
+// (WinoBatch: every Winograd layer of a model in one launch — blockIdx.x runs over all layers'
+// 16 x 16 blocks, the layer found from the prefix sums in the kernel arguments)
+__device__ __forceinline__ void wino_weights_block(const float* __restrict__ w, float* __restrict__ u, int Co, int C,
+                                                   int uu, int blk, float (&tr)[4][16][17]) {
   const int nci = C / 16;
-  const int uu = blockIdx.y, cob = blockIdx.x / nci, cib = blockIdx.x - cob * nci;
+  const int cob = blk / nci, cib = blk - cob * nci;
   const int n = Co * C;
   {
     const int col = threadIdx.x >> 4, cil = threadIdx.x & 15;
@@ -328,6 +329,20 @@ __global__ __launch_bounds__(256) void wino_weights_kernel(const float* __restri
   for (int v = 0; v < 4; ++v) ub[(int64_t)wino_pi(4 * uu + v) * n + (int64_t)ci * Co + co] = tr[v][cil][col];
 }
 
+__global__ __launch_bounds__(256) void wino_weights_kernel(const float* __restrict__ w, float* __restrict__ u, int Co,
+                                                           int C) {
+  __shared__ float tr[4][16][17];
+  wino_weights_block(w, u, Co, C, blockIdx.y, blockIdx.x, tr);
+}
+
+__global__ __launch_bounds__(256) void wino_weights_many_kernel(WinoBatch b) {
+  __shared__ float tr[4][16][17];
+  const int blk = blockIdx.x;
+  int e = 0;
+  while (e + 1 < b.n && blk >= b.end[e]) ++e;
+  wino_weights_block(b.w[e], b.u[e], b.Co[e], b.C[e], blockIdx.y, blk - (e ? b.end[e - 1] : 0), tr);
+}
+
 }  // namespace
 
 // The Winograd path applies to the layer1 3x3 class (8x8, stride 1, pad 1) — forward, and grad-x
@@ -354,6 +369,11 @@ void wino_set_enabled(bool on) { g_wino = on ? 1 : 0; }
 
 void launch_wino_weights(const float* w, float* u, int Co, int C, hipStream_t s) {
   hipLaunchKernelGGL(wino_weights_kernel, dim3((unsigned)((Co / 16) * (C / 16)), 4), dim3(256), 0, s, w, u, Co, C);
+}
+
+void launch_wino_weights_many(const WinoBatch& b, hipStream_t s) {
+  if (b.n <= 0) return;
+  hipLaunchKernelGGL(wino_weights_many_kernel, dim3((unsigned)b.end[b.n - 1], 4), dim3(256), 0, s, b);
 }
 
 // y[B][outC][8][8] = conv3x3(x[B][inC][8 / iups][8 / iups] (zero-inserted when iups = 2), W) with

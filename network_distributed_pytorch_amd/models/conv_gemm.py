@@ -194,6 +194,7 @@ class GemmConv2d(nn.Conv2d):
         self.direct = direct
         self._maps: Dict[Tuple, tuple] = {}
         self.bank: "ToeplitzBank | None" = None  # set by the owning model (one expand launch per pass)
+        self.wbank = None  # ops/conv.WinoBank, set by the owning model (one Winograd transform launch per pass)
 
     def _plan(self, x):
         C, H, W = x.shape[1:]
@@ -235,7 +236,7 @@ class GemmConv2d(nn.Conv2d):
         if self.direct:
             plan = direct_plan(x, self.weight, s, p)
             if plan is not None:
-                return DirectConvFn.apply(x, self.weight, plan, link, slab_out, grad_slab, branch)
+                return DirectConvFn.apply(x, self.weight, plan, link, slab_out, grad_slab, branch, self.wbank)
             padded = direct_plan_padded(x, self.weight, s, p)
             if padded is not None:  # ragged batch: zero-padded images, same kernels (links left empty)
                 plan, Bp = padded

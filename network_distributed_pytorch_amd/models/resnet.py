@@ -27,6 +27,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.batchnorm import BatchNormAct2d
+from ..ops.conv import WinoBank
 from ..ops.gradlink import BranchLink, GradLink
 from ..ops.linear import Linear
 from ..ops.pool import MaxPool2d
@@ -177,11 +178,13 @@ class ResNet(nn.Module):
         # found unreliable under hipGraph replay), same parameters / state_dict as nn.Linear
         self.fc = (Linear if fused_bn else nn.Linear)(512 * block.expansion, num_classes)
         bank = ToeplitzBank()  # every Toeplitz layer's W_big in one launch per forward
+        wbank = WinoBank()     # every Winograd layer's weight transforms in one launch per forward
         for m in self.modules():
             if isinstance(m, GemmConv2d):
                 m.gemm = gemm_convs
                 m.direct = gemm_convs
                 m.bank = bank
+                m.wbank = wbank
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
             elif isinstance(m, nn.BatchNorm2d):  # includes BatchNormAct2d

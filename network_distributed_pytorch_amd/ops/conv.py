@@ -24,7 +24,7 @@ from ._ext import ext
 from .gradarena import grad_buffer
 from ..knobs import fusion_on
 
-__all__ = ["direct_plan", "conv2d_direct", "DirectConvFn"]
+__all__ = ["direct_plan", "conv2d_direct", "DirectConvFn", "WinoBank"]
 
 _PLANS: dict = {}
 _STATS: dict = {}
@@ -35,6 +35,41 @@ CONV_BN_STATS = fusion_on("conv_bnstats")
 
 
 _WINO: dict = {}
+
+
+class WinoBank:
+    """Winograd weight transforms (csrc/winograd.hip, forward + grad-x layouts) of every Winograd
+    layer of one model, rebuilt by ONE launch per forward pass instead of one per layer — the
+    scheme of models/conv_gemm.ToeplitzBank: layers join on their first device forward (eager
+    warm-up, never inside a capture); afterwards the first member to run in a pass (forward
+    order is fixed) transforms every member.  Valid because weights change only between passes
+    (optimizer step); a transform saved for backward is rebuilt by the NEXT forward."""
+
+    MAX = 16  # csrc/ndp_kernels.h kMaxWino
+
+    def __init__(self):
+        self.members: list = []  # [(weight Parameter, u)]
+        self._index: dict = {}
+
+    def get(self, weight: torch.Tensor) -> torch.Tensor:
+        key = id(weight)
+        i = self._index.get(key)
+        numel = 32 * weight.numel() // 9
+        if i is None or self.members[i][1].device != weight.device or self.members[i][1].numel() != numel:
+            assert not torch.cuda.is_current_stream_capturing(), "Winograd bank grows during capture"
+            u = torch.empty(numel, device=weight.device, dtype=torch.float32)
+            ext().wino_weights(weight.contiguous(), u)
+            if i is None:
+                self._index[key] = len(self.members)
+                self.members.append((weight, u))
+            else:
+                self.members[i] = (weight, u)
+            return u
+        if i == 0:
+            batch = [(w, u) for w, u in self.members]
+            for j in range(0, len(batch), self.MAX):
+                ext().wino_weights_many(batch[j: j + self.MAX])
+        return self.members[i][1]
 
 
 def wino_dirs(geom, B: int) -> Tuple[bool, bool]:
@@ -94,7 +129,7 @@ def direct_plan_padded(x: torch.Tensor, weight: torch.Tensor, stride: int, paddi
 
 class DirectConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, plan, link=None, slab_out=None, grad_slab=None, branch=None):
+    def forward(ctx, x, weight, plan, link=None, slab_out=None, grad_slab=None, branch=None, wbank=None):
         """``slab_out`` / ``grad_slab`` (ops/slablink.py): leave the forward / grad-x split-K
         slabs for the fused BN kernel that consumes them instead of summing them here.
         ``branch`` (ops/gradlink.BranchLink): grad-x shared with a sibling conv of the same input
@@ -120,7 +155,9 @@ class DirectConvFn(torch.autograd.Function):
         # forward and the grad-x launch (saved for backward)
         wf, wd = wino_dirs(geom, B)
         wu = None
-        if wf or wd:
+        if (wf or wd) and wbank is not None:  # the model's bank: one transform launch per pass
+            wu = wbank.get(wparam)
+        elif wf or wd:
             wu = torch.empty(32 * weight.numel() // 9, device=x.device, dtype=x.dtype)  # fwd + grad-x layouts
             ext().wino_weights(weight, wu)
         left = ext().conv_fwd(x, weight, y, list(geom), part, slab_out is not None and part is not None, stats,
@@ -207,7 +244,7 @@ class DirectConvFn(torch.autograd.Function):
                 if br is not None and other is None:  # first of the two: the sibling adds onto it
                     br.put(dx)
                     dx = None
-        return dx, dw, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None
 
 
 def _takes_addend(geom) -> bool:

@@ -143,3 +143,35 @@ def test_winograd_vs_direct_vs_fp64(device, cin, cout, s, B):
         ed = (res[False][i] - ref).abs().max().item() / scale
         print(f"{name}: winograd rel err {ew:.2e}, direct {ed:.2e}")
         assert ew <= 4e-6 * (cin * 9) ** 0.5, (name, ew, ed)
+
+
+@pytest.mark.gpu
+def test_wino_bank_matches_per_layer_transforms(device):
+    """ResNet-18 at batch 512 (Winograd layer1): the model's WinoBank (one transform launch per
+    forward for every Winograd layer) == per-layer transforms, bitwise, across SGD steps."""
+    from network_distributed_pytorch_amd.models import build_resnet
+    from network_distributed_pytorch_amd.models.conv_gemm import GemmConv2d
+
+    torch.manual_seed(7)
+    a = build_resnet(18, 10).to(device)
+    b = build_resnet(18, 10).to(device)
+    b.load_state_dict(a.state_dict())
+    for m in b.modules():
+        if isinstance(m, GemmConv2d):
+            m.wbank = None
+    x = torch.randn(512, 3, 32, 32, device=device)
+    y = torch.randint(0, 10, (512,), device=device)
+    for _ in range(3):
+        losses = []
+        for m in (a, b):
+            m.zero_grad(set_to_none=True)
+            loss = F.cross_entropy(m(x), y)
+            loss.backward()
+            with torch.no_grad():
+                for p in m.parameters():
+                    p.add_(p.grad, alpha=-0.05)
+            losses.append(loss.detach())
+        assert torch.equal(losses[0], losses[1])
+    assert len(a.layer1[0].conv1.wbank.members) >= 4
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        assert torch.equal(pa, pb)
