@@ -1247,9 +1247,10 @@ int conv_ksplit(int cls, const ConvGeom& g, int B, bool dgrad) {
 // Winograd F(2x2, 3x3) (winograd.hip) for the 8x8 3x3 classes: forward of class 0, grad-x of
 // class 0 and of class 2 (its zero-inserted dY), unsplit launches that tile exactly
 bool conv_wino(int cls, const ConvGeom& g, int B, bool dgrad) {
-  if (dgrad)
-    return (cls == 0 || cls == 2) && conv_ksplit(cls, g, B, true) == 1 && wino_ok(g.Co, g.C, B, 8, 8);
-  return cls == 0 && conv_ksplit(cls, g, B, false) == 1 && wino_ok(g.C, g.Co, B, 8, 8);
+  if (dgrad)  // class 2's grad-x is an 8x8 map (its zero-inserted dY)
+    return (cls == 0 || cls == 1 || cls == 2) && conv_ksplit(cls, g, B, true) == 1 &&
+           wino_ok(g.Co, g.C, B, g.H, g.W);
+  return (cls == 0 || cls == 1) && conv_ksplit(cls, g, B, false) == 1 && wino_ok(g.C, g.Co, B, g.H, g.W);
 }
 
 int conv_fwd_stats_slices(int cls, const ConvGeom& g, int B) {
@@ -1258,7 +1259,7 @@ int conv_fwd_stats_slices(int cls, const ConvGeom& g, int B) {
                 "statistics epilogue fits every layer1 / stem tile");
   if (cls != 0 && cls != 3) return 0;
   if (conv_ksplit(cls, g, B, false) != 1) return 0;
-  return conv_wino(cls, g, B, false) ? B / wino_imgs() : B / conv_fwd_imgs(cls);
+  return conv_wino(cls, g, B, false) ? B / wino_imgs(g.H) : B / conv_fwd_imgs(cls);
 }
 // backward-mode BN partial sums from the grad-x epilogue: the layer1 3x3 class (its BN takes the
 // two-kernel large-map path), unsplit grad-x launches only; 0 = none
@@ -1267,7 +1268,7 @@ int conv_dgrad_stats_slices(int cls, const ConvGeom& g, int B) {
                 "backward statistics epilogue fits the layer1 grad-x tiles");
   // class 2 (3x3 stride 2) runs the layer1 grad-x kernel on the zero-inserted dY: one image per tile
   if ((cls != 0 && cls != 2) || conv_ksplit(cls, g, B, true) != 1) return 0;
-  if (conv_wino(cls, g, B, true)) return B / wino_imgs();
+  if (conv_wino(cls, g, B, true)) return B / wino_imgs(g.H);
   return cls == 2 ? B : B / conv_fwd_imgs(cls);
 }
 // Every class runs its grad-x natively.  The 3x3 stride-2 grad-x runs on the zero-inserted dY
@@ -1287,7 +1288,7 @@ int launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvG
   const int cls = conv_direct_class(g);
   const int ks = conv_ksplit(cls, g, B, false);
   if (wino_u != nullptr && conv_wino(cls, g, B, false)) {
-    launch_wino_conv(x, wino_u, y, B, g.C, g.Co, false, 1, nullptr, stats, s);
+    launch_wino_conv(x, wino_u, y, B, g.C, g.Co, g.H, false, 1, nullptr, stats, s);
     return 1;
   }
   switch (cls) {
@@ -1320,7 +1321,7 @@ int launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const C
   const int cls = conv_direct_class(g);
   const int ks = conv_ksplit(cls, g, B, true);
   if (wino_u != nullptr && conv_wino(cls, g, B, true)) {
-    launch_wino_conv(dy, wino_u, dx, B, g.Co, g.C, true, cls == 2 ? 2 : 1, addend, stats, s);
+    launch_wino_conv(dy, wino_u, dx, B, g.Co, g.C, g.H, true, cls == 2 ? 2 : 1, addend, stats, s);
     return 1;
   }
   switch (cls) {

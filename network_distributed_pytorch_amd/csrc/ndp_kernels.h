@@ -290,7 +290,7 @@ bool conv_wino(int cls, const ConvGeom& g, int B, bool dgrad);
 bool wino_ok(int inC, int outC, int B, int H, int W);
 bool wino_disabled();
 void wino_set_enabled(bool on);
-int wino_imgs();
+int wino_imgs(int H);
 int64_t wino_u_numel(int inC, int outC);
 void launch_wino_weights(const float* w, float* u, int Co, int C, hipStream_t s);
 // several layers' transforms in one launch (ops/conv.py WinoBank)
@@ -304,8 +304,8 @@ struct WinoBatch {
   int n;
 };
 void launch_wino_weights_many(const WinoBatch& b, hipStream_t s);
-void launch_wino_conv(const float* x, const float* u, float* y, int B, int inC, int outC, bool transw, int iups,
-                      const float* addend, const ConvBnStats& st, hipStream_t s);
+void launch_wino_conv(const float* x, const float* u, float* y, int B, int inC, int outC, int H, bool transw,
+                      int iups, const float* addend, const ConvBnStats& st, hipStream_t s);
 // out[i] = sum_{z < nslab} part[z * n + i] (+ addend[i]) in z order (n % 4 == 0), same order as
 // the split-K sums; out may alias addend
 void launch_slab_sum(const float* part, float* out, int64_t n, int nslab, hipStream_t s,

@@ -1,35 +1,39 @@
-// Winograd F(2x2, 3x3) convolution for ResNet's layer1 shape (3x3, stride 1, pad 1, 8x8 maps),
-// exact fp32 arithmetic on v_mfma_f32_16x16x4_f32 (gfx950).
+// Winograd F(2x2, 3x3) convolution for ResNet's 3x3 stride-1 pad-1 layers on 8x8 (layer1) and
+// 4x4 (layer2) maps, exact fp32 arithmetic on v_mfma_f32_16x16x4_f32 (gfx950).
 //
 // The direct implicit-GEMM kernels (conv.hip) spend 9 MACs per output pixel per input channel;
 // F(2x2, 3x3) spends 4 (16 per 2x2 output tile): Y = A^T [ (G g G^T) (.) (B^T d B) ] A with
 //   B^T = [1 0 -1 0; 0 1 1 0; 0 -1 1 0; 0 1 0 -1], G = [1 0 0; .5 .5 .5; .5 -.5 .5; 0 0 1],
 //   A^T = [1 1 1 0; 0 1 -1 -1]
 // (Lavin & Gray; the transform constants are 0, +-1, +-0.5: no precision is given up beyond the
-// reassociation of fp32 sums — same class of rounding as the direct kernels' MFMA order, and
+// reassociation of fp32 sums — measured 2-3x closer to an fp64 oracle than the direct kernels, and
 // what cuDNN / MIOpen themselves run for fp32 3x3 convolutions).  The 16 transform-domain
 // products are 16 independent GEMMs  M[e][co][tile] = sum_ci U[e][co][ci] V[e][ci][tile].
 //
-// gfx950 mapping (one workgroup = 4 waves = 4 images x 32 output channels):
-//  * wave w owns image w of the tile: its 16 2x2 output tiles are the N = 16 columns of a
-//    16x16x4 MFMA, so every lane computes the input transform of ITS OWN tile for its own 4
-//    channels (lane = (tile j, channel quad kq): the B operand of MFMA step t is V[e][4kq+t][j])
-//    straight from the zero-bordered raw input in LDS: the transformed input never touches LDS
-//    or HBM, and no transform is computed twice;
-//  * all 16 transform-domain accumulators of the 32 output channels stay in AGPRs (16 e x 2
-//    channel blocks x 4 = 128 per lane — the 512-entry gfx950 register file at one wave per
-//    SIMD), so the output transform is lane-local register arithmetic: no LDS exchange;
-//  * U (the transformed weights, [e][co][ci] with ci contiguous, built per pass by
-//    wino_weights_kernel) is staged per 16-channel chunk in LDS and read as one ds_read_b128 per
-//    4 MFMAs (row stride 20 floats: the 8 lanes of a b128 phase start in distinct 4-bank groups);
-//  * global loads of chunk i+1 are issued before the MFMAs of chunk i (register prefetch, two LDS
-//    buffers, one barrier per chunk).
+// gfx950 mapping (one workgroup = 4 waves x 16 output channels; a wave = 16 tiles: one 8x8 image
+// or four 4x4 images):
+//  * the 16 tiles are the N = 16 columns of a 16x16x4 MFMA, so every lane computes the input
+//    transform of ITS OWN tile for its own 4 channels (lane = (tile j, channel quad kq): the B
+//    operand of MFMA step t is V[e][4kq+t][j]) — no transform is computed twice and the
+//    transformed input never touches LDS or HBM;
+//  * a tile's 4x4 input patch = its own 2x2 core (global loads straight into registers, one
+//    chunk ahead) + 12 halo values of the 8 neighbour tiles exchanged by DPP row shifts (the 16
+//    lanes of a channel quad are one DPP row; lane-constant masks give the zero padding and image
+//    boundaries);
+//  * the 16 transform-domain accumulators (64 registers) stay in the register file and the
+//    output transform is lane-local: two waves per SIMD;
+//  * U (the transformed weights, [e][co][ci] with ci contiguous, built once per pass for every
+//    Winograd layer of a model by wino_weights_many_kernel, ops/conv.WinoBank) is staged per
+//    16-channel chunk in LDS (double-buffered, one barrier per chunk) and read as one
+//    ds_read_b128 per 4 MFMAs.
 // Epilogues match the direct kernel's: `addend` (a residual-branch gradient added to grad-x),
 // and the BatchNorm partial sums of the output (forward: sum / sum of squares; backward mode:
-// sum dz / sum dz * xhat with dz = (by > 0) ? v : 0) per (channel, 4-image tile) in the
-// [c][s][2] fp64 layout the BN kernels fold in a fixed order (deterministic).
-// Grad-x of the same conv runs this kernel with U' = the transform of the flipped, transposed
-// weights (conv of dY with w'[c][k][r][s] = w[k][c][2-r][2-s]).
+// sum dz / sum dz * xhat with dz = (by > 0) ? v : 0) per (channel, workgroup) in the [c][s][2]
+// fp64 layout the BN kernels fold in a fixed order (deterministic).
+// Grad-x of the same conv runs this kernel on U' = the transform of the flipped, transposed
+// weights, which is a permutation of U (wino_pi), written next to it by the same launch.
+// Measured (tools/diag/wino_scan.py, 1x MI355X, batch 512, graph-timed): 64 -> 64 channels on 8x8
+// 17.3 us vs 29.9 us direct; 128 -> 128 on 8x8 50.5 vs 89.1 us.
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
@@ -52,22 +56,10 @@ constexpr int kWCK = 16;       // input channels per chunk
 // 128 AGPRs at one wave per SIMD with double-buffered LDS left the MFMA pipe ~11 % busy: every
 // phase of a chunk — global wait, LDS stores, barrier, transform — ran exposed; PMC round 5.)
 constexpr int kWBM = 16;
-// Raw input planes in LDS: 10 x 10 zero-bordered, each row stored de-interleaved (padded column c
-// at (c & 1) * 5 + c / 2), row stride 10, plane stride 100 (= 4 mod 32).  A patch read of a
-// half-wave (16 tiles (ty, tx) x 2 channel quads) then lands on 32 distinct banks: tile offsets
-// 20 ty + tx cover 16 banks, the second quad (4 planes on) the other 16.  (Interleaved rows put
-// the stride-2 tile starts on even banks only: 3-way conflicts, 46-55 % of LDS cycles, PMC.)
-constexpr int kWRW = 10;
-constexpr int kWPL = 100;
-constexpr int kWIMG = kWCK * kWPL;
-constexpr int kWXS = kWImgs * kWIMG;       // raw input floats per buffer
 constexpr int kWLDU = 20;                  // U row stride (16 ci + 4)
 constexpr int kWUS = 16 * kWBM * kWLDU;    // U floats per buffer
-constexpr int kWNB = 1;                    // LDS buffers
 constexpr int kWUPT = 16 * kWBM * kWCK / 4 / 256;  // U float4 per thread per chunk
-constexpr size_t kWLds = (size_t)kWNB * (kWXS + kWUS) * sizeof(float);
-
-__device__ __forceinline__ constexpr int wcpos(int c) { return (c & 1) * 5 + (c >> 1); }
+constexpr size_t kWLds = (size_t)2 * kWUS * sizeof(float);  // two U buffers
 
 __device__ __forceinline__ f32x4w mfma16(float a, float b, f32x4w c) {
   // D(16x16) += A(16x4) B(4x16); lane l: A[l&15][l>>4], B[l>>4][l&15]; D: col l&15, row 4(l>>4)+reg
@@ -82,96 +74,112 @@ __device__ __forceinline__ int wino_pi(int e) {
   return 4 * (uu == 0 ? 3 : uu == 3 ? 0 : uu) + (vv == 0 ? 3 : vv == 3 ? 0 : vv);
 }
 
-// u: [16][Cout][Cin] (ci contiguous) — the forward transform, or for grad-x the backward layout
-// wino_weights_kernel writes next to it.  IUPS = 2: the input is a 4x4 map staged onto the even
-// pixels of the 8x8 interior (grad-x of the stride-2 conv on its zero-inserted dY).
-template <int IUPS>
-__global__ __launch_bounds__(256, 2) void wino_fwd_kernel(const float* __restrict__ x, const float* __restrict__ u,
-                                                       float* __restrict__ y, int Cin, int Cout,
-                                                       const float* __restrict__ addend, ConvBnStats st) {
+// ---- register-halo variant ------------------------------------------------------------------
+// The input patch of a tile is its own 2x2 "core" (loaded straight from global memory into
+// registers, one chunk ahead) plus the 12 halo values of the 8 neighbouring tiles, exchanged with
+// DPP row shifts: a wave's 16 lanes of one channel quad are exactly the 16 tiles of its image
+// (lane j = 4 ty + tx), i.e. one DPP row, and out-of-row sources read 0 — the top / bottom zero
+// padding for free; the left / right padding is a lane-constant select.  No raw input in LDS: no
+// staging stores, no zero fill, no 64 patch reads per chunk (the LDS path's 45 s_waitcnt per
+// chunk at lgkmcnt's 15-op depth); only the transformed weights are staged (shared by the 4 waves).
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+// (DPP controls: row_shl:n = 0x100 + n, row_shr:n = 0x110 + n; bound_ctrl: out-of-row reads 0)
+
+// H x H output maps (H = 8: layer1; H = 4: layer2, 4 images per wave so the 16 lanes of a channel
+// quad are still 16 tiles); IUPS = 2: grad-x of the stride-2 8x8 -> 4x4 conv on its zero-inserted dY
+template <int H, int IUPS>
+__global__ __launch_bounds__(256, 2) void wino_dpp_kernel(const float* __restrict__ x, const float* __restrict__ u,
+                                                        float* __restrict__ y, int Cin, int Cout,
+                                                        const float* __restrict__ addend, ConvBnStats st) {
+  constexpr int TW = H / 2, TPI = TW * TW, IPW = 16 / TPI, HW = H * H;  // tiles per row / image, images per wave
+  static_assert((H == 8 || H == 4) && (IUPS == 1 || H == 8), "shapes");
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* Xs = smem;                 // [kWNB][kWXS]
-  float* Us = smem + kWNB * kWXS;   // [kWNB][kWUS]
+  float* Us = smem;  // [2][kWUS]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int j = lane & 15, kq = lane >> 4, ty = j >> 2, tx = j & 3;
-  const int b0 = blockIdx.x * kWImgs, co0 = blockIdx.y * kWBM;
+  const int j = lane & 15, kq = lane >> 4;
+  const int ii = j / TPI, tj = j - ii * TPI, ty = tj / TW, tx = tj - ty * TW;
+  const int b0 = blockIdx.x * kWImgs * IPW, co0 = blockIdx.y * kWBM;
+  const int img = b0 + wave * IPW + ii;
   const int nchunks = Cin / kWCK;
+  constexpr int IPL = HW / (IUPS * IUPS);  // input plane floats
 
-  for (int i = tid; i < kWNB * kWXS; i += 256) Xs[i] = 0.f;  // zero borders (interiors rewritten per chunk)
-
-  constexpr int IPL = 64 / (IUPS * IUPS), IW = 8 / IUPS;  // input plane floats / row width
-  constexpr int XPT = kWImgs * kWCK * IPL / 4 / 256;      // float4 per thread: 4 or 1
-  f32x4w rx[XPT], ru[kWUPT];
-  auto load = [&](int ch) {
-    const int c0 = ch * kWCK;
-#pragma unroll
-    for (int i = 0; i < XPT; ++i) {
-      const int e4 = tid + 256 * i;
-      const int img = e4 / (kWCK * IPL / 4), rem = e4 - img * (kWCK * IPL / 4);
-      const int ci = (4 * rem) / IPL, q = 4 * rem - ci * IPL;
-      rx[i] = *reinterpret_cast<const f32x4w*>(x + ((int64_t)(b0 + img) * Cin + c0 + ci) * IPL + q);
-    }
-#pragma unroll
-    for (int i = 0; i < kWUPT; ++i) {  // U chunk: 16 e x kWBM co x 16 ci
-      const int e4 = tid + 256 * i;
-      const int e = e4 / (kWBM * 4), rem = e4 - e * (kWBM * 4), co = rem >> 2, c4 = rem & 3;
-      ru[i] = *reinterpret_cast<const f32x4w*>(u + ((int64_t)e * Cout + co0 + co) * Cin + c0 + 4 * c4);
-    }
-  };
-  auto store = [&](int buf) {
-    float* X = Xs + buf * kWXS;
-#pragma unroll
-    for (int i = 0; i < XPT; ++i) {
-      const int e4 = tid + 256 * i;
-      const int img = e4 / (kWCK * IPL / 4), rem = e4 - img * (kWCK * IPL / 4);
-      const int ci = (4 * rem) / IPL, q = 4 * rem - ci * IPL;
-      const int row = q / IW, col = q - row * IW;
-      float* d = X + img * kWIMG + ci * kWPL + (IUPS * row + 1) * kWRW;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) d[wcpos(IUPS * (col + k) + 1)] = rx[i][k];
-    }
-    float* U = Us + buf * kWUS;
-#pragma unroll
-    for (int i = 0; i < kWUPT; ++i) {
-      const int e4 = tid + 256 * i;
-      const int e = e4 / (kWBM * 4), rem = e4 - e * (kWBM * 4), co = rem >> 2, c4 = rem & 3;
-      *reinterpret_cast<f32x4w*>(U + (e * kWBM + co) * kWLDU + 4 * c4) = ru[i];
-    }
-  };
-
-  constexpr int NB = kWBM / 16;  // 16-row channel blocks
-  f32x4w acc[16][NB];
-#pragma unroll
-  for (int e = 0; e < 16; ++e)
-#pragma unroll
-    for (int b = 0; b < NB; ++b) acc[e][b] = f32x4w{0.f, 0.f, 0.f, 0.f};
-
-  load(0);
-  __syncthreads();  // zero fill before interior writes
-  store(0);
-  __syncthreads();
-  for (int ch = 0; ch < nchunks; ++ch) {
-    const int cur = kWNB == 2 ? (ch & 1) : 0;
-    if (ch + 1 < nchunks) load(ch + 1);
-    const float* X = Xs + cur * kWXS + wave * kWIMG;
-    const float* U = Us + cur * kWUS;
-    // input transform of this lane's tile for channels 4kq .. 4kq + 3 (all 64 reads issued first)
-    float v[4][16];
+  // core loads: IUPS 1: rows 2ty, 2ty + 1 x columns 2tx, 2tx + 1 of channel 4 kq + t; IUPS 2 (the
+  // zero-inserted dY of a stride-2 grad-x): only the core's (0, 0) pixel is nonzero = dY[ty][tx]
+  const float* xb = x + ((int64_t)img * Cin + 4 * kq) * IPL + (IUPS == 1 ? 2 * H * ty + 2 * tx : TW * ty + tx);
+  f32x4w core[2][4];
+  auto load_core = [&](int ch, f32x4w (&c)[4]) __attribute__((always_inline)) {
+    const float* p = xb + (int64_t)ch * kWCK * IPL;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const float* p = X + (4 * kq + t) * kWPL + 2 * ty * kWRW + tx;
-      float d[1][4][4];
+      if constexpr (IUPS == 1) {
+        const f32x2w r0 = *reinterpret_cast<const f32x2w*>(p + t * IPL);
+        const f32x2w r1 = *reinterpret_cast<const f32x2w*>(p + t * IPL + H);
+        c[t] = f32x4w{r0.x, r0.y, r1.x, r1.y};
+      } else {
+        c[t] = f32x4w{p[t * IPL], 0.f, 0.f, 0.f};
+      }
+    }
+  };
+  int ug[kWUPT], ul[kWUPT];
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
+  for (int i = 0; i < kWUPT; ++i) {
+    const int e4 = tid + 256 * i;
+    const int e = e4 / (kWBM * 4), rem = e4 - e * (kWBM * 4), co = rem >> 2, c4 = rem & 3;
+    ug[i] = (e * Cout + co0 + co) * Cin + 4 * c4;
+    ul[i] = (e * kWBM + co) * kWLDU + 4 * c4;
+  }
+  f32x4w ru[kWUPT];
+  auto load_u = [&](int ch) __attribute__((always_inline)) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) d[0][r][c] = p[r * kWRW + (c & 1) * 5 + (c >> 1)];
+    for (int i = 0; i < kWUPT; ++i) ru[i] = *reinterpret_cast<const f32x4w*>(u + ug[i] + ch * kWCK);
+  };
+  auto store_u = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < kWUPT; ++i) *reinterpret_cast<f32x4w*>(Us + buf * kWUS + ul[i]) = ru[i];
+  };
+  // neighbour tiles are lanes j -+ 1 (left / right), j -+ TW (above / below) and j -+ TW -+ 1:
+  // lane-constant masks supply the zero padding (and, for H = 4, the image boundaries)
+  const bool lok = tx > 0, rok = tx < TW - 1, uok = ty > 0, dok = ty < TW - 1;
+  constexpr int U1 = 0x110 + TW, D1 = 0x100 + TW;                          // row_shr / row_shl TW
+  constexpr int UL = 0x110 + TW + 1, UR = 0x110 + TW - 1, DL = 0x100 + TW - 1, DR = 0x100 + TW + 1;
+  // V[t][e] of this lane's tile for channel 4 kq + t (core c = {c00, c01, c10, c11})
+  auto xform = [&](const f32x4w (&c)[4], float (&v)[4][16]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float c00 = c[t][0], c01 = c[t][1], c10 = c[t][2], c11 = c[t][3];
+      float d[4][4];
+      d[1][1] = c00; d[1][2] = c01; d[2][1] = c10; d[2][2] = c11;
+      if constexpr (IUPS == 1) {
+        const float u0 = dppf<U1>(c10), u1 = dppf<U1>(c11);          // tile above: its bottom row
+        const float w0 = dppf<D1>(c00), w1 = dppf<D1>(c01);          // below: its top row
+        const float l1 = dppf<0x111>(c01), l2 = dppf<0x111>(c11);    // left: its right column
+        const float r1 = dppf<0x101>(c00), r2 = dppf<0x101>(c10);    // right: its left column
+        const float ul = dppf<UL>(c11), ur = dppf<UR>(c10);
+        const float dl = dppf<DL>(c01), dr = dppf<DR>(c00);
+        d[0][1] = uok ? u0 : 0.f; d[0][2] = uok ? u1 : 0.f;
+        d[3][1] = dok ? w0 : 0.f; d[3][2] = dok ? w1 : 0.f;
+        d[1][0] = lok ? l1 : 0.f; d[2][0] = lok ? l2 : 0.f;
+        d[1][3] = rok ? r1 : 0.f; d[2][3] = rok ? r2 : 0.f;
+        d[0][0] = (lok && uok) ? ul : 0.f; d[3][0] = (lok && dok) ? dl : 0.f;
+        d[0][3] = (rok && uok) ? ur : 0.f; d[3][3] = (rok && dok) ? dr : 0.f;
+      } else {  // only the cores' (0, 0) pixels are nonzero
+        d[0][0] = d[0][1] = d[0][2] = d[0][3] = 0.f;
+        d[1][0] = d[2][0] = d[3][0] = d[3][2] = 0.f;
+        const float w0 = dppf<D1>(c00), r1 = dppf<0x101>(c00), dr = dppf<DR>(c00);
+        d[3][1] = dok ? w0 : 0.f;
+        d[1][3] = rok ? r1 : 0.f; d[2][3] = 0.f;
+        d[3][3] = (rok && dok) ? dr : 0.f;
+      }
       float s4[4][4];  // B^T d
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        s4[0][c] = d[0][0][c] - d[0][2][c];
-        s4[1][c] = d[0][1][c] + d[0][2][c];
-        s4[2][c] = d[0][2][c] - d[0][1][c];
-        s4[3][c] = d[0][1][c] - d[0][3][c];
+      for (int cc = 0; cc < 4; ++cc) {
+        s4[0][cc] = d[0][cc] - d[2][cc];
+        s4[1][cc] = d[1][cc] + d[2][cc];
+        s4[2][cc] = d[2][cc] - d[1][cc];
+        s4[3][cc] = d[1][cc] - d[3][cc];
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {  // (B^T d) B
@@ -181,15 +189,29 @@ __global__ __launch_bounds__(256, 2) void wino_fwd_kernel(const float* __restric
         v[t][4 * r + 3] = s4[r][1] - s4[r][3];
       }
     }
-    // A operands (one ds_read_b128 = 4 MFMA steps) read two e ahead of their MFMAs; the two
-    // channel blocks' accumulator chains alternate (16x16x4 f32: 32-cycle issue, 40-cycle
-    // dependent latency).  sched_barrier keeps each prefetch ahead of the MFMA group it must
-    // overlap — left alone, the scheduler sinks every ds_read next to its first use.
-    f32x4w a[3][NB];
-    auto lda = [&](int e, int slot) {
+  };
+
+  f32x4w acc[16];
 #pragma unroll
-      for (int b = 0; b < NB; ++b)
-        a[slot][b] = *reinterpret_cast<const f32x4w*>(U + (e * kWBM + 16 * b + j) * kWLDU + 4 * kq);
+  for (int e = 0; e < 16; ++e) acc[e] = f32x4w{0.f, 0.f, 0.f, 0.f};
+
+  load_core(0, core[0]);
+  load_u(0);
+  store_u(0);
+  __syncthreads();
+  auto step = [&](int ch, f32x4w (&cc)[4], f32x4w (&cn)[4]) __attribute__((always_inline)) {
+    const bool next = ch + 1 < nchunks;
+    if (next) {
+      load_core(ch + 1, cn);
+      load_u(ch + 1);
+    }
+    float v[4][16];
+    xform(cc, v);
+    const float* U = Us + (ch & 1) * kWUS;
+    // A operands (one ds_read_b128 = the 4 k-steps of an element) read two elements ahead
+    f32x4w a[3];
+    auto lda = [&](int e, int slot) __attribute__((always_inline)) {
+      a[slot] = *reinterpret_cast<const f32x4w*>(U + (e * kWBM + j) * kWLDU + 4 * kq);
     };
     lda(0, 0);
     lda(1, 1);
@@ -199,82 +221,74 @@ __global__ __launch_bounds__(256, 2) void wino_fwd_kernel(const float* __restric
       if (e + 2 < 16) lda(e + 2, (e + 2) % 3);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int b = 0; b < NB; ++b) acc[e][b] = mfma16(a[e % 3][b][t], v[t][e], acc[e][b]);
+      for (int t = 0; t < 4; ++t) acc[e] = mfma16(a[e % 3][t], v[t][e], acc[e]);
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (ch + 1 < nchunks) {
-      if (kWNB == 1) __syncthreads();  // single buffer: everyone is done reading it
-      store(kWNB == 2 ? (cur ^ 1) : 0);
-    }
+    if (next) store_u((ch + 1) & 1);
     __syncthreads();
+  };
+  for (int ch = 0; ch < nchunks; ch += 2) {  // nchunks even (Cin % 32 == 0): the core sets swap
+    step(ch, core[0], core[1]);
+    step(ch + 1, core[1], core[0]);
   }
 
   // output transform Y = A^T M A per (channel, tile), lane-local
-  const int img = b0 + wave;
   const bool stats = st.out != nullptr;
   const bool bstats = stats && st.bx != nullptr;
-  double ps[NB][4], pq[NB][4];
+  double ps[4], pq[4];
 #pragma unroll
-  for (int b = 0; b < NB; ++b)
+  for (int r = 0; r < 4; ++r) {
+    const int co = co0 + 4 * kq + r;
+    float m[16];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int co = co0 + 16 * b + 4 * kq + r;
-      float m[16];
+    for (int e = 0; e < 16; ++e) m[e] = acc[e][r];
+    float t0[4], t1[4];
 #pragma unroll
-      for (int e = 0; e < 16; ++e) m[e] = acc[e][b][r];
-      float t0[4], t1[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        t0[c] = m[c] + m[4 + c] + m[8 + c];
-        t1[c] = m[4 + c] - m[8 + c] - m[12 + c];
-      }
-      f32x2w y0 = {t0[0] + t0[1] + t0[2], t0[1] - t0[2] - t0[3]};
-      f32x2w y1 = {t1[0] + t1[1] + t1[2], t1[1] - t1[2] - t1[3]};
-      const int64_t o = ((int64_t)img * Cout + co) * 64 + (2 * ty) * 8 + 2 * tx;
-      if (addend != nullptr) {
-        y0 += *reinterpret_cast<const f32x2w*>(addend + o);
-        y1 += *reinterpret_cast<const f32x2w*>(addend + o + 8);
-      }
-      *reinterpret_cast<f32x2w*>(y + o) = y0;
-      *reinterpret_cast<f32x2w*>(y + o + 8) = y1;
-      ps[b][r] = pq[b][r] = 0.0;
-      if (bstats) {
-        const f32x2w bx0 = *reinterpret_cast<const f32x2w*>(st.bx + o);
-        const f32x2w bx1 = *reinterpret_cast<const f32x2w*>(st.bx + o + 8);
-        const f32x2w by0 = *reinterpret_cast<const f32x2w*>(st.by + o);
-        const f32x2w by1 = *reinterpret_cast<const f32x2w*>(st.by + o + 8);
-        const float mu = st.mean[co], is = st.invstd[co];
-        const float z0 = by0.x > 0.f ? y0.x : 0.f, z1 = by0.y > 0.f ? y0.y : 0.f;
-        const float z2 = by1.x > 0.f ? y1.x : 0.f, z3 = by1.y > 0.f ? y1.y : 0.f;
-        ps[b][r] = (double)((z0 + z1) + (z2 + z3));
-        pq[b][r] = (double)((z0 * ((bx0.x - mu) * is) + z1 * ((bx0.y - mu) * is)) +
-                            (z2 * ((bx1.x - mu) * is) + z3 * ((bx1.y - mu) * is)));
-      } else if (stats) {
-        ps[b][r] = (double)((y0.x + y0.y) + (y1.x + y1.y));
-        pq[b][r] = (double)((y0.x * y0.x + y0.y * y0.y) + (y1.x * y1.x + y1.y * y1.y));
-      }
+    for (int c = 0; c < 4; ++c) {
+      t0[c] = m[c] + m[4 + c] + m[8 + c];
+      t1[c] = m[4 + c] - m[8 + c] - m[12 + c];
     }
+    f32x2w y0 = {t0[0] + t0[1] + t0[2], t0[1] - t0[2] - t0[3]};
+    f32x2w y1 = {t1[0] + t1[1] + t1[2], t1[1] - t1[2] - t1[3]};
+    const int64_t o = ((int64_t)img * Cout + co) * HW + (2 * ty) * H + 2 * tx;
+    if (addend != nullptr) {
+      y0 += *reinterpret_cast<const f32x2w*>(addend + o);
+      y1 += *reinterpret_cast<const f32x2w*>(addend + o + H);
+    }
+    *reinterpret_cast<f32x2w*>(y + o) = y0;
+    *reinterpret_cast<f32x2w*>(y + o + H) = y1;
+    ps[r] = pq[r] = 0.0;
+    if (bstats) {
+      const f32x2w bx0 = *reinterpret_cast<const f32x2w*>(st.bx + o);
+      const f32x2w bx1 = *reinterpret_cast<const f32x2w*>(st.bx + o + H);
+      const f32x2w by0 = *reinterpret_cast<const f32x2w*>(st.by + o);
+      const f32x2w by1 = *reinterpret_cast<const f32x2w*>(st.by + o + H);
+      const float mu = st.mean[co], is = st.invstd[co];
+      const float z0 = by0.x > 0.f ? y0.x : 0.f, z1 = by0.y > 0.f ? y0.y : 0.f;
+      const float z2 = by1.x > 0.f ? y1.x : 0.f, z3 = by1.y > 0.f ? y1.y : 0.f;
+      ps[r] = (double)((z0 + z1) + (z2 + z3));
+      pq[r] = (double)((z0 * ((bx0.x - mu) * is) + z1 * ((bx0.y - mu) * is)) +
+                       (z2 * ((bx1.x - mu) * is) + z3 * ((bx1.y - mu) * is)));
+    } else if (stats) {
+      ps[r] = (double)((y0.x + y0.y) + (y1.x + y1.y));
+      pq[r] = (double)((y0.x * y0.x + y0.y * y0.y) + (y1.x * y1.x + y1.y * y1.y));
+    }
+  }
   if (!stats) return;
-  // per channel: the 16 tiles of this wave's image (lanes j, fixed xor butterfly), then the 4
-  // images in wave order through LDS; S = gridDim.x partials per channel
   double* red = reinterpret_cast<double*>(smem);  // [4 waves][kWBM co][2]; the loop ended on a barrier
 #pragma unroll
-  for (int b = 0; b < NB; ++b)
+  for (int r = 0; r < 4; ++r) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        ps[b][r] += __shfl_xor(ps[b][r], o, 64);
-        pq[b][r] += __shfl_xor(pq[b][r], o, 64);
-      }
-      if (j == 0) {
-        const int c = 16 * b + 4 * kq + r;
-        red[(wave * kWBM + c) * 2] = ps[b][r];
-        red[(wave * kWBM + c) * 2 + 1] = pq[b][r];
-      }
+    for (int o = 1; o < 16; o <<= 1) {
+      ps[r] += __shfl_xor(ps[r], o, 64);
+      pq[r] += __shfl_xor(pq[r], o, 64);
     }
+    if (j == 0) {
+      const int c = 4 * kq + r;
+      red[(wave * kWBM + c) * 2] = ps[r];
+      red[(wave * kWBM + c) * 2 + 1] = pq[r];
+    }
+  }
   __syncthreads();
   if (tid < kWBM) {
     double s0 = 0.0, s1 = 0.0;
@@ -350,10 +364,12 @@ __global__ __launch_bounds__(256) void wino_weights_many_kernel(WinoBatch b) {
 // launch is unsplit (the direct kernel's split-K serves small batches) and tiles exactly:
 // Cin % 16, Cout % 32, B % 4.
 bool wino_ok(int inC, int outC, int B, int H, int W) {
-  return H == 8 && W == 8 && inC % kWCK == 0 && outC % kWBM == 0 && B % kWImgs == 0 &&
-         (int64_t)(B / kWImgs) * (outC / kWBM) >= 256 && !wino_disabled();
+  const int wimgs = wino_imgs(H);
+  return H == W && (H == 8 || H == 4) && inC % (2 * kWCK) == 0 && outC % kWBM == 0 && B % wimgs == 0 &&
+         (int64_t)(B / wimgs) * (outC / kWBM) >= 256 && !wino_disabled();
 }
-int wino_imgs() { return kWImgs; }
+// images per workgroup: 4 waves x (16 tiles / tiles per image)
+int wino_imgs(int H) { return kWImgs * (H == 4 ? 4 : 1); }
 int64_t wino_u_numel(int inC, int outC) { return (int64_t)32 * inC * outC; }  // both layouts
 
 static int g_wino = -1;
@@ -379,22 +395,28 @@ void launch_wino_weights_many(const WinoBatch& b, hipStream_t s) {
 // y[B][outC][8][8] = conv3x3(x[B][inC][8 / iups][8 / iups] (zero-inserted when iups = 2), W) with
 // u = launch_wino_weights(W) of the FORWARD conv (transw: this is its grad-x, inC = Co, outC = C,
 // and the kernel reads the grad-x half of u)
-void launch_wino_conv(const float* x, const float* u, float* y, int B, int inC, int outC, bool transw, int iups,
-                      const float* addend, const ConvBnStats& st, hipStream_t s) {
-  static bool attr[2] = {false, false};
-  const int k = iups == 2 ? 1 : 0;
-  if (!attr[k]) {
-    hipFuncSetAttribute(k ? reinterpret_cast<const void*>(wino_fwd_kernel<2>)
-                          : reinterpret_cast<const void*>(wino_fwd_kernel<1>),
+template <int H, int IUPS>
+static void run_wino(const float* x, const float* u, float* y, int B, int inC, int outC, const float* addend,
+                     const ConvBnStats& st, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(wino_dpp_kernel<H, IUPS>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWLds);
-    attr[k] = true;
+    attr = true;
   }
+  hipLaunchKernelGGL((wino_dpp_kernel<H, IUPS>), dim3((unsigned)(B / wino_imgs(H)), (unsigned)(outC / kWBM)),
+                     dim3(256), kWLds, s, x, u, y, inC, outC, addend, st);
+}
+
+// y[B][outC][H][H] = conv3x3(x (zero-inserted 4x4 -> 8x8 when iups = 2), W) with u =
+// launch_wino_weights(W) of the FORWARD conv (transw: this is its grad-x, inC = Co, outC = C, and
+// the kernel reads the grad-x half of u)
+void launch_wino_conv(const float* x, const float* u, float* y, int B, int inC, int outC, int H, bool transw,
+                      int iups, const float* addend, const ConvBnStats& st, hipStream_t s) {
   const float* uk = transw ? u + 16 * (int64_t)inC * outC : u;
-  const dim3 grid((unsigned)(B / kWImgs), (unsigned)(outC / kWBM));
-  if (k)
-    hipLaunchKernelGGL(wino_fwd_kernel<2>, grid, dim3(256), kWLds, s, x, uk, y, inC, outC, addend, st);
-  else
-    hipLaunchKernelGGL(wino_fwd_kernel<1>, grid, dim3(256), kWLds, s, x, uk, y, inC, outC, addend, st);
+  if (H == 4) run_wino<4, 1>(x, uk, y, B, inC, outC, addend, st, s);
+  else if (iups == 2) run_wino<8, 2>(x, uk, y, B, inC, outC, addend, st, s);
+  else run_wino<8, 1>(x, uk, y, B, inC, outC, addend, st, s);
 }
 
 }  // namespace ndp

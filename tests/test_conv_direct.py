@@ -106,22 +106,30 @@ def test_strided_1x1_dgrad_addend(device, cin, cout, hw, B):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cin,cout,s,B", [(64, 64, 1, 512), (128, 64, 1, 512), (64, 128, 2, 512), (64, 64, 1, 1024)])
-def test_winograd_vs_direct_vs_fp64(device, cin, cout, s, B):
-    """Winograd F(2x2,3x3) (csrc/winograd.hip: layer1 forward / grad-x, the stride-2 class's grad-x on
-    the zero-inserted dY) against the direct MFMA kernels and an fp64 oracle: its error stays within
-    a small factor of the direct kernels' and of the fp64 tolerance; bitwise run-to-run."""
+@pytest.mark.parametrize("cin,cout,s,B,hw", [(64, 64, 1, 512, 8), (128, 64, 1, 512, 8), (64, 128, 2, 512, 8),
+                                            (64, 64, 1, 1024, 8), (128, 128, 1, 512, 4), (128, 128, 1, 1024, 4),
+                                            (256, 128, 1, 512, 4)])
+def test_winograd_vs_direct_vs_fp64(device, cin, cout, s, B, hw):
+    """Winograd F(2x2,3x3) (csrc/winograd.hip: layer1 / layer2 forward and grad-x, the stride-2 class's
+    grad-x on the zero-inserted dY) against the direct MFMA kernels and an fp64 oracle: its error
+    stays within a small factor of the direct kernels' and of the fp64 tolerance; bitwise
+    run-to-run.  The Winograd path must actually be taken (conv_wino) for these shapes."""
+    from network_distributed_pytorch_amd.ops.conv import wino_dirs
     from network_distributed_pytorch_amd.ops._ext import ext
     from network_distributed_pytorch_amd.ops.conv import conv2d_direct
 
     torch.manual_seed(6)
-    x = torch.randn(B, cin, 8, 8, dtype=torch.float64)
+    x = torch.randn(B, cin, hw, hw, dtype=torch.float64)
     w = torch.randn(cout, cin, 3, 3, dtype=torch.float64) / (cin * 9) ** 0.5
     xr = x.clone().requires_grad_(True)
     wr = w.clone().requires_grad_(True)
     yr = F.conv2d(xr, wr, stride=s, padding=1)
     g = torch.randn_like(yr)
     yr.backward(g)
+    geom = (cin, hw, hw, cout, 3, 3, s, 1)
+    ext().wino_set_enabled(True)
+    assert bool(ext().conv_wino(list(geom), B, True)), "grad-x should take the Winograd kernel"
+    assert s == 2 or bool(ext().conv_wino(list(geom), B, False)), "forward should take the Winograd kernel"
     res = {}
     try:
         for wino in (True, False, True):
