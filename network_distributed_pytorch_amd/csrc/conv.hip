@@ -1347,6 +1347,19 @@ void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, 
                        hipStream_t s) {
   const int cls = conv_direct_class(g);
   const int imgs = conv_wgrad_imgs(cls, g, B);
+  if (cls == 0 && wino_wgrad_ok(g.C, g.Co, g.H)) {
+    // Winograd-domain grad-W (winograd.hip): same slab layout and slicing as the direct kernel.
+    // Layer1 only: ResNet-18 at batch 512 90.7 vs 130.2 µs per step (4 launches), batch 64 31.1 vs
+    // 38.5; the 4x4 maps (one tile per lane group and image: a load per 16 MFMAs) measured slower,
+    // 142.8 vs 99.0 µs at batch 512 and 64.0 vs 29.5 at batch 64 (profiles/r5)
+    launch_wino_wgrad(x, dy, part, B, g.C, g.Co, g.H, imgs, s);
+    if (dw != nullptr) {
+      const int64_t n = (int64_t)g.Co * g.C * 9;
+      hipLaunchKernelGGL(conv_slab_sum_kernel, dim3((unsigned)((n / 4 + 15) / 16)), dim3(256), 0, s, part, dw, n,
+                         B / imgs);
+    }
+    return;
+  }
   switch (cls) {
     case 0: run_wgrad<3, 3, 1, 1, 8, 8, 32, 32, 3, 3, 4>(x, dy, part, dw, B, g.C, g.Co, imgs, s); break;
     case 1: run_wgrad<3, 3, 1, 1, 4, 4, 32, 32, 3, 3, 4>(x, dy, part, dw, B, g.C, g.Co, imgs, s); break;

@@ -303,6 +303,157 @@ __global__ __launch_bounds__(256, 2) void wino_dpp_kernel(const float* __restric
   }
 }
 
+// ---- grad-W in the transform domain --------------------------------------------------------
+// With Y_tile = A^T (U (.) V) A:  dU_e[co][ci] = sum_(images, tiles) Yh_e[co][tile] V_e[ci][tile],
+// Yh = A dY_tile A^T (the 2x2 output gradient of a tile lifted to 4x4), and dW = G^T dU G
+// (4x4 -> 3x3): 16 GEMMs with K = tiles, 4 / 9 of the direct grad-W's MACs.  A wave owns a 16 x 16
+// (co, ci) block of dW over an image slice: lane (i, kq) lifts the output gradient of channel
+// co0 + i and transforms the input of channel ci0 + i for its tile group kq (H = 8: tile row kq,
+// 4 tiles; H = 4: tile kq) — the two MFMA operands of the same k — and 16 accumulators (one per e)
+// hold the block.  The slice's dW goes back through G^T . G in registers and is written as one
+// grad-W slab in the direct kernel's [co][ci][3][3] layout (conv_slab_sum / gradfinish sum the
+// slabs in slice order, deterministic).
+template <int H>
+__global__ __launch_bounds__(256, 2) void wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                                          float* __restrict__ part, int Cin, int Cout, int imgs) {
+  constexpr int TW = H / 2, TPL = TW * TW / 4, HW = H * H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 15, kq = lane >> 4;
+  const int blk = blockIdx.y * 4 + wave, nbc = Cin / 16;
+  const int cob = blk / nbc, cib = blk - cob * nbc;
+  if (cob * 16 >= Cout) return;  // no barriers in this kernel
+  const int slice = blockIdx.x, b0 = slice * imgs;
+  // tile group kq: H = 8 -> tile row ty = kq (tiles tx = 0..3); H = 4 -> tile (kq / 2, kq % 2)
+  const int ty = H == 8 ? kq : kq >> 1, tx0 = H == 8 ? 0 : (kq & 1);
+  const float* xp = x + ((int64_t)b0 * Cin + cib * 16 + i) * HW;
+  const float* gp = dy + ((int64_t)b0 * Cout + cob * 16 + i) * HW;
+  // per image: input rows 2ty - 1 .. 2ty + 2 (zero outside), output-gradient rows 2ty, 2ty + 1
+  float xr[2][4][H], gr[2][2][H];
+  auto load = [&](int n, float (&xv)[4][H], float (&gv)[2][H]) __attribute__((always_inline)) {
+    const float* xa = xp + (int64_t)n * Cin * HW;
+    const float* ga = gp + (int64_t)n * Cout * HW;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 2 * ty - 1 + r;
+      const bool ok = row >= 0 && row < H;
+#pragma unroll
+      for (int c4 = 0; c4 < H / 4; ++c4) {
+        const f32x4w v = ok ? *reinterpret_cast<const f32x4w*>(xa + row * H + 4 * c4) : f32x4w{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) xv[r][4 * c4 + k] = v[k];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int c4 = 0; c4 < H / 4; ++c4) {
+        const f32x4w v = *reinterpret_cast<const f32x4w*>(ga + (2 * ty + r) * H + 4 * c4);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) gv[r][4 * c4 + k] = v[k];
+      }
+  };
+  f32x4w acc[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = f32x4w{0.f, 0.f, 0.f, 0.f};
+  auto step = [&](const float (&xv)[4][H], const float (&gv)[2][H]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < TPL; ++s) {
+      const int tx = H == 8 ? s : tx0;
+      float d[4][4];
+      if constexpr (H == 8) {  // tx = s: static columns
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const int col = 2 * s - 1 + c;
+            d[r][c] = (col >= 0 && col < H) ? xv[r][col < 0 ? 0 : (col >= H ? H - 1 : col)] : 0.f;
+          }
+      } else {  // tx = kq & 1 (lane constant): columns -1..2 or 1..4 of the 4-wide rows, by select
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          d[r][0] = tx ? xv[r][1] : 0.f;
+          d[r][1] = tx ? xv[r][2] : xv[r][0];
+          d[r][2] = tx ? xv[r][3] : xv[r][1];
+          d[r][3] = tx ? 0.f : xv[r][2];
+        }
+      }
+      float v[16], sd[4][4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {  // B^T d
+        sd[0][c] = d[0][c] - d[2][c];
+        sd[1][c] = d[1][c] + d[2][c];
+        sd[2][c] = d[2][c] - d[1][c];
+        sd[3][c] = d[1][c] - d[3][c];
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {  // (B^T d) B
+        v[4 * r + 0] = sd[r][0] - sd[r][2];
+        v[4 * r + 1] = sd[r][1] + sd[r][2];
+        v[4 * r + 2] = sd[r][2] - sd[r][1];
+        v[4 * r + 3] = sd[r][1] - sd[r][3];
+      }
+      // Yh = A g A^T, A = [1 0; 1 1; 1 -1; 0 -1]
+      float g00, g01, g10, g11;
+      if constexpr (H == 8) {
+        g00 = gv[0][2 * s]; g01 = gv[0][2 * s + 1]; g10 = gv[1][2 * s]; g11 = gv[1][2 * s + 1];
+      } else {
+        g00 = tx ? gv[0][2] : gv[0][0]; g01 = tx ? gv[0][3] : gv[0][1];
+        g10 = tx ? gv[1][2] : gv[1][0]; g11 = tx ? gv[1][3] : gv[1][1];
+      }
+      const float t[4][2] = {{g00, g01}, {g00 + g10, g01 + g11}, {g00 - g10, g01 - g11}, {-g10, -g11}};
+      float yh[16];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        yh[4 * u + 0] = t[u][0];
+        yh[4 * u + 1] = t[u][0] + t[u][1];
+        yh[4 * u + 2] = t[u][0] - t[u][1];
+        yh[4 * u + 3] = -t[u][1];
+      }
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = mfma16(yh[e], v[e], acc[e]);
+      __builtin_amdgcn_sched_barrier(0);  // one tile's operands live at a time (else: spills)
+    }
+  };
+  if constexpr (H == 4) {
+    load(0, xr[0], gr[0]);
+    for (int n = 0; n < imgs; n += 2) {  // two register sets, swapped by unrolling (imgs even or 1)
+      if (n + 1 < imgs) load(n + 1, xr[1], gr[1]);
+      step(xr[0], gr[0]);
+      if (n + 1 >= imgs) break;
+      if (n + 2 < imgs) load(n + 2, xr[0], gr[0]);
+      step(xr[1], gr[1]);
+    }
+  } else {  // 8x8: the 48 raw values of a second image in flight spill; two waves per SIMD hide it
+    for (int n = 0; n < imgs; ++n) {
+      load(n, xr[0], gr[0]);
+      step(xr[0], gr[0]);
+    }
+  }
+  // dW = G^T dU G per (co, ci) = (row 4 kq + r, column i) of the block, lane-local
+  float* out = part + (int64_t)slice * Cout * Cin * 9;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int co = cob * 16 + 4 * kq + r, ci = cib * 16 + i;
+    float m[4][4];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) m[e >> 2][e & 3] = acc[e][r];
+    float t[3][4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      t[0][v] = m[0][v] + 0.5f * (m[1][v] + m[2][v]);
+      t[1][v] = 0.5f * (m[1][v] - m[2][v]);
+      t[2][v] = 0.5f * (m[1][v] + m[2][v]) + m[3][v];
+    }
+    float* o = out + ((int64_t)co * Cin + ci) * 9;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      o[3 * a + 0] = t[a][0] + 0.5f * (t[a][1] + t[a][2]);
+      o[3 * a + 1] = 0.5f * (t[a][1] - t[a][2]);
+      o[3 * a + 2] = 0.5f * (t[a][1] + t[a][2]) + t[a][3];
+    }
+  }
+}
+
 // u[0 .. 16 Co C):  U[e][co][ci] = (G w[co][ci] G^T)[e]            (forward, ci contiguous)
 // u[16 Co C ..):    U'[e][c][k]  = U[pi(e)][k][c]                  (grad-x: the flipped,
 //                   transposed weights' transform, k contiguous)
@@ -417,6 +568,16 @@ void launch_wino_conv(const float* x, const float* u, float* y, int B, int inC, 
   if (H == 4) run_wino<4, 1>(x, uk, y, B, inC, outC, addend, st, s);
   else if (iups == 2) run_wino<8, 2>(x, uk, y, B, inC, outC, addend, st, s);
   else run_wino<8, 1>(x, uk, y, B, inC, outC, addend, st, s);
+}
+
+// grad-W slabs part[B / imgs][Co][C][3][3] of the 8x8 / 4x4 3x3 stride-1 classes
+// 8x8 maps only: the 4x4 instantiation (one tile per lane group and image) measured slower than
+// the direct grad-W kernel and is not built (conv.hip launch_conv_wgrad)
+bool wino_wgrad_ok(int C, int Co, int H) { return H == 8 && C % 16 == 0 && Co % 16 == 0 && !wino_disabled(); }
+void launch_wino_wgrad(const float* x, const float* dy, float* part, int B, int C, int Co, int H, int imgs,
+                       hipStream_t s) {
+  const dim3 grid((unsigned)(B / imgs), (unsigned)(((Co / 16) * (C / 16) + 3) / 4));
+  if (H == 8) hipLaunchKernelGGL(wino_wgrad_kernel<8>, grid, dim3(256), 0, s, x, dy, part, C, Co, imgs);
 }
 
 }  // namespace ndp
