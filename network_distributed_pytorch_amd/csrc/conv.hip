@@ -1244,13 +1244,24 @@ int conv_ksplit(int cls, const ConvGeom& g, int B, bool dgrad) {
 // BatchNorm statistics from the forward epilogue: the layer1 3x3 and stem 7x7 classes (their
 // BatchNorms take the two-kernel large-map path; layer2's single-launch BN computes its own),
 // unsplit launches only.  Returns the partial count S (= workgroups along the batch), 0 = none.
+// split-K Winograd slabs: left to the consumer (defer: it sums them, and an addend after them) or
+// summed here in slab order (+ addend), like run_fwd
+static int wino_slabs(const float* part, float* out, int64_t n, int ks, bool defer, const float* addend,
+                      hipStream_t s) {
+  if (defer) return ks;
+  hipLaunchKernelGGL(conv_slab_sum_kernel, dim3((unsigned)((n / 4 + 15) / 16)), dim3(256), 0, s, part, out, n, ks,
+                     addend);
+  return 1;
+}
+
 // Winograd F(2x2, 3x3) (winograd.hip) for the 8x8 3x3 classes: forward of class 0, grad-x of
 // class 0 and of class 2 (its zero-inserted dY), unsplit launches that tile exactly
 bool conv_wino(int cls, const ConvGeom& g, int B, bool dgrad) {
+  // the direct kernel's split-K factor (small batches) is kept: the Winograd slabs then go to the
+  // same consumers (slab sum / the fused BN kernel)
   if (dgrad)  // class 2's grad-x is an 8x8 map (its zero-inserted dY)
-    return (cls == 0 || cls == 1 || cls == 2) && conv_ksplit(cls, g, B, true) == 1 &&
-           wino_ok(g.Co, g.C, B, g.H, g.W);
-  return (cls == 0 || cls == 1) && conv_ksplit(cls, g, B, false) == 1 && wino_ok(g.C, g.Co, B, g.H, g.W);
+    return (cls == 0 || cls == 1 || cls == 2) && wino_ok(g.Co, g.C, B, g.H, g.W, conv_ksplit(cls, g, B, true));
+  return (cls == 0 || cls == 1) && wino_ok(g.C, g.Co, B, g.H, g.W, conv_ksplit(cls, g, B, false));
 }
 
 int conv_fwd_stats_slices(int cls, const ConvGeom& g, int B) {
@@ -1288,8 +1299,8 @@ int launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvG
   const int cls = conv_direct_class(g);
   const int ks = conv_ksplit(cls, g, B, false);
   if (wino_u != nullptr && conv_wino(cls, g, B, false)) {
-    launch_wino_conv(x, wino_u, y, B, g.C, g.Co, g.H, false, 1, nullptr, stats, s);
-    return 1;
+    launch_wino_conv(x, wino_u, y, B, g.C, g.Co, g.H, false, 1, nullptr, ks > 1 ? ConvBnStats{} : stats, ks, part, s);
+    return ks > 1 ? wino_slabs(part, y, (int64_t)B * g.Co * g.H * g.W, ks, defer, nullptr, s) : 1;
   }
   switch (cls) {
     case 0:
@@ -1321,8 +1332,9 @@ int launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const C
   const int cls = conv_direct_class(g);
   const int ks = conv_ksplit(cls, g, B, true);
   if (wino_u != nullptr && conv_wino(cls, g, B, true)) {
-    launch_wino_conv(dy, wino_u, dx, B, g.Co, g.C, g.H, true, cls == 2 ? 2 : 1, addend, stats, s);
-    return 1;
+    launch_wino_conv(dy, wino_u, dx, B, g.Co, g.C, g.H, true, cls == 2 ? 2 : 1, addend,
+                     ks > 1 ? ConvBnStats{} : stats, ks, part, s);
+    return ks > 1 ? wino_slabs(part, dx, (int64_t)B * g.C * g.H * g.W, ks, defer, addend, s) : 1;
   }
   switch (cls) {
     case 0:

@@ -287,7 +287,7 @@ int conv_dgrad_stats_slices(int cls, const ConvGeom& g, int B);
 // Winograd F(2x2, 3x3) path of the 8x8 3x3 classes (winograd.hip): whether a launch takes it,
 // and the U scratch it needs (16 * inC * outC floats)
 bool conv_wino(int cls, const ConvGeom& g, int B, bool dgrad);
-bool wino_ok(int inC, int outC, int B, int H, int W);
+bool wino_ok(int inC, int outC, int B, int H, int W, int ks);
 bool wino_disabled();
 void wino_set_enabled(bool on);
 int wino_imgs(int H);
@@ -308,7 +308,7 @@ struct WinoBatch {
 };
 void launch_wino_weights_many(const WinoBatch& b, hipStream_t s);
 void launch_wino_conv(const float* x, const float* u, float* y, int B, int inC, int outC, int H, bool transw,
-                      int iups, const float* addend, const ConvBnStats& st, hipStream_t s);
+                      int iups, const float* addend, const ConvBnStats& st, int ks, float* part, hipStream_t s);
 // out[i] = sum_{z < nslab} part[z * n + i] (+ addend[i]) in z order (n % 4 == 0), same order as
 // the split-K sums; out may alias addend
 void launch_slab_sum(const float* part, float* out, int64_t n, int nslab, hipStream_t s,

@@ -91,9 +91,13 @@ __device__ __forceinline__ float dppf(float v) {
 // H x H output maps (H = 8: layer1; H = 4: layer2, 4 images per wave so the 16 lanes of a channel
 // quad are still 16 tiles); IUPS = 2: grad-x of the stride-2 8x8 -> 4x4 conv on its zero-inserted dY
 template <int H, int IUPS>
+// Split-K (gridDim.z > 1, small batches): workgroup z reduces the input channels [z cps, (z + 1)
+// cps) x 16 into slab z of `part` (the output layout; no addend, no statistics) — the consumer sums
+// the slabs in z order like the direct kernels' (deterministic).
 __global__ __launch_bounds__(256, 2) void wino_dpp_kernel(const float* __restrict__ x, const float* __restrict__ u,
                                                         float* __restrict__ y, int Cin, int Cout,
-                                                        const float* __restrict__ addend, ConvBnStats st) {
+                                                        const float* __restrict__ addend, ConvBnStats st,
+                                                        int cps, float* __restrict__ part, int64_t slab) {
   constexpr int TW = H / 2, TPI = TW * TW, IPW = 16 / TPI, HW = H * H;  // tiles per row / image, images per wave
   static_assert((H == 8 || H == 4) && (IUPS == 1 || H == 8), "shapes");
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -103,12 +107,12 @@ __global__ __launch_bounds__(256, 2) void wino_dpp_kernel(const float* __restric
   const int ii = j / TPI, tj = j - ii * TPI, ty = tj / TW, tx = tj - ty * TW;
   const int b0 = blockIdx.x * kWImgs * IPW, co0 = blockIdx.y * kWBM;
   const int img = b0 + wave * IPW + ii;
-  const int nchunks = Cin / kWCK;
+  const int nchunks = cps, cz = blockIdx.z * cps;  // chunk range of this split
   constexpr int IPL = HW / (IUPS * IUPS);  // input plane floats
 
   // core loads: IUPS 1: rows 2ty, 2ty + 1 x columns 2tx, 2tx + 1 of channel 4 kq + t; IUPS 2 (the
   // zero-inserted dY of a stride-2 grad-x): only the core's (0, 0) pixel is nonzero = dY[ty][tx]
-  const float* xb = x + ((int64_t)img * Cin + 4 * kq) * IPL + (IUPS == 1 ? 2 * H * ty + 2 * tx : TW * ty + tx);
+  const float* xb = x + ((int64_t)img * Cin + cz * kWCK + 4 * kq) * IPL + (IUPS == 1 ? 2 * H * ty + 2 * tx : TW * ty + tx);
   f32x4w core[2][4];
   auto load_core = [&](int ch, f32x4w (&c)[4]) __attribute__((always_inline)) {
     const float* p = xb + (int64_t)ch * kWCK * IPL;
@@ -128,7 +132,7 @@ __global__ __launch_bounds__(256, 2) void wino_dpp_kernel(const float* __restric
   for (int i = 0; i < kWUPT; ++i) {
     const int e4 = tid + 256 * i;
     const int e = e4 / (kWBM * 4), rem = e4 - e * (kWBM * 4), co = rem >> 2, c4 = rem & 3;
-    ug[i] = (e * Cout + co0 + co) * Cin + 4 * c4;
+    ug[i] = (e * Cout + co0 + co) * Cin + cz * kWCK + 4 * c4;
     ul[i] = (e * kWBM + co) * kWLDU + 4 * c4;
   }
   f32x4w ru[kWUPT];
@@ -227,9 +231,29 @@ __global__ __launch_bounds__(256, 2) void wino_dpp_kernel(const float* __restric
     if (next) store_u((ch + 1) & 1);
     __syncthreads();
   };
-  for (int ch = 0; ch < nchunks; ch += 2) {  // nchunks even (Cin % 32 == 0): the core sets swap
+  for (int ch = 0; ch < nchunks; ch += 2) {  // the two core sets swap (unrolled by two)
     step(ch, core[0], core[1]);
-    step(ch + 1, core[1], core[0]);
+    if (ch + 1 < nchunks) step(ch + 1, core[1], core[0]);
+  }
+  if (gridDim.z > 1) {  // split-K: this slice's partial output
+    float* pz = part + (int64_t)blockIdx.z * slab;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = co0 + 4 * kq + r;
+      float m[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) m[e] = acc[e][r];
+      float t0[4], t1[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        t0[c] = m[c] + m[4 + c] + m[8 + c];
+        t1[c] = m[4 + c] - m[8 + c] - m[12 + c];
+      }
+      const int64_t o = ((int64_t)img * Cout + co) * HW + (2 * ty) * H + 2 * tx;
+      *reinterpret_cast<f32x2w*>(pz + o) = f32x2w{t0[0] + t0[1] + t0[2], t0[1] - t0[2] - t0[3]};
+      *reinterpret_cast<f32x2w*>(pz + o + H) = f32x2w{t1[0] + t1[1] + t1[2], t1[1] - t1[2] - t1[3]};
+    }
+    return;
   }
 
   // output transform Y = A^T M A per (channel, tile), lane-local
@@ -514,10 +538,10 @@ __global__ __launch_bounds__(256) void wino_weights_many_kernel(WinoBatch b) {
 // of that class and of the stride-2 8x8 -> 4x4 class (zero-inserted dY, iups = 2) — when the
 // launch is unsplit (the direct kernel's split-K serves small batches) and tiles exactly:
 // Cin % 16, Cout % 32, B % 4.
-bool wino_ok(int inC, int outC, int B, int H, int W) {
+bool wino_ok(int inC, int outC, int B, int H, int W, int ks) {
   const int wimgs = wino_imgs(H);
-  return H == W && (H == 8 || H == 4) && inC % (2 * kWCK) == 0 && outC % kWBM == 0 && B % wimgs == 0 &&
-         (int64_t)(B / wimgs) * (outC / kWBM) >= 256 && !wino_disabled();
+  return H == W && (H == 8 || H == 4) && inC % kWCK == 0 && (inC / kWCK) % ks == 0 && outC % kWBM == 0 &&
+         B % wimgs == 0 && (int64_t)(B / wimgs) * (outC / kWBM) * ks >= 128 && !wino_disabled();
 }
 // images per workgroup: 4 waves x (16 tiles / tiles per image)
 int wino_imgs(int H) { return kWImgs * (H == 4 ? 4 : 1); }
@@ -548,31 +572,34 @@ void launch_wino_weights_many(const WinoBatch& b, hipStream_t s) {
 // and the kernel reads the grad-x half of u)
 template <int H, int IUPS>
 static void run_wino(const float* x, const float* u, float* y, int B, int inC, int outC, const float* addend,
-                     const ConvBnStats& st, hipStream_t s) {
+                     const ConvBnStats& st, int ks, float* part, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(wino_dpp_kernel<H, IUPS>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWLds);
     attr = true;
   }
-  hipLaunchKernelGGL((wino_dpp_kernel<H, IUPS>), dim3((unsigned)(B / wino_imgs(H)), (unsigned)(outC / kWBM)),
-                     dim3(256), kWLds, s, x, u, y, inC, outC, addend, st);
+  const int64_t slab = (int64_t)B * outC * H * H;
+  hipLaunchKernelGGL((wino_dpp_kernel<H, IUPS>),
+                     dim3((unsigned)(B / wino_imgs(H)), (unsigned)(outC / kWBM), (unsigned)ks), dim3(256), kWLds, s,
+                     x, u, y, inC, outC, ks > 1 ? nullptr : addend, st, (inC / kWCK) / ks, part, slab);
 }
 
 // y[B][outC][H][H] = conv3x3(x (zero-inserted 4x4 -> 8x8 when iups = 2), W) with u =
 // launch_wino_weights(W) of the FORWARD conv (transw: this is its grad-x, inC = Co, outC = C, and
-// the kernel reads the grad-x half of u)
+// the kernel reads the grad-x half of u).  ks > 1: split-K into `part` (ks slabs of y's layout);
+// the caller sums them (or leaves them to the consuming BN kernel).
 void launch_wino_conv(const float* x, const float* u, float* y, int B, int inC, int outC, int H, bool transw,
-                      int iups, const float* addend, const ConvBnStats& st, hipStream_t s) {
+                      int iups, const float* addend, const ConvBnStats& st, int ks, float* part, hipStream_t s) {
   const float* uk = transw ? u + 16 * (int64_t)inC * outC : u;
-  if (H == 4) run_wino<4, 1>(x, uk, y, B, inC, outC, addend, st, s);
-  else if (iups == 2) run_wino<8, 2>(x, uk, y, B, inC, outC, addend, st, s);
-  else run_wino<8, 1>(x, uk, y, B, inC, outC, addend, st, s);
+  if (H == 4) run_wino<4, 1>(x, uk, y, B, inC, outC, addend, st, ks, part, s);
+  else if (iups == 2) run_wino<8, 2>(x, uk, y, B, inC, outC, addend, st, ks, part, s);
+  else run_wino<8, 1>(x, uk, y, B, inC, outC, addend, st, ks, part, s);
 }
 
-// grad-W slabs part[B / imgs][Co][C][3][3] of the 8x8 / 4x4 3x3 stride-1 classes
-// 8x8 maps only: the 4x4 instantiation (one tile per lane group and image) measured slower than
-// the direct grad-W kernel and is not built (conv.hip launch_conv_wgrad)
+// grad-W slabs part[B / imgs][Co][C][3][3] of the layer1 class.  8x8 maps only: the 4x4
+// instantiation (one tile per lane group and image: a load per 16 MFMAs) measured slower than the
+// direct grad-W kernel (conv.hip launch_conv_wgrad) and is not built
 bool wino_wgrad_ok(int C, int Co, int H) { return H == 8 && C % 16 == 0 && Co % 16 == 0 && !wino_disabled(); }
 void launch_wino_wgrad(const float* x, const float* dy, float* part, int B, int C, int Co, int H, int imgs,
                        hipStream_t s) {

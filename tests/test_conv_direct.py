@@ -108,7 +108,10 @@ def test_strided_1x1_dgrad_addend(device, cin, cout, hw, B):
 @pytest.mark.gpu
 @pytest.mark.parametrize("cin,cout,s,B,hw", [(64, 64, 1, 512, 8), (128, 64, 1, 512, 8), (64, 128, 2, 512, 8),
                                             (64, 64, 1, 1024, 8), (128, 128, 1, 512, 4), (128, 128, 1, 1024, 4),
-                                            (256, 128, 1, 512, 4)])
+                                            (256, 128, 1, 512, 4),
+                                            # split-K (small per-GPU batches): slabs summed in order
+                                            (64, 64, 1, 64, 8), (64, 64, 1, 128, 8), (64, 128, 2, 64, 8),
+                                            (128, 128, 1, 64, 4), (128, 128, 1, 128, 4)])
 def test_winograd_vs_direct_vs_fp64(device, cin, cout, s, B, hw):
     """Winograd F(2x2,3x3) (csrc/winograd.hip: layer1 / layer2 forward and grad-x, the stride-2 class's
     grad-x on the zero-inserted dY) against the direct MFMA kernels and an fp64 oracle: its error
