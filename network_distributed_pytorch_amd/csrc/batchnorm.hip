@@ -1048,9 +1048,14 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_v4_kernel(
 // workgroups, one per channel) measured slower than the two-kernel path at batch 64 / 128
 // (1.0797 vs 1.0772 / 1.2322 vs 1.2122 ms) and so did row splits over a cross-workgroup barrier
 // (batch 512 1.908 -> 1.960 / 1.966 ms; round 4, removed in round 5).
+// The 8x8 maps (layer1) take it too at per-GPU batch <= 128 (the float4 kernel, one channel per
+// workgroup, <= 128 rows): the split-K convs there emit no epilogue statistics, so the two-kernel
+// path ran a statistics pass and an apply pass per direction.
+constexpr int kFusedMaxN64 = 128;
 static bool bn_fused_ok(int N, int C, int HW) {
-  return (HW == 1 || HW == 2 || HW == 4 || HW == 8 || HW == 16) && N >= 1 && N <= kFusedMaxN &&
-         (int64_t)N * C * HW < (1LL << 30);
+  return (((HW == 1 || HW == 2 || HW == 4 || HW == 8 || HW == 16) && N <= kFusedMaxN) ||
+          (HW == 64 && N <= kFusedMaxN64 && !vec_off())) &&
+         N >= 1 && (int64_t)N * C * HW < (1LL << 30);
 }
 
 // column-block width for one launch: the widest block that still gives >= 256 workgroups (one per
@@ -1107,6 +1112,18 @@ static void launch_small_fused(int HW, const float* x, const float* res, const f
                                float* sm, float* si, float* dgamma, float* dbeta, float* out, float* dres, int N,
                                int C, float eps, float momentum, int relu, hipStream_t s, const float* src,
                                int nslab) {
+  if (HW == 64) {  // one channel per workgroup (bn_fused_ok); float4 unless an operand is unaligned
+    auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    if (a16(x) && a16(res) && a16(dy) && a16(yin) && a16(out) && a16(dres) && a16(src))
+      hipLaunchKernelGGL((bn_small_fused_v4_kernel<64, BWD, 64, kFusedMaxN64>), dim3((unsigned)C),
+                         dim3(kFusedThreads), 0, s, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma,
+                         dbeta, out, dres, N, C, eps, momentum, relu, src, nslab);
+    else
+      hipLaunchKernelGGL((bn_small_fused_kernel<64, BWD, 64, kFusedMaxN64>), dim3((unsigned)C), dim3(kFusedThreads),
+                         0, s, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out, dres, N, C,
+                         eps, momentum, relu, src, nslab);
+    return;
+  }
   switch (bn_colw_for(HW, C, N)) {
     case 16:
       launch_small_fused_cw<BWD, 16>(HW, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out,

@@ -134,7 +134,8 @@ def test_bn_single_launch_row_splits_running_stats(device, shape):
 
 @pytest.mark.parametrize("shape", [(512, 512, 1, 1), (64, 512, 1, 1), (512, 256, 2, 2), (64, 256, 2, 2),
                                    (512, 128, 4, 4), (64, 128, 4, 4), (40, 96, 2, 1), (3, 20, 1, 1),
-                                   (100, 64, 4, 2), (33, 300, 1, 1)])
+                                   (100, 64, 4, 2), (33, 300, 1, 1), (64, 64, 8, 8), (128, 64, 8, 8),
+                                   (200, 256, 2, 2)])
 @pytest.mark.parametrize("res,relu", [(False, True), (True, True), (False, False)])
 def test_bn_vec4_vs_fp64(device, shape, res, relu):
     """float4 single-launch small-map BN (csrc/batchnorm.hip bn_small_fused_v4): forward output,
