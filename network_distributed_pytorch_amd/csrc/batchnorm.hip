@@ -681,30 +681,53 @@ __device__ __forceinline__ int xcd_block(int bid, int nblk) {
   return xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
 }
 
-template <int HW, int BWD, int CW, int MAXN = kFusedMaxN>
+// PAIR = 1: the downsample block's two BatchNorms in one launch (BnPair: the second BN, over x2 =
+// the 1x1 downsample conv's output, same shape).  Forward: out = relu(bn(x) + bn2(x2)), the
+// downsample branch's BN output is never stored.  Backward: both BNs see the same
+// dz = dy * (out > 0), so one pass forms sum dz, sum dz * xhat, sum dz * xhat2 and writes both
+// input gradients (out, p2.out2).  One launch and one tensor round trip fewer per direction and
+// downsample block than two single launches.
+struct BnPair {
+  const float* x2;
+  const float* gamma2;
+  const float* beta2;
+  float* rmean2;
+  float* rvar2;
+  int64_t* nbt2;
+  float* save_mean2;
+  float* save_invstd2;
+  float* dgamma2;
+  float* dbeta2;
+  float* out2;
+  const float* src2;  // forward: x2 as nslab2 unsummed split-K slabs (summed here, stored to x2), or null
+  int nslab2;
+};
+
+template <int HW, int BWD, int CW, int MAXN = kFusedMaxN, int PAIR = 0>
 __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
     const float* __restrict__ x, const float* __restrict__ res, const float* __restrict__ dy,
     const float* __restrict__ yin, const float* __restrict__ gamma, const float* __restrict__ beta,
     float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt, float* __restrict__ save_mean,
     float* __restrict__ save_invstd, float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ out,
     float* __restrict__ dres, int N, int C, float eps, float momentum, int relu, const float* __restrict__ src,
-    int nslab) {
+    int nslab, BnPair p2) {
   constexpr int RG = kFusedThreads / CW;
   constexpr int NP = MAXN / RG;  // rows per thread
   constexpr int NW = kFusedThreads / 64;
   static_assert(CW % HW == 0 && 64 % CW == 0, "bad column block");
   static_assert(NP >= 1, "bad row count");
-  __shared__ double red[2][NW][CW];
+  __shared__ double red[PAIR ? 4 : 2][NW][CW];
   const int CHW = C * HW;
   const int col = threadIdx.x % CW, g = threadIdx.x / CW;
   const int cb = xcd_block((int)blockIdx.x, (int)gridDim.x);
   const int j = cb * CW + col;
   const bool ok_col = j < CHW;
   const int c = ok_col ? j / HW : 0;
-  float v[NP], d[NP], m[NP];
+  float v[NP], d[NP], m[NP], v2[PAIR ? NP : 1];
   // every per-channel operand is loaded up front, alongside the tensor stream: read after the
   // reduction they were a second dependent memory round trip (~2 µs of a ~6 µs launch)
   float mean_s = 0.f, invstd_s = 0.f, gam = 1.f, bet = 0.f, rm = 0.f, rv = 0.f;
+  float mean2 = 0.f, invstd2 = 0.f, gam2 = 1.f, bet2 = 0.f, rm2 = 0.f, rv2 = 0.f;
   if (ok_col) {
     if (BWD) {
       mean_s = save_mean[c];
@@ -715,6 +738,18 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
     if (!BWD && rmean != nullptr && g == 0 && (j % HW) == 0) {
       rm = rmean[c];
       rv = rvar[c];
+    }
+    if constexpr (PAIR) {
+      if (BWD) {
+        mean2 = p2.save_mean2[c];
+        invstd2 = p2.save_invstd2[c];
+      }
+      if (p2.gamma2) gam2 = p2.gamma2[c];
+      if (!BWD && p2.beta2) bet2 = p2.beta2[c];
+      if (!BWD && p2.rmean2 != nullptr && g == 0 && (j % HW) == 0) {
+        rm2 = p2.rmean2[c];
+        rv2 = p2.rvar2[c];
+      }
     }
   }
 #pragma unroll
@@ -731,11 +766,23 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
     }
     if (!BWD) {
       v[k] = ok ? (src ? sum : x[o]) : 0.f;
-      d[k] = (ok && res) ? res[o] : 0.f;
+      if constexpr (PAIR) {  // the downsample conv output (or its split-K slabs, slab order)
+        float t = 0.f;
+        if (ok && p2.src2 != nullptr) {
+          t = p2.src2[o];
+          for (int z = 1; z < p2.nslab2; ++z) t += p2.src2[z * (int64_t)N * CHW + o];
+        } else if (ok) {
+          t = p2.x2[o];
+        }
+        d[k] = t;
+      } else {
+        d[k] = (ok && res) ? res[o] : 0.f;
+      }
     } else {
       v[k] = ok ? x[o] : 0.f;
       d[k] = ok ? (src ? sum : dy[o]) : 0.f;
       m[k] = (ok && relu) ? yin[o] : 1.f;
+      if constexpr (PAIR) v2[k] = ok ? p2.x2[o] : 0.f;
     }
   }
   if (!BWD && src != nullptr) {  // BN's saved input = the conv output
@@ -745,17 +792,31 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
       if (ok_col && n < N) const_cast<float*>(x)[(int64_t)n * CHW + j] = v[k];
     }
   }
-  double a = 0.0, b = 0.0;
+  if constexpr (PAIR) {
+    if (!BWD && p2.src2 != nullptr) {
+#pragma unroll
+      for (int k = 0; k < NP; ++k) {
+        const int n = g + k * RG;
+        if (ok_col && n < N) const_cast<float*>(p2.x2)[(int64_t)n * CHW + j] = d[k];
+      }
+    }
+  }
+  double a = 0.0, b = 0.0, a2 = 0.0, b2 = 0.0;
 #pragma unroll
   for (int k = 0; k < NP; ++k) {
     if (ok_col && g + k * RG < N) {
       if (!BWD) {
         a += (double)v[k];
         b += (double)v[k] * (double)v[k];
+        if constexpr (PAIR) {
+          a2 += (double)d[k];
+          b2 += (double)d[k] * (double)d[k];
+        }
       } else {
         const float dz = (m[k] > 0.f) ? d[k] : 0.f;
         a += (double)dz;
         b += (double)dz * (double)((v[k] - mean_s) * invstd_s);
+        if constexpr (PAIR) b2 += (double)dz * (double)((v2[k] - mean2) * invstd2);
       }
     }
   }
@@ -763,23 +824,39 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
   for (int o = HW / 2; o > 0; o >>= 1) {  // the HW columns of a channel are adjacent lanes
     a += __shfl_xor(a, o, 64);
     b += __shfl_xor(b, o, 64);
+    if constexpr (PAIR) {
+      a2 += __shfl_xor(a2, o, 64);
+      b2 += __shfl_xor(b2, o, 64);
+    }
   }
 #pragma unroll
   for (int o = CW; o < 64; o <<= 1) {  // row groups inside the wave
     a += __shfl_xor(a, o, 64);
     b += __shfl_xor(b, o, 64);
+    if constexpr (PAIR) {
+      a2 += __shfl_xor(a2, o, 64);
+      b2 += __shfl_xor(b2, o, 64);
+    }
   }
   const int wave = threadIdx.x / 64;
   if ((threadIdx.x % 64) < CW) {
     red[0][wave][col] = a;
     red[1][wave][col] = b;
+    if constexpr (PAIR) {
+      red[PAIR ? 2 : 0][wave][col] = a2;
+      red[PAIR ? 3 : 0][wave][col] = b2;
+    }
   }
   __syncthreads();
-  double A = 0.0, B = 0.0;
+  double A = 0.0, B = 0.0, A2 = 0.0, B2 = 0.0;
 #pragma unroll
   for (int k = 0; k < NW; ++k) {
     A += red[0][k][col];
     B += red[1][k][col];
+    if constexpr (PAIR) {
+      A2 += red[PAIR ? 2 : 0][k][col];
+      B2 += red[PAIR ? 3 : 0][k][col];
+    }
   }
   if (!ok_col) return;
   const double M = (double)N * HW;
@@ -791,6 +868,25 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
     const float mean = (float)mu, invstd = (float)(1.0 / sqrt(var + (double)eps));
     const float scale = gam * invstd;
     const float shift = bet - mean * scale;
+    float scale2 = 0.f, shift2 = 0.f;
+    if constexpr (PAIR) {
+      const double mu2 = A2 / M;
+      double var2 = B2 / M - mu2 * mu2;
+      if (var2 < 0.0) var2 = 0.0;
+      const float mean2f = (float)mu2, invstd2f = (float)(1.0 / sqrt(var2 + (double)eps));
+      scale2 = gam2 * invstd2f;
+      shift2 = bet2 - mean2f * scale2;
+      if (writer) {
+        p2.save_mean2[c] = mean2f;
+        p2.save_invstd2[c] = invstd2f;
+        if (p2.rmean2 != nullptr) {
+          const double unb2 = M > 1.0 ? var2 * M / (M - 1.0) : var2;
+          p2.rmean2[c] = (float)((1.0 - momentum) * (double)rm2 + momentum * mu2);
+          p2.rvar2[c] = (float)((1.0 - momentum) * (double)rv2 + momentum * unb2);
+        }
+        if (p2.nbt2 != nullptr && c == 0) p2.nbt2[0] += 1;
+      }
+    }
     if (writer) {
       save_mean[c] = mean;
       save_invstd[c] = invstd;
@@ -805,7 +901,7 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
     for (int k = 0; k < NP; ++k) {
       const int n = g + k * RG;
       if (n < N) {
-        const float z = fmaf(v[k], scale, shift) + d[k];
+        const float z = PAIR ? fmaf(v[k], scale, shift) + fmaf(d[k], scale2, shift2) : fmaf(v[k], scale, shift) + d[k];
         out[(int64_t)n * CHW + j] = relu ? fmaxf(z, 0.f) : z;
       }
     }
@@ -813,9 +909,14 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
     if (writer) {
       if (dgamma) dgamma[c] = (float)B;
       if (dbeta) dbeta[c] = (float)A;
+      if constexpr (PAIR) {
+        if (p2.dgamma2) p2.dgamma2[c] = (float)B2;
+        if (p2.dbeta2) p2.dbeta2[c] = (float)A;
+      }
     }
     const float k1 = gam * invstd_s;
     const float mdz = (float)(A / M), mdzx = (float)(B / M);
+    const float k12 = gam2 * invstd2, mdzx2 = (float)(B2 / M);
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
       const int n = g + k * RG;
@@ -824,7 +925,12 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
         const float xh = (v[k] - mean_s) * invstd_s;
         const int64_t o = (int64_t)n * CHW + j;
         out[o] = k1 * (dz - mdz - xh * mdzx);
-        if (dres) dres[o] = dz;
+        if constexpr (PAIR) {
+          const float xh2 = (v2[k] - mean2) * invstd2;
+          p2.out2[o] = k12 * (dz - mdz - xh2 * mdzx2);
+        } else if (dres) {
+          dres[o] = dz;
+        }
       }
     }
   }
@@ -837,14 +943,14 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
 // the bytes per address cycle.  A float4 holds whole channels' pixel runs: one channel (HW >= 4,
 // its HW/4 float4s on adjacent lanes) or 4 / HW channels (HW = 1, 2: separate sums per
 // channel).  Same fp64 sums, same fixed-order fold: deterministic run to run.
-template <int HW, int BWD, int CW, int MAXN = kFusedMaxN>
+template <int HW, int BWD, int CW, int MAXN = kFusedMaxN, int PAIR = 0>
 __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_v4_kernel(
     const float* __restrict__ x, const float* __restrict__ res, const float* __restrict__ dy,
     const float* __restrict__ yin, const float* __restrict__ gamma, const float* __restrict__ beta,
     float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt, float* __restrict__ save_mean,
     float* __restrict__ save_invstd, float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ out,
     float* __restrict__ dres, int N, int C, float eps, float momentum, int relu, const float* __restrict__ src,
-    int nslab) {
+    int nslab, BnPair p2) {
   constexpr int CT = CW / 4;                   // threads per row
   constexpr int RG = kFusedThreads / CT;       // row groups
   constexpr int NP = (MAXN + RG - 1) / RG;     // rows per thread
@@ -854,7 +960,7 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_v4_kernel(
   constexpr int LPC = HW >= 4 ? HW / 4 : 1;    // lanes per channel
   constexpr int CPW = CW / HW;                 // channels per workgroup
   static_assert(CW % 4 == 0 && CW % HW == 0 && CT <= 64 && 64 % CT == 0, "bad column block");
-  __shared__ double red[2][NW][CPW];
+  __shared__ double red[PAIR ? 4 : 2][NW][CPW];
   const int CHW = C * HW;
   const int ct = threadIdx.x % CT, g = threadIdx.x / CT, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int cb = xcd_block((int)blockIdx.x, (int)gridDim.x);
@@ -862,10 +968,12 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_v4_kernel(
   const bool ok_col = j0 < CHW;
   const int c0 = ok_col ? j0 / HW : 0;  // first channel of this float4
   float mean_s[NCH], invstd_s[NCH], gam[NCH], bet[NCH], rm[NCH], rv[NCH];
+  float mean2[NCH], invstd2[NCH], gam2[NCH], bet2[NCH], rm2[NCH], rv2[NCH];
 #pragma unroll
   for (int i = 0; i < NCH; ++i) {
     const int c = c0 + i;
     mean_s[i] = 0.f; invstd_s[i] = 0.f; gam[i] = 1.f; bet[i] = 0.f; rm[i] = 0.f; rv[i] = 0.f;
+    mean2[i] = 0.f; invstd2[i] = 0.f; gam2[i] = 1.f; bet2[i] = 0.f; rm2[i] = 0.f; rv2[i] = 0.f;
     if (ok_col) {
       if (BWD) {
         mean_s[i] = save_mean[c];
@@ -877,9 +985,21 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_v4_kernel(
         rm[i] = rmean[c];
         rv[i] = rvar[c];
       }
+      if constexpr (PAIR) {
+        if (BWD) {
+          mean2[i] = p2.save_mean2[c];
+          invstd2[i] = p2.save_invstd2[c];
+        }
+        if (p2.gamma2) gam2[i] = p2.gamma2[c];
+        if (!BWD && p2.beta2) bet2[i] = p2.beta2[c];
+        if (!BWD && p2.rmean2 != nullptr && g == 0) {
+          rm2[i] = p2.rmean2[c];
+          rv2[i] = p2.rvar2[c];
+        }
+      }
     }
   }
-  f32x4 v[NP], d[NP], m[NP];
+  f32x4 v[NP], d[NP], m[NP], v2[PAIR ? NP : 1];
   const f32x4 zero = {0.f, 0.f, 0.f, 0.f}, one = {1.f, 1.f, 1.f, 1.f};
   const int64_t slab = (int64_t)N * CHW;
 #pragma unroll
@@ -895,11 +1015,23 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_v4_kernel(
     }
     if (!BWD) {
       v[k] = ok ? (src ? sum : *reinterpret_cast<const f32x4*>(x + o)) : zero;
-      d[k] = (ok && res) ? *reinterpret_cast<const f32x4*>(res + o) : zero;
+      if constexpr (PAIR) {  // the downsample conv output (or its split-K slabs, slab order)
+        f32x4 t = zero;
+        if (ok && p2.src2 != nullptr) {
+          t = *reinterpret_cast<const f32x4*>(p2.src2 + o);
+          for (int z = 1; z < p2.nslab2; ++z) t += *reinterpret_cast<const f32x4*>(p2.src2 + z * slab + o);
+        } else if (ok) {
+          t = *reinterpret_cast<const f32x4*>(p2.x2 + o);
+        }
+        d[k] = t;
+      } else {
+        d[k] = (ok && res) ? *reinterpret_cast<const f32x4*>(res + o) : zero;
+      }
     } else {
       v[k] = ok ? *reinterpret_cast<const f32x4*>(x + o) : zero;
       d[k] = ok ? (src ? sum : *reinterpret_cast<const f32x4*>(dy + o)) : zero;
       m[k] = (ok && relu) ? *reinterpret_cast<const f32x4*>(yin + o) : one;
+      if constexpr (PAIR) v2[k] = ok ? *reinterpret_cast<const f32x4*>(p2.x2 + o) : zero;
     }
   }
   if (!BWD && src != nullptr) {  // BN's saved input = the conv output
@@ -909,9 +1041,21 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_v4_kernel(
       if (ok_col && n < N) *reinterpret_cast<f32x4*>(const_cast<float*>(x) + (int64_t)n * CHW + j0) = v[k];
     }
   }
-  double a[NCH], b[NCH];
+  if constexpr (PAIR) {
+    if (!BWD && p2.src2 != nullptr) {
 #pragma unroll
-  for (int i = 0; i < NCH; ++i) a[i] = b[i] = 0.0;
+      for (int k = 0; k < NP; ++k) {
+        const int n = g + k * RG;
+        if (ok_col && n < N) *reinterpret_cast<f32x4*>(const_cast<float*>(p2.x2) + (int64_t)n * CHW + j0) = d[k];
+      }
+    }
+  }
+  constexpr int NR = PAIR ? 4 : 2;  // reduced sums per channel: a, b (+ a2, b2)
+  double r[NR][NCH];
+#pragma unroll
+  for (int q = 0; q < NR; ++q)
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) r[q][i] = 0.0;
 #pragma unroll
   for (int k = 0; k < NP; ++k) {
     if (ok_col && g + k * RG < N) {
@@ -919,27 +1063,32 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_v4_kernel(
       for (int e = 0; e < 4; ++e) {
         const int i = e / CPC;
         if (!BWD) {
-          a[i] += (double)v[k][e];
-          b[i] += (double)v[k][e] * (double)v[k][e];
+          r[0][i] += (double)v[k][e];
+          r[1][i] += (double)v[k][e] * (double)v[k][e];
+          if constexpr (PAIR) {
+            r[NR - 2][i] += (double)d[k][e];
+            r[NR - 1][i] += (double)d[k][e] * (double)d[k][e];
+          }
         } else {
           const float dz = (m[k][e] > 0.f) ? d[k][e] : 0.f;
-          a[i] += (double)dz;
-          b[i] += (double)dz * (double)((v[k][e] - mean_s[i]) * invstd_s[i]);
+          r[0][i] += (double)dz;
+          r[1][i] += (double)dz * (double)((v[k][e] - mean_s[i]) * invstd_s[i]);
+          if constexpr (PAIR) r[NR - 1][i] += (double)dz * (double)((v2[k][e] - mean2[i]) * invstd2[i]);
         }
       }
     }
   }
 #pragma unroll
-  for (int i = 0; i < NCH; ++i) {
+  for (int q = 0; q < NR; ++q) {
+    if (BWD && PAIR && q == 2) continue;  // backward: sum dz is shared by both BNs
 #pragma unroll
-    for (int o = LPC / 2; o > 0; o >>= 1) {  // the float4s of a channel are adjacent lanes
-      a[i] += __shfl_xor(a[i], o, 64);
-      b[i] += __shfl_xor(b[i], o, 64);
-    }
+    for (int i = 0; i < NCH; ++i) {
 #pragma unroll
-    for (int o = CT; o < 64; o <<= 1) {  // row groups inside the wave
-      a[i] += __shfl_xor(a[i], o, 64);
-      b[i] += __shfl_xor(b[i], o, 64);
+      for (int o = LPC / 2; o > 0; o >>= 1)  // the float4s of a channel are adjacent lanes
+        r[q][i] += __shfl_xor(r[q][i], o, 64);
+#pragma unroll
+      for (int o = CT; o < 64; o <<= 1)  // row groups inside the wave
+        r[q][i] += __shfl_xor(r[q][i], o, 64);
     }
   }
   // channel slot of this thread's first channel inside the workgroup
@@ -947,27 +1096,54 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_v4_kernel(
   const bool lead = HW >= 4 ? ((4 * ct) % HW) == 0 : true;  // one writer lane per channel
   if (lane < CT && lead) {
 #pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      red[0][wave][slot + i] = a[i];
-      red[1][wave][slot + i] = b[i];
-    }
+    for (int q = 0; q < NR; ++q)
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) red[q][wave][slot + i] = r[q][i];
   }
   __syncthreads();
-  double A[NCH], B[NCH];
+  double R[NR][NCH];
 #pragma unroll
-  for (int i = 0; i < NCH; ++i) {
-    A[i] = B[i] = 0.0;
+  for (int q = 0; q < NR; ++q)
 #pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      A[i] += red[0][w][slot + i];
-      B[i] += red[1][w][slot + i];
+    for (int i = 0; i < NCH; ++i) {
+      R[q][i] = 0.0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) R[q][i] += red[q][w][slot + i];
     }
-  }
+  const double* A = R[0];
+  const double* B = R[1];
   if (!ok_col) return;
   const double M = (double)N * HW;
   const bool writer = g == 0 && lead;
   if (!BWD) {
-    f32x4 sc, sh;
+    f32x4 sc, sh, sc2 = zero, sh2 = zero;
+    if constexpr (PAIR) {
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        const double mu = R[NR - 2][i] / M;
+        double var = R[NR - 1][i] / M - mu * mu;
+        if (var < 0.0) var = 0.0;
+        const float mean = (float)mu, invstd = (float)(1.0 / sqrt(var + (double)eps));
+        const float scale = gam2[i] * invstd;
+        const float shift = bet2[i] - mean * scale;
+#pragma unroll
+        for (int e = 0; e < CPC; ++e) {
+          sc2[i * CPC + e] = scale;
+          sh2[i * CPC + e] = shift;
+        }
+        if (writer) {
+          const int c = c0 + i;
+          p2.save_mean2[c] = mean;
+          p2.save_invstd2[c] = invstd;
+          if (p2.rmean2 != nullptr) {
+            const double unb = M > 1.0 ? var * M / (M - 1.0) : var;
+            p2.rmean2[c] = (float)((1.0 - momentum) * (double)rm2[i] + momentum * mu);
+            p2.rvar2[c] = (float)((1.0 - momentum) * (double)rv2[i] + momentum * unb);
+          }
+          if (p2.nbt2 != nullptr && c == 0) p2.nbt2[0] += 1;
+        }
+      }
+    }
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const double mu = A[i] / M;
@@ -1000,19 +1176,24 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_v4_kernel(
         f32x4 z;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float t = fmaf(v[k][e], sc[e], sh[e]) + d[k][e];
+          const float t = PAIR ? fmaf(v[k][e], sc[e], sh[e]) + fmaf(d[k][e], sc2[e], sh2[e])
+                               : fmaf(v[k][e], sc[e], sh[e]) + d[k][e];
           z[e] = relu ? fmaxf(t, 0.f) : t;
         }
         *reinterpret_cast<f32x4*>(out + (int64_t)n * CHW + j0) = z;
       }
     }
   } else {
-    f32x4 k1, mdz, mdzx, mu, is;
+    f32x4 k1, mdz, mdzx, mu, is, k12, mdzx2, mu2, is2;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       if (writer) {
         if (dgamma) dgamma[c0 + i] = (float)B[i];
         if (dbeta) dbeta[c0 + i] = (float)A[i];
+        if constexpr (PAIR) {
+          if (p2.dgamma2) p2.dgamma2[c0 + i] = (float)R[NR - 1][i];
+          if (p2.dbeta2) p2.dbeta2[c0 + i] = (float)A[i];
+        }
       }
 #pragma unroll
       for (int e = 0; e < CPC; ++e) {
@@ -1021,6 +1202,10 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_v4_kernel(
         mdzx[i * CPC + e] = (float)(B[i] / M);
         mu[i * CPC + e] = mean_s[i];
         is[i * CPC + e] = invstd_s[i];
+        k12[i * CPC + e] = gam2[i] * invstd2[i];
+        mdzx2[i * CPC + e] = (float)(R[NR - 1][i] / M);
+        mu2[i * CPC + e] = mean2[i];
+        is2[i * CPC + e] = invstd2[i];
       }
     }
 #pragma unroll
@@ -1033,11 +1218,13 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_v4_kernel(
           const float dz = (m[k][e] > 0.f) ? d[k][e] : 0.f;
           const float xh = (v[k][e] - mu[e]) * is[e];
           o4[e] = k1[e] * (dz - mdz[e] - xh * mdzx[e]);
-          z4[e] = dz;
+          if constexpr (PAIR) z4[e] = k12[e] * (dz - mdz[e] - (v2[k][e] - mu2[e]) * is2[e] * mdzx2[e]);
+          else z4[e] = dz;
         }
         const int64_t o = (int64_t)n * CHW + j0;
         *reinterpret_cast<f32x4*>(out + o) = o4;
-        if (dres) *reinterpret_cast<f32x4*>(dres + o) = z4;
+        if constexpr (PAIR) *reinterpret_cast<f32x4*>(p2.out2 + o) = z4;
+        else if (dres) *reinterpret_cast<f32x4*>(dres + o) = z4;
       }
     }
   }
@@ -1076,25 +1263,34 @@ static void launch_small_fused_cw(int HW, const float* x, const float* res, cons
                                   const float* gamma, const float* beta, float* rmean, float* rvar, int64_t* nbt,
                                   float* sm, float* si, float* dgamma, float* dbeta, float* out, float* dres, int N,
                                   int C, float eps, float momentum, int relu, hipStream_t s, const float* src,
-                                  int nslab) {
+                                  int nslab, const BnPair* pr) {
   const int nblk = (int)(((int64_t)C * HW + CW - 1) / CW);
+  const BnPair pp = pr ? *pr : BnPair{};
   auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
   // float4 kernel: rows of whole float4s, 16-B aligned operands.  Not for small maps at small
   // batches: with HW <= 4 and N <= 128 the scalar kernel's 4-column blocks keep 4x more threads
   // busy per row and its reduction is shorter — ResNet-18 at batch 64: HW = 1 4.8 vs 6.7 µs, HW = 4
   // 4.8 vs 5.0 µs per launch (v4 wins everywhere at batch 512 and for HW = 16: 8.0 -> 5.3 µs at 64)
   const bool v4 = ((int64_t)C * HW) % 4 == 0 && a16(x) && a16(res) && a16(dy) && a16(yin) && a16(out) &&
-                  a16(dres) && a16(src) && !vec_off() && (HW >= 8 || N > 128);
+                  a16(dres) && a16(src) && (pr == nullptr || (a16(pr->x2) && a16(pr->out2) && a16(pr->src2) && HW >= 4)) &&
+                  !vec_off() && (HW >= 8 || N > 128);  // (pair at HW < 4: 4 channels' operands per float4 spill)
+#define NDP_BN_FUSED_P(HWV, P)                                                                                     \
+  if (v4) {                                                                                                        \
+    if constexpr (P == 0 || HWV >= 4)                                                                              \
+      hipLaunchKernelGGL((bn_small_fused_v4_kernel<HWV, BWD, CW, kFusedMaxN, P>), dim3((unsigned)nblk),            \
+                         dim3(kFusedThreads), 0, s, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma,  \
+                         dbeta, out, dres, N, C, eps, momentum, relu, src, nslab, pp);                               \
+  } else                                                                                                           \
+    hipLaunchKernelGGL((bn_small_fused_kernel<HWV, BWD, CW, kFusedMaxN, P>), dim3((unsigned)nblk),                 \
+                       dim3(kFusedThreads), 0, s, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma,    \
+                       dbeta, out, dres, N, C, eps, momentum, relu, src, nslab, pp);
 #define NDP_BN_FUSED(HWV)                                                                                          \
   if constexpr (CW % HWV == 0) {                                                                                   \
-    if (v4)                                                                                                        \
-      hipLaunchKernelGGL((bn_small_fused_v4_kernel<HWV, BWD, CW, kFusedMaxN>), dim3((unsigned)nblk),               \
-                         dim3(kFusedThreads), 0, s, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma,  \
-                         dbeta, out, dres, N, C, eps, momentum, relu, src, nslab);                                   \
-    else                                                                                                           \
-      hipLaunchKernelGGL((bn_small_fused_kernel<HWV, BWD, CW, kFusedMaxN>), dim3((unsigned)nblk),                  \
-                         dim3(kFusedThreads), 0, s, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma,  \
-                         dbeta, out, dres, N, C, eps, momentum, relu, src, nslab);                                   \
+    if (pr) {                                                                                                      \
+      NDP_BN_FUSED_P(HWV, 1)                                                                                       \
+    } else {                                                                                                       \
+      NDP_BN_FUSED_P(HWV, 0)                                                                                       \
+    }                                                                                                              \
   }
   switch (HW) {  // the caller picks CW >= HW
     case 1: NDP_BN_FUSED(1); break;
@@ -1104,6 +1300,7 @@ static void launch_small_fused_cw(int HW, const float* x, const float* res, cons
     default: NDP_BN_FUSED(16); break;
   }
 #undef NDP_BN_FUSED
+#undef NDP_BN_FUSED_P
 }
 
 template <int BWD>
@@ -1111,31 +1308,32 @@ static void launch_small_fused(int HW, const float* x, const float* res, const f
                                const float* gamma, const float* beta, float* rmean, float* rvar, int64_t* nbt,
                                float* sm, float* si, float* dgamma, float* dbeta, float* out, float* dres, int N,
                                int C, float eps, float momentum, int relu, hipStream_t s, const float* src,
-                               int nslab) {
+                               int nslab, const BnPair* pr = nullptr) {
   if (HW == 64) {  // one channel per workgroup (bn_fused_ok); float4 unless an operand is unaligned
     auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    if (pr != nullptr) return;  // (bn_pair_ok: no pair on the 8x8 maps)
     if (a16(x) && a16(res) && a16(dy) && a16(yin) && a16(out) && a16(dres) && a16(src))
       hipLaunchKernelGGL((bn_small_fused_v4_kernel<64, BWD, 64, kFusedMaxN64>), dim3((unsigned)C),
                          dim3(kFusedThreads), 0, s, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma,
-                         dbeta, out, dres, N, C, eps, momentum, relu, src, nslab);
+                         dbeta, out, dres, N, C, eps, momentum, relu, src, nslab, BnPair{});
     else
       hipLaunchKernelGGL((bn_small_fused_kernel<64, BWD, 64, kFusedMaxN64>), dim3((unsigned)C), dim3(kFusedThreads),
                          0, s, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out, dres, N, C,
-                         eps, momentum, relu, src, nslab);
+                         eps, momentum, relu, src, nslab, BnPair{});
     return;
   }
   switch (bn_colw_for(HW, C, N)) {
     case 16:
       launch_small_fused_cw<BWD, 16>(HW, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out,
-                                     dres, N, C, eps, momentum, relu, s, src, nslab);
+                                     dres, N, C, eps, momentum, relu, s, src, nslab, pr);
       break;
     case 4:
       launch_small_fused_cw<BWD, 4>(HW, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out,
-                                    dres, N, C, eps, momentum, relu, s, src, nslab);
+                                    dres, N, C, eps, momentum, relu, s, src, nslab, pr);
       break;
     default:
       launch_small_fused_cw<BWD, 8>(HW, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma, dbeta, out,
-                                    dres, N, C, eps, momentum, relu, s, src, nslab);
+                                    dres, N, C, eps, momentum, relu, s, src, nslab, pr);
   }
 }
 
@@ -1267,6 +1465,50 @@ void launch_bn_relu_maxpool(const float* x, float* y, uint8_t* idx, const float*
   hipLaunchKernelGGL(bn_relu_maxpool_kernel, dim3(Sa, C), dim3(256), 0, s, x, y, idx, gamma, beta, rmean, rvar, nbt,
                      save_mean, save_invstd, xstats != nullptr ? xstats : part, N, C, H, W, Sa, eps, momentum,
                      xstats != nullptr ? xS : 0);
+}
+
+// The downsample block's two BatchNorms in one launch (BnPair): the small-map single-launch
+// kernels, i.e. layers 2-4 of the ResNet-18 step at per-GPU batch <= 512 (not the 8x8 maps).
+bool bn_pair_ok(int N, int C, int HW) { return HW != 64 && bn_fused_ok(N, C, HW); }
+
+void launch_bn_pair_fwd(const float* x, const float* x2, float* y, const float* gamma, const float* beta,
+                        float* rmean, float* rvar, int64_t* nbt, float* save_mean, float* save_invstd,
+                        const float* gamma2, const float* beta2, float* rmean2, float* rvar2, int64_t* nbt2,
+                        float* save_mean2, float* save_invstd2, int N, int C, int HW, float eps, float momentum,
+                        hipStream_t s, const float* xpart, int nslab, const float* x2part, int nslab2) {
+  if (xpart != nullptr && nslab < 2) xpart = nullptr;
+  if (xpart != nullptr && nslab > kMaxFusedSlabs) {
+    launch_slab_sum(xpart, const_cast<float*>(x), (int64_t)N * C * HW, nslab, s);
+    xpart = nullptr;
+  }
+  if (x2part != nullptr && nslab2 < 2) x2part = nullptr;
+  if (x2part != nullptr && nslab2 > kMaxFusedSlabs) {
+    launch_slab_sum(x2part, const_cast<float*>(x2), (int64_t)N * C * HW, nslab2, s);
+    x2part = nullptr;
+  }
+  const BnPair pr{x2, gamma2, beta2, rmean2, rvar2, nbt2, save_mean2, save_invstd2, nullptr, nullptr, nullptr,
+                  x2part, x2part ? nslab2 : 0};
+  launch_small_fused<0>(HW, x, nullptr, nullptr, nullptr, gamma, beta, rmean, rvar, nbt, save_mean, save_invstd,
+                        nullptr, nullptr, y, nullptr, N, C, eps, momentum, 1, s, xpart, nslab, &pr);
+}
+
+void launch_bn_pair_bwd(const float* dy, const float* y, const float* x, const float* x2, const float* gamma,
+                        const float* save_mean, const float* save_invstd, const float* gamma2,
+                        const float* save_mean2, const float* save_invstd2, float* dx, float* dx2, float* dgamma,
+                        float* dbeta, float* dgamma2, float* dbeta2, int N, int C, int HW, hipStream_t s,
+                        const float* dypart, int nslab, const float* dyadd) {
+  if (dypart != nullptr && nslab < 2) dypart = nullptr;
+  if (dypart == nullptr) dyadd = nullptr;
+  if (dypart != nullptr && nslab > kMaxFusedSlabs) {
+    launch_slab_sum(dypart, const_cast<float*>(dy), (int64_t)N * C * HW, nslab, s, dyadd);
+    dypart = nullptr;
+    dyadd = nullptr;
+  }
+  const BnPair pr{x2, gamma2, nullptr, nullptr, nullptr, nullptr, const_cast<float*>(save_mean2),
+                  const_cast<float*>(save_invstd2), dgamma2, dbeta2, dx2, nullptr, 0};
+  launch_small_fused<1>(HW, x, dyadd, dy, y, gamma, nullptr, nullptr, nullptr, nullptr, const_cast<float*>(save_mean),
+                        const_cast<float*>(save_invstd), dgamma, dbeta, dx, nullptr, N, C, 0.f, 0.f, 1, s, dypart,
+                        nslab, &pr);
 }
 
 bool bn_two_kernel_path(int N, int C, int HW, int single) {

@@ -431,6 +431,66 @@ void bn_bwd(torch::Tensor dy, c10::optional<torch::Tensor> y, torch::Tensor x, c
   check_launch("launch_bn_bwd");
 }
 
+// the downsample block's relu(BN(x) + BN2(x2)) in one launch (training); momentum applies to both
+void bn_pair_fwd(torch::Tensor x, torch::Tensor x2, torch::Tensor y, torch::Tensor gamma, torch::Tensor beta,
+                 torch::Tensor rmean, torch::Tensor rvar, torch::Tensor nbt, torch::Tensor save_mean,
+                 torch::Tensor save_invstd, torch::Tensor gamma2, torch::Tensor beta2, torch::Tensor rmean2,
+                 torch::Tensor rvar2, torch::Tensor nbt2, torch::Tensor save_mean2, torch::Tensor save_invstd2,
+                 double eps, double momentum, c10::optional<torch::Tensor> xpart, int64_t nslab,
+                 c10::optional<torch::Tensor> x2part, int64_t nslab2) {
+  for (auto* t : {&x, &x2, &y, &gamma, &beta, &rmean, &rvar, &save_mean, &save_invstd, &gamma2, &beta2, &rmean2,
+                  &rvar2, &save_mean2, &save_invstd2})
+    check_f32(*t, "bn_pair_fwd operand");
+  TORCH_CHECK(x.dim() >= 2 && x.sizes() == y.sizes() && x.sizes() == x2.sizes() && x.is_contiguous() &&
+                  x2.is_contiguous() && y.is_contiguous(), "bn_pair_fwd: x, x2, y must be contiguous, one shape");
+  const int N = (int)x.size(0), C = (int)x.size(1);
+  const int HW = (int)(x.numel() / ((int64_t)N * C));
+  TORCH_CHECK(ndp::bn_pair_ok(N, C, HW), "bn_pair_fwd: shape outside the single-launch path (bn_pair_ok)");
+  for (auto* t : {&gamma, &beta, &rmean, &rvar, &save_mean, &save_invstd, &gamma2, &beta2, &rmean2, &rvar2,
+                  &save_mean2, &save_invstd2})
+    TORCH_CHECK(t->numel() >= C, "bn_pair_fwd: per-channel operand too small");
+  check_dev(nbt, "nbt"); check_dev(nbt2, "nbt2");
+  TORCH_CHECK(nbt.scalar_type() == torch::kInt64 && nbt2.scalar_type() == torch::kInt64, "num_batches_tracked int64");
+  ndp::launch_bn_pair_fwd(x.data_ptr<float>(), x2.data_ptr<float>(), y.data_ptr<float>(), gamma.data_ptr<float>(),
+                          beta.data_ptr<float>(), rmean.data_ptr<float>(), rvar.data_ptr<float>(),
+                          nbt.data_ptr<int64_t>(), save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(),
+                          gamma2.data_ptr<float>(), beta2.data_ptr<float>(), rmean2.data_ptr<float>(),
+                          rvar2.data_ptr<float>(), nbt2.data_ptr<int64_t>(), save_mean2.data_ptr<float>(),
+                          save_invstd2.data_ptr<float>(), N, C, HW, (float)eps, (float)momentum, cur_stream(),
+                          slab_input(xpart, nslab, x.numel(), "bn_pair_fwd"), (int)nslab,
+                          slab_input(x2part, nslab2, x.numel(), "bn_pair_fwd"), (int)nslab2);
+  check_launch("launch_bn_pair_fwd");
+}
+
+void bn_pair_bwd(torch::Tensor dy, torch::Tensor y, torch::Tensor x, torch::Tensor x2, torch::Tensor gamma,
+                 torch::Tensor save_mean, torch::Tensor save_invstd, torch::Tensor gamma2, torch::Tensor save_mean2,
+                 torch::Tensor save_invstd2, torch::Tensor dx, torch::Tensor dx2, torch::Tensor dgamma,
+                 torch::Tensor dbeta, torch::Tensor dgamma2, torch::Tensor dbeta2, c10::optional<torch::Tensor> dypart,
+                 int64_t nslab, c10::optional<torch::Tensor> dyadd) {
+  for (auto* t : {&dy, &y, &x, &x2, &gamma, &save_mean, &save_invstd, &gamma2, &save_mean2, &save_invstd2, &dx, &dx2,
+                  &dgamma, &dbeta, &dgamma2, &dbeta2})
+    check_f32(*t, "bn_pair_bwd operand");
+  for (auto* t : {&dy, &y, &x2, &dx, &dx2})
+    TORCH_CHECK(t->sizes() == x.sizes() && t->is_contiguous(), "bn_pair_bwd: tensors must be contiguous, one shape");
+  TORCH_CHECK(x.is_contiguous(), "bn_pair_bwd: contiguous x");
+  if (dyadd.has_value()) {
+    check_f32(*dyadd, "dyadd");
+    TORCH_CHECK(dyadd->sizes() == dy.sizes() && dyadd->is_contiguous() && dypart.has_value(),
+                "bn_pair_bwd: dyadd must match dy and come with dypart");
+  }
+  const int N = (int)x.size(0), C = (int)x.size(1);
+  const int HW = (int)(x.numel() / ((int64_t)N * C));
+  TORCH_CHECK(ndp::bn_pair_ok(N, C, HW), "bn_pair_bwd: shape outside the single-launch path (bn_pair_ok)");
+  ndp::launch_bn_pair_bwd(dy.data_ptr<float>(), y.data_ptr<float>(), x.data_ptr<float>(), x2.data_ptr<float>(),
+                          gamma.data_ptr<float>(), save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(),
+                          gamma2.data_ptr<float>(), save_mean2.data_ptr<float>(), save_invstd2.data_ptr<float>(),
+                          dx.data_ptr<float>(), dx2.data_ptr<float>(), dgamma.data_ptr<float>(),
+                          dbeta.data_ptr<float>(), dgamma2.data_ptr<float>(), dbeta2.data_ptr<float>(), N, C, HW,
+                          cur_stream(), slab_input(dypart, nslab, dy.numel(), "bn_pair_bwd"), (int)nslab,
+                          opt_f32(dyadd, "dyadd"));
+  check_launch("launch_bn_pair_bwd");
+}
+
 // max-pool 2-D (stride/pad symmetric, dilation 1, floor mode): x [N, C, H, W] -> y, idx [N, C, OH, OW]
 static ndp::PoolGeom pool_geom(const torch::Tensor& x, const torch::Tensor& y, int64_t k, int64_t stride,
                                int64_t pad) {
@@ -1276,6 +1336,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return ndp::bn_two_kernel_path((int)N, (int)C, (int)HW, single ? 1 : 0);
   });
   m.def("bn_set_vec4", &ndp::bn_set_vec4);
+  m.def("bn_pair_ok", &ndp::bn_pair_ok);
+  m.def("bn_pair_fwd", &bn_pair_fwd);
+  m.def("bn_pair_bwd", &bn_pair_bwd);
   m.def("wino_set_enabled", &ndp::wino_set_enabled);
   m.def("bn_slices", &bn_slices);
   m.def("slab_sum", &slab_sum);
@@ -1341,6 +1404,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ce_bwd", &ce_bwd);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
+  m.def("attn_set_chains", &ndp::attn_set_chains);
   register_comm(m);
   register_ipc(m);
 }

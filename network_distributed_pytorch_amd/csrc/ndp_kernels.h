@@ -148,6 +148,18 @@ void launch_bn_bwd(const float* dy, const float* y, const float* x, const float*
 // mbeta (nullable, relu, two-kernel path only): y was never stored; the ReLU mask is recomputed
 // from x as fmaf(x, gamma * invstd, beta - mean * gamma * invstd) > 0 (the forward's own ops)
 bool bn_two_kernel_path(int N, int C, int HW, int single);
+// the downsample block's BN(x) + BN2(x2) -> ReLU in one launch per direction (batchnorm.hip BnPair)
+bool bn_pair_ok(int N, int C, int HW);
+void launch_bn_pair_fwd(const float* x, const float* x2, float* y, const float* gamma, const float* beta,
+                        float* rmean, float* rvar, int64_t* nbt, float* save_mean, float* save_invstd,
+                        const float* gamma2, const float* beta2, float* rmean2, float* rvar2, int64_t* nbt2,
+                        float* save_mean2, float* save_invstd2, int N, int C, int HW, float eps, float momentum,
+                        hipStream_t s, const float* xpart, int nslab, const float* x2part, int nslab2);
+void launch_bn_pair_bwd(const float* dy, const float* y, const float* x, const float* x2, const float* gamma,
+                        const float* save_mean, const float* save_invstd, const float* gamma2,
+                        const float* save_mean2, const float* save_invstd2, float* dx, float* dx2, float* dgamma,
+                        float* dbeta, float* dgamma2, float* dbeta2, int N, int C, int HW, hipStream_t s,
+                        const float* dypart, int nslab, const float* dyadd);
 void bn_set_vec4(bool on);
 // BN (training) -> ReLU -> MaxPool(3, 2, 1) in one pass without storing the BN output (the
 // ResNet stem tail); y / idx: the pooled output and its uint8 window offsets (pool.hip layout)
@@ -366,6 +378,8 @@ void launch_attn_fwd(const float* q, const float* k, const float* v, const int32
                      int64_t ldq = 0);
 // ldq: token row stride of q / k / v (and dq / dk / dv): 0 = H*64 (contiguous), 3*H*64 for
 // views into a packed [B, S, 3, H, 64] QKV projection.  delta: [B, H, S] scratch
+// 1 or 2 accumulator chains per product in the attention backward (A/B switch)
+void attn_set_chains(int n);
 void launch_attn_bwd(const float* q, const float* k, const float* v, const int32_t* mask, const float* o,
                      const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv, int B,
                      int S, int H, float scale, const int32_t* seed, float p_drop, hipStream_t s,

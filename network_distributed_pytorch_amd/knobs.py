@@ -26,6 +26,7 @@ FUSIONS = {
     "bn_vec4": "float4 single-launch small-map BN kernel (csrc/batchnorm.hip; off: the scalar one)",
     "winograd": "F(2x2,3x3) Winograd for the layer1 3x3 forward / grad-x (csrc/winograd.hip)",
     "stem_pool": "stem BN -> ReLU -> max-pool in one pass (ops/batchnorm.py)",
+    "bn_pair": "downsample block's bn2 + downsample BN + ReLU in one launch per direction (ops/batchnorm.py)",
     "defer_gradw": "grad-W slab sums / folds batched at the end of backward (ops/gradfinish.py)",
     "grad_arena": "dense-arm gradients written straight into the bucket arena (ops/gradarena.py)",
     "tgemm": "strided / tabled MFMA GEMM convs for 1x1 layers (ops/tgconv.py)",

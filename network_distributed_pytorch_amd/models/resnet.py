@@ -26,7 +26,7 @@ from typing import List, Optional, Type, Union
 import torch
 import torch.nn as nn
 
-from ..ops.batchnorm import BatchNormAct2d
+from ..ops.batchnorm import BatchNormAct2d, bn_pair_act
 from ..ops.conv import WinoBank
 from ..ops.gradlink import BranchLink, GradLink
 from ..ops.linear import Linear
@@ -95,16 +95,22 @@ class BasicBlock(nn.Module):
                 # x's gradient is autograd's sum of two grad-x tensors: conv1's cannot be left
                 # as unsummed slabs for the previous BN2
                 grad_in = None
+            cds = None  # the downsample conv's output, its BN paired with bn2 (bn_pair_act)
             if self.downsample is not None:
                 ds = self.downsample
                 if train and len(ds) == 2 and isinstance(ds[0], GemmConv2d) and isinstance(ds[1], BatchNormAct2d):
-                    identity = ds[1](ds[0](x, slab_out=sd, branch=br), slab_in=sd)
+                    cds = ds[0](x, slab_out=sd, branch=br)
                 else:
                     identity = ds(x)
             out = self.bn1(self.conv1(x, link=link, slab_out=s1, grad_slab=grad_in, branch=br), relu=True,
                            slab_in=s1, grad_slab=g1)
-            return self.bn2(self.conv2(out, slab_out=s2, grad_slab=g1), residual=identity, relu=True, link=link,
-                            slab_in=s2, grad_slab=grad_out)
+            c2 = self.conv2(out, slab_out=s2, grad_slab=g1)
+            if cds is not None:
+                y = bn_pair_act(self.bn2, self.downsample[1], c2, cds, slab_in=s2, slab_in2=sd, grad_slab=grad_out)
+                if y is not None:
+                    return y
+                identity = self.downsample[1](cds, slab_in=sd)
+            return self.bn2(c2, residual=identity, relu=True, link=link, slab_in=s2, grad_slab=grad_out)
         identity = x if self.downsample is None else self.downsample(x)
         out = self.relu(self.bn1(self.conv1(x)))
         out = self.bn2(self.conv2(out))

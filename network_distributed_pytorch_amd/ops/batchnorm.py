@@ -23,7 +23,7 @@ from ._ext import ext
 from .gradarena import grad_buffer
 from ..knobs import fusion_on
 
-__all__ = ["BatchNormAct2d", "bn_act"]
+__all__ = ["BatchNormAct2d", "bn_act", "bn_pair_act"]
 
 
 class _BNActFn(torch.autograd.Function):
@@ -120,6 +120,69 @@ class _BNReluPoolFn(torch.autograd.Function):
             ext().bn_bwd(dz, None, x, weight, save_mean, save_invstd, dx, None, dgamma, dbeta, part, True, ctx.single,
                          None, 0, None, bias)
         return dx, dgamma, dbeta, None, None, None, None, None, None, None, None
+
+
+class _BNPairFn(torch.autograd.Function):
+    """relu(bn(x) + bn2(x2)) — a ResNet downsample block's bn2 and downsample BN in one launch per
+    direction (csrc/batchnorm.hip BnPair).  The downsample BN's output is never stored; backward
+    forms both BNs' sums from the shared dz = dy * (y > 0) and writes both input gradients."""
+
+    @staticmethod
+    def forward(ctx, x, x2, w, b, rm, rv, nbt, w2, b2, rm2, rv2, nbt2, eps, momentum, slab_in=None, slab_in2=None,
+                grad_slab=None):
+        x, x2 = x.contiguous(), x2.contiguous()
+        C = x.shape[1]
+        y = torch.empty_like(x)
+        sm, si, sm2, si2 = (torch.empty(C, device=x.device, dtype=torch.float32) for _ in range(4))
+        xpart, nslab = slab_in.take_fwd() if slab_in is not None else (None, 0)
+        x2part, nslab2 = slab_in2.take_fwd() if slab_in2 is not None else (None, 0)
+        for link in (slab_in, slab_in2):  # the kernel forms its own statistics
+            if link is not None:
+                link.take_stats()
+        ext().bn_pair_fwd(x, x2, y, w, b, rm, rv, nbt, sm, si, w2, b2, rm2, rv2, nbt2, sm2, si2, float(eps),
+                          float(momentum), xpart, nslab, x2part, nslab2)
+        ctx.grad_slab = grad_slab
+        ctx.params = (w, b, w2, b2)
+        ctx.save_for_backward(x, x2, y, w, w2, sm, si, sm2, si2)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, x2, y, w, w2, sm, si, sm2, si2 = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx, dx2 = torch.empty_like(x), torch.empty_like(x2)
+        pw, pb, pw2, pb2 = ctx.params
+        dg, db = grad_buffer(pw, w), grad_buffer(pb, w)
+        dg2, db2 = grad_buffer(pw2, w2), grad_buffer(pb2, w2)
+        dypart, nslab, dyadd = None, 0, None
+        if ctx.grad_slab is not None:
+            dypart, nslab = ctx.grad_slab.take_bwd()
+            dyadd = ctx.grad_slab.take_bwd_add()
+            ctx.grad_slab.take_bwd_stats()
+            ctx.grad_slab.bn_saved = None
+        ext().bn_pair_bwd(dy, y, x, x2, w, sm, si, w2, sm2, si2, dx, dx2, dg, db, dg2, db2, dypart, nslab, dyadd)
+        return (dx, dx2, dg, db, None, None, None, dg2, db2, None, None, None, None, None, None, None, None)
+
+
+# the downsample block's two BNs in one launch per direction (NDP_FUSION_OFF=bn_pair: two launches)
+BN_PAIR = fusion_on("bn_pair")
+
+
+def bn_pair_act(bn: "BatchNormAct2d", bn2: "BatchNormAct2d", x: torch.Tensor, x2: torch.Tensor, slab_in=None,
+                slab_in2=None, grad_slab=None) -> Optional[torch.Tensor]:
+    """``relu(bn(x) + bn2(x2))`` as one training launch per direction where the single-launch
+    small-map kernels apply, else None (the caller runs the two BNs)."""
+    if not (BN_PAIR and x.is_cuda and x.dtype == torch.float32 and x2.dtype == torch.float32
+            and torch.is_grad_enabled() and bn.training and bn2.training and x.shape == x2.shape and x.dim() == 4
+            and bn.fused_small and bn2.fused_small and bn.eps == bn2.eps and bn.momentum == bn2.momentum
+            and all(m.affine and m.track_running_stats and m.momentum is not None for m in (bn, bn2))):
+        return None
+    N, C = x.shape[:2]
+    if not ext().bn_pair_ok(N, C, x.shape[2] * x.shape[3]):
+        return None
+    return _BNPairFn.apply(x, x2, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.num_batches_tracked,
+                           bn2.weight, bn2.bias, bn2.running_mean, bn2.running_var, bn2.num_batches_tracked,
+                           bn.eps, bn.momentum, slab_in, slab_in2, grad_slab)
 
 
 # BN backward statistics from the grad-x epilogue of the conv producing dy (ops/slablink.py;
