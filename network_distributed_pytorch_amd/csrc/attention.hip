@@ -254,11 +254,9 @@ struct AttnBwdArgs {
 // Recompute one 16(query) x 64(key) probability tile in the S^T layout used by the forward:
 // lane (g, c16): query = q (lane), keys 16kt + 4g + r.
 // dK, dV: one wave owns 16 keys (rows = d on MFMA outputs), loops over all queries.
-// NCH = accumulator chains per product: 1 (shipped) or 2 (each dK / dV / dQ tile accumulates even
-// and odd r into separate registers, summed at the end: half the dependent MFMA chain length, 2x
-// the accumulator registers).  Both are checked against fp64 (tests/test_attention.py); the A/B is
-// in profiles/r5/attn_chains.md.
-template <int NCH>
+// One accumulator chain per product: 8 independent dK / dV accumulators are already in flight.
+// A two-chain variant (even / odd r summed at the end) passed the fp64 tests but spilled (32 ->
+// 232 B/lane scratch) and ran 53 % slower: profiles/r5/attn_chains.md (code at commit 831b94e).
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void attn_bwd_dkdv_kernel(AttnBwdArgs a) {
   const uint32_t seed = (a.drop_thr && a.seedp) ? (uint32_t)*a.seedp : 0u;
   __shared__ __attribute__((aligned(16))) float Qs[64 * kLD];    // Q[q][d] (scaled)
@@ -300,14 +298,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       Vr[cc][t] = vv[t];
     }
   }
-  f32x4 dK[NCH][4], dV[NCH][4];   // transposed: rows d (16dt + 4g + r), col = key (lane)
+  f32x4 dK[4], dV[4];   // transposed: rows d (16dt + 4g + r), col = key (lane)
 #pragma unroll
-  for (int c = 0; c < NCH; ++c)
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      dK[c][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      dV[c][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+  for (int dt = 0; dt < 4; ++dt) {
+    dK[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dV[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 
   for (int q0 = 0; q0 < a.S; q0 += 64) {
     __syncthreads();
@@ -365,8 +361,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         const float* qp = &Qs[(16 * qt + 4 * g) * kLD + 16 * dt + c16];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          dV[r % NCH][dt] = mfma16(gr[r * kLD], Pd[r], dV[r % NCH][dt]);
-          dK[r % NCH][dt] = mfma16(qp[r * kLD], dS[r], dK[r % NCH][dt]);
+          dV[dt] = mfma16(gr[r * kLD], Pd[r], dV[dt]);
+          dK[dt] = mfma16(qp[r * kLD], dS[r], dK[dt]);
         }
       }
       (void)P;
@@ -376,20 +372,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   // dK^T tile: col = key (lane), rows d = 16dt + 4g + r.  Q was pre-scaled -> dK = dS^T (Q*scale)
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) {
-    f32x4 sk = dK[0][dt], sv = dV[0][dt];
-#pragma unroll
-    for (int c = 1; c < NCH; ++c) {
-      sk += dK[c][dt];
-      sv += dV[c][dt];
-    }
-    *reinterpret_cast<f32x4*>(a.dk + qbase + (int64_t)key * qrs + 16 * dt + 4 * g) = sk;
-    *reinterpret_cast<f32x4*>(a.dv + qbase + (int64_t)key * qrs + 16 * dt + 4 * g) = sv;
+    *reinterpret_cast<f32x4*>(a.dk + qbase + (int64_t)key * qrs + 16 * dt + 4 * g) = dK[dt];
+    *reinterpret_cast<f32x4*>(a.dv + qbase + (int64_t)key * qrs + 16 * dt + 4 * g) = dV[dt];
   }
 }
 
 // dQ: one wave owns 16 queries, loops over keys (recomputes P and dP).  4 waves per SIMD: its
 // registers fit 128 VGPRs without spilling (160 with AGPRs by default -> 3 waves).
-template <int NCH>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   const uint32_t seed = (a.drop_thr && a.seedp) ? (uint32_t)*a.seedp : 0u;
   __shared__ __attribute__((aligned(16))) float Ks[kBK * kLD];   // K[key][d]
@@ -422,11 +411,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   const float L = qok ? a.lse[(int64_t)bh * a.S + q] : 0.f;
   const float LL = qok ? a.lse[(int64_t)a.B * a.H * a.S + (int64_t)bh * a.S + q] : 0.f;
   const float Dl = qok ? a.delta[(int64_t)bh * a.S + q] : 0.f;
-  f32x4 dQ[NCH][4];
+  f32x4 dQ[4];
 #pragma unroll
-  for (int c = 0; c < NCH; ++c)
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) dQ[c][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int dt = 0; dt < 4; ++dt) dQ[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   for (int k0 = 0; k0 < a.S; k0 += kBK) {
     if (skip_block(a.mask, row_any, blkv, k0)) continue;
@@ -479,24 +466,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       for (int dt = 0; dt < 4; ++dt) {
         const float* kp = &Ks[(16 * kt + 4 * g) * kLD + 16 * dt + c16];  // K^T[d][key] = K[key][d]
 #pragma unroll
-        for (int r = 0; r < 4; ++r) dQ[r % NCH][dt] = mfma16(kp[r * kLD], dS[r], dQ[r % NCH][dt]);
+        for (int r = 0; r < 4; ++r) dQ[dt] = mfma16(kp[r * kLD], dS[r], dQ[dt]);
       }
     }
   }
   if (!qok) return;
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt) {
-    f32x4 sq = dQ[0][dt];
-#pragma unroll
-    for (int c = 1; c < NCH; ++c) sq += dQ[c][dt];
-    *reinterpret_cast<f32x4*>(a.dq + qbase + (int64_t)q * qrs + 16 * dt + 4 * g) = sq * a.scale;
-  }
+  for (int dt = 0; dt < 4; ++dt)
+    *reinterpret_cast<f32x4*>(a.dq + qbase + (int64_t)q * qrs + 16 * dt + 4 * g) = dQ[dt] * a.scale;
 }
 
 // ------------------------------------ launchers ------------------------------------------
-static int g_attn_chains = 1;
-void attn_set_chains(int n) { g_attn_chains = n == 2 ? 2 : 1; }
-
 void launch_attn_fwd(const float* q, const float* k, const float* v, const int32_t* mask, float* o, float* lse,
                      int B, int S, int H, float scale, const int32_t* seed, float p_drop, hipStream_t s,
                      int64_t ldq) {
@@ -519,14 +499,8 @@ void launch_attn_bwd(const float* q, const float* k, const float* v, const int32
     a.drop_thr = (uint32_t)fminf(p_drop * 4294967296.0f, 4294967295.0f);
     a.drop_scale = 1.f / (1.f - p_drop);
   }
-  const dim3 grid((S + 63) / 64, B * H);
-  if (g_attn_chains == 2) {
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<2>, grid, dim3(256), 0, s, a);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<2>, grid, dim3(256), 0, s, a);
-  } else {
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<1>, grid, dim3(256), 0, s, a);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<1>, grid, dim3(256), 0, s, a);
-  }
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((S + 63) / 64, B * H), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((S + 63) / 64, B * H), dim3(256), 0, s, a);
 }
 
 }  // namespace ndp

@@ -1404,7 +1404,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ce_bwd", &ce_bwd);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
-  m.def("attn_set_chains", &ndp::attn_set_chains);
   register_comm(m);
   register_ipc(m);
 }

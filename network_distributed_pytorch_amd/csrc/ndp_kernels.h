@@ -378,8 +378,6 @@ void launch_attn_fwd(const float* q, const float* k, const float* v, const int32
                      int64_t ldq = 0);
 // ldq: token row stride of q / k / v (and dq / dk / dv): 0 = H*64 (contiguous), 3*H*64 for
 // views into a packed [B, S, 3, H, 64] QKV projection.  delta: [B, H, S] scratch
-// 1 or 2 accumulator chains per product in the attention backward (A/B switch)
-void attn_set_chains(int n);
 void launch_attn_bwd(const float* q, const float* k, const float* v, const int32_t* mask, const float* o,
                      const float* dout, const float* lse, float* delta, float* dq, float* dk, float* dv, int B,
                      int S, int H, float scale, const int32_t* seed, float p_drop, hipStream_t s,

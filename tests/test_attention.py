@@ -36,20 +36,10 @@ def _check(o, r, tol=2e-5):
     assert err <= tol * scale + 1e-6, (err, scale)
 
 
-@pytest.fixture(params=[1, 2], ids=["chain1", "chain2"])
-def chains(request):
-    """Backward accumulator chains per product (csrc/attention.hip NCH): 1 ships, 2 is the A/B arm
-    (round 4 left an uncommitted 2-chain variant that failed this check; rebuilt here, it passes)."""
-    from network_distributed_pytorch_amd.ops._ext import ext
-    ext().attn_set_chains(request.param)
-    yield request.param
-    ext().attn_set_chains(1)
-
-
 @pytest.mark.gpu
 @pytest.mark.parametrize("B,S,H,masked", [(2, 128, 3, False), (2, 100, 2, True), (1, 512, 2, True), (3, 17, 1, True),
                                            (3, 300, 2, True)])
-def test_fused_attention_fwd_bwd(device, B, S, H, masked, chains):
+def test_fused_attention_fwd_bwd(device, B, S, H, masked):
     q, k, v = _inputs(B, S, H, device)
     mask = None
     if masked:
@@ -114,7 +104,7 @@ def test_distilbert_fused_matches_explicit(device):
 
 
 @pytest.mark.gpu
-def test_fused_attention_distilbert_shape(device, chains):
+def test_fused_attention_distilbert_shape(device):
     """The bench shape (B=16, S=512, H=12) with padding + dropout, vs fp64 explicit math."""
     B, S, H, p = 16, 512, 12, 0.1
     q, k, v = _inputs(B, S, H, device, seed=2)

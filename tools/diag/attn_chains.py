@@ -4,6 +4,9 @@ backward of ops.attention with CUDA events (median of 7 reps of 20 iterations) a
 against fp64 explicit math.  One JSON line per arm.
 
     python tools/diag/attn_chains.py > gpurun_out/attn_chains.jsonl
+
+Needs the ``attn_set_chains`` binding, which exists at commit 831b94e only (the two-chain
+variant was measured slower and removed; profiles/r5/attn_chains.md).
 """
 import json
 import os
