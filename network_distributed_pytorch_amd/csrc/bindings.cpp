@@ -1340,6 +1340,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_pair_fwd", &bn_pair_fwd);
   m.def("bn_pair_bwd", &bn_pair_bwd);
   m.def("wino_set_enabled", &ndp::wino_set_enabled);
+  m.def("conv_set_stem_psplit", &ndp::conv_set_stem_psplit);
   m.def("bn_slices", &bn_slices);
   m.def("slab_sum", &slab_sum);
   m.def("bn_part_numel", &bn_part_numel);

@@ -346,9 +346,14 @@ __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
-template <int R, int S, int ST, int PD, int H, int W, int CK, int BM, int IMGS, int WM, int NBUF, int KB, bool TRANSW>
+// PSPLIT (one image per tile only): the tile covers P / PSPLIT output rows of its image
+// (blockIdx.x = image * PSPLIT + row block); the whole image is still staged in LDS.  The stem at
+// small per-GPU batches: one 16x16-output image per workgroup left 3/4 of the CUs idle at batch 64.
+template <int R, int S, int ST, int PD, int H, int W, int CK, int BM, int IMGS, int WM, int NBUF, int KB, bool TRANSW,
+          int PSPLIT = 1>
 struct ConvFwdCfg {
   static constexpr int P = (H + 2 * PD - R) / ST + 1, Q = (W + 2 * PD - S) / ST + 1, PQ = P * Q;
+  static_assert(PSPLIT == 1 || (IMGS == 1 && P % PSPLIT == 0), "row blocks of one image");
   // Bank-conflict-free LDS image (ds_read_b32: bank = dword % 32, one 32-lane half-wave per
   // LDS cycle; the B read of a half-wave is 32 output pixels at pixel_base + tap):
   //  * 8x8 stride 1, one image per tile: lanes cover 8 rows x 4 columns (MAP 1) of a
@@ -399,7 +404,7 @@ struct ConvFwdCfg {
   }
   static constexpr int RS = R * S, KK = CK * RS;
   static constexpr int NSTEP = (CK / 2) * RS, NBLK = NSTEP / KB;
-  static constexpr int BN = IMGS * PQ;
+  static constexpr int BN = IMGS * PQ / PSPLIT;
   static constexpr int WN = 4 / WM;
   static constexpr int TM = BM / 32 / WM, TN = BN / 32 / WN;
   // [kk][m] A image.  Reads (32 consecutive m) are conflict-free for any stride; the stride is
@@ -446,12 +451,12 @@ struct ConvFwdCfg {
 //   dX[c, h, w] = sum_{k,r,s} W[k, c, 2-r, 2-s] * Z[k, h-1+r, w-1+s],  Z[k, 2p, 2q] = dY[k, p, q]
 
 template <int R, int S, int ST, int PD, int H, int W, int CK, int BM, int IMGS, int WM, int NBUF, int KB, bool TRANSW,
-          bool VEC, int UPS = 1, int SCH = 0, int IUPS = 1>
+          bool VEC, int UPS = 1, int SCH = 0, int IUPS = 1, int PSPLIT = 1>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                        float* __restrict__ y, float* __restrict__ part, int Cin,
                                                        int Kout, int cps, int64_t slab,
                                                        const float* __restrict__ addend, ConvBnStats st) {
-  using G = ConvFwdCfg<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW>;
+  using G = ConvFwdCfg<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW, PSPLIT>;
   constexpr int AE = (BM * G::KK + 3) / 4;  // float4 slots (scalar path: 4 scalars per slot)
   constexpr int A_PER_T = (AE + 255) / 256;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -461,7 +466,8 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
   const int wm = wave % WM, wn = wave / WM;
   const int h = lane >> 5, l32 = lane & 31;
   const int m0 = blockIdx.y * BM;
-  const int b0 = blockIdx.x * IMGS;
+  const int b0 = (PSPLIT == 1 ? blockIdx.x : blockIdx.x / PSPLIT) * IMGS;
+  const int prow0 = PSPLIT == 1 ? 0 : (blockIdx.x % PSPLIT) * (G::P / PSPLIT);  // first output row
   // split-K: workgroup z reduces channel chunks [ch0, ch0 + nchunks) into output slab z
   const int ch0 = blockIdx.z * cps;
   const int nchunks = min((Cin + CK - 1) / CK - ch0, cps);
@@ -478,6 +484,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
     const int n = (wn * G::TN + tn) * 32 + l32;
     int img, p, q;
     G::pix(n, img, p, q);
+    p += prow0;
     b_base[tn] = img * G::IMGSTR + h * (CK / 2) * G::HWp + p * ST * G::Wp + (G::DEINT ? q : q * ST);
   }
 
@@ -673,6 +680,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
         const int n = (wn * G::TN + tn) * 32 + l32;
         int img, p, q;
         G::pix(n, img, p, q);
+        p += prow0;
         float* pb = pz + (int64_t)(b0 + img) * Kout * G::PQ + p * G::Q + q;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -702,6 +710,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
       const int n = (wn * G::TN + tn) * 32 + l32;
       int img, pp, qq;
       G::pix(n, img, pp, qq);
+      pp += prow0;
       const int opix = UPS == 1 ? pp * G::Q + qq : pp * UPS * (UPS * G::Q) + qq * UPS;
       const int64_t yoff = (int64_t)(b0 + img) * Kout * OPQ + opix;
       float* yb = y + yoff;
@@ -1120,12 +1129,12 @@ static void set_lds(KernelT k, size_t bytes) {
 // (deterministic).  Used where B / IMGS * Kout / BM alone cannot fill the 256 CUs
 // (small per-GPU batches: the strong-scaling shapes 512 / N).
 template <int R, int S, int ST, int PD, int H, int W, int CK, int BM, int IMGS, int WM, int NBUF, int KB, bool TRANSW,
-          bool VEC, int UPS = 1, int SCH = 0, int IUPS = 1>
+          bool VEC, int UPS = 1, int SCH = 0, int IUPS = 1, int PSPLIT = 1>
 static int run_fwd(const float* x, const float* w, float* y, int B, int Cin, int Kout, int ksplit, float* part,
                    hipStream_t s, const float* addend = nullptr, bool defer = false,
                    ConvBnStats stats = ConvBnStats{nullptr, nullptr, nullptr, nullptr, nullptr}) {
-  using G = ConvFwdCfg<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW>;
-  auto k = conv_fwd_kernel<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW, VEC, UPS, SCH, IUPS>;
+  using G = ConvFwdCfg<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW, PSPLIT>;
+  auto k = conv_fwd_kernel<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW, VEC, UPS, SCH, IUPS, PSPLIT>;
   static bool attr = false;  // once per instantiation (> 64 KiB of LDS needs the opt-in)
   if (!attr) { set_lds(k, G::LDS_BYTES); attr = true; }
   const int nchunks = (Cin + CK - 1) / CK;
@@ -1135,7 +1144,7 @@ static int run_fwd(const float* x, const float* w, float* y, int B, int Cin, int
   const int64_t slab = (int64_t)B * Kout * G::PQ;  // compact partial tile layout
   // stats: only unsplit launches of statistics-capable tiles (conv_fwd_stats_slices says which)
   if (!(G::STATS_OK && UPS == 1) || ksplit > 1 || (stats.bx != nullptr && !G::STATS2_OK)) stats.out = nullptr;
-  hipLaunchKernelGGL(k, dim3(B / IMGS, Kout / BM, ksplit), dim3(256), G::LDS_BYTES, s, x, w, y, part, Cin, Kout, cps,
+  hipLaunchKernelGGL(k, dim3(B / IMGS * PSPLIT, Kout / BM, ksplit), dim3(256), G::LDS_BYTES, s, x, w, y, part, Cin, Kout, cps,
                      slab, ksplit > 1 ? nullptr : addend, stats);
   // defer: leave the ksplit slabs for the consumer (the fused BN kernel sums them while it
   // reads its input, ops/slablink.py) — one launch fewer per conv
@@ -1264,12 +1273,27 @@ bool conv_wino(int cls, const ConvGeom& g, int B, bool dgrad) {
   return (cls == 0 || cls == 1) && wino_ok(g.C, g.Co, B, g.H, g.W, conv_ksplit(cls, g, B, false));
 }
 
+// Output-row blocks per image of the stem forward (ConvFwdCfg PSPLIT): enough workgroups for
+// the 256 CUs at the small per-GPU batches of the strong-scaling runs.  Every split re-stages
+// the image and the 64 x 196 weight image, so more blocks only pay below one workgroup per CU.
+// Stem forward + statistics epilogue on 1x MI355X (tools/diag/stem_psplit.py, µs, split 1/2/4):
+// batch 64 24.9 / 19.2 / 15.3, 128 25.6 / 20.1 / 29.4, 256 27.4 / 37.5 / 56.1, 512 51.5 / 72.3 / 110.
+static int g_stem_psplit = 0;  // 0 = by batch (A/B override: conv_set_stem_psplit)
+void conv_set_stem_psplit(int p) { g_stem_psplit = (p == 1 || p == 2 || p == 4) ? p : 0; }
+int stem_psplit(int B) {
+  if (g_stem_psplit) return g_stem_psplit;
+  return B >= 256 ? 1 : B >= 128 ? 2 : 4;
+}
+
 int conv_fwd_stats_slices(int cls, const ConvGeom& g, int B) {
   static_assert(ConvFwdCfg<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, false>::STATS_OK &&
-                    ConvFwdCfg<7, 7, 2, 3, 32, 32, 4, 64, 1, 2, 1, 7, false>::STATS_OK,
+                    ConvFwdCfg<7, 7, 2, 3, 32, 32, 4, 64, 1, 2, 1, 7, false>::STATS_OK &&
+                    ConvFwdCfg<7, 7, 2, 3, 32, 32, 4, 64, 1, 2, 1, 7, false, 2>::STATS_OK &&
+                    ConvFwdCfg<7, 7, 2, 3, 32, 32, 4, 64, 1, 2, 1, 7, false, 4>::STATS_OK,
                 "statistics epilogue fits every layer1 / stem tile");
   if (cls != 0 && cls != 3) return 0;
   if (conv_ksplit(cls, g, B, false) != 1) return 0;
+  if (cls == 3) return B * stem_psplit(B);  // one partial per (image, row block)
   return conv_wino(cls, g, B, false) ? B / wino_imgs(g.H) : B / conv_fwd_imgs(cls);
 }
 // backward-mode BN partial sums from the grad-x epilogue: the layer1 3x3 class (its BN takes the
@@ -1313,8 +1337,17 @@ int launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvG
       return run_fwd<3, 3, 2, 1, 8, 8, 8, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s, nullptr,
                                                                        defer);
     case 3:
-      return run_fwd<7, 7, 2, 3, 32, 32, 4, 64, 1, 2, 1, 7, false, false>(x, w, y, B, g.C, g.Co, 1, nullptr, s, nullptr,
-                                                                          false, stats);
+      switch (stem_psplit(B)) {
+        case 4:
+          return run_fwd<7, 7, 2, 3, 32, 32, 4, 64, 1, 2, 1, 7, false, false, 1, 0, 1, 4>(x, w, y, B, g.C, g.Co, 1, nullptr,
+                                                                                        s, nullptr, false, stats);
+        case 2:
+          return run_fwd<7, 7, 2, 3, 32, 32, 4, 64, 1, 2, 1, 7, false, false, 1, 0, 1, 2>(x, w, y, B, g.C, g.Co, 1, nullptr,
+                                                                                        s, nullptr, false, stats);
+        default:
+          return run_fwd<7, 7, 2, 3, 32, 32, 4, 64, 1, 2, 1, 7, false, false>(x, w, y, B, g.C, g.Co, 1, nullptr, s,
+                                                                              nullptr, false, stats);
+      }
     case 4:
       return run_fwd<1, 1, 2, 0, 8, 8, 8, 64, 4, 2, 2, 4, false, true>(x, w, y, B, g.C, g.Co, ks, part, s, nullptr,
                                                                        defer);

@@ -287,6 +287,9 @@ struct ConvBnStats {
 // layouts, 32 * Co * C floats) when conv_wino(cls, g, B, dgrad) — the launch then runs the Winograd kernel
 int launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s,
                     bool defer = false, double* stats = nullptr, float* wino_u = nullptr);
+// stem forward output-row blocks per image (by batch; A/B override 1 / 2 / 4, 0 = auto)
+int stem_psplit(int B);
+void conv_set_stem_psplit(int p);
 int conv_fwd_stats_slices(int cls, const ConvGeom& g, int B);
 // addend (nullable, 3x3 classes): dx += addend in the epilogue / split-K sum; with defer the
 // slabs are left unsummed and the consumer adds the addend after them (launch_bn_bwd dyadd)

@@ -38,11 +38,16 @@ def test_epilogue_stats_match_fp64(device, case):
     ref = F.conv2d(x.double(), w.double(), stride=s, padding=p)
     assert (y.double() - ref).abs().max().item() < 1e-4 * ref.abs().max().item()
     st = stats.view(Co, S, 2)
-    imgs = B // S
-    yt = y.double().view(S, imgs, Co, OH * OH)
+    if S > B:  # the stem's output-row blocks (conv.hip PSPLIT): one partial per (image, block)
+        rb = S // B
+        yt = y.double().view(B, Co, rb, OH * OH // rb).permute(0, 2, 1, 3).reshape(S, 1, Co, OH * OH // rb)
+        imgs, npix = 1, OH * OH // rb
+    else:
+        imgs, npix = B // S, OH * OH
+        yt = y.double().view(S, imgs, Co, npix)
     tile_sum = yt.sum((1, 3)).t()  # [Co][S]
     tile_sq = (yt * yt).sum((1, 3)).t()
-    assert torch.allclose(st[..., 0], tile_sum, rtol=1e-9, atol=1e-6 * imgs * OH * OH)
+    assert torch.allclose(st[..., 0], tile_sum, rtol=1e-9, atol=1e-6 * imgs * npix)
     assert torch.allclose(st[..., 1], tile_sq, rtol=1e-6, atol=1e-6)
 
 

@@ -11,7 +11,7 @@ CASES = [(64, 64, 3, 1, 1, 8, 8), (128, 128, 3, 1, 1, 4, 16), (64, 128, 3, 2, 1,
          (64, 64, 3, 1, 1, 8, 6), (64, 128, 1, 2, 0, 8, 8), (64, 128, 1, 2, 0, 8, 64), (256, 512, 1, 2, 0, 8, 16),
          (64, 128, 3, 2, 1, 8, 64), (128, 128, 3, 2, 1, 8, 32), (64, 128, 3, 2, 1, 8, 512),
          (128, 256, 1, 2, 0, 4, 16), (128, 256, 1, 2, 0, 4, 64), (128, 256, 1, 2, 0, 4, 512),
-         (512, 1024, 1, 2, 0, 4, 32)]
+         (512, 1024, 1, 2, 0, 4, 32), (3, 64, 7, 2, 3, 32, 64), (3, 64, 7, 2, 3, 32, 256)]
 
 
 @pytest.mark.gpu
@@ -38,6 +38,29 @@ def test_direct_conv_vs_fp64(device, cin, cout, k, s, p, hw, B):
         err = (got - ref).abs().max().item()
         scale = ref.abs().max().item()
         assert err <= 2e-6 * scale * (cin * k * k) ** 0.5 + 1e-6, (name, err, scale)
+
+
+@pytest.mark.gpu
+def test_stem_row_blocks_bitwise(device):
+    """The stem forward split into 1 / 2 / 4 output-row blocks per image (conv.hip PSPLIT):
+    every output pixel keeps its own k-ordered MFMA chain, so y is bitwise the same."""
+    from network_distributed_pytorch_amd.ops._ext import ext
+
+    torch.manual_seed(2)
+    B = 32
+    x = torch.randn(B, 3, 32, 32, device=device)
+    w = torch.randn(64, 3, 7, 7, device=device) * 0.1
+    geom = [3, 32, 32, 64, 7, 7, 2, 3]
+    outs = []
+    try:
+        for ps in (1, 2, 4):
+            ext().conv_set_stem_psplit(ps)
+            y = torch.empty(B, 64, 16, 16, device=device)
+            assert ext().conv_fwd(x, w, y, geom, None, False) == 1
+            outs.append(y)
+    finally:
+        ext().conv_set_stem_psplit(0)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
 
 
 @pytest.mark.gpu
