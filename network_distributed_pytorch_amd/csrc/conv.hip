@@ -403,7 +403,26 @@ struct ConvFwdCfg {
     }
   }
   static constexpr int RS = R * S, KK = CK * RS;
-  static constexpr int NSTEP = (CK / 2) * RS, NBLK = NSTEP / KB;
+  // PAIRK (the 3-channel 7x7 stem): the two k values of an MFMA step (lane halves h = 0 / 1)
+  // were channels c and c + 2 of CK = 4 (98 steps, a quarter of them on the zero 4th channel).
+  // Now: steps 0-48 pair channel 0 with channel 1 at the same tap (B offset + 1 plane), steps
+  // 49-55 channel 2's kernel row 3 with the zero plane (+ 1 plane), steps 56-76 channel 2's rows
+  // 0-2 with its rows 4-6 (+ 4 rows): 77 steps, each half's B offset still a compile-time
+  // immediate on one of two per-lane bases.  The A image is staged in the same step order.
+  static constexpr bool PAIRK = DEINT && R == 7 && S == 7;
+  static constexpr int NSTEP = PAIRK ? 77 : (CK / 2) * RS, NBLK = NSTEP / KB;
+  static_assert(!PAIRK || (CK == 4 && 2 * NSTEP <= KK), "stem k pairing");
+  // PAIRK: the (c, r, s) tap of lane half 0 at step t
+  __device__ static __forceinline__ constexpr int pk_c(int t) { return t < 49 ? 0 : 2; }
+  __device__ static __forceinline__ constexpr int pk_r(int t) { return t < 49 ? t / 7 : t < 56 ? 3 : (t - 56) / 7; }
+  __device__ static __forceinline__ constexpr int pk_s(int t) { return t < 49 ? t % 7 : t < 56 ? t - 49 : (t - 56) % 7; }
+  // PAIRK: A-image row (h * NSTEP + t) of flattened weight index kk = c * 49 + r * 7 + s, or -1
+  // (kk < 147: the three real channels; branch-free, every weight of the tile is staged through it)
+  __device__ static __forceinline__ int pk_row(int kk) {
+    const int c = kk / 49, rem = kk - 49 * c, r = rem / 7, sc = rem - 7 * r;
+    const int v2 = r == 3 ? 49 + sc : (r < 3 ? 56 + rem : NSTEP + 28 + rem);
+    return c == 0 ? rem : (c == 1 ? NSTEP + rem : v2);
+  }
   static constexpr int BN = IMGS * PQ / PSPLIT;
   static constexpr int WN = 4 / WM;
   static constexpr int TM = BM / 32 / WM, TN = BN / 32 / WN;
@@ -474,7 +493,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
 
   for (int i = tid; i < NBUF * G::B_SZ; i += 256) Bs[i] = 0.f;  // zero borders (never rewritten)
 
-  int a_base[G::TM], b_base[G::TN];
+  int a_base[G::TM], b_base[G::TN], b_base2[G::PAIRK ? G::TN : 1];
 #pragma unroll
   for (int tm = 0; tm < G::TM; ++tm)
     a_base[tm] = G::AV ? ((wm * G::TM + tm) * 32 + l32) * G::LDAM + h * G::NSTEP
@@ -485,7 +504,8 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
     int img, p, q;
     G::pix(n, img, p, q);
     p += prow0;
-    b_base[tn] = img * G::IMGSTR + h * (CK / 2) * G::HWp + p * ST * G::Wp + (G::DEINT ? q : q * ST);
+    b_base[tn] = img * G::IMGSTR + (G::PAIRK ? h : h * (CK / 2)) * G::HWp + p * ST * G::Wp + (G::DEINT ? q : q * ST);
+    if constexpr (G::PAIRK) b_base2[tn] = b_base[tn] - h * G::HWp + h * 4 * G::Wp;
   }
 
   // B staging: float4 of the (possibly half-size, IUPS) input planes
@@ -494,10 +514,18 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
   // a 2x2 unpadded plane is one float4 stored whole (row stride Wp = W = 2)
   static_assert((IW % 4 == 0 || (PD == 0 && IUPS == 1 && IHW == 4)) && (IUPS == 1 || (ST == 1 && UPS == 1)),
                 "input staging");
-  f32x4c ra[A_PER_T];
+  // PAIRK stem: the BM x 147 weights of the tile are one contiguous run (Cin = 3): float4 loads
+  // of the flat run, scattered to the paired-step rows at the LDS store (the generic scalar path
+  // computed and held a 64-bit address and a branch per weight: 400+ registers, 1 wave / SIMD)
+  constexpr int PKE = G::PAIRK ? BM * 3 * G::RS / 4 : 1, PK_PER_T = (PKE + 255) / 256;
+  static_assert(!G::PAIRK || (BM * 3 * G::RS) % 4 == 0, "stem weight run in float4");
+  f32x4c ra[A_PER_T > PK_PER_T ? A_PER_T : PK_PER_T];
   f32x4c rb[BPT];
   auto load = [&](int ch) {
     const int c0 = (ch0 + ch) * CK;
+    if constexpr (G::PAIRK) {
+      // (staged straight from global in store(): no register copy of the weights)
+    } else
 #pragma unroll
     for (int i = 0; i < A_PER_T; ++i) {
       const int e = tid + 256 * i;
@@ -537,6 +565,19 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
   auto store = [&](int buf) {
     float* A = As + buf * G::A_SZ;
     float* B = Bs + buf * G::B_SZ;
+    if constexpr (G::PAIRK) {
+      const f32x4c* w4 = reinterpret_cast<const f32x4c*>(w + (int64_t)m0 * 3 * G::RS);
+      for (int e = tid; e < PKE; e += 256) {
+        const f32x4c v = w4[e];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int f = 4 * e + j, m = f / (3 * G::RS), kk = f - m * (3 * G::RS);
+          A[G::pk_row(kk) * G::LDA + m] = v[j];
+        }
+      }
+      for (int idx = tid; idx < 7 * BM; idx += 256)  // the zero partners of channel 2's row 3
+        A[(G::NSTEP + 49 + idx / BM) * G::LDA + idx % BM] = 0.f;
+    } else
 #pragma unroll
     for (int i = 0; i < A_PER_T; ++i) {
       const int e = tid + 256 * i;
@@ -565,8 +606,14 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
           for (int j = 0; j < 4; ++j) {
             const int f = 4 * e + j, m = f / G::KK, kk = f - m * G::KK;
             if (f < BM * G::KK) {
-              if constexpr (G::AV) A[m * G::LDAM + kk] = ra[i][j];
-              else A[kk * G::LDA + m] = ra[i][j];
+              if constexpr (G::PAIRK) {
+                const int row = G::pk_row(kk);
+                if (row >= 0) A[row * G::LDA + m] = ra[i][j];
+              } else if constexpr (G::AV) {
+                A[m * G::LDAM + kk] = ra[i][j];
+              } else {
+                A[kk * G::LDA + m] = ra[i][j];
+              }
             }
           }
         }
@@ -614,14 +661,22 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
 #pragma unroll
       for (int i = 0; i < KB; ++i) {
         const int t = blk * KB + i;
-        const int c = t / G::RS, rs = t - c * G::RS, r = rs / S, s = rs - r * S;
+        int c = t / G::RS, rs = t - c * G::RS, r = rs / S, s = rs - r * S;
+        if constexpr (G::PAIRK) {
+          c = G::pk_c(t);
+          r = G::pk_r(t);
+          s = G::pk_s(t);
+        }
         const int offb = c * G::HWp + r * G::Wp + (G::DEINT ? (s & 1) * G::HALF + (s >> 1) : s);
         if constexpr (!G::AV) {
 #pragma unroll
           for (int tm = 0; tm < G::TM; ++tm) av[slot][i][tm] = A[a_base[tm] + t * G::LDA];
         }
 #pragma unroll
-        for (int tn = 0; tn < G::TN; ++tn) bv[slot][i][tn] = B[b_base[tn] + offb];
+        for (int tn = 0; tn < G::TN; ++tn) {
+          if constexpr (G::PAIRK) bv[slot][i][tn] = B[(t < 56 ? b_base[tn] : b_base2[tn]) + offb];
+          else bv[slot][i][tn] = B[b_base[tn] + offb];
+        }
       }
       if constexpr (G::AV) {
 #pragma unroll
@@ -1276,8 +1331,10 @@ bool conv_wino(int cls, const ConvGeom& g, int B, bool dgrad) {
 // Output-row blocks per image of the stem forward (ConvFwdCfg PSPLIT): enough workgroups for
 // the 256 CUs at the small per-GPU batches of the strong-scaling runs.  Every split re-stages
 // the image and the 64 x 196 weight image, so more blocks only pay below one workgroup per CU.
-// Stem forward + statistics epilogue on 1x MI355X (tools/diag/stem_psplit.py, µs, split 1/2/4):
-// batch 64 24.9 / 19.2 / 15.3, 128 25.6 / 20.1 / 29.4, 256 27.4 / 37.5 / 56.1, 512 51.5 / 72.3 / 110.
+// Stem forward + statistics epilogue on 1x MI355X (tools/diag/stem_psplit.py, µs, split 1/2/4;
+// profiles/r5/stem_psplit*.jsonl): batch 64 20.8 / 15.9 / 12.1, 128 21.4 / 16.7 / 16.9,
+// 256 22.9 / 23.5 / 30.9, 512 34.1 / 43.6 / 58.2 (paired-k stem with float4 weight staging;
+// before it, 512: 51.5 / 72.3 / 110 — 1 wave per SIMD from 400+ registers of staging state).
 static int g_stem_psplit = 0;  // 0 = by batch (A/B override: conv_set_stem_psplit)
 void conv_set_stem_psplit(int p) { g_stem_psplit = (p == 1 || p == 2 || p == 4) ? p : 0; }
 int stem_psplit(int B) {

@@ -18,18 +18,9 @@
 
 namespace ndp {
 
-// columns per wide P item: kPKW, or NDP_PSGD_PKW = 256 / 512 (A/B: smaller items, more of them;
-// the kernel masks the slices past an item's k1)
-static int64_t p_item_cols() {
-  static int64_t v = -1;
-  if (v < 0) {
-    const char* e = getenv("NDP_PSGD_PKW");
-    v = e ? atoll(e) : kPKW;
-    if (v != 256 && v != 512) v = kPKW;
-  }
-  return v;
-}
-
+// columns per wide P item (narrower items, 256 / 512 columns, measured slower in round 5:
+// profiles/r5/bench_psgd_pkw_ab.jsonl)
+static int64_t p_item_cols() { return kPKW; }
 
 static int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
