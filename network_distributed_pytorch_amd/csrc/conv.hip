@@ -1279,10 +1279,14 @@ static int pow2_floor(int v) {
 // grid has >= kFillWgs workgroups.  Workgroups per slice = (Kout / 32) * ceil(Cin / CB).
 // (Larger slices = fewer slabs to sum measured slower in round 3: batch 512 x2 1.9937, x4
 // 1.9969 vs 1.9904 / 1.9927 ms; batch 256 1.4473 / 1.4444 vs 1.441.)
+// Round 5 (Winograd grad-W, deferred batched slab sums): doubling the layer1 (Winograd), 3x3/2 and
+// stem slices halves their slabs — ResNet-18 r=4 batch 512 1.5118 / 1.5129 -> 1.4977 / 1.4957 ms;
+// doubling layer2's (class 1) was slower, 1.5043 -> 1.5165 (profiles/r5/bench_wgrad_slices.jsonl).
 int conv_wgrad_imgs(int cls, const ConvGeom& g, int B) {
-  int def = cls == 0 ? 4 : cls == 1 ? 16 : cls == 2 ? 8 : cls == 4 ? 8 : cls == 5 ? 16 : 2;
+  int def = cls == 0 ? 8 : cls == 1 ? 16 : cls == 2 ? 16 : cls == 4 ? 8 : cls == 5 ? 16 : 4;
   const int cb = cls == 3 ? 3 : 32;
   const int per_slice = (g.Co / 32) * ((g.C + cb - 1) / cb);
+  while (def > 1 && B % def != 0) def /= 2;  // a batch that is not a multiple of the default
   while (def > 1 && (B / def) * per_slice < kFillWgs && B % (def / 2) == 0) def /= 2;
   return def;
 }
