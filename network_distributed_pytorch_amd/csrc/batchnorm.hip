@@ -396,56 +396,77 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(
     // column 4j - 1 from the left lane (the W/4 lanes of a row are adjacent in the wave)
     const int W4 = W >> 2, pairs = OH * W4;
     const int total = (int)(sl.n1 - sl.n0) * pairs;
-    for (int base = 0; base < total; base += 256) {  // uniform trip count: every lane shuffles
-      const int t = base + (int)threadIdx.x;
-      const bool live = t < total;
-      const int ni = live ? t / pairs : 0, r = live ? t - ni * pairs : 0;
-      const int oh = r / W4, j = r - oh * W4;
-      const int64_t plane = (sl.n0 + ni) * C + c;
-      const float* xp = x + plane * HW;
-      float v[3][5];
+    // two items per thread per trip: both items' three input rows are loaded before either is
+    // normalised / pooled / stored (one HBM round trip per two items)
+    constexpr int U = 2;
+    for (int base = 0; base < total; base += 256 * U) {  // uniform trip count: every lane shuffles
+      f32x4 q[U][3];
+      int tt[U], jj[U], oo[U];
+      int64_t pl[U];
+      bool lv[U];
 #pragma unroll
-      for (int kh = 0; kh < 3; ++kh) {
-        const int hh = 2 * oh - 1 + kh;
-        f32x4 q = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-        if (live && hh >= 0 && hh < H) {
-          q = *reinterpret_cast<const f32x4*>(xp + hh * W + 4 * j);
-#pragma unroll
-          for (int u = 0; u < 4; ++u) q[u] = fmaxf(fmaf(q[u], scale, shift) + 0.f, 0.f);
-        }
-        const float left = __shfl_up(q[3], 1, 64);
-        v[kh][0] = (j > 0) ? left : -INFINITY;
-        v[kh][1] = q[0]; v[kh][2] = q[1]; v[kh][3] = q[2]; v[kh][4] = q[3];
-      }
-      if (!live) continue;
-      float out[2];
-      uint8_t arg[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {  // output column ow = 2j + u: taps at columns 4j - 1 + 2u + kw
-        const int ow = 2 * j + u;
-        const int kh0 = oh == 0 ? 1 : 0, kw0 = ow == 0 ? 1 : 0;
-        float best = -INFINITY;
-        int a0 = kh0 * 3 + kw0;
+      for (int k = 0; k < U; ++k) {
+        const int t = base + 256 * k + (int)threadIdx.x;
+        lv[k] = t < total;
+        const int ni = lv[k] ? t / pairs : 0, r = lv[k] ? t - ni * pairs : 0;
+        oo[k] = r / W4;
+        jj[k] = r - oo[k] * W4;
+        tt[k] = t;
+        pl[k] = (sl.n0 + ni) * C + c;
+        const float* xp = x + pl[k] * HW;
 #pragma unroll
         for (int kh = 0; kh < 3; ++kh) {
-          if (kh < kh0 || 2 * oh - 1 + kh >= H) continue;
+          const int hh = 2 * oo[k] - 1 + kh;
+          q[k][kh] = (lv[k] && hh >= 0 && hh < H) ? *reinterpret_cast<const f32x4*>(xp + hh * W + 4 * jj[k])
+                                                   : f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        }
+      }
 #pragma unroll
-          for (int kw = 0; kw < 3; ++kw) {
-            if (kw < kw0 || 2 * ow - 1 + kw >= W) continue;
-            const float val = v[kh][2 * u + kw];
-            if (val > best || isnan(val)) {
-              best = val;
-              a0 = kh * 3 + kw;
+      for (int k = 0; k < U; ++k) {
+        const int oh = oo[k], j = jj[k];
+        float v[3][5];
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+          const int hh = 2 * oh - 1 + kh;
+          f32x4 qq = q[k][kh];
+          if (lv[k] && hh >= 0 && hh < H) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) qq[u] = fmaxf(fmaf(qq[u], scale, shift) + 0.f, 0.f);
+          }
+          const float left = __shfl_up(qq[3], 1, 64);
+          v[kh][0] = (j > 0) ? left : -INFINITY;
+          v[kh][1] = qq[0]; v[kh][2] = qq[1]; v[kh][3] = qq[2]; v[kh][4] = qq[3];
+        }
+        if (!lv[k]) continue;
+        float out[2];
+        uint8_t arg[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {  // output column ow = 2j + u: taps at columns 4j - 1 + 2u + kw
+          const int ow = 2 * j + u;
+          const int kh0 = oh == 0 ? 1 : 0, kw0 = ow == 0 ? 1 : 0;
+          float best = -INFINITY;
+          int a0 = kh0 * 3 + kw0;
+#pragma unroll
+          for (int kh = 0; kh < 3; ++kh) {
+            if (kh < kh0 || 2 * oh - 1 + kh >= H) continue;
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+              if (kw < kw0 || 2 * ow - 1 + kw >= W) continue;
+              const float val = v[kh][2 * u + kw];
+              if (val > best || isnan(val)) {
+                best = val;
+                a0 = kh * 3 + kw;
+              }
             }
           }
+          out[u] = best;
+          arg[u] = (uint8_t)a0;
         }
-        out[u] = best;
-        arg[u] = (uint8_t)a0;
+        const int64_t o = pl[k] * PQ + oh * OW + 2 * j;
+        *reinterpret_cast<float2*>(y + o) = make_float2(out[0], out[1]);
+        *reinterpret_cast<uint16_t*>(idx + o) = (uint16_t)(arg[0] | (arg[1] << 8));  // o even: 2-B aligned
       }
-      const int64_t o = plane * PQ + oh * OW + 2 * j;
-      *reinterpret_cast<float2*>(y + o) = make_float2(out[0], out[1]);
-      idx[o] = arg[0];
-      idx[o + 1] = arg[1];
+      (void)tt;
     }
     return;
   }
