@@ -1267,12 +1267,16 @@ static bool bn_fused_ok(int N, int C, int HW) {
 }
 
 // column-block width for one launch: the widest block that still gives >= 256 workgroups (one per
-// CU), else the narrowest allowed one — 4 columns (16-B row segments) only at per-GPU batch <= 128,
-// where grid size matters more than segment width.  Measured (1x MI355X, profiles/r3/bn_colw.md)
+// CU), else the narrowest allowed one (4 columns, 16-B row segments: grid size matters more than
+// segment width).  Measured in round 3 with 4 columns at batch <= 128 only (profiles/r3/bn_colw.md)
 // against a fixed 8: ResNet-18 r=4 batch 512 1.945 -> 1.943 ms, batch 64 1.012 -> 1.000 ms,
 // ResNet-152 r=4 15.19 -> 14.78 ms, ResNet-50 dense 6.246 -> 6.178 ms.
+// Round 5 (float4 kernel): 4-column blocks at every batch, not only <= 128 — ResNet-18 r=4 batch
+// 512 1.4994 / 1.4922 -> 1.4864 / 1.4862 ms, batch 256 1.1095 -> 1.1033 (layer3 / layer4 BNs get
+// 2x the workgroups; profiles/r5/bench_bn_colw.jsonl).
 static int bn_colw_for(int HW, int C, int N) {
-  const int lo = N <= 128 ? 4 : 8;
+  (void)N;
+  const int lo = 4;
   const int64_t cols = (int64_t)C * HW;
   for (int cw = 16; cw >= lo; cw >>= 1)
     if (cw >= HW && cols / cw >= 256) return cw;
