@@ -1283,6 +1283,19 @@ static int pow2_floor(int v) {
 // stem slices halves their slabs — ResNet-18 r=4 batch 512 1.5118 / 1.5129 -> 1.4977 / 1.4957 ms;
 // doubling layer2's (class 1) was slower, 1.5043 -> 1.5165 (profiles/r5/bench_wgrad_slices.jsonl).
 int conv_wgrad_imgs(int cls, const ConvGeom& g, int B) {
+  // (the geometry test only, not the runtime Winograd switch: the slicing stays fixed for a shape,
+  // so scratch sized from a cached plan fits whichever grad-W kernel runs)
+  if (cls == 0 && g.H == 8 && g.C % 16 == 0 && g.Co % 16 == 0 && B <= 128 && B % 4 == 0) {
+    // Winograd grad-W with the 4-wave reduction (winograd.hip wino_wgrad_kernel RED = 4) at the
+    // small per-GPU batches: a workgroup per 16 x 16 block and slice, >= one image per wave.
+    // ResNet-18 r=4 batch 64 0.843 -> 0.830 ms (4x fewer slabs: grad-W 31.7 -> 29.9 µs, slab sum
+    // 16.0 -> 13.3); at batch 256 / 512 the 4 waves of a workgroup reading different images lost
+    // (512: grad-W + slab sum 120.9 -> 124.0 µs; 256: 1.102 -> 1.120 ms at 4 images per slice)
+    const int per_slice = (g.Co / 16) * (g.C / 16);
+    int d = 32;
+    while (d > 4 && (B % d != 0 || (B / d) * per_slice < kFillWgs)) d /= 2;
+    if (B % d == 0 && wino_wgrad_red(B, d)) return d;
+  }
   int def = cls == 0 ? 8 : cls == 1 ? 16 : cls == 2 ? 16 : cls == 4 ? 8 : cls == 5 ? 16 : 4;
   const int cb = cls == 3 ? 3 : 32;
   const int per_slice = (g.Co / 32) * ((g.C + cb - 1) / cb);

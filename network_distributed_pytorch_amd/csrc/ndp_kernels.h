@@ -308,6 +308,7 @@ void wino_set_enabled(bool on);
 int wino_imgs(int H);
 int64_t wino_u_numel(int inC, int outC);
 void launch_wino_weights(const float* w, float* u, int Co, int C, hipStream_t s);
+bool wino_wgrad_red(int B, int imgs);
 bool wino_wgrad_ok(int C, int Co, int H);
 void launch_wino_wgrad(const float* x, const float* dy, float* part, int B, int C, int Co, int H, int imgs,
                        hipStream_t s);

@@ -337,16 +337,22 @@ __global__ __launch_bounds__(256, 2) void wino_dpp_kernel(const float* __restric
 // hold the block.  The slice's dW goes back through G^T . G in registers and is written as one
 // grad-W slab in the direct kernel's [co][ci][3][3] layout (conv_slab_sum / gradfinish sum the
 // slabs in slice order, deterministic).
-template <int H>
+// RED = 4: the workgroup's 4 waves share ONE block, each over a quarter of the slice's images, and
+// are summed through LDS in wave order before the single slab store — 4x fewer (larger) slices
+// for the same wave count, i.e. 4x less slab traffic for the grad-W sum.  RED = 1: a wave per
+// block (the slice's images all in one wave), for batches the 4-way split does not divide.
+template <int H, int RED = 1>
 __global__ __launch_bounds__(256, 2) void wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy,
                                                           float* __restrict__ part, int Cin, int Cout, int imgs) {
   constexpr int TW = H / 2, TPL = TW * TW / 4, HW = H * H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i = lane & 15, kq = lane >> 4;
-  const int blk = blockIdx.y * 4 + wave, nbc = Cin / 16;
+  const int blk = RED == 4 ? blockIdx.y : blockIdx.y * 4 + wave, nbc = Cin / 16;
   const int cob = blk / nbc, cib = blk - cob * nbc;
-  if (cob * 16 >= Cout) return;  // no barriers in this kernel
-  const int slice = blockIdx.x, b0 = slice * imgs;
+  if (cob * 16 >= Cout) return;  // (RED = 4: uniform over the workgroup, before its barrier)
+  const int slice = blockIdx.x;
+  const int b0 = RED == 4 ? slice * imgs + wave * (imgs / 4) : slice * imgs;
+  if (RED == 4) imgs /= 4;  // this wave's images
   // tile group kq: H = 8 -> tile row ty = kq (tiles tx = 0..3); H = 4 -> tile (kq / 2, kq % 2)
   const int ty = H == 8 ? kq : kq >> 1, tx0 = H == 8 ? 0 : (kq & 1);
   const float* xp = x + ((int64_t)b0 * Cin + cib * 16 + i) * HW;
@@ -452,6 +458,19 @@ __global__ __launch_bounds__(256, 2) void wino_wgrad_kernel(const float* __restr
       load(n, xr[0], gr[0]);
       step(xr[0], gr[0]);
     }
+  }
+  if constexpr (RED == 4) {  // waves 1..3 -> LDS, wave 0 adds them in wave order
+    __shared__ __attribute__((aligned(16))) f32x4w red[3][16][64];
+    if (wave > 0) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) red[wave - 1][e][lane] = acc[e];
+    }
+    __syncthreads();
+    if (wave > 0) return;
+#pragma unroll
+    for (int w = 0; w < 3; ++w)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] += red[w][e][lane];
   }
   // dW = G^T dU G per (co, ci) = (row 4 kq + r, column i) of the block, lane-local
   float* out = part + (int64_t)slice * Cout * Cin * 9;
@@ -601,10 +620,19 @@ void launch_wino_conv(const float* x, const float* u, float* y, int B, int inC, 
 // instantiation (one tile per lane group and image: a load per 16 MFMAs) measured slower than the
 // direct grad-W kernel (conv.hip launch_conv_wgrad) and is not built
 bool wino_wgrad_ok(int C, int Co, int H) { return H == 8 && C % 16 == 0 && Co % 16 == 0 && !wino_disabled(); }
+// the 4-wave reduction at per-GPU batch <= 128 for slices of imgs % 4 == 0 images (conv.hip
+// conv_wgrad_imgs sizes the slices for it: one workgroup per block and slice)
+bool wino_wgrad_red(int B, int imgs) { return B <= 128 && imgs % 4 == 0; }
 void launch_wino_wgrad(const float* x, const float* dy, float* part, int B, int C, int Co, int H, int imgs,
                        hipStream_t s) {
-  const dim3 grid((unsigned)(B / imgs), (unsigned)(((Co / 16) * (C / 16) + 3) / 4));
-  if (H == 8) hipLaunchKernelGGL(wino_wgrad_kernel<8>, grid, dim3(256), 0, s, x, dy, part, C, Co, imgs);
+  if (H != 8) return;
+  if (wino_wgrad_red(B, imgs)) {
+    const dim3 grid((unsigned)(B / imgs), (unsigned)((Co / 16) * (C / 16)));
+    hipLaunchKernelGGL((wino_wgrad_kernel<8, 4>), grid, dim3(256), 0, s, x, dy, part, C, Co, imgs);
+  } else {
+    const dim3 grid((unsigned)(B / imgs), (unsigned)(((Co / 16) * (C / 16) + 3) / 4));
+    hipLaunchKernelGGL((wino_wgrad_kernel<8, 1>), grid, dim3(256), 0, s, x, dy, part, C, Co, imgs);
+  }
 }
 
 }  // namespace ndp
