@@ -7,8 +7,8 @@ early-layer gradient change, the same size as each arm's own error against the e
 (tools/diag/wino_model_check.py, profiles/r5/wino_model_check.txt).  Comparing the arms with
 each other therefore either needs a loose tolerance or flakes.  Instead each fused arm is
 compared with the exact (fp64) step: per parameter, its L2-relative gradient error must stay
-within FACTOR x the unfused arm's own error (plus a small floor), and the unfused arm must be
-accurate itself.  Small systematic drifts are the per-op fp64 tests' job (1e-5-level bounds on
+within FACTOR x the unfused arm's own error or below an absolute ABS, its mean over parameters
+within MEAN_FACTOR x the unfused arm's mean, and the unfused arm must be accurate itself.  Small systematic drifts are the per-op fp64 tests' job (1e-5-level bounds on
 every fused kernel); this whole-step check catches wiring bugs.  A real fusion bug (a wrong statistic, a missing addend) is orders of magnitude
 above that bound; rounding-order differences are not.
 """
@@ -21,11 +21,13 @@ from network_distributed_pytorch_amd.models import build_resnet
 
 _CACHE: Dict[tuple, Tuple[float, Dict[str, torch.Tensor]]] = {}
 
-# the arms' errors vs the exact step vary by up to ~2x from one rounding state to another (same
-# build, different library GEMM choices: bn1.weight 2.4e-3 unfused vs 5.0e-3 fused in one full
-# suite run, equal in isolation); a fusion bug is >> 1e-2
+# Per parameter the two arms' errors vs the exact step vary by up to ~8x from one rounding state
+# to another (layer4.1.bn1.weight: 5.7e-4 unfused vs 4.7e-3 fused in one full-suite run, within
+# 2x in isolation), so the per-parameter bound is absolute (ABS) unless the fused arm is
+# within FACTOR of the unfused one, and the systematic check is on the mean over parameters.
 FACTOR = 3.0
-FLOOR = 1e-4      # L2-relative: parameters both arms get (nearly) exact
+ABS = 2e-2        # L2-relative, per parameter: a wiring bug is O(1)
+MEAN_FACTOR = 1.5  # mean over parameters of the fused arm's error vs the unfused arm's
 UNFUSED_MAX = 5e-2  # the reference arm itself (fp32 MFMA kernels) vs the exact step
 
 
@@ -49,9 +51,14 @@ def rel_err(g: torch.Tensor, r: torch.Tensor) -> float:
 
 
 def assert_fused_no_worse(g_fused: Dict[str, torch.Tensor], g_unfused: Dict[str, torch.Tensor],
-                          ref: Dict[str, torch.Tensor], factor: float = FACTOR, floor: float = FLOOR) -> None:
+                          ref: Dict[str, torch.Tensor]) -> None:
+    ef_all, eu_all = [], []
     for n, r in ref.items():
         eu = rel_err(g_unfused[n], r)
         ef = rel_err(g_fused[n], r)
         assert eu < UNFUSED_MAX, (n, "unfused arm vs fp64", eu)
-        assert ef <= factor * eu + floor, (n, "fused vs fp64", ef, "unfused vs fp64", eu)
+        assert ef <= max(FACTOR * eu, ABS), (n, "fused vs fp64", ef, "unfused vs fp64", eu)
+        ef_all.append(ef)
+        eu_all.append(eu)
+    mf, mu = sum(ef_all) / len(ef_all), sum(eu_all) / len(eu_all)
+    assert mf <= MEAN_FACTOR * mu + 1e-5, ("mean over parameters: fused", mf, "unfused", mu)
