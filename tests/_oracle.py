@@ -23,11 +23,13 @@ _CACHE: Dict[tuple, Tuple[float, Dict[str, torch.Tensor]]] = {}
 
 # Per parameter the two arms' errors vs the exact step vary by up to ~8x from one rounding state
 # to another (layer4.1.bn1.weight: 5.7e-4 unfused vs 4.7e-3 fused in one full-suite run, within
-# 2x in isolation), so the per-parameter bound is absolute (ABS) unless the fused arm is
-# within FACTOR of the unfused one, and the systematic check is on the mean over parameters.
+# 2x in isolation), and even the mean over parameters by up to 2.2x in either direction
+# (profiles/r5/stats_arm_check.txt: seeds 0-3 x GEMM table on / off, once the fused arm is the
+# worse one, once the unfused).  So the per-parameter bound is absolute (ABS) unless the fused
+# arm is within FACTOR of the unfused one, and the mean over parameters within MEAN_FACTOR.
 FACTOR = 3.0
 ABS = 2e-2        # L2-relative, per parameter: a wiring bug is O(1)
-MEAN_FACTOR = 1.5  # mean over parameters of the fused arm's error vs the unfused arm's
+MEAN_FACTOR = 3.0  # mean over parameters of the fused arm's error vs the unfused arm's
 UNFUSED_MAX = 5e-2  # the reference arm itself (fp32 MFMA kernels) vs the exact step
 
 
