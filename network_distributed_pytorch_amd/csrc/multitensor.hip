@@ -20,6 +20,11 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+// the entry table's pointers, re-typed as global (address space 1): read through the table they
+// would compile to FLAT accesses, which also wait on the scalar-cache counter
+#define NDP_GLOBAL __attribute__((address_space(1)))
+__device__ __forceinline__ f32x4 ld4(const float NDP_GLOBAL* p) { return *reinterpret_cast<const f32x4 NDP_GLOBAL*>(p); }
+__device__ __forceinline__ void st4(float NDP_GLOBAL* p, f32x4 v) { *reinterpret_cast<f32x4 NDP_GLOBAL*>(p) = v; }
 
 __global__ __launch_bounds__(256) void seg_reduce_kernel(const SegEntry* __restrict__ ents,
                                                          const int64_t* __restrict__ prefix,
@@ -31,6 +36,8 @@ __global__ __launch_bounds__(256) void seg_reduce_kernel(const SegEntry* __restr
     if (prefix[mid] <= blk) lo = mid; else hi = mid - 1;
   }
   const SegEntry E = ents[lo];
+  const float NDP_GLOBAL* const src = (const float NDP_GLOBAL*)E.src;
+  float NDP_GLOBAL* const dst = (float NDP_GLOBAL*)E.dst;
   const int64_t base = (blk - prefix[lo]) * kSegBlockElems;
   const bool scale = E.div != 1.0f;
   if (E.vec) {
@@ -46,7 +53,7 @@ __global__ __launch_bounds__(256) void seg_reduce_kernel(const SegEntry* __restr
     for (int q = 0; q < QN; ++q) {
       kq[q] = base + (int64_t)(q * 256 + threadIdx.x) * 4;
       full[q] = kq[q] + 3 < E.numel;
-      acc[q] = full[q] ? ld4(E.src + kq[q]) : f32x4{0.f, 0.f, 0.f, 0.f};
+      acc[q] = full[q] ? ld4(src + kq[q]) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
     int c = 1;
     for (; c + kSegBatch <= E.chunks; c += kSegBatch) {
@@ -55,7 +62,7 @@ __global__ __launch_bounds__(256) void seg_reduce_kernel(const SegEntry* __restr
       for (int j = 0; j < kSegBatch; ++j)
 #pragma unroll
         for (int q = 0; q < QN; ++q)
-          t[q][j] = full[q] ? ld4(E.src + (int64_t)(c + j) * E.stride + kq[q]) : f32x4{0.f, 0.f, 0.f, 0.f};
+          t[q][j] = full[q] ? ld4(src + (int64_t)(c + j) * E.stride + kq[q]) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int q = 0; q < QN; ++q)
 #pragma unroll
@@ -64,20 +71,20 @@ __global__ __launch_bounds__(256) void seg_reduce_kernel(const SegEntry* __restr
     for (; c < E.chunks; ++c)
 #pragma unroll
       for (int q = 0; q < QN; ++q)
-        if (full[q]) acc[q] += ld4(E.src + (int64_t)c * E.stride + kq[q]);
+        if (full[q]) acc[q] += ld4(src + (int64_t)c * E.stride + kq[q]);
 #pragma unroll
     for (int q = 0; q < QN; ++q) {
       const int64_t k = kq[q];
       if (full[q]) {
         if (scale) acc[q] = acc[q] / E.div;
-        st4(E.dst + k, acc[q]);
+        st4(dst + k, acc[q]);
       } else if (k < E.numel) {
         for (int j = 0; j < 4; ++j) {
           if (k + j >= E.numel) break;
-          float t = E.src[k + j];
-          for (int z = 1; z < E.chunks; ++z) t += E.src[(int64_t)z * E.stride + k + j];
+          float t = src[k + j];
+          for (int z = 1; z < E.chunks; ++z) t += src[(int64_t)z * E.stride + k + j];
           if (scale) t = t / E.div;
-          E.dst[k + j] = t;
+          dst[k + j] = t;
         }
       }
     }
@@ -85,10 +92,10 @@ __global__ __launch_bounds__(256) void seg_reduce_kernel(const SegEntry* __restr
     for (int q = 0; q < kSegBlockElems / 256; ++q) {
       const int64_t k = base + q * 256 + threadIdx.x;
       if (k >= E.numel) break;
-      float acc = E.src[k];
-      for (int c = 1; c < E.chunks; ++c) acc += E.src[(int64_t)c * E.stride + k];
+      float acc = src[k];
+      for (int c = 1; c < E.chunks; ++c) acc += src[(int64_t)c * E.stride + k];
       if (scale) acc = acc / E.div;
-      E.dst[k] = acc;
+      dst[k] = acc;
     }
   }
 }

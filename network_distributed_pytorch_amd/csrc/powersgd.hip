@@ -35,6 +35,29 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
 
+// The per-matrix pointers come from a table in memory, so the compiler cannot prove they are
+// global: every HBM stream through them compiled to FLAT loads / stores, which also count on
+// lgkmcnt — each scalar-cache wait (s_load of a P-hat row, a table entry) then drained every
+// outstanding stream load as well.  GPtrs re-types them as global (address space 1).
+#define NDP_GLOBAL __attribute__((address_space(1)))
+struct GPtrs {
+  const float NDP_GLOBAL* min;
+  float NDP_GLOBAL* e;
+  const float NDP_GLOBAL* mread;
+  float NDP_GLOBAL* out;
+  float NDP_GLOBAL* mem;
+  float NDP_GLOBAL* mom;
+  float NDP_GLOBAL* x;
+  float NDP_GLOBAL* g;
+};
+__device__ __forceinline__ GPtrs gptrs(const MatPtrs& p) {
+  return GPtrs{(const float NDP_GLOBAL*)p.min, (float NDP_GLOBAL*)p.e,   (const float NDP_GLOBAL*)p.mread,
+               (float NDP_GLOBAL*)p.out,       (float NDP_GLOBAL*)p.mem, (float NDP_GLOBAL*)p.mom,
+               (float NDP_GLOBAL*)p.x,         (float NDP_GLOBAL*)p.g};
+}
+__device__ __forceinline__ f32x4 ld4(const float NDP_GLOBAL* p) { return *reinterpret_cast<const f32x4 NDP_GLOBAL*>(p); }
+__device__ __forceinline__ void st4(float NDP_GLOBAL* p, f32x4 v) { *reinterpret_cast<f32x4 NDP_GLOBAL*>(p) = v; }
+
 __device__ __forceinline__ float wave_sum(float v) {
   // xor butterfly: every lane ends with the bitwise-identical total (fp add commutes)
 #pragma unroll
@@ -58,7 +81,7 @@ __global__ __launch_bounds__(256) void psgd_p_kernel(const MatGeom* __restrict__
   constexpr int CW = 16 * NCG;
   const PItem it = items[blockIdx.x];
   const MatGeom g = geom[it.mat];
-  const MatPtrs pt = ptrs[it.mat];
+  const GPtrs pt = gptrs(ptrs[it.mat]);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = g.r;
   const int klen = it.k1 - it.k0;
@@ -214,7 +237,7 @@ __global__ __launch_bounds__(256) void psgd_p_wide_kernel(const MatGeom* __restr
   constexpr int V = 4 * RQ;
   const PItem it = items[blockIdx.x];
   const MatGeom g = geom[it.mat];
-  const MatPtrs pt = ptrs[it.mat];
+  const GPtrs pt = gptrs(ptrs[it.mat]);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = g.r, n = g.n, m = g.m;
@@ -348,7 +371,7 @@ __global__ __launch_bounds__(256) void psgd_q_kernel(const MatGeom* __restrict__
   constexpr int LDP = CW + (NCG > 1 ? 16 : 0);
   const QItem it = items[blockIdx.x];
   const MatGeom g = geom[it.mat];
-  const MatPtrs pt = ptrs[it.mat];
+  const GPtrs pt = gptrs(ptrs[it.mat]);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = g.r;
   const int nrows = it.row1 - it.row0;
@@ -367,7 +390,7 @@ __global__ __launch_bounds__(256) void psgd_q_kernel(const MatGeom* __restrict__
   const int bl = b0 + 4 * (lane & 15);
   const int rsub = lane >> 4;
   const int cl = lane & 15;
-  const float* Mb = pt.mread + (int64_t)it.row0 * g.m;
+  const float NDP_GLOBAL* Mb = pt.mread + (int64_t)it.row0 * g.m;
 
   f32x4 acc[NCG][4];
 #pragma unroll
@@ -379,7 +402,7 @@ __global__ __launch_bounds__(256) void psgd_q_kernel(const MatGeom* __restrict__
     const int al = s + rsub;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
     if (al < nrows) {
-      const float* row = Mb + (int64_t)al * g.m;
+      const float NDP_GLOBAL* row = Mb + (int64_t)al * g.m;
       if (g.vec) {
         if (bl < g.m) v = ld4(row + bl);
       } else {
@@ -441,7 +464,7 @@ __global__ __launch_bounds__(256) void psgd_update_kernel(
     float lr, float momentum) {
   const UItem it = items[blockIdx.x];
   const MatGeom g = geom[it.mat];
-  const MatPtrs pt = ptrs[it.mat];
+  const GPtrs pt = gptrs(ptrs[it.mat]);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = g.r, n = g.n, m = g.m;
   const float* P = p_hat + g.p_off;
@@ -555,7 +578,7 @@ __global__ __launch_bounds__(256) void psgd_update_wide_kernel(
     float lr, float momentum, float* __restrict__ p_prev) {
   const UItem it = items[blockIdx.x];
   const MatGeom g = geom[it.mat];
-  const MatPtrs pt = ptrs[it.mat];
+  const GPtrs pt = gptrs(ptrs[it.mat]);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = g.r, n = g.n, m = g.m;
