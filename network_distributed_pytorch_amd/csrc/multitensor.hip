@@ -108,16 +108,18 @@ __global__ __launch_bounds__(256) void sgd_momentum_vec_kernel(float* __restrict
   const bool scale = div != 1.0f;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (int64_t)gridDim.x * blockDim.x) {
-    f32x4 gg = ld4(g + 4 * i);
+    // gradient and momentum buffer through non-temporal accesses (each touched once per step; the
+    // parameters are cached for the next forward), as in powersgd.hip's update pass
+    f32x4 gg = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(g + 4 * i));
     if (scale) gg = gg / div;
-    f32x4 b = ld4(buf + 4 * i);
+    f32x4 b = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(buf + 4 * i));
     f32x4 xx = ld4(x + 4 * i);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       b[j] = __fadd_rn(__fmul_rn(b[j], mu), gg[j]);
       xx[j] = fmaf(-lr, b[j], xx[j]);
     }
-    st4(buf + 4 * i, b);
+    __builtin_nontemporal_store(b, reinterpret_cast<f32x4*>(buf + 4 * i));
     st4(x + 4 * i, xx);
   }
 }

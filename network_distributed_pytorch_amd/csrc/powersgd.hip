@@ -225,7 +225,7 @@ __device__ __forceinline__ bool spread_writer(int lane) {
 // update's exact arithmetic (Qs = the warm-start Q it reads anyway, the same fmaf chain over
 // c), so M = g + e is bitwise the eager formula's.  p_prev = 0 (first step, after a
 // checkpoint materialised e) makes the correction an exact zero.
-template <int RQ>
+template <int RQ, int NT = 0>
 __global__ __launch_bounds__(256) void psgd_p_wide_kernel(const MatGeom* __restrict__ geom,
                                                           const MatPtrs* __restrict__ ptrs,
                                                           const PItem* __restrict__ items,
@@ -263,8 +263,15 @@ __global__ __launch_bounds__(256) void psgd_p_wide_kernel(const MatGeom* __restr
           const int b = it.k0 + 256 * (s0 + sb) + 4 * lane;
           const bool ok = arow0 + i < n && b < it.k1;  // vec: k1 - b >= 4 whenever b < k1
           const int64_t o = (int64_t)(arow0 + i) * m + b;
-          mv[i][sb] = ok ? ld4(pt.min + o) : f32x4{0.f, 0.f, 0.f, 0.f};
-          ev[i][sb] = (ok && fuse_ef) ? ld4(pt.e + o) : f32x4{0.f, 0.f, 0.f, 0.f};
+          if constexpr (NT >= 1) {
+            mv[i][sb] = ok ? __builtin_nontemporal_load(reinterpret_cast<const f32x4 NDP_GLOBAL*>(pt.min + o))
+                           : f32x4{0.f, 0.f, 0.f, 0.f};
+            ev[i][sb] = (ok && fuse_ef) ? __builtin_nontemporal_load(reinterpret_cast<const f32x4 NDP_GLOBAL*>(pt.e + o))
+                                        : f32x4{0.f, 0.f, 0.f, 0.f};
+          } else {
+            mv[i][sb] = ok ? ld4(pt.min + o) : f32x4{0.f, 0.f, 0.f, 0.f};
+            ev[i][sb] = (ok && fuse_ef) ? ld4(pt.e + o) : f32x4{0.f, 0.f, 0.f, 0.f};
+          }
         }
     } else {
 #pragma unroll
@@ -327,7 +334,10 @@ __global__ __launch_bounds__(256) void psgd_p_wide_kernel(const MatGeom* __restr
           if (arow0 + i < n) {
             const int64_t o = (int64_t)(arow0 + i) * m + b;
             if (g.vec) {
-              if (b < it.k1) st4(pt.e + o, mv[i][sb]);
+              if (b < it.k1) {
+                if constexpr (NT >= 2) __builtin_nontemporal_store(mv[i][sb], reinterpret_cast<f32x4 NDP_GLOBAL*>(pt.e + o));
+                else st4(pt.e + o, mv[i][sb]);
+              }
             } else {
 #pragma unroll
               for (int j = 0; j < 4; ++j)
@@ -570,7 +580,7 @@ constexpr int kURowsPerWave = kUWideRows / 4;
 // p_prev != nullptr (lazy error feedback, modes 1 / 2): e is not written — M is not even read —
 // and the column-block-0 workgroup of each row block keeps its P-hat rows in p_prev for the
 // next P pass.  mode 3: e -= p_hat Qs^T only (the lazy state materialised: checkpoint, API).
-template <int RQ>
+template <int RQ, int NT = 0>
 __global__ __launch_bounds__(256) void psgd_update_wide_kernel(
     const MatGeom* __restrict__ geom, const MatPtrs* __restrict__ ptrs,
     const UItem* __restrict__ items, const float* __restrict__ p_hat,
@@ -611,7 +621,12 @@ __global__ __launch_bounds__(256) void psgd_update_wide_kernel(
       const int64_t o = (int64_t)(arow0 + i) * m + b;
       Mv[i] = (ok && !lazy) ? ld4(pt.mread + o) : f32x4{0.f, 0.f, 0.f, 0.f};
       if (mode == 1 || mode == 2) {
-        Mm[i] = ok ? ld4(pt.mom + o) : f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (NT >= 1) {
+          Mm[i] = ok ? __builtin_nontemporal_load(reinterpret_cast<const f32x4 NDP_GLOBAL*>(pt.mom + o))
+                     : f32x4{0.f, 0.f, 0.f, 0.f};
+        } else {
+          Mm[i] = ok ? ld4(pt.mom + o) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
         Xv[i] = ok ? ld4(pt.x + o) : f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
@@ -664,7 +679,8 @@ __global__ __launch_bounds__(256) void psgd_update_wide_kernel(
         const f32x4 up = o + mm;
 #pragma unroll
         for (int j = 0; j < 4; ++j) xx[j] = fmaf(-lr, up[j], xx[j]);
-        st4(pt.mom + ro + b, mm);
+        if constexpr (NT >= 2) __builtin_nontemporal_store(mm, reinterpret_cast<f32x4 NDP_GLOBAL*>(pt.mom + ro + b));
+        else st4(pt.mom + ro + b, mm);
         st4(pt.x + ro + b, xx);
         if (mode == 2) st4(pt.g + ro + b, up);
       }
@@ -725,13 +741,15 @@ void launch_psgd_p(const MatGeom* geom, const MatPtrs* ptrs, const PItem* items,
   if (n_items <= 0) return;
   // the item shape follows the plan's max rank (plan.cpp): wide 16 x kPKW items up to rank 16
   if (max_rank <= 4) {
-    hipLaunchKernelGGL(psgd_p_wide_kernel<4>, dim3(n_items), dim3(256), 0, s, geom, ptrs, items, q_warm, p_part, fuse_ef,
-                       p_prev);
+    // non-temporal g / e loads (read once per step): ResNet-18 r=4 batch 64 0.8306 / 0.8294 ->
+    // 0.8245 / 0.8233 ms (profiles/r5/bench_psgd_nt.jsonl)
+    hipLaunchKernelGGL((psgd_p_wide_kernel<4, 1>), dim3(n_items), dim3(256), 0, s, geom, ptrs, items, q_warm, p_part,
+                       fuse_ef, p_prev);
     return;
   }
   if (max_rank <= 8) {
-    hipLaunchKernelGGL(psgd_p_wide_kernel<8>, dim3(n_items), dim3(256), 0, s, geom, ptrs, items, q_warm, p_part, fuse_ef,
-                       p_prev);
+    hipLaunchKernelGGL((psgd_p_wide_kernel<8, 1>), dim3(n_items), dim3(256), 0, s, geom, ptrs, items, q_warm, p_part,
+                       fuse_ef, p_prev);
     return;
   }
   if (max_rank <= kUWideMaxRank) {
@@ -777,11 +795,14 @@ void launch_psgd_update(const MatGeom* geom, const MatPtrs* ptrs, const UItem* i
                         hipStream_t s, float* p_prev) {
   if (n_items <= 0) return;
   // the item tiles follow the plan's max rank (plan.cpp): wide 16 x 256 tiles up to rank 16
+  // momentum through non-temporal loads / stores (touched once per step, 4 B per parameter): it
+  // no longer evicts the next forward's weights and activations from the caches — ResNet-18 r=4
+  // batch 64 0.8245 / 0.8233 -> 0.7896 / 0.7855 ms, batch 512 unchanged (1.4905 / 1.4930)
   if (max_rank <= 4)
-    hipLaunchKernelGGL(psgd_update_wide_kernel<4>, dim3(n_items), dim3(256), 0, s, geom, ptrs,
+    hipLaunchKernelGGL((psgd_update_wide_kernel<4, 2>), dim3(n_items), dim3(256), 0, s, geom, ptrs,
                        items, p_hat, q_sum, q_div, q_warm, mode, lr, momentum, p_prev);
   else if (max_rank <= 8)
-    hipLaunchKernelGGL(psgd_update_wide_kernel<8>, dim3(n_items), dim3(256), 0, s, geom, ptrs,
+    hipLaunchKernelGGL((psgd_update_wide_kernel<8, 2>), dim3(n_items), dim3(256), 0, s, geom, ptrs,
                        items, p_hat, q_sum, q_div, q_warm, mode, lr, momentum, p_prev);
   else if (max_rank <= kUWideMaxRank)
     hipLaunchKernelGGL(psgd_update_wide_kernel<kUWideMaxRank>, dim3(n_items), dim3(256), 0, s,
