@@ -1126,7 +1126,10 @@ __global__ __launch_bounds__(256) void conv_slab_sum_many_kernel(SlabBatch b) {
   f32x4c acc = {0.f, 0.f, 0.f, 0.f};
   if (i4 < n) {
 #pragma unroll 4
-    for (int sl = g; sl < n_slices; sl += 16) acc += *reinterpret_cast<const f32x4c*>(part + (int64_t)sl * n + i4);
+    for (int sl = g; sl < n_slices; sl += 16) {
+      if (b.nt) acc += __builtin_nontemporal_load(reinterpret_cast<const f32x4c*>(part + (int64_t)sl * n + i4));
+      else acc += *reinterpret_cast<const f32x4c*>(part + (int64_t)sl * n + i4);
+    }
   }
   red[g][col] = acc;
   __syncthreads();
@@ -1139,6 +1142,7 @@ __global__ __launch_bounds__(256) void conv_slab_sum_many_kernel(SlabBatch b) {
 }
 
 void launch_slab_sum_many(const SlabBatch& b, hipStream_t s) {
+  const_cast<SlabBatch&>(b).nt = 1;  // slabs are read once: non-temporal loads (with the Q pass's, b64 -2.5 %)
   if (b.n <= 0) return;
   hipLaunchKernelGGL(conv_slab_sum_many_kernel, dim3((unsigned)b.end[b.n - 1]), dim3(256), 0, s, b);
 }

@@ -255,6 +255,7 @@ struct SlabBatch {
   int slices[kMaxExpand];
   int64_t end[kMaxExpand];  // inclusive prefix sums of blocks (64 floats per block)
   int n;
+  int nt;  // non-temporal slab loads (set by launch_slab_sum_many)
 };
 void launch_slab_sum_many(const SlabBatch& b, hipStream_t s);
 // dW [Co, C, KH, KW] <- fold of dWt_big [Co*OH*OW, C*H*W]  (fixed-order sum, deterministic)

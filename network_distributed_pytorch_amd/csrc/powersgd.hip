@@ -370,7 +370,7 @@ __global__ __launch_bounds__(256) void psgd_p_wide_kernel(const MatGeom* __restr
 // wave instruction.  MFMA j consumes component j (column b0 + 4i + j of row block).
 // P-hat rows [row0,row1) are staged in LDS (row stride LDP, bank-conflict padded).
 // ----------------------------------------------------------------------------------
-template <int NCG>
+template <int NCG, bool kQNT = false>
 __global__ __launch_bounds__(256) void psgd_q_kernel(const MatGeom* __restrict__ geom,
                                                      const MatPtrs* __restrict__ ptrs,
                                                      const QItem* __restrict__ items,
@@ -414,7 +414,8 @@ __global__ __launch_bounds__(256) void psgd_q_kernel(const MatGeom* __restrict__
     if (al < nrows) {
       const float NDP_GLOBAL* row = Mb + (int64_t)al * g.m;
       if (g.vec) {
-        if (bl < g.m) v = ld4(row + bl);
+        if (bl < g.m) v = kQNT ? __builtin_nontemporal_load(reinterpret_cast<const f32x4 NDP_GLOBAL*>(row + bl))
+                               : ld4(row + bl);
       } else {
         float t[4];
 #pragma unroll
@@ -778,8 +779,10 @@ void launch_psgd_q(const MatGeom* geom, const MatPtrs* ptrs, const QItem* items,
   const int ldp = 16 * ncg + (ncg > 1 ? 16 : 0);
   const size_t lds = sizeof(float) * kQRowsMax * ldp;
   if (ncg == 4) allow_lds(reinterpret_cast<const void*>(psgd_q_kernel<4>), lds);
+  // non-temporal M loads (the step's last read of e): ResNet-18 r=4 batch 64 0.796 / 0.808 ->
+  // 0.779 / 0.783 ms with the non-temporal slab sums (profiles/r5/bench_psgd_nt.jsonl)
   if (ncg == 1)
-    hipLaunchKernelGGL(psgd_q_kernel<1>, dim3(n_items), dim3(256), lds, s, geom, ptrs, items,
+    hipLaunchKernelGGL((psgd_q_kernel<1, true>), dim3(n_items), dim3(256), lds, s, geom, ptrs, items,
                        p_hat, q_part);
   else if (ncg == 2)
     hipLaunchKernelGGL(psgd_q_kernel<2>, dim3(n_items), dim3(256), lds, s, geom, ptrs, items,
