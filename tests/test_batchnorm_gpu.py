@@ -113,10 +113,10 @@ def test_bn_single_launch_small_path(device, shape):
 
 
 @pytest.mark.parametrize("shape", [(512, 512, 1, 1), (512, 256, 2, 2), (512, 128, 4, 4), (256, 64, 2, 2)])
-def test_bn_single_launch_row_splits_running_stats(device, shape):
-    """(Run with NDP_BN_ROWSPLIT=4 to exercise the opt-in row splits.)  Row-split single-launch BN (workgroups of a column block exchanging partial sums behind
-    a counter barrier): running statistics written once per channel, equal to the 3-kernel
-    path; repeated launches (counters never reset) stay exact."""
+def test_bn_single_launch_running_stats(device, shape):
+    """Single-launch small-map BN over repeated steps: output and running statistics (written
+    once per channel) equal to the statistics + apply path's, num_batches_tracked advanced once
+    per call.  (The round-4 row-split variant this test also covered was removed in round 5.)"""
     torch.manual_seed(3)
     C = shape[1]
     a = BatchNormAct2d(C).to(device)
