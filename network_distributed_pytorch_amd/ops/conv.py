@@ -24,7 +24,7 @@ from ._ext import ext
 from .gradarena import grad_buffer
 from ..knobs import fusion_on
 
-__all__ = ["direct_plan", "conv2d_direct", "DirectConvFn", "WinoBank"]
+__all__ = ["direct_plan", "conv2d_direct", "DirectConvFn", "WinoBank", "set_winograd"]
 
 _PLANS: dict = {}
 _STATS: dict = {}
@@ -41,17 +41,24 @@ class WinoBank:
     """Winograd weight transforms (csrc/winograd.hip, forward + grad-x layouts) of every Winograd
     layer of one model, rebuilt by ONE launch per forward pass instead of one per layer — the
     scheme of models/conv_gemm.ToeplitzBank: layers join on their first device forward (eager
-    warm-up, never inside a capture); afterwards the first member to run in a pass (forward
-    order is fixed) transforms every member.  Valid because weights change only between passes
-    (optimizer step); a transform saved for backward is rebuilt by the NEXT forward."""
+    warm-up, never inside a capture); afterwards the first member to run in a pass transforms
+    every member.  Valid because weights change only between passes (optimizer step); a
+    transform saved for backward is rebuilt by the NEXT forward.
+
+    Which layers take the Winograd path depends on the batch size (``wino_dirs``), so "the
+    first member of a pass" is recorded per batch size (forward order is fixed, so for one batch
+    size it is always the same layer), not taken to be member 0: in a Bottleneck ResNet at
+    per-GPU batch 20 the first Winograd layer is layer2.0.conv2, and a refresh tied to member 0
+    would leave it one step stale."""
 
     MAX = 16  # csrc/ndp_kernels.h kMaxWino
 
     def __init__(self):
         self.members: list = []  # [(weight Parameter, u)]
         self._index: dict = {}
+        self._lead: dict = {}  # batch size -> index of the first member to run in a pass
 
-    def get(self, weight: torch.Tensor) -> torch.Tensor:
+    def get(self, weight: torch.Tensor, batch: int) -> torch.Tensor:
         key = id(weight)
         i = self._index.get(key)
         numel = 32 * weight.numel() // 9
@@ -60,16 +67,26 @@ class WinoBank:
             u = torch.empty(numel, device=weight.device, dtype=torch.float32)
             ext().wino_weights(weight.contiguous(), u)
             if i is None:
-                self._index[key] = len(self.members)
+                i = self._index[key] = len(self.members)
                 self.members.append((weight, u))
             else:
                 self.members[i] = (weight, u)
+            self._lead.setdefault(int(batch), i)
             return u
-        if i == 0:
-            batch = [(w, u) for w, u in self.members]
-            for j in range(0, len(batch), self.MAX):
-                ext().wino_weights_many(batch[j: j + self.MAX])
+        if self._lead.setdefault(int(batch), i) == i:
+            batch_ = [(w, u) for w, u in self.members]
+            for j in range(0, len(batch_), self.MAX):
+                ext().wino_weights_many(batch_[j: j + self.MAX])
         return self.members[i][1]
+
+
+def set_winograd(on: bool) -> None:
+    """Switch the Winograd kernels on / off (csrc/winograd.hip) and drop every cached decision
+    that depends on the switch (plans, Winograd directions, epilogue statistics slices)."""
+    ext().wino_set_enabled(bool(on))
+    _PLANS.clear()
+    _WINO.clear()
+    _STATS.clear()
 
 
 def wino_dirs(geom, B: int) -> Tuple[bool, bool]:
@@ -156,7 +173,7 @@ class DirectConvFn(torch.autograd.Function):
         wf, wd = wino_dirs(geom, B)
         wu = None
         if (wf or wd) and wbank is not None:  # the model's bank: one transform launch per pass
-            wu = wbank.get(wparam)
+            wu = wbank.get(wparam, B)
         elif wf or wd:
             wu = torch.empty(32 * weight.numel() // 9, device=x.device, dtype=x.dtype)  # fwd + grad-x layouts
             ext().wino_weights(weight, wu)

@@ -15,7 +15,7 @@ per-layer launches.
 """
 from __future__ import annotations
 
-import os
+import warnings
 
 import torch
 
@@ -50,14 +50,19 @@ def _queue():
 
 def _end_of_backward():
     _queued[0] = False
+    _CLAIMED.clear()  # claims live for one graph task (ids of dead params may be reused)
     flush()
 
 
-def _task_id() -> int:
+def _task_id():
+    """The running autograd graph task's id, or None when this torch exposes none."""
     try:
         return int(torch._C._current_graph_task_id())
     except Exception:  # pragma: no cover - older torch: no task ids
-        return -2
+        return None
+
+
+_NO_TASK_WARNED = [False]
 
 
 # id(param) -> autograd graph task in which a gradient of the param was deferred
@@ -77,6 +82,13 @@ def can_defer(param: torch.Tensor) -> bool:
     if not (_ENABLED and param.grad is None and not torch.is_grad_enabled()):
         return False
     task = _task_id()
+    if task is None:
+        # without task ids a shared parameter's second gradient cannot be told from the next
+        # backward's first: defer nothing, say so once
+        if not _NO_TASK_WARNED[0]:
+            _NO_TASK_WARNED[0] = True
+            warnings.warn("torch exposes no autograd graph-task id: deferred grad-W finishing is off")
+        return False
     if _CLAIMED.get(id(param)) == task:
         flush()
         return False

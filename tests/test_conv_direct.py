@@ -142,7 +142,7 @@ def test_winograd_vs_direct_vs_fp64(device, cin, cout, s, B, hw):
     run-to-run.  The Winograd path must actually be taken (conv_wino) for these shapes."""
     from network_distributed_pytorch_amd.ops.conv import wino_dirs
     from network_distributed_pytorch_amd.ops._ext import ext
-    from network_distributed_pytorch_amd.ops.conv import conv2d_direct
+    from network_distributed_pytorch_amd.ops.conv import conv2d_direct, set_winograd
 
     torch.manual_seed(6)
     x = torch.randn(B, cin, hw, hw, dtype=torch.float64)
@@ -153,13 +153,13 @@ def test_winograd_vs_direct_vs_fp64(device, cin, cout, s, B, hw):
     g = torch.randn_like(yr)
     yr.backward(g)
     geom = (cin, hw, hw, cout, 3, 3, s, 1)
-    ext().wino_set_enabled(True)
+    set_winograd(True)
     assert bool(ext().conv_wino(list(geom), B, True)), "grad-x should take the Winograd kernel"
     assert s == 2 or bool(ext().conv_wino(list(geom), B, False)), "forward should take the Winograd kernel"
     res = {}
     try:
         for wino in (True, False, True):
-            ext().wino_set_enabled(wino)
+            set_winograd(wino)
             xd = x.float().to(device).requires_grad_(True)
             wd = w.float().to(device).requires_grad_(True)
             y = conv2d_direct(xd, wd, s, 1)
@@ -170,7 +170,7 @@ def test_winograd_vs_direct_vs_fp64(device, cin, cout, s, B, hw):
                     assert torch.equal(a, b)  # deterministic
             res[wino] = out
     finally:
-        ext().wino_set_enabled(True)
+        set_winograd(True)
     for i, (ref, name) in enumerate(((yr, "y"), (xr.grad, "dx"), (wr.grad, "dw"))):
         scale = ref.abs().max().item()
         ew = (res[True][i] - ref).abs().max().item() / scale
@@ -209,3 +209,41 @@ def test_wino_bank_matches_per_layer_transforms(device):
     assert len(a.layer1[0].conv1.wbank.members) >= 4
     for pa, pb in zip(a.parameters(), b.parameters()):
         assert torch.equal(pa, pb)
+
+
+@pytest.mark.gpu
+def test_wino_bank_bottleneck_alternating_batches(device):
+    """A Bottleneck ResNet whose set of Winograd layers changes with the batch size (ADVICE r5:
+    at batch 20 the first Winograd layer is layer2.0.conv2, at batch 64 it is layer1's): the
+    bank, alternating batches 64 and 20 (and first touched at 20 by a no-grad forward), stays
+    bitwise equal to per-layer transforms across SGD steps."""
+    from network_distributed_pytorch_amd.models import build_resnet
+    from network_distributed_pytorch_amd.models.conv_gemm import GemmConv2d
+    torch.manual_seed(8)
+    a = build_resnet(50, 10).to(device)
+    b = build_resnet(50, 10).to(device)
+    b.load_state_dict(a.state_dict())
+    for m in b.modules():
+        if isinstance(m, GemmConv2d):
+            m.wbank = None
+    xs = {B: torch.randn(B, 3, 32, 32, device=device) for B in (64, 20)}
+    ys = {B: torch.randint(0, 10, (B,), device=device) for B in (64, 20)}
+    with torch.no_grad():  # first touch at the small batch
+        for m in (a, b):
+            m(xs[20])
+    for B in (64, 20, 64, 20, 64):
+        losses = []
+        for m in (a, b):
+            m.zero_grad(set_to_none=True)
+            loss = F.cross_entropy(m(xs[B]), ys[B])
+            loss.backward()
+            with torch.no_grad():
+                for p in m.parameters():
+                    p.add_(p.grad, alpha=-0.05)
+            losses.append(loss.detach())
+        assert torch.equal(losses[0], losses[1]), B
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        assert torch.equal(pa, pb)
+    # the premise: a pass at each batch size is led by a different Winograd layer
+    bank = next(m.wbank for m in a.modules() if isinstance(m, GemmConv2d) and m.wbank is not None)
+    assert set(bank._lead) == {64, 20} and bank._lead[64] != bank._lead[20], bank._lead

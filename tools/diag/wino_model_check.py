@@ -10,6 +10,7 @@ sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
 from network_distributed_pytorch_amd.models import build_resnet  # noqa: E402
 from network_distributed_pytorch_amd.ops import conv as conv_mod  # noqa: E402
 from network_distributed_pytorch_amd.ops._ext import ext  # noqa: E402
+from network_distributed_pytorch_amd.ops.conv import set_winograd  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 dev = torch.device("cuda", 0)
@@ -26,7 +27,7 @@ names = ["conv1.weight", "layer1.0.conv1.weight", "layer1.1.conv2.weight", "laye
 arms = {}
 for wino in (True, False):
     for stats in (True, False):
-        ext().wino_set_enabled(wino)
+        set_winograd(wino)
         conv_mod.CONV_BN_STATS = stats
         conv_mod._STATS.clear()
         m.load_state_dict(state)

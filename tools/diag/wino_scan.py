@@ -6,6 +6,7 @@ import torch
 
 sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
 from network_distributed_pytorch_amd.ops._ext import ext  # noqa: E402
+from network_distributed_pytorch_amd.ops.conv import set_winograd  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 dev = torch.device("cuda", 0)
@@ -39,12 +40,12 @@ for cin, cout in [(64, 64), (128, 64), (256, 64), (512, 64), (64, 128), (128, 12
     u = torch.empty(32 * cout * cin, device=dev)
     ext().wino_weights(w, u)
     geom = [cin, 8, 8, cout, 3, 3, 1, 1]
-    ext().wino_set_enabled(True)
+    set_winograd(True)
     tw = timeit(lambda: ext().conv_fwd(x, w, y, geom, None, False, None, u))
-    ext().wino_set_enabled(False)
+    set_winograd(False)
     try:
         td = timeit(lambda: ext().conv_fwd(x, w, y, geom, None, False, None, None))
     except Exception as e:  # noqa: BLE001
         td = float("nan")
-    ext().wino_set_enabled(True)
+    set_winograd(True)
     print(f"Cin {cin:4d} Cout {cout:4d}: winograd {tw:7.2f} us   direct {td:7.2f} us", flush=True)
