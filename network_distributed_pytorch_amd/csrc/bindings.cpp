@@ -63,6 +63,9 @@ py::dict build_plan(const std::vector<std::pair<int64_t, int64_t>>& shapes, int 
   d["pp_total"] = pl.pp_total;
   d["qp_total"] = pl.qp_total;
   d["max_rank"] = pl.max_rank;
+  d["n_p_blocks"] = pl.n_p_blocks;
+  d["p_cols"] = (int64_t)pl.p_cols;
+  d["n_q_blocks"] = pl.n_q_blocks;
   // first work item of every matrix (+ sentinel) in each list: a PowerSGD group of
   // matrices [lo, hi) launches the contiguous item slice [start[lo], start[hi])
   auto starts = [&](auto const& items) {
@@ -162,8 +165,19 @@ py::tuple make_orth_geom(const std::vector<std::tuple<int64_t, int64_t, int64_t>
 
 int64_t n_of(const torch::Tensor& bytes, size_t sz) { return bytes.numel() / (int64_t)sz; }
 
+using OptT = c10::optional<torch::Tensor>;
+
+unsigned long long* ctr_ptr(const torch::Tensor& c, int64_t need, const char* what) {
+  check_dev(c, what);
+  TORCH_CHECK(c.scalar_type() == torch::kInt64 && c.numel() >= need, what, ": int64 counters, one per block");
+  return reinterpret_cast<unsigned long long*>(c.data_ptr());
+}
+
+// p_out + p_ctr: in-kernel split-K finish (P written into p_out, wide plans only); seg_*: the
+// rank-1 pack run by the same launch's extra blocks
 void psgd_p(torch::Tensor geom, torch::Tensor ptrs, torch::Tensor items, torch::Tensor q_warm,
-            torch::Tensor p_part, bool fuse_ef, int max_rank, c10::optional<torch::Tensor> p_prev) {
+            torch::Tensor p_part, bool fuse_ef, int max_rank, OptT p_prev, OptT p_out, OptT p_ctr,
+            OptT seg_entries, OptT seg_prefix, int64_t seg_n, int64_t seg_blocks, int64_t p_cols) {
   check_dev(geom, "geom"); check_dev(ptrs, "ptrs"); check_dev(items, "items");
   check_f32(q_warm, "q_warm"); check_f32(p_part, "p_part");
   const float* pp = nullptr;
@@ -172,23 +186,51 @@ void psgd_p(torch::Tensor geom, torch::Tensor ptrs, torch::Tensor items, torch::
     TORCH_CHECK(fuse_ef && max_rank <= ndp::kUWideMaxRank, "psgd_p: lazy error feedback needs fuse_ef, rank <= 16");
     pp = p_prev->data_ptr<float>();
   }
+  const int n_items = (int)n_of(items, sizeof(PItem));
+  ndp::PFin fin{};
+  if (p_out.has_value()) {
+    TORCH_CHECK(max_rank <= ndp::kUWideMaxRank, "psgd_p: in-kernel split-K finish needs rank <= 16");
+    TORCH_CHECK(p_ctr.has_value(), "psgd_p: p_out needs p_ctr");
+    check_f32(*p_out, "p_out");
+    fin.out = p_out->data_ptr<float>();
+    fin.ctr = ctr_ptr(*p_ctr, 1, "p_ctr");  // sized n_p_blocks by the plan (parallel/powersgd.py)
+  }
+  int64_t nsb = 0;
+  if (seg_entries.has_value() && seg_n > 0 && seg_blocks > 0) {
+    TORCH_CHECK(max_rank <= ndp::kUWideMaxRank, "psgd_p: fused rank-1 pack needs rank <= 16");
+    TORCH_CHECK(seg_prefix.has_value(), "psgd_p: seg table needs its prefix");
+    check_dev(*seg_entries, "seg_entries"); check_dev(*seg_prefix, "seg_prefix");
+    TORCH_CHECK(seg_entries->numel() >= seg_n * (int64_t)sizeof(SegEntry) && seg_prefix->numel() >= seg_n,
+                "seg table size mismatch");
+    fin.seg = reinterpret_cast<const SegEntry*>(seg_entries->data_ptr());
+    fin.seg_prefix = seg_prefix->data_ptr<int64_t>();
+    fin.n_seg = (int)seg_n;
+    nsb = seg_blocks;
+  }
   ndp::launch_psgd_p(reinterpret_cast<const MatGeom*>(geom.data_ptr()),
                      reinterpret_cast<const MatPtrs*>(ptrs.data_ptr()),
-                     reinterpret_cast<const PItem*>(items.data_ptr()),
-                     (int)n_of(items, sizeof(PItem)), q_warm.data_ptr<float>(),
-                     p_part.data_ptr<float>(), fuse_ef ? 1 : 0, max_rank, cur_stream(), pp);
+                     reinterpret_cast<const PItem*>(items.data_ptr()), n_items, q_warm.data_ptr<float>(),
+                     p_part.data_ptr<float>(), fuse_ef ? 1 : 0, max_rank, cur_stream(), pp, fin, nsb, (int)p_cols);
   check_launch("launch_psgd_p");
 }
 
 void psgd_q(torch::Tensor geom, torch::Tensor ptrs, torch::Tensor items, torch::Tensor p_hat,
-            torch::Tensor q_part, int max_rank) {
+            torch::Tensor q_part, int max_rank, OptT q_out, OptT q_ctr, int64_t q_fin_max) {
   check_dev(geom, "geom"); check_dev(ptrs, "ptrs"); check_dev(items, "items");
   check_f32(p_hat, "p_hat"); check_f32(q_part, "q_part");
+  ndp::QFin fin{};
+  if (q_out.has_value()) {
+    TORCH_CHECK(q_ctr.has_value(), "psgd_q: q_out needs q_ctr");
+    check_f32(*q_out, "q_out");
+    fin.out = q_out->data_ptr<float>();
+    fin.ctr = ctr_ptr(*q_ctr, 1, "q_ctr");
+    fin.max_chunks = (int)q_fin_max;
+  }
   ndp::launch_psgd_q(reinterpret_cast<const MatGeom*>(geom.data_ptr()),
                      reinterpret_cast<const MatPtrs*>(ptrs.data_ptr()),
                      reinterpret_cast<const QItem*>(items.data_ptr()),
                      (int)n_of(items, sizeof(QItem)), p_hat.data_ptr<float>(),
-                     q_part.data_ptr<float>(), max_rank, cur_stream());
+                     q_part.data_ptr<float>(), max_rank, cur_stream(), fin);
   check_launch("launch_psgd_q");
 }
 
@@ -220,7 +262,8 @@ void psgd_orth(torch::Tensor geom, torch::Tensor items, torch::Tensor p, double 
 
 void psgd_update(torch::Tensor geom, torch::Tensor ptrs, torch::Tensor items, torch::Tensor p_hat,
                  torch::Tensor q_sum, double q_div, c10::optional<torch::Tensor> q_warm, int mode,
-                 double lr, double momentum, int max_rank, c10::optional<torch::Tensor> p_prev) {
+                 double lr, double momentum, int max_rank, c10::optional<torch::Tensor> p_prev,
+                 OptT r1_buf, double r1_div, OptT r1_mom, OptT r1_x, OptT r1_g) {
   check_dev(geom, "geom"); check_dev(ptrs, "ptrs"); check_dev(items, "items");
   check_f32(p_hat, "p_hat"); check_f32(q_sum, "q_sum");
   TORCH_CHECK(mode >= 0 && mode <= 3, "psgd_update: mode 0..3");
@@ -230,12 +273,29 @@ void psgd_update(torch::Tensor geom, torch::Tensor ptrs, torch::Tensor items, to
   if (q_warm.has_value()) { check_f32(*q_warm, "q_warm"); qw = q_warm->data_ptr<float>(); }
   float* pp = nullptr;
   if (p_prev.has_value()) { check_f32(*p_prev, "p_prev"); pp = p_prev->data_ptr<float>(); }
+  ndp::R1Step r1{};
+  if (r1_buf.has_value()) {  // the rank-1 group's step rides in the same launch
+    TORCH_CHECK(mode == 1 || mode == 2, "psgd_update: the rank-1 step needs the engine modes 1 / 2");
+    TORCH_CHECK(r1_mom.has_value() && r1_x.has_value(), "psgd_update: rank-1 step needs mom and x");
+    check_f32(*r1_buf, "r1_buf"); check_f32(*r1_mom, "r1_mom"); check_f32(*r1_x, "r1_x");
+    TORCH_CHECK(r1_buf->numel() == r1_mom->numel() && r1_buf->numel() == r1_x->numel(), "rank-1 size mismatch");
+    r1.buf = r1_buf->data_ptr<float>();
+    r1.mom = r1_mom->data_ptr<float>();
+    r1.x = r1_x->data_ptr<float>();
+    if (r1_g.has_value()) {
+      check_f32(*r1_g, "r1_g");
+      TORCH_CHECK(r1_g->numel() == r1_buf->numel(), "rank-1 size mismatch");
+      r1.g = r1_g->data_ptr<float>();
+    }
+    r1.n = r1_buf->numel();
+    r1.div = (float)r1_div;
+  }
   ndp::launch_psgd_update(reinterpret_cast<const MatGeom*>(geom.data_ptr()),
                           reinterpret_cast<const MatPtrs*>(ptrs.data_ptr()),
                           reinterpret_cast<const UItem*>(items.data_ptr()),
                           (int)n_of(items, sizeof(UItem)), p_hat.data_ptr<float>(),
                           q_sum.data_ptr<float>(), (float)q_div, qw, mode, (float)lr,
-                          (float)momentum, max_rank, cur_stream(), pp);
+                          (float)momentum, max_rank, cur_stream(), pp, r1);
   check_launch("launch_psgd_update");
 }
 
@@ -1304,15 +1364,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("make_seg_table", &make_seg_table);
   m.def("make_orth_geom", &make_orth_geom);
   m.def("psgd_p", &psgd_p, py::arg("geom"), py::arg("ptrs"), py::arg("items"), py::arg("q_warm"), py::arg("p_part"),
-        py::arg("fuse_ef"), py::arg("max_rank"), py::arg("p_prev") = c10::optional<torch::Tensor>());
-  m.def("psgd_q", &psgd_q);
+        py::arg("fuse_ef"), py::arg("max_rank"), py::arg("p_prev") = OptT(), py::arg("p_out") = OptT(),
+        py::arg("p_ctr") = OptT(), py::arg("seg_entries") = OptT(), py::arg("seg_prefix") = OptT(),
+        py::arg("seg_n") = 0, py::arg("seg_blocks") = 0, py::arg("p_cols") = (int64_t)ndp::kPKW);
+  m.def("psgd_q", &psgd_q, py::arg("geom"), py::arg("ptrs"), py::arg("items"), py::arg("p_hat"), py::arg("q_part"),
+        py::arg("max_rank"), py::arg("q_out") = OptT(), py::arg("q_ctr") = OptT(), py::arg("q_fin_max") = 1 << 30);
   m.def("psgd_orth", &psgd_orth, py::arg("geom"), py::arg("items"), py::arg("p"), py::arg("p_div"),
         py::arg("eps"), py::arg("max_rank"), py::arg("scratch"), py::arg("ctr"), py::arg("n_items_total") = -1,
         py::arg("max_spins") = -1);
   m.def("orth_coresident_cap", &ndp::orth_coresident_cap);
   m.def("psgd_update", &psgd_update, py::arg("geom"), py::arg("ptrs"), py::arg("items"), py::arg("p_hat"),
         py::arg("q_sum"), py::arg("q_div"), py::arg("q_warm"), py::arg("mode"), py::arg("lr"), py::arg("momentum"),
-        py::arg("max_rank"), py::arg("p_prev") = c10::optional<torch::Tensor>());
+        py::arg("max_rank"), py::arg("p_prev") = c10::optional<torch::Tensor>(), py::arg("r1_buf") = OptT(),
+        py::arg("r1_div") = 1.0, py::arg("r1_mom") = OptT(), py::arg("r1_x") = OptT(), py::arg("r1_g") = OptT());
   m.def("rank1_step", &rank1_step);
   m.def("seg_reduce", &seg_reduce);
   m.def("sgd_momentum", &sgd_momentum);

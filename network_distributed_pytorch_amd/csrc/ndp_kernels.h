@@ -40,8 +40,10 @@ struct MatPtrs {
 };
 
 // Work items.  One workgroup (4 waves) per item.
-struct PItem { int32_t mat, row0, k0, k1, chunk, pad[3]; };   // 64 rows x [k0,k1)
-struct QItem { int32_t mat, col0, row0, row1, chunk, pad[3]; }; // [row0,row1) x 256 cols
+// rb / cb: ordinal of the item's P row block / Q column block in the plan (the arrival counter
+// of the in-kernel split-K finish, PFin / QFin)
+struct PItem { int32_t mat, row0, k0, k1, chunk, rb, pad[2]; };   // 64 rows x [k0,k1)
+struct QItem { int32_t mat, col0, row0, row1, chunk, cb, pad[2]; }; // [row0,row1) x 256 cols
 struct UItem { int32_t mat, row0, col0, pad; };                 // 64 rows x 64 cols
 // orth: rows [row0,row1) of matrix `mat`; workgroup `wg` of `nwg`; slab0 = first item of mat
 struct OrthItem { int32_t mat, row0, row1, wg, nwg, slab0, pad[2]; };
@@ -76,11 +78,42 @@ constexpr int kSegBlockElems = 2048;  // elements per workgroup in seg_reduce
 
 // ---- launchers (powersgd.hip) --------------------------------------------------
 // p_prev (rank <= kUWideMaxRank only): lazy error feedback, e = M_prev - P_prev Qs^T formed here
+// In-kernel split-K finish of the P / Q passes: every chunk item stores its
+// partial write-through (sc1), drains, and bumps its row / column block's monotonic arrival
+// counter; the block's last arriver sums the chunk partials in chunk order (the order of the
+// seg_reduce it replaces: bitwise identical) and writes the final P / Q.  out == nullptr: leave
+// the partials for a separate seg_reduce.  P's extra blocks [n_items, grid) run a seg table (the
+// rank-1 group's pack into the comm buffer), so the P stage is ONE launch.
+struct PFin {
+  float* out;                    // final P (comm buffer, MatGeom.p_off)
+  unsigned long long* ctr;       // [n row blocks]
+  const SegEntry* seg;           // optional reduce-copy table run by the extra blocks
+  const int64_t* seg_prefix;
+  int n_seg;
+  int n_items;
+};
+struct QFin {
+  float* out;                    // final Q sums (q_memory, MatGeom.q_off)
+  unsigned long long* ctr;       // [n column blocks]
+  int max_chunks;                // matrices with more row chunks leave their partials to seg_reduce
+};
+// the rank-1 (<= 1-D) group's momentum / SGD step, run by the update pass's extra blocks
+struct R1Step {
+  const float* buf;
+  float* mom;
+  float* x;
+  float* g;
+  int64_t n;
+  float div;
+  int n_items;
+};
+
 void launch_psgd_p(const MatGeom* geom, const MatPtrs* ptrs, const PItem* items, int n_items,
                    const float* q_warm, float* p_part, int fuse_ef, int max_rank, hipStream_t s,
-                   const float* p_prev = nullptr);
+                   const float* p_prev = nullptr, PFin fin = PFin{}, int64_t n_seg_blocks = 0,
+                   int item_cols = kPKW);
 void launch_psgd_q(const MatGeom* geom, const MatPtrs* ptrs, const QItem* items, int n_items,
-                   const float* p_hat, float* q_part, int max_rank, hipStream_t s);
+                   const float* p_hat, float* q_part, int max_rank, hipStream_t s, QFin fin = QFin{});
 // partial: 2 * n_items_total * kMaxRank floats; counters: n_mats uint64 (zeroed once, never reset);
 // items may be a slice [k0, k0 + n_items) of an n_items_total list (slab0 indexes are global)
 void launch_psgd_orth(const MatGeom* geom, const OrthItem* items, int n_items, int n_mats, float* p,
@@ -97,7 +130,7 @@ constexpr unsigned kOrthMaxSpins = 1u << 25;  // ~seconds of s_sleep 2
 void launch_psgd_update(const MatGeom* geom, const MatPtrs* ptrs, const UItem* items,
                         int n_items, const float* p_hat, const float* q_sum, float q_div,
                         float* q_warm, int mode, float lr, float momentum, int max_rank,
-                        hipStream_t s, float* p_prev = nullptr);
+                        hipStream_t s, float* p_prev = nullptr, R1Step r1 = R1Step{});
 // rank-1 (<=1-D) group of the fused engine: out = buf/div; m = lam*m + out; x -= lr*(out+m)
 void launch_rank1_step(const float* buf, float div, float* mom, float* x, float* g,
                        int64_t n, float lr, float momentum, hipStream_t s);

@@ -14,9 +14,9 @@
 //    <u_i, v_j>, j >= i, taken before u_i is normalised.
 //  * Column reductions: wave butterfly (bitwise-identical in every lane) -> fixed-order LDS
 //    combine -> for nwg_i > 1 a fixed-order sum of per-workgroup partial slabs exchanged
-//    through the agent-scope release / acquire protocol of cdna_hip_programming.md §6
-//    Guideline 16 (plain stores + vmcnt drain + release fence + relaxed agent counter;
-//    poller: relaxed loads, ONE acquire fence).  Every workgroup of a matrix, and every
+//    through the sc1 form of cdna_hip_programming.md §6 Guideline 16 (write-through stores +
+//    vmcnt drain + relaxed agent counter; poller: relaxed loads; every slab read an sc1 load,
+//    so no fence: round 5's release fence wrote back the L2 at each of the r barriers).  Every workgroup of a matrix, and every
 //    rank (same plan), computes the bitwise-identical result: replicas stay consistent.
 //  * Partial slabs are double-buffered by barrier parity (a fast workgroup can be at most
 //    one barrier ahead).  Counters are never reset (no memset node per launch): every
@@ -74,16 +74,19 @@ __device__ __forceinline__ void group_sum(float (&v)[K], float* red, const OrthI
   block_sum_o<K>(v, red);
   if (it.nwg == 1) return;
   float* slab = cx.partial + ((size_t)(bar & 1) * cx.n_items + it.slab0) * kMaxRank;
+  // payload stored write-through (sc1 = relaxed agent-scope atomic store) and drained by the
+  // storing wave; every read of another workgroup's slab below is an sc1 load, so neither a
+  // release nor an acquire fence is needed (§6 Guideline 16, sc1 form).  The release fence of
+  // the plain-store form wrote back every dirty L2 line at each of the r barriers.
   if (threadIdx.x < K) {
 #pragma unroll
     for (int k = 0; k < K; ++k)
-      if ((int)threadIdx.x == k) slab[it.wg * kMaxRank + k] = v[k];
+      if ((int)threadIdx.x == k)
+        __hip_atomic_store(slab + it.wg * kMaxRank + k, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (threadIdx.x < 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_fetch_add(cx.ctr + it.mat, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long target = base + (unsigned long long)(bar + 1) * (unsigned long long)it.nwg;
     unsigned spins = 0;
@@ -95,15 +98,28 @@ __device__ __forceinline__ void group_sum(float (&v)[K], float* red, const OrthI
         break;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler order only: sc1 loads follow
+  // sc1 buffer loads (not atomics, which the compiler serialises): all K values of 4 workgroups
+  // in flight before their adds (past the slab they return 0 and are not added); the adds keep
+  // workgroup order (deterministic)
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(slab, (short)0, it.nwg * kMaxRank * 4, 0x00020000);
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    float acc = 0.f;
-    for (int w = 0; w < it.nwg; ++w) acc += slab[w * kMaxRank + k];
-    v[k] = acc;
+  for (int k = 0; k < K; ++k) v[k] = 0.f;
+  int w = 0;
+  for (; w < it.nwg; w += 4) {
+    float t[4][K];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        t[u][k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, ((w + u) * kMaxRank + k) * 4, 0, 16));
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        if (w + u < it.nwg) v[k] += t[u][k];
   }
   ++bar;
 }

@@ -18,9 +18,17 @@
 
 namespace ndp {
 
-// columns per wide P item (narrower items, 256 / 512 columns, measured slower in round 5:
-// profiles/r5/bench_psgd_pkw_ab.jsonl)
-static int64_t p_item_cols() { return kPKW; }
+// columns per wide P item: 1024 (default), 512 or 256 (NDP_PSGD_PKW, A/B).  Round 5 measured
+// narrower items slower (profiles/r5/bench_psgd_pkw_ab.jsonl) with a kernel that still looped over
+// 1024 columns (3/4 of its loads masked off); the kernel now has one instance per width.
+// Default by the plan's max rank (tools/psgd_bench.py, round 6): rank <= 4 -> 512 (ResNet-18 r=4
+// reducer 112.0 -> 106.4 µs; 256: 109.1), else 1024 (DistilBERT r=8: 676 µs; 512: 700, 256: 799).
+int64_t p_item_cols(int plan_rank) {
+  const int64_t dflt = plan_rank <= 4 ? 512 : kPKW;
+  const char* e = getenv("NDP_PSGD_PKW");
+  const int64_t v = e ? atoll(e) : dflt;
+  return (v == 256 || v == 512 || v == 1024) ? v : dflt;
+}
 
 static int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
@@ -46,7 +54,7 @@ Plan build_plan(const std::vector<std::pair<int64_t, int64_t>>& shapes, int rank
     g.vec = 0;
     g.p_off = (int32_t)p_off;
     g.q_off = (int32_t)q_off;
-    const int64_t p_rows = wide ? kPWRows : kPRows, p_k = wide ? p_item_cols() : kPK;
+    const int64_t p_rows = wide ? kPWRows : kPRows, p_k = wide ? p_item_cols(plan_rank) : kPK;
     g.p_chunks = (int32_t)cdiv(m, p_k);
     // Q split over n: 64-row chunks, but at most 64 chunks (cap the slab scratch), and
     // never more rows than the LDS tile holds.
@@ -59,7 +67,7 @@ Plan build_plan(const std::vector<std::pair<int64_t, int64_t>>& shapes, int rank
     pl.geom.push_back(g);
     pl.q_rows.push_back((int32_t)rc);
 
-    for (int64_t row0 = 0; row0 < n; row0 += p_rows)
+    for (int64_t row0 = 0; row0 < n; row0 += p_rows, ++pl.n_p_blocks)
       for (int64_t c = 0; c < g.p_chunks; ++c) {
         PItem it{};
         it.mat = (int32_t)i;
@@ -67,18 +75,24 @@ Plan build_plan(const std::vector<std::pair<int64_t, int64_t>>& shapes, int rank
         it.k0 = (int32_t)(c * p_k);
         it.k1 = (int32_t)std::min<int64_t>(m, (c + 1) * p_k);
         it.chunk = (int32_t)c;
+        it.rb = (int32_t)pl.n_p_blocks;  // arrival counter of the in-kernel split-K finish
         pl.p_items.push_back(it);
       }
-    for (int64_t c = 0; c < g.q_chunks; ++c)
-      for (int64_t col0 = 0; col0 < m; col0 += kQCols) {
+    // a column block's row chunks are consecutive in the grid, so the in-kernel finishes
+    // (last arriver per column block) are spread over the launch instead of all at its end
+    const int32_t cb0 = (int32_t)pl.n_q_blocks;
+    for (int64_t col0 = 0; col0 < m; col0 += kQCols)
+      for (int64_t c = 0; c < g.q_chunks; ++c) {
         QItem it{};
         it.mat = (int32_t)i;
         it.col0 = (int32_t)col0;
         it.row0 = (int32_t)(c * rc);
         it.row1 = (int32_t)std::min<int64_t>(n, (c + 1) * rc);
         it.chunk = (int32_t)c;
+        it.cb = cb0 + (int32_t)(col0 / kQCols);
         pl.q_items.push_back(it);
       }
+    pl.n_q_blocks += cdiv(m, kQCols);
     for (int64_t row0 = 0; row0 < n; row0 += u_rows)
       for (int64_t col0 = 0; col0 < m; col0 += u_cols) {
         UItem it{};
@@ -97,6 +111,7 @@ Plan build_plan(const std::vector<std::pair<int64_t, int64_t>>& shapes, int rank
         qp_off > (1LL << 31) - 1)
       throw std::invalid_argument("PowerSGD plan exceeds int32 offsets");
   }
+  pl.p_cols = wide ? (int32_t)p_item_cols(plan_rank) : (int32_t)kPK;
   pl.p_total = p_off;
   pl.q_total = q_off;
   pl.pp_total = pp_off;

@@ -20,7 +20,10 @@
 //    update passes read one array; the update pass fuses decompression, error feedback,
 //    momentum and the parameter update (one read-modify-write of e, m, x).
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include "ndp_kernels.h"
+#include "seg_block.h"
 
 namespace ndp {
 
@@ -225,16 +228,74 @@ __device__ __forceinline__ bool spread_writer(int lane) {
 // update's exact arithmetic (Qs = the warm-start Q it reads anyway, the same fmaf chain over
 // c), so M = g + e is bitwise the eager formula's.  p_prev = 0 (first step, after a
 // checkpoint materialised e) makes the correction an exact zero.
-template <int RQ, int NT = 0>
+// In-kernel split-K finish (PFin): the item's wave-reduced partial is stored write-through (sc1)
+// and drained, the row block's arrival counter is bumped (relaxed, agent scope: no release fence
+// is needed for sc1 payloads, and none is wanted — it would write back the L2's dirty e lines),
+// and the last arriver sums the chunk partials with sc1 loads in chunk order
+// (cdna_hip_programming.md §5 'In-launch split-K reduction', sc1 form).
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// sum_{ch < chunks} base[ch * cstride + o] in chunk order, every load an sc1 buffer load (not an
+// atomic: the compiler issues a batch of 8 before the first add — relaxed atomic loads were
+// serialised, one memory round trip per chunk).  base is wave-uniform; nbytes bounds the slabs.
+__device__ __forceinline__ float chunk_sum_sc1(const float* base, int64_t cstride, int chunks, int64_t o,
+                                               int64_t nbytes) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)nbytes, 0x00020000);
+  auto ld = [&](int ch) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (int)((ch * cstride + o) * 4), 0, 16));
+  };
+  float sum = ld(0);
+  int ch = 1;
+  for (; ch + 8 <= chunks; ch += 8) {
+    float t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = ld(ch + j);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sum += t[j];
+  }
+  if (ch < chunks) {  // the last 1..7 chunks, issued together too (loads past nbytes return 0)
+    float t[7];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) t[j] = ld(ch + j);
+#pragma unroll
+    for (int j = 0; j < 7; ++j)
+      if (ch + j < chunks) sum += t[j];
+  }
+  return sum;
+}
+
+// every wave: drain the sc1 partial stores; one lane draws the arrival ticket; true in every
+// thread of the block that drew the last of `chunks` tickets
+__device__ __forceinline__ bool last_arrival(unsigned long long* ctr, int chunks, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long old = __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = (int)((old + 1ull) % (unsigned long long)chunks == 0ull);
+  }
+  __syncthreads();
+  const bool last = *flag != 0;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler order only: the loads after are sc1
+  return last;
+}
+
+template <int RQ, int NT = 0, int NS = kPKW / 256, int SB = (RQ <= 4 ? NS : (NS < 2 ? NS : 2))>
 __global__ __launch_bounds__(256) void psgd_p_wide_kernel(const MatGeom* __restrict__ geom,
                                                           const MatPtrs* __restrict__ ptrs,
                                                           const PItem* __restrict__ items,
                                                           const float* __restrict__ q_warm,
                                                           float* __restrict__ p_part, int fuse_ef,
-                                                          const float* __restrict__ p_prev) {
-  constexpr int NS = kPKW / 256;          // 256-column slices per item
-  constexpr int SB = RQ <= 8 ? NS : 2;    // slices whose loads are in flight together
+                                                          const float* __restrict__ p_prev, PFin fin) {
+  // NS: 256-column slices per item; SB: slices whose loads are in flight together (RQ = 8
+  // with SB = 4 held 228 VGPRs = 2 waves / SIMD; SB = 2 keeps it at 3)
   constexpr int V = 4 * RQ;
+  __shared__ int last_flag;
+  if ((int)blockIdx.x >= fin.n_items) {  // rank-1 group pack (seg table), same launch
+    seg_reduce_block(fin.seg, fin.seg_prefix, fin.n_seg, (int64_t)blockIdx.x - fin.n_items);
+    return;
+  }
   const PItem it = items[blockIdx.x];
   const MatGeom g = geom[it.mat];
   const GPtrs pt = gptrs(ptrs[it.mat]);
@@ -242,7 +303,7 @@ __global__ __launch_bounds__(256) void psgd_p_wide_kernel(const MatGeom* __restr
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = g.r, n = g.n, m = g.m;
   const int arow0 = it.row0 + wave * 4;
-  if (arow0 >= n) return;  // no barriers in this kernel
+  const bool active = arow0 < n;  // inactive waves still reach the finish's barriers
   const float* Q = q_warm + g.q_off;
   const bool q4 = (r & 3) == 0 && (g.q_off & 3) == 0;
 
@@ -250,6 +311,7 @@ __global__ __launch_bounds__(256) void psgd_p_wide_kernel(const MatGeom* __restr
 #pragma unroll
   for (int v = 0; v < V; ++v) acc[v] = 0.f;
 
+  if (active) {
 #pragma unroll
   for (int s0 = 0; s0 < NS; s0 += SB) {
     // the HBM stream of SB slices first: g and e of the wave's 4 rows (combined below, once
@@ -354,13 +416,29 @@ __global__ __launch_bounds__(256) void psgd_p_wide_kernel(const MatGeom* __restr
           for (int c = 0; c < RQ; ++c) acc[i * RQ + c] = fmaf(mv[i][sb][j], qv[j][c], acc[i * RQ + c]);
     }
   }
+  }  // active
 
   wave_reduce_spread<V>(acc, lane);
-  if (!spread_writer<V>(lane)) return;
   const int idx = spread_index<V>(lane);
   const int i = idx / RQ, c = idx % RQ;
   const int a = arow0 + i;
-  if (c < r && a < n) p_part[g.pp_off + (int64_t)it.chunk * n * r + (int64_t)a * r + c] = acc[0];
+  const bool wr = active && spread_writer<V>(lane) && c < r && a < n;
+  const int chunks = g.p_chunks;
+  if (fin.out == nullptr) {  // partials for a separate seg_reduce
+    if (wr) p_part[g.pp_off + (int64_t)it.chunk * n * r + (int64_t)a * r + c] = acc[0];
+    return;
+  }
+  if (chunks == 1) {  // unsplit: the item IS the row block's P
+    if (wr) fin.out[g.p_off + (int64_t)a * r + c] = acc[0];
+    return;
+  }
+  if (wr) st_sc1(p_part + g.pp_off + (int64_t)it.chunk * n * r + (int64_t)a * r + c, acc[0]);
+  if (!last_arrival(fin.ctr + it.rb, chunks, &last_flag)) return;
+  const int rows = min(kPWRows, n - it.row0);
+  for (int t = threadIdx.x; t < rows * r; t += 256) {
+    const int64_t o = (int64_t)it.row0 * r + t;  // row-major n x r: the block's rows are contiguous
+    fin.out[g.p_off + o] = chunk_sum_sc1(p_part + g.pp_off, (int64_t)n * r, chunks, o, (int64_t)chunks * n * r * 4);
+  }
 }
 
 // ----------------------------------------------------------------------------------
@@ -375,7 +453,7 @@ __global__ __launch_bounds__(256) void psgd_q_kernel(const MatGeom* __restrict__
                                                      const MatPtrs* __restrict__ ptrs,
                                                      const QItem* __restrict__ items,
                                                      const float* __restrict__ p_hat,
-                                                     float* __restrict__ q_part) {
+                                                     float* __restrict__ q_part, QFin fin) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int CW = 16 * NCG;
   constexpr int LDP = CW + (NCG > 1 ? 16 : 0);
@@ -396,7 +474,7 @@ __global__ __launch_bounds__(256) void psgd_q_kernel(const MatGeom* __restrict__
   __syncthreads();
 
   const int b0 = it.col0 + wave * 64;
-  if (b0 >= g.m) return;
+  const bool active = b0 < g.m;  // inactive waves still reach the finish's barriers
   const int bl = b0 + 4 * (lane & 15);
   const int rsub = lane >> 4;
   const int cl = lane & 15;
@@ -436,29 +514,64 @@ __global__ __launch_bounds__(256) void psgd_q_kernel(const MatGeom* __restrict__
     }
   };
 
-  int s = 0;
-  for (; s + 16 <= nrows4; s += 16) {
-    const f32x4 m0 = load_m(s), m1 = load_m(s + 4), m2 = load_m(s + 8), m3 = load_m(s + 12);
-    consume(s, m0);
-    consume(s + 4, m1);
-    consume(s + 8, m2);
-    consume(s + 12, m3);
+  if (active) {
+    // 32-row batches, double-buffered: the next batch's 8 loads are in flight while this one is
+    // consumed (round 5 kept 4 loads in flight and paid one memory round trip per 16 rows: the
+    // 64-row ResNet items took 4 dependent trips, 2.4 TB/s)
+    constexpr int QB = 8;
+    f32x4 b0[QB], b1[QB];
+    auto load_batch = [&](int s0, f32x4 (&b)[QB]) {
+#pragma unroll
+      for (int u = 0; u < QB; ++u) b[u] = load_m(s0 + 4 * u);  // rows past nrows load 0
+    };
+    auto consume_batch = [&](int s0, const f32x4 (&b)[QB]) {
+#pragma unroll
+      for (int u = 0; u < QB; ++u)
+        if (s0 + 4 * u < nrows4) consume(s0 + 4 * u, b[u]);  // LDS rows past nrows4 are not staged
+    };
+    load_batch(0, b0);
+    for (int s0 = 0; s0 < nrows4; s0 += 2 * 4 * QB) {
+      if (s0 + 4 * QB < nrows4) load_batch(s0 + 4 * QB, b1);
+      consume_batch(s0, b0);
+      if (s0 + 4 * QB >= nrows4) break;
+      if (s0 + 8 * QB < nrows4) load_batch(s0 + 8 * QB, b0);
+      consume_batch(s0 + 4 * QB, b1);
+    }
   }
-  for (; s < nrows4; s += 4) consume(s, load_m(s));
 
-  float* dst = q_part + g.qp_off + (int64_t)it.chunk * g.m * r;
+  const int chunks = g.q_chunks;
+  // destination: the partial slab (separate seg_reduce / in-kernel finish) or, unsplit, Q itself;
+  // matrices split in more than fin.max_chunks row chunks (the DistilBERT embedding: 120) keep
+  // the separate seg_reduce — one workgroup summing them all would be the launch's long tail
+  const bool direct = fin.out != nullptr && chunks == 1;
+  const bool sc1 = fin.out != nullptr && chunks > 1 && chunks <= fin.max_chunks;
+  float* dst = direct ? fin.out + g.q_off : q_part + g.qp_off + (int64_t)it.chunk * g.m * r;
+  if (active) {
 #pragma unroll
-  for (int cg = 0; cg < NCG; ++cg) {
-    const int c = cg * 16 + cl;
-    if (c >= r) continue;
+    for (int cg = 0; cg < NCG; ++cg) {
+      const int c = cg * 16 + cl;
+      if (c >= r) continue;
 #pragma unroll
-    for (int reg = 0; reg < 4; ++reg) {
+      for (int reg = 0; reg < 4; ++reg) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int b = b0 + 4 * (4 * rsub + reg) + j;
-        if (b < g.m) dst[(int64_t)b * r + c] = acc[cg][j][reg];
+        for (int j = 0; j < 4; ++j) {
+          const int b = b0 + 4 * (4 * rsub + reg) + j;
+          if (b < g.m) {
+            if (sc1) st_sc1(dst + (int64_t)b * r + c, acc[cg][j][reg]);
+            else dst[(int64_t)b * r + c] = acc[cg][j][reg];
+          }
+        }
       }
     }
+  }
+  if (!sc1) return;
+  __syncthreads();  // every wave is done reading the P-hat tile: smem[0] may carry the flag
+  if (!last_arrival(fin.ctr + it.cb, chunks, reinterpret_cast<int*>(smem))) return;
+  const int cols = min(kQCols, g.m - it.col0);
+  for (int t = threadIdx.x; t < cols * r; t += 256) {
+    const int64_t o = (int64_t)it.col0 * r + t;  // row-major m x r: the block's columns are contiguous
+    fin.out[g.q_off + o] = chunk_sum_sc1(q_part + g.qp_off, (int64_t)g.m * r, chunks, o,
+                                         (int64_t)chunks * g.m * r * 4);
   }
 }
 
@@ -586,7 +699,19 @@ __global__ __launch_bounds__(256) void psgd_update_wide_kernel(
     const MatGeom* __restrict__ geom, const MatPtrs* __restrict__ ptrs,
     const UItem* __restrict__ items, const float* __restrict__ p_hat,
     const float* __restrict__ q_sum, float q_div, float* __restrict__ q_warm, int mode,
-    float lr, float momentum, float* __restrict__ p_prev) {
+    float lr, float momentum, float* __restrict__ p_prev, R1Step r1) {
+  if ((int)blockIdx.x >= r1.n_items) {  // the rank-1 group's step, same launch (rank1_step_kernel)
+    const int64_t stride = (int64_t)(gridDim.x - r1.n_items) * 256;
+    for (int64_t k = (int64_t)(blockIdx.x - r1.n_items) * 256 + threadIdx.x; k < r1.n; k += stride) {
+      const float o = r1.buf[k] / r1.div;
+      const float mm = __fadd_rn(__fmul_rn(r1.mom[k], momentum), o);
+      r1.mom[k] = mm;
+      const float up = o + mm;
+      r1.x[k] = fmaf(-lr, up, r1.x[k]);
+      if (r1.g) r1.g[k] = up;
+    }
+    return;
+  }
   const UItem it = items[blockIdx.x];
   const MatGeom g = geom[it.mat];
   const GPtrs pt = gptrs(ptrs[it.mat]);
@@ -736,28 +861,36 @@ static inline int ncg_for(int max_rank) {
   return c <= 1 ? 1 : (c == 2 ? 2 : 4);
 }
 
+template <int RQ, int NT>
+static void launch_p_wide(int item_cols, unsigned grid, hipStream_t s, const MatGeom* geom, const MatPtrs* ptrs,
+                          const PItem* items, const float* q_warm, float* p_part, int fuse_ef, const float* p_prev,
+                          PFin fin) {
+  if (item_cols == 256)
+    hipLaunchKernelGGL((psgd_p_wide_kernel<RQ, NT, 1>), dim3(grid), dim3(256), 0, s, geom, ptrs, items, q_warm, p_part,
+                       fuse_ef, p_prev, fin);
+  else if (item_cols == 512)
+    hipLaunchKernelGGL((psgd_p_wide_kernel<RQ, NT, 2>), dim3(grid), dim3(256), 0, s, geom, ptrs, items, q_warm, p_part,
+                       fuse_ef, p_prev, fin);
+  else
+    hipLaunchKernelGGL((psgd_p_wide_kernel<RQ, NT, 4>), dim3(grid), dim3(256), 0, s, geom, ptrs, items, q_warm, p_part,
+                       fuse_ef, p_prev, fin);
+}
+
 void launch_psgd_p(const MatGeom* geom, const MatPtrs* ptrs, const PItem* items, int n_items,
                    const float* q_warm, float* p_part, int fuse_ef, int max_rank,
-                   hipStream_t s, const float* p_prev) {
-  if (n_items <= 0) return;
-  // the item shape follows the plan's max rank (plan.cpp): wide 16 x kPKW items up to rank 16
-  if (max_rank <= 4) {
-    // non-temporal g / e loads (read once per step): ResNet-18 r=4 batch 64 0.8306 / 0.8294 ->
-    // 0.8245 / 0.8233 ms (profiles/r5/bench_psgd_nt.jsonl)
-    hipLaunchKernelGGL((psgd_p_wide_kernel<4, 1>), dim3(n_items), dim3(256), 0, s, geom, ptrs, items, q_warm, p_part,
-                       fuse_ef, p_prev);
-    return;
-  }
-  if (max_rank <= 8) {
-    hipLaunchKernelGGL((psgd_p_wide_kernel<8, 1>), dim3(n_items), dim3(256), 0, s, geom, ptrs, items, q_warm, p_part,
-                       fuse_ef, p_prev);
-    return;
-  }
-  if (max_rank <= kUWideMaxRank) {
-    hipLaunchKernelGGL(psgd_p_wide_kernel<kUWideMaxRank>, dim3(n_items), dim3(256), 0, s, geom, ptrs, items, q_warm,
-                       p_part, fuse_ef, p_prev);
-    return;
-  }
+                   hipStream_t s, const float* p_prev, PFin fin, int64_t n_seg_blocks, int item_cols) {
+  if (n_items <= 0 && n_seg_blocks <= 0) return;
+  fin.n_items = n_items;
+  if (fin.seg == nullptr) n_seg_blocks = 0;
+  const unsigned grid = (unsigned)(n_items + n_seg_blocks);
+  // the item shape follows the plan (plan.cpp): wide 16 x item_cols items up to rank 16;
+  // non-temporal g / e loads (read once per step): ResNet-18 r=4 batch 64 0.8306 / 0.8294 ->
+  // 0.8245 / 0.8233 ms (profiles/r5/bench_psgd_nt.jsonl)
+  if (max_rank <= 4) return launch_p_wide<4, 1>(item_cols, grid, s, geom, ptrs, items, q_warm, p_part, fuse_ef, p_prev, fin);
+  if (max_rank <= 8) return launch_p_wide<8, 1>(item_cols, grid, s, geom, ptrs, items, q_warm, p_part, fuse_ef, p_prev, fin);
+  if (max_rank <= kUWideMaxRank)
+    return launch_p_wide<kUWideMaxRank, 0>(item_cols, grid, s, geom, ptrs, items, q_warm, p_part, fuse_ef, p_prev, fin);
+  if (fin.out != nullptr || n_seg_blocks > 0) return;  // the caller checks: wide plans only (bindings.cpp)
   const int ncg = ncg_for(max_rank);
   const size_t lds = sizeof(float) * 16 * ncg * (kPK + 4);
   if (ncg == 4) allow_lds(reinterpret_cast<const void*>(psgd_p_kernel<4>), lds);
@@ -773,7 +906,7 @@ void launch_psgd_p(const MatGeom* geom, const MatPtrs* ptrs, const PItem* items,
 }
 
 void launch_psgd_q(const MatGeom* geom, const MatPtrs* ptrs, const QItem* items, int n_items,
-                   const float* p_hat, float* q_part, int max_rank, hipStream_t s) {
+                   const float* p_hat, float* q_part, int max_rank, hipStream_t s, QFin fin) {
   if (n_items <= 0) return;
   const int ncg = ncg_for(max_rank);
   const int ldp = 16 * ncg + (ncg > 1 ? 16 : 0);
@@ -783,36 +916,42 @@ void launch_psgd_q(const MatGeom* geom, const MatPtrs* ptrs, const QItem* items,
   // 0.779 / 0.783 ms with the non-temporal slab sums (profiles/r5/bench_psgd_nt.jsonl)
   if (ncg == 1)
     hipLaunchKernelGGL((psgd_q_kernel<1, true>), dim3(n_items), dim3(256), lds, s, geom, ptrs, items,
-                       p_hat, q_part);
+                       p_hat, q_part, fin);
   else if (ncg == 2)
     hipLaunchKernelGGL(psgd_q_kernel<2>, dim3(n_items), dim3(256), lds, s, geom, ptrs, items,
-                       p_hat, q_part);
+                       p_hat, q_part, fin);
   else
     hipLaunchKernelGGL(psgd_q_kernel<4>, dim3(n_items), dim3(256), lds, s, geom, ptrs, items,
-                       p_hat, q_part);
+                       p_hat, q_part, fin);
 }
 
 void launch_psgd_update(const MatGeom* geom, const MatPtrs* ptrs, const UItem* items,
                         int n_items, const float* p_hat, const float* q_sum, float q_div,
                         float* q_warm, int mode, float lr, float momentum, int max_rank,
-                        hipStream_t s, float* p_prev) {
-  if (n_items <= 0) return;
+                        hipStream_t s, float* p_prev, R1Step r1) {
+  r1.n_items = n_items;
+  int64_t r1_blocks = r1.n > 0 ? std::min<int64_t>((r1.n + 255) / 256, 512) : 0;
+  if (n_items <= 0 && r1_blocks <= 0) return;
+  const unsigned grid = (unsigned)(n_items + r1_blocks);
   // the item tiles follow the plan's max rank (plan.cpp): wide 16 x 256 tiles up to rank 16
   // momentum through non-temporal loads / stores (touched once per step, 4 B per parameter): it
   // no longer evicts the next forward's weights and activations from the caches — ResNet-18 r=4
   // batch 64 0.8245 / 0.8233 -> 0.7896 / 0.7855 ms, batch 512 unchanged (1.4905 / 1.4930)
   if (max_rank <= 4)
-    hipLaunchKernelGGL((psgd_update_wide_kernel<4, 2>), dim3(n_items), dim3(256), 0, s, geom, ptrs,
-                       items, p_hat, q_sum, q_div, q_warm, mode, lr, momentum, p_prev);
+    hipLaunchKernelGGL((psgd_update_wide_kernel<4, 2>), dim3(grid), dim3(256), 0, s, geom, ptrs,
+                       items, p_hat, q_sum, q_div, q_warm, mode, lr, momentum, p_prev, r1);
   else if (max_rank <= 8)
-    hipLaunchKernelGGL((psgd_update_wide_kernel<8, 2>), dim3(n_items), dim3(256), 0, s, geom, ptrs,
-                       items, p_hat, q_sum, q_div, q_warm, mode, lr, momentum, p_prev);
+    hipLaunchKernelGGL((psgd_update_wide_kernel<8, 2>), dim3(grid), dim3(256), 0, s, geom, ptrs,
+                       items, p_hat, q_sum, q_div, q_warm, mode, lr, momentum, p_prev, r1);
   else if (max_rank <= kUWideMaxRank)
-    hipLaunchKernelGGL(psgd_update_wide_kernel<kUWideMaxRank>, dim3(n_items), dim3(256), 0, s,
-                       geom, ptrs, items, p_hat, q_sum, q_div, q_warm, mode, lr, momentum, p_prev);
-  else
-    hipLaunchKernelGGL(psgd_update_kernel, dim3(n_items), dim3(256), 0, s, geom, ptrs, items,
-                       p_hat, q_sum, q_div, q_warm, mode, lr, momentum);
+    hipLaunchKernelGGL(psgd_update_wide_kernel<kUWideMaxRank>, dim3(grid), dim3(256), 0, s,
+                       geom, ptrs, items, p_hat, q_sum, q_div, q_warm, mode, lr, momentum, p_prev, r1);
+  else {
+    if (n_items > 0)
+      hipLaunchKernelGGL(psgd_update_kernel, dim3(n_items), dim3(256), 0, s, geom, ptrs, items,
+                         p_hat, q_sum, q_div, q_warm, mode, lr, momentum);
+    if (r1.n > 0) launch_rank1_step(r1.buf, r1.div, r1.mom, r1.x, r1.g, r1.n, lr, momentum, s);
+  }
 }
 
 void launch_rank1_step(const float* buf, float div, float* mom, float* x, float* g, int64_t n,

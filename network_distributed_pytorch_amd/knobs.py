@@ -32,6 +32,7 @@ FUSIONS = {
     "tgemm": "strided / tabled MFMA GEMM convs for 1x1 layers (ops/tgconv.py)",
     "tuned_gemms": "hipBLASLt algorithm table for the Toeplitz GEMMs (ops/gemm_tuning.py)",
     "lazy_ef": "PowerSGD error feedback formed in the next P pass (parallel/powersgd.py)",
+    "psgd_fin": "PowerSGD P / Q split-K sums, rank-1 pack and rank-1 step inside the P / Q / update launches",
     "defer_uploads": "capture-safe table uploads batched per graph (utils/graph.py)",
     "fused_ce": "native softmax cross-entropy (ops/loss.py)",
     "fused_ln": "native residual add + LayerNorm (+ dropout) (ops/layernorm.py)",

@@ -226,6 +226,13 @@ class SegPlan:
         upload(self._prefix, prefix)
         self._n_ent, self._n_blocks = int(n_ent), int(n_blocks)
 
+    def table(self):
+        """(entries, prefix, n_entries, n_blocks) of the device table, for a kernel that runs the
+        plan in its own launch (the PowerSGD P pass's rank-1 pack); None when there is nothing to do."""
+        if not self.specs or self.device.type != "cuda" or not self._n_ent:
+            return None
+        return self._ent, self._prefix, self._n_ent, self._n_blocks
+
     def run(self) -> None:
         if not self.specs:
             return

@@ -170,6 +170,13 @@ class _PlanBuffers:
             self.ptrs = torch.zeros(nb, dtype=torch.uint8, device=device)
             self._bind_key = None
             self.q_seg = SegPlan(self.q_seg_specs(0, len(shapes)), device)
+            # in-kernel split-K finish of P / Q (csrc/powersgd.hip PFin / QFin): monotonic arrival
+            # counters, one per P row block / Q column block (zeroed once, never reset)
+            self.p_cols = int(d["p_cols"])  # columns per P item
+            self.p_ctr = torch.zeros(max(1, d["n_p_blocks"]), dtype=torch.int64, device=device)
+            self.q_ctr = torch.zeros(max(1, d["n_q_blocks"]), dtype=torch.int64, device=device)
+            self._q_seg_fused = SegPlan(self.q_seg_specs(0, len(shapes), fused=True), device)
+            self.fused = self.max_rank <= _LAZY_MAX_RANK and fusion_on("psgd_fin")
 
     # -- per-matrix-range views (a PowerSGD overlap group = matrices [lo, hi)) ----------------
     def p_seg_specs(self, lo: int = 0, hi: Optional[int] = None):
@@ -178,10 +185,13 @@ class _PlanBuffers:
                  self.p_chunks[i], n * r, 1.0)
                 for i, ((n, m), r) in enumerate(zip(self.shapes, self.ranks)) if lo <= i < hi]
 
-    def q_seg_specs(self, lo: int, hi: int):
+    def q_seg_specs(self, lo: int, hi: int, fused: bool = False):
+        """Split-K sums of Q for matrices [lo, hi); ``fused``: only those the Q kernel does not
+        finish itself (more than ``Q_FIN_MAX`` row chunks)."""
         return [(self.q_part[self.qp_offs[i]:], self.q_memory[self.q_offs[i]: self.q_offs[i] + m * r],
                  self.q_chunks[i], m * r, 1.0)
-                for i, ((n, m), r) in enumerate(zip(self.shapes, self.ranks)) if lo <= i < hi]
+                for i, ((n, m), r) in enumerate(zip(self.shapes, self.ranks))
+                if lo <= i < hi and (not fused or self.q_chunks[i] > Q_FIN_MAX)]
 
     def items(self, kind: str, lo: int, hi: int) -> torch.Tensor:
         """Byte slice of a work-item table covering matrices [lo, hi)."""
@@ -197,6 +207,37 @@ class _PlanBuffers:
     def q_range(self, lo: int, hi: int) -> Tuple[int, int]:
         end = self.q_offs[hi - 1] + self.shapes[hi - 1][1] * self.ranks[hi - 1]
         return self.q_offs[lo], end
+
+    def run_p(self, items: torch.Tensor, fuse_ef: bool, p_prev: Optional[torch.Tensor] = None,
+              seg: Optional[SegPlan] = None, p_seg: Optional[SegPlan] = None):
+        """P = M Q for the matrices of ``items`` (+ the rank-1 pack ``seg``): one launch when the
+        split-K sums run in-kernel (``fused``), else the kernel + ``p_seg`` (sums and pack)."""
+        X = ext()
+        if not self.fused:
+            if self.shapes:
+                X.psgd_p(self.geom, self.ptrs, items, self.q_warm, self.p_part, fuse_ef, self.max_rank, p_prev,
+                         p_cols=self.p_cols)
+            if p_seg is not None:
+                p_seg.run()
+            return
+        t = seg.table() if seg is not None else None
+        if not self.shapes and t is None:
+            return
+        kw = dict(seg_entries=t[0], seg_prefix=t[1], seg_n=t[2], seg_blocks=t[3]) if t is not None else {}
+        X.psgd_p(self.geom, self.ptrs, items, self.q_warm, self.p_part, fuse_ef, self.max_rank, p_prev,
+                 p_out=self.comm_buf, p_ctr=self.p_ctr, p_cols=self.p_cols, **kw)
+
+    def run_q(self, items: torch.Tensor, q_seg: SegPlan, q_seg_fused: Optional[SegPlan] = None):
+        """Q = M^T P-hat into q_memory: split-K sums in-kernel when ``fused`` (+ ``q_seg_fused`` for
+        the matrices with more than Q_FIN_MAX row chunks), else + ``q_seg``."""
+        X = ext()
+        if self.fused:
+            X.psgd_q(self.geom, self.ptrs, items, self.comm_buf, self.q_part, self.max_rank,
+                     q_out=self.q_memory, q_ctr=self.q_ctr, q_fin_max=Q_FIN_MAX)
+            (self._q_seg_fused if q_seg_fused is None else q_seg_fused).run()
+        else:
+            X.psgd_q(self.geom, self.ptrs, items, self.comm_buf, self.q_part, self.max_rank)
+            q_seg.run()
 
     def orth(self, p_div: float, eps: float, items: Optional[torch.Tensor] = None, max_spins: int = -1):
         """P-hat = MGS(P / p_div) for every matrix (or a group's item slice), one launch."""
@@ -316,7 +357,7 @@ class PowerSGDReducer(Reducer):
             rows.append(row)
             vec.append(_vec_ok(mm, row))
         B.bind(rows, vec)
-        specs = B.p_seg_specs()
+        specs = [] if B.fused else B.p_seg_specs()  # fused: the P launch sums its slabs itself
         off = 0
         for t, _, _ in rank1:
             specs.append((t.reshape(-1), B.rank1_buf[off: off + t.numel()], 1, 0, 1.0))
@@ -338,14 +379,11 @@ class PowerSGDReducer(Reducer):
         B = self._buf
         X = ext()
         self._bind(high, rank1)
-        if B.shapes:
-            X.psgd_p(B.geom, B.ptrs, B.p_items, B.q_warm, B.p_part, False, B.max_rank)
-        self._p_seg.run()                                   # P split-K sum + rank-1 pack
+        B.run_p(B.p_items, False, seg=self._p_seg, p_seg=self._p_seg)   # P (+ split-K sum) + rank-1 pack
         self.comm.all_reduce(B.comm_buf)                    # reducer.py:126 + :132 fused
         if B.shapes:
             B.orth(float(N), self.eps)
-            X.psgd_q(B.geom, B.ptrs, B.q_items, B.comm_buf, B.q_part, B.max_rank)
-            B.q_seg.run()
+            B.run_q(B.q_items, B.q_seg)
             self.comm.all_reduce(B.q_memory)                # reducer.py:145
             X.psgd_update(B.geom, B.ptrs, B.u_items, B.comm_buf, B.q_memory, float(N),
                           B.q_warm, 0, 0.0, 0.0, B.max_rank)
@@ -380,6 +418,9 @@ class PowerSGDReducer(Reducer):
 
 
 _LAZY_MAX_RANK = 16  # csrc/ndp_kernels.h kUWideMaxRank: the wide P / update kernels
+# Q split-K chunks the Q kernel's last arriver sums itself; taller matrices (DistilBERT's 30522-row
+# embedding: 120 chunks) keep a seg_reduce launch, which spreads that sum over the whole device
+Q_FIN_MAX = int(os.environ.get("NDP_QFIN_MAX", "32"))
 
 
 class _Group:
@@ -395,6 +436,7 @@ class _Group:
         self.key = None
         self.p_seg: Optional[SegPlan] = None
         self.q_seg: Optional[SegPlan] = None
+        self.q_seg_fused: Optional[SegPlan] = None
 
 
 class PowerSGDOptimizer:
@@ -543,6 +585,8 @@ class PowerSGDOptimizer:
             g = _Group(gi, lo, hi, self.high[lo:hi])
             g.p_seg = SegPlan([], self.device, capacity=hi - lo + 1)
             g.q_seg = SegPlan(self.buf.q_seg_specs(lo, hi), self.device)
+            if self.buf.native:
+                g.q_seg_fused = SegPlan(self.buf.q_seg_specs(lo, hi, fused=True), self.device)
             self.groups.append(g)
             for p in g.params:
                 self._group_of[id(p)] = g
@@ -598,12 +642,10 @@ class PowerSGDOptimizer:
         pp = self.p_prev if self.lazy_ef else None
 
         def pipeline():
-            X.psgd_p(B.geom, B.ptrs, B.items("p", g.lo, g.hi), B.q_warm, B.p_part, True, B.max_rank, pp)
-            g.p_seg.run()
+            B.run_p(B.items("p", g.lo, g.hi), True, pp, p_seg=g.p_seg)
             self.comm.all_reduce(B.comm_buf[p0:p1])                       # reducer.py:126 (group g)
             B.orth(float(N), self.eps, B.items("orth", g.lo, g.hi), spins)
-            X.psgd_q(B.geom, B.ptrs, B.items("q", g.lo, g.hi), B.comm_buf, B.q_part, B.max_rank)
-            g.q_seg.run()
+            B.run_q(B.items("q", g.lo, g.hi), g.q_seg, g.q_seg_fused)
             self.comm.all_reduce(B.q_memory[q0:q1])                       # reducer.py:145 (group g)
             X.psgd_update(B.geom, B.ptrs, B.items("u", g.lo, g.hi), B.comm_buf, B.q_memory, float(N),
                           B.q_warm, mode, lr, mom, B.max_rank, pp)
@@ -693,14 +735,16 @@ class PowerSGDOptimizer:
             rows.append(row)
             vec.append(_vec_ok(m, row))
         B.bind(rows, vec)
-        specs = B.p_seg_specs()
-        outs = []
+        pack, outs = [], []
         for p in self.rank1:
             s = self.offsets[id(p)] - self.r1_start
-            specs.append((gmap[id(p)].view(-1), B.rank1_buf[s: s + p.numel()], 1, 0, 1.0))
+            pack.append((gmap[id(p)].view(-1), B.rank1_buf[s: s + p.numel()], 1, 0, 1.0))
             if self.write_grad:
                 outs.append((self.r1_upd[s: s + p.numel()], gmap[id(p)].view(-1), 1, 0, 1.0))
-        self._p_seg.set(specs)
+        if B.fused:  # the P launch sums its split-K slabs itself and packs the rank-1 group
+            self._r1_pack.set(pack)
+        else:
+            self._p_seg.set(B.p_seg_specs() + pack)
         self._r1_out.set(outs)
         self._grad_key = key
 
@@ -766,10 +810,8 @@ class PowerSGDOptimizer:
         if not self.native:
             return
         self._bind()
-        if B.shapes:
-            ext().psgd_p(B.geom, B.ptrs, B.p_items, B.q_warm, B.p_part, True, B.max_rank,
-                         self.p_prev if self.lazy_ef else None)
-        self._p_seg.run()                                      # P split-K sum + rank-1 pack
+        B.run_p(B.p_items, True, self.p_prev if self.lazy_ef else None,   # P (+ split-K sum + rank-1 pack)
+                seg=self._r1_pack, p_seg=self._p_seg)
 
     @torch.no_grad()
     def comm_p(self):
@@ -780,10 +822,8 @@ class PowerSGDOptimizer:
     def phase_q(self):
         B = self.buf
         if self.native and B.shapes:
-            X = ext()
             B.orth(float(self.comm.world_size), self.eps, max_spins=self.orth_max_spins)
-            X.psgd_q(B.geom, B.ptrs, B.q_items, B.comm_buf, B.q_part, B.max_rank)
-            B.q_seg.run()
+            B.run_q(B.q_items, B.q_seg)
 
     @torch.no_grad()
     def comm_q(self):
@@ -796,12 +836,19 @@ class PowerSGDOptimizer:
         N = self.comm.world_size
         if self.native:
             X = ext()
-            if B.shapes:
+            r1 = slice(self.r1_start, self.arena_numel)
+            if B.shapes and B.fused and self.r1_numel:  # the rank-1 step rides in the update launch
+                X.psgd_update(B.geom, B.ptrs, B.u_items, B.comm_buf, B.q_memory, float(N), B.q_warm,
+                              2 if self.write_grad else 1, self.lr, self.momentum, B.max_rank,
+                              self.p_prev if self.lazy_ef else None, r1_buf=B.rank1_buf, r1_div=float(N),
+                              r1_mom=self.m[r1], r1_x=self.x[r1], r1_g=self.r1_upd if self.write_grad else None)
+                if self.write_grad:
+                    self._r1_out.run()
+            elif B.shapes:
                 X.psgd_update(B.geom, B.ptrs, B.u_items, B.comm_buf, B.q_memory, float(N), B.q_warm,
                               2 if self.write_grad else 1, self.lr, self.momentum, B.max_rank,
                               self.p_prev if self.lazy_ef else None)
-            if self.r1_numel:
-                r1 = slice(self.r1_start, self.arena_numel)
+            if self.r1_numel and not (B.shapes and B.fused):
                 X.rank1_step(B.rank1_buf, float(N), self.m[r1], self.x[r1],
                              self.r1_upd if self.write_grad else None, self.lr, self.momentum)
                 if self.write_grad:
