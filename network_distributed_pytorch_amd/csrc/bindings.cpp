@@ -961,7 +961,7 @@ py::tuple tg_plan(const std::vector<int64_t>& geom, int64_t B) {
   const ndp::ConvGeom g = conv_geom(geom);
   const int cls = ndp::tg_class(g);
   const int64_t ny = B * g.Co * g.OH * g.OW, nx = B * g.C * g.H * g.W;
-  const int64_t nw = cls == ndp::TG_POINTWISE ? (int64_t)g.Co * g.C : (int64_t)g.Co * g.OH * g.OW * g.C * g.H * g.W;
+  const int64_t nw = (int64_t)g.Co * g.C;
   // split-K slab sums run on float4: every output must hold a multiple of 4 floats
   if (cls < 0 || B <= 0 || ny % 4 || nx % 4 || nw % 4) return py::make_tuple(-1, 1, 1, 1);
   // tgemm addresses its operands with 32-bit byte offsets of raw buffer descriptors
@@ -980,9 +980,7 @@ py::dict tg_describe(const std::vector<int64_t>& geom, int64_t B, int64_t dir) {
   py::dict d;
   d["am"] = idx(a.am); d["ak"] = idx(a.ak); d["bk"] = idx(a.bk); d["bn"] = idx(a.bn);
   d["cm"] = idx(a.cm); d["cn"] = idx(a.cn);
-  d["M"] = a.M; d["N"] = a.N; d["K"] = a.K; d["slab"] = a.slab; d["gather"] = a.gather;
-  std::vector<int> tab(a.tab, a.tab + 64);
-  d["tab"] = tab;
+  d["M"] = a.M; d["N"] = a.N; d["K"] = a.K; d["slab"] = a.slab;
   d["akf"] = akf; d["bnf"] = bnf;
   d["splits"] = ndp::tg_splits(g, (int)B, (int)dir);
   return d;
@@ -1039,8 +1037,7 @@ int64_t tg_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, const std:
   return left;
 }
 
-// out: dW [Co, C, 1, 1] (pointwise) or dWbig^T [Co*OH*OW, C*H*W] (small map); returns the
-// number of slabs left in part (defer, pointwise only) or 1
+// out: dW [Co, C, 1, 1]; returns the number of slabs left in part (defer) or 1
 int64_t tg_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor out, const std::vector<int64_t>& geom,
                  c10::optional<torch::Tensor> part, bool defer) {
   const ndp::ConvGeom g = conv_geom(geom);
@@ -1048,12 +1045,11 @@ int64_t tg_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor out, const std
   conv_check(x, "x", B, g.C, g.H, g.W);
   conv_check(dy, "dy", B, g.Co, g.OH, g.OW);
   check_f32(out, "out");
-  const bool pw = ndp::tg_class(g) == ndp::TG_POINTWISE;
-  const int64_t n = pw ? (int64_t)g.Co * g.C : (int64_t)g.Co * g.OH * g.OW * g.C * g.H * g.W;
+  const int64_t n = (int64_t)g.Co * g.C;
   TORCH_CHECK(out.numel() == n, "tg_wgrad: out must hold ", n, " floats");
   float* pp = tg_part(part, ndp::tg_splits(g, B, 2), n, "tg_wgrad");
   const int left = ndp::launch_tg_wgrad(x.data_ptr<float>(), dy.data_ptr<float>(), out.data_ptr<float>(), B, g, pp,
-                                        cur_stream(), defer && pw);
+                                        cur_stream(), defer);
   check_launch("launch_tg_wgrad");
   return left;
 }

@@ -373,9 +373,8 @@ struct TgIndex {
   int64_t so, si;
   int32_t sh, pad;
 };
-// C[m, n] (+)= sum_k A[m, k] B[k, n];  A(m,k) = a[am(m) + ak(k)], B(k,n) = b[bk(k) + bn(n)] or,
-// gathered, b[(k >> bk.sh) * bk.so + (n >> bn.sh) * bn.so + tab[(k & kmask) << bn.sh | (n & nmask)]]
-// (tab < 0: zero); C(m,n) = c[cm(m) + cn(n)]; split z writes part + z * slab when part != null
+// C[m, n] (+)= sum_k A[m, k] B[k, n];  A(m,k) = a[am(m) + ak(k)], B(k,n) = b[bk(k) + bn(n)];
+// C(m,n) = c[cm(m) + cn(n)]; split z writes part + z * slab when part != null
 struct TgArgs {
   const float* a;
   const float* b;
@@ -385,11 +384,8 @@ struct TgArgs {
   TgIndex am, ak, bk, bn, cm, cn;
   int32_t M, N, K, kchunk;
   int64_t slab;
-  int32_t gather, pad;
-  int8_t tab[64];
 };
-constexpr int TG_POINTWISE = 0;  // 1x1 stride-1, power-of-two map
-constexpr int TG_SMALL = 1;      // input map <= 16, output map <= 4 pixels (powers of two)
+constexpr int TG_POINTWISE = 0;  // 1x1 stride-1, power-of-two map of >= 2 pixels
 int tg_class(const ConvGeom& g);
 // the GEMM description of direction dir (pointers null) + the load mappings of its launch
 TgArgs tg_args(const ConvGeom& g, int B, int dir, bool* akf, bool* bnf);

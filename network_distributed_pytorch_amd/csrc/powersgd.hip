@@ -464,15 +464,6 @@ __global__ __launch_bounds__(256) void psgd_q_kernel(const MatGeom* __restrict__
   const int r = g.r;
   const int nrows = it.row1 - it.row0;
   const int nrows4 = (nrows + 3) & ~3;
-  const float* P = p_hat + g.p_off + (int64_t)it.row0 * r;
-  for (int idx = tid; idx < nrows4 * CW; idx += 256) {
-    const int a = idx / CW, c = idx - (idx / CW) * CW;
-    float v = 0.f;
-    if (a < nrows && c < r) v = P[(int64_t)a * r + c];
-    smem[a * LDP + c] = v;
-  }
-  __syncthreads();
-
   const int b0 = it.col0 + wave * 64;
   const bool active = b0 < g.m;  // inactive waves still reach the finish's barriers
   const int bl = b0 + 4 * (lane & 15);
@@ -480,6 +471,16 @@ __global__ __launch_bounds__(256) void psgd_q_kernel(const MatGeom* __restrict__
   const int cl = lane & 15;
   const float NDP_GLOBAL* Mb = pt.mread + (int64_t)it.row0 * g.m;
 
+  const float* P = p_hat + g.p_off + (int64_t)it.row0 * r;
+  auto stage_p = [&]() {
+    for (int idx = tid; idx < nrows4 * CW; idx += 256) {
+      const int a = idx / CW, c = idx - (idx / CW) * CW;
+      float v = 0.f;
+      if (a < nrows && c < r) v = P[(int64_t)a * r + c];
+      smem[a * LDP + c] = v;
+    }
+    __syncthreads();
+  };
   f32x4 acc[NCG][4];
 #pragma unroll
   for (int cg = 0; cg < NCG; ++cg)
@@ -519,7 +520,7 @@ __global__ __launch_bounds__(256) void psgd_q_kernel(const MatGeom* __restrict__
     // consumed (round 5 kept 4 loads in flight and paid one memory round trip per 16 rows: the
     // 64-row ResNet items took 4 dependent trips, 2.4 TB/s)
     constexpr int QB = 8;
-    f32x4 b0[QB], b1[QB];
+    f32x4 bufa[QB], bufb[QB];
     auto load_batch = [&](int s0, f32x4 (&b)[QB]) {
 #pragma unroll
       for (int u = 0; u < QB; ++u) b[u] = load_m(s0 + 4 * u);  // rows past nrows load 0
@@ -529,14 +530,18 @@ __global__ __launch_bounds__(256) void psgd_q_kernel(const MatGeom* __restrict__
       for (int u = 0; u < QB; ++u)
         if (s0 + 4 * u < nrows4) consume(s0 + 4 * u, b[u]);  // LDS rows past nrows4 are not staged
     };
-    load_batch(0, b0);
+    load_batch(0, bufa);
+    if (4 * QB < nrows4) load_batch(4 * QB, bufb);
+    stage_p();  // the P-hat tile is staged while the first two batches of M are in flight
     for (int s0 = 0; s0 < nrows4; s0 += 2 * 4 * QB) {
-      if (s0 + 4 * QB < nrows4) load_batch(s0 + 4 * QB, b1);
-      consume_batch(s0, b0);
+      if (s0 > 0 && s0 + 4 * QB < nrows4) load_batch(s0 + 4 * QB, bufb);
+      consume_batch(s0, bufa);
       if (s0 + 4 * QB >= nrows4) break;
-      if (s0 + 8 * QB < nrows4) load_batch(s0 + 8 * QB, b0);
-      consume_batch(s0 + 4 * QB, b1);
+      if (s0 + 8 * QB < nrows4) load_batch(s0 + 8 * QB, bufa);
+      consume_batch(s0 + 4 * QB, bufb);
     }
+  } else {
+    stage_p();  // every wave reaches the staging barrier
   }
 
   const int chunks = g.q_chunks;

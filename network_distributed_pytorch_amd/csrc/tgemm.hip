@@ -8,21 +8,13 @@
 //      forward  Y[co, (b,p)]  = sum_c  W[co, c]  X[c, (b,p)]        M = Co, N = B*HW, K = C
 //      grad-x   dX[c, (b,p)]  = sum_co W[co, c]  dY[co, (b,p)]      M = C,  N = B*HW, K = Co
 //      grad-W   dW[co, c]     = sum_(b,p) dY[co, (b,p)] X[c, (b,p)] M = Co, N = C,    K = B*HW
-//  * SMALL MAP ("Toeplitz" form without materialising W_big): any KHxKW / stride / pad conv
-//    with an input map of <= 16 and an output map of <= 4 pixels (ResNet layer3 / layer4 on
-//    32x32 inputs).  With T = KH*KW and tap(ipix, opix) the kernel tap joining an input and an
-//    output pixel (-1: none),
-//      forward  Y[b, (co,o)] = sum_(c,i) X[b, (c,i)] * W[co, c, tap(i, o)]
-//      grad-x   dX[b, (c,i)] = sum_(co,o) dY[b, (co,o)] * W[co, c, tap(i, o)]
-//    the weight operand is GATHERED from W through a <= 64-entry tap table held in the kernel
-//    arguments (no W_big expand launch, no W_big buffer, no zero MACs beyond the table's);
-//      grad-W   dWbig^T[(co,o), (c,i)] = sum_b dY[b, (co,o)] X[b, (c,i)]
-//    folded into dW by the existing deterministic fold (conv.hip toeplitz_fold_many,
-//    batched per backward by ops/gradfinish.py).
+//  (Round 3-5 also carried a SMALL-MAP family here — the Toeplitz product of ResNet layer3 /
+//  layer4 with the weight gathered through a tap table.  It measured 0.46-0.72x the hipBLASLt
+//  Toeplitz GEMMs, stayed off by default and was deleted in round 6: profiles/r3/tg_bench.md.)
 //
-// One kernel serves all six: C[m, n] = sum_k A[m, k] B[k, n] with every operand index
+// One kernel serves all three: C[m, n] = sum_k A[m, k] B[k, n] with every operand index
 // split as (i >> sh) * so + (i & (2^sh - 1)) * si — NCHW's (image, pixel) pairs are such
-// composites when the map is a power of two — and an optional tap-table gather for B.
+// composites when the map is a power of two.
 // Tiles: 64 x 64 x 32, 4 waves of 32 x 32 (one f32x16 accumulator each), operands staged
 // in LDS as [m][k] / [n][k] (k contiguous, padded rows: b128 fragment reads), register
 // double buffering: the global loads of tile t+1 are
@@ -79,10 +71,10 @@ __device__ __forceinline__ float vget(const typename VecT<W>::type& v, int j) {
 // 32 x 32 (64 x 64 x 32: one tile per wave; 128 x 128 x 16: 2 x 2 tiles per wave, one LDS read
 // per MFMA instead of two, half the global-load instructions per FLOP).
 // WA / WB: elements per global load of A / B along the operand's unit-stride index (4 =
-// one 16-B load; the host checks contiguity, alignment and extents); GATHER implies WB = 1
+// one 16-B load; the host checks contiguity, alignment and extents)
 // D: register prefetch slots.  The loads of tile t+1 are issued D-1 k-steps before its LDS
 // store, so D-1 MFMA phases (~1024 cycles each at one wave per SIMD) cover the memory latency.
-template <int TBM, int TBN, int TBK, bool AKF, bool BNF, bool GATHER, int WA, int WB, int D>
+template <int TBM, int TBN, int TBK, bool AKF, bool BNF, int WA, int WB, int D>
 __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
   typedef typename VecT<WA>::type VA;
   typedef typename VecT<WB>::type VB;
@@ -111,13 +103,11 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
   // per-element part and a per-tile part that is uniform across the workgroup: tiles start
   // at multiples of TBK and every composite inner extent is a power of two, so
   // off(k0 + kk) = off(k0) + off(kk) for kk < TBK (if the extent E >= TBK the tile stays
-  // inside one E-block; if E < TBK, k0 is a multiple of E).  The gathered tap is therefore
-  // fixed per element too (the k inner extent, a map of <= 16 pixels, divides TBK).  Only a
-  // scalar base moves per tile: no per-element index arithmetic in the K loop.
+  // inside one E-block; if E < TBK, k0 is a multiple of E).  Only a scalar base moves per
+  // tile: no per-element index arithmetic in the K loop.
   int ak[NVA], am[NVA], bk[NVB], bn[NVB];
   int64_t aoff[NVA], boff[NVB];
   bool aok[NVA], bok[NVB];
-  const int nmask = (1 << g.bn.sh) - 1, kmask = (1 << g.bk.sh) - 1;
 #pragma unroll
   for (int v = 0; v < NVA; ++v) {
     const int e = tid + 256 * v;
@@ -136,13 +126,7 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
     bk[v] = BNF ? slow : fast;
     const int gn = n0 + bn[v];
     bok[v] = gn < g.N;
-    if (GATHER) {
-      const int t = g.tab[((bk[v] & kmask) << g.bn.sh) | (gn & nmask)];
-      bok[v] = bok[v] && t >= 0;  // no tap joins these pixels: a structural zero
-      boff[v] = bok[v] ? (int64_t)(gn >> g.bn.sh) * g.bn.so + (int64_t)(bk[v] >> g.bk.sh) * g.bk.so + t : 0;
-    } else {
-      boff[v] = bok[v] ? tg_off(g.bn, gn) + tg_off(g.bk, bk[v]) : 0;
-    }
+    boff[v] = bok[v] ? tg_off(g.bn, gn) + tg_off(g.bk, bk[v]) : 0;
   }
 
   // D register slots: the global loads of tiles t+1 .. t+D-1 are in flight while tile t's
@@ -164,7 +148,7 @@ __global__ __launch_bounds__(256) void tgemm_kernel(TgArgs g) {
   VB rb[D][NVB];
   auto load = [&](int k0, int slot) {
     const uint32_t ta = (uint32_t)(tg_off(g.ak, k0) * 4);
-    const uint32_t tb = (uint32_t)((GATHER ? (int64_t)(k0 >> g.bk.sh) * g.bk.so : tg_off(g.bk, k0)) * 4);
+    const uint32_t tb = (uint32_t)(tg_off(g.bk, k0) * 4);
 #pragma unroll
     for (int v = 0; v < NVA; ++v) {
       const bool ok = (aoffb[v] != kOOB) & (k0 + ak[v] < kend);  // WA = 4 along k: K % 4 == 0
@@ -355,25 +339,19 @@ bool vec_ok(const TgIndex& fast, const TgIndex& slow, const float* base, int ext
 
 template <int BM, int BN, int BK, int DEPTH>
 void launch_tile(const TgArgs& a, bool akf, bool bnf, bool va, bool vb, dim3 grid, hipStream_t s) {
-#define NDP_TG_LAUNCH(AK, BN_, GA, W1, W2) \
-  hipLaunchKernelGGL((tgemm_kernel<BM, BN, BK, AK, BN_, GA, W1, W2, DEPTH>), grid, dim3(256), 0, s, a)
-#define NDP_TG_W(AK, BN_, GA)                                  \
-  do {                                                         \
-    if (va && vb) NDP_TG_LAUNCH(AK, BN_, GA, 4, 4);            \
-    else if (va) NDP_TG_LAUNCH(AK, BN_, GA, 4, 1);             \
-    else if (vb) NDP_TG_LAUNCH(AK, BN_, GA, 1, 4);             \
-    else NDP_TG_LAUNCH(AK, BN_, GA, 1, 1);                     \
+#define NDP_TG_LAUNCH(AK, BN_, W1, W2) \
+  hipLaunchKernelGGL((tgemm_kernel<BM, BN, BK, AK, BN_, W1, W2, DEPTH>), grid, dim3(256), 0, s, a)
+#define NDP_TG_W(AK, BN_)                                  \
+  do {                                                     \
+    if (va && vb) NDP_TG_LAUNCH(AK, BN_, 4, 4);            \
+    else if (va) NDP_TG_LAUNCH(AK, BN_, 4, 1);             \
+    else if (vb) NDP_TG_LAUNCH(AK, BN_, 1, 4);             \
+    else NDP_TG_LAUNCH(AK, BN_, 1, 1);                     \
   } while (0)
-  if (a.gather) {
-    if (akf) {
-      if (va) NDP_TG_LAUNCH(true, false, true, 4, 1); else NDP_TG_LAUNCH(true, false, true, 1, 1);
-    } else {
-      if (va) NDP_TG_LAUNCH(false, false, true, 4, 1); else NDP_TG_LAUNCH(false, false, true, 1, 1);
-    }
-  } else if (akf && bnf) NDP_TG_W(true, true, false);
-  else if (akf) NDP_TG_W(true, false, false);
-  else if (bnf) NDP_TG_W(false, true, false);
-  else NDP_TG_W(false, false, false);
+  if (akf && bnf) NDP_TG_W(true, true);
+  else if (akf) NDP_TG_W(true, false);
+  else if (bnf) NDP_TG_W(false, true);
+  else NDP_TG_W(false, false);
 #undef NDP_TG_W
 #undef NDP_TG_LAUNCH
 }
@@ -388,7 +366,7 @@ int run(TgArgs a, bool akf, bool bnf, int splits, float* final_out, hipStream_t 
   if (splits <= 1) a.part = nullptr;
   const dim3 grid((a.N + tile.bn - 1) / tile.bn, (a.M + tile.bm - 1) / tile.bm, splits);
   const bool va = vec_ok(akf ? a.ak : a.am, akf ? a.am : a.ak, a.a, akf ? a.K : a.M);
-  const bool vb = !a.gather && vec_ok(bnf ? a.bn : a.bk, bnf ? a.bk : a.bn, a.b, bnf ? a.N : a.K);
+  const bool vb = vec_ok(bnf ? a.bn : a.bk, bnf ? a.bk : a.bn, a.b, bnf ? a.N : a.K);
   launch_tile<kTile64.bm, kTile64.bn, kTile64.bk, 2>(a, akf, bnf, va, vb, grid, s);
   if (splits <= 1) return 1;
   if (defer && a.addend == nullptr) return splits;  // the consumer (fused BN, gradfinish) sums them
@@ -396,45 +374,23 @@ int run(TgArgs a, bool akf, bool bnf, int splits, float* final_out, hipStream_t 
   return 1;
 }
 
-// tap(i, o) of a small-map conv, row-major [rows][cols] as the kernel reads it
-void fill_tab(TgArgs& a, const ConvGeom& g, bool by_input_rows) {
-  const int IHW = g.H * g.W, OHW = g.OH * g.OW;
-  for (int i = 0; i < 64; ++i) a.tab[i] = -1;
-  for (int i = 0; i < IHW; ++i)
-    for (int o = 0; o < OHW; ++o) {
-      const int ih = i / g.W, iw = i % g.W, oh = o / g.OW, ow = o % g.OW;
-      const int kh = ih - oh * g.stride + g.pad, kw = iw - ow * g.stride + g.pad;
-      const int t = (kh >= 0 && kh < g.KH && kw >= 0 && kw < g.KW) ? kh * g.KW + kw : -1;
-      if (by_input_rows) a.tab[i * OHW + o] = (int8_t)t;
-      else a.tab[o * IHW + i] = (int8_t)t;
-    }
-}
-
 }  // namespace
 
 int tg_class(const ConvGeom& g) {
   const int hw = g.H * g.W;
-  if (g.KH == 1 && g.KW == 1 && g.stride == 1 && g.pad == 0 && ilog2_exact(hw) >= 0) return TG_POINTWISE;
-  const int ohw = g.OH * g.OW;
-  if (hw <= 16 && ohw <= 4 && ilog2_exact(hw) >= 0 && ilog2_exact(ohw) >= 0 && g.KH * g.KW <= 127 &&
-      g.OH >= 1 && g.OW >= 1)
-    return TG_SMALL;
+  // 1x1 maps excluded: there the plain hipBLASLt GEMM (Toeplitz path) measured faster
+  if (g.KH == 1 && g.KW == 1 && g.stride == 1 && g.pad == 0 && hw > 1 && ilog2_exact(hw) >= 0) return TG_POINTWISE;
   return -1;
 }
 
 // slabs `part` must hold for direction dir (0 fwd, 1 grad-x, 2 grad-W); 1 = no scratch
 int tg_splits(const ConvGeom& g, int B, int dir) {
   const int cls = tg_class(g);
-  const int hw = g.H * g.W, ohw = g.OH * g.OW;
+  const int hw = g.H * g.W;
   if (cls == TG_POINTWISE) {
     if (dir == 0) return tg_pick_splits(g.Co, B * hw, g.C, tg_cap());
     if (dir == 1) return tg_pick_splits(g.C, B * hw, g.Co, tg_cap());
     return tg_pick_splits(g.Co, g.C, B * hw, 64);
-  }
-  if (cls == TG_SMALL) {
-    if (dir == 0) return tg_pick_splits(B, g.Co * ohw, g.C * hw, tg_cap());
-    if (dir == 1) return tg_pick_splits(B, g.C * hw, g.Co * ohw, tg_cap());
-    return tg_pick_splits(g.Co * ohw, g.C * hw, B, tg_cap());
   }
   return 1;
 }
@@ -443,58 +399,30 @@ int tg_splits(const ConvGeom& g, int B, int dir) {
 // the GEMM description of one direction (operand pointers / scratch left null), and the
 // load mappings (A k-fast, B n-fast) the launch uses
 TgArgs tg_args(const ConvGeom& g, int B, int dir, bool* akf, bool* bnf) {
-  const int cls = tg_class(g);
-  const int hw = g.H * g.W, ohw = g.OH * g.OW, T = g.KH * g.KW;
+  const int hw = g.H * g.W;
+  const int sh = ilog2_exact(hw);
   TgArgs a{};
-  if (dir == 0 && cls == TG_POINTWISE) {
-    const int sh = ilog2_exact(hw);
+  if (dir == 0) {
     a.am = plain(g.C); a.ak = plain(1);                         // W [Co][C]
     a.bk = plain(hw); a.bn = comp(sh, (int64_t)g.C * hw, 1);    // X [b][c][p]
     a.cm = plain(hw); a.cn = comp(sh, (int64_t)g.Co * hw, 1);   // Y [b][co][p]
     a.M = g.Co; a.N = B * hw; a.K = g.C;
     a.slab = (int64_t)B * g.Co * hw;
     *akf = true; *bnf = hw >= 4;
-  } else if (dir == 0) {
-    a.am = plain((int64_t)g.C * hw); a.ak = plain(1);           // X [b][(c,i)]
-    a.gather = 1;                                               // W[co, c, tap(i, o)]
-    a.bk = comp(ilog2_exact(hw), T, 0); a.bn = comp(ilog2_exact(ohw), (int64_t)g.C * T, 0);
-    fill_tab(a, g, true);                                       // rows: i (k inner), cols: o (n inner)
-    a.cm = plain((int64_t)g.Co * ohw); a.cn = plain(1);         // Y [b][(co,o)]
-    a.M = B; a.N = g.Co * ohw; a.K = g.C * hw;
-    a.slab = (int64_t)B * g.Co * ohw;
-    *akf = true; *bnf = false;
-  } else if (dir == 1 && cls == TG_POINTWISE) {
-    const int sh = ilog2_exact(hw);
+  } else if (dir == 1) {
     a.am = plain(1); a.ak = plain(g.C);                         // W^T: A[c][co] = W[co][c]
     a.bk = plain(hw); a.bn = comp(sh, (int64_t)g.Co * hw, 1);   // dY [b][co][p]
     a.cm = plain(hw); a.cn = comp(sh, (int64_t)g.C * hw, 1);    // dX [b][c][p]
     a.M = g.C; a.N = B * hw; a.K = g.Co;
     a.slab = (int64_t)B * g.C * hw;
     *akf = false; *bnf = hw >= 4;
-  } else if (dir == 1) {
-    a.am = plain((int64_t)g.Co * ohw); a.ak = plain(1);         // dY [b][(co,o)]
-    a.gather = 1;                                               // B[(co,o), (c,i)] = W[co, c, tap(i, o)]
-    a.bk = comp(ilog2_exact(ohw), (int64_t)g.C * T, 0); a.bn = comp(ilog2_exact(hw), T, 0);
-    fill_tab(a, g, false);                                      // rows: o (k inner), cols: i (n inner)
-    a.cm = plain((int64_t)g.C * hw); a.cn = plain(1);           // dX [b][(c,i)]
-    a.M = B; a.N = g.C * hw; a.K = g.Co * ohw;
-    a.slab = (int64_t)B * g.C * hw;
-    *akf = true; *bnf = false;
-  } else if (cls == TG_POINTWISE) {
-    const int sh = ilog2_exact(hw);
+  } else {
     a.am = plain(hw); a.ak = comp(sh, (int64_t)g.Co * hw, 1);   // dY as A[co][(b,p)]
     a.bk = comp(sh, (int64_t)g.C * hw, 1); a.bn = plain(hw);    // X as B[(b,p)][c]
     a.cm = plain(g.C); a.cn = plain(1);                         // dW [co][c]
     a.M = g.Co; a.N = g.C; a.K = B * hw;
     a.slab = (int64_t)g.Co * g.C;
     *akf = hw >= 4; *bnf = hw == 1;
-  } else {
-    a.am = plain(1); a.ak = plain((int64_t)g.Co * ohw);         // dY as A[(co,o)][b]
-    a.bk = plain((int64_t)g.C * hw); a.bn = plain(1);           // X as B[b][(c,i)]
-    a.cm = plain((int64_t)g.C * hw); a.cn = plain(1);           // dWbig^T [(co,o)][(c,i)]
-    a.M = g.Co * ohw; a.N = g.C * hw; a.K = B;
-    a.slab = (int64_t)g.Co * ohw * g.C * hw;
-    *akf = false; *bnf = true;
   }
   return a;
 }
@@ -503,9 +431,8 @@ int launch_tg_fwd(const float* x, const float* w, float* y, int B, const ConvGeo
                   bool defer) {
   bool akf, bnf;
   TgArgs a = tg_args(g, B, 0, &akf, &bnf);
-  const bool pw = tg_class(g) == TG_POINTWISE;
-  a.a = pw ? w : x;
-  a.b = pw ? x : w;
+  a.a = w;
+  a.b = x;
   a.c = y;
   a.part = part;
   return run(a, akf, bnf, tg_splits(g, B, 0), y, s, defer);
@@ -516,18 +443,16 @@ int launch_tg_dgrad(const float* dy, const float* w, float* dx, int B, const Con
                     hipStream_t s, const float* addend, bool defer) {
   bool akf, bnf;
   TgArgs a = tg_args(g, B, 1, &akf, &bnf);
-  const bool pw = tg_class(g) == TG_POINTWISE;
-  a.a = pw ? w : dy;
-  a.b = pw ? dy : w;
+  a.a = w;
+  a.b = dy;
   a.c = dx;
   a.part = part;
   a.addend = addend;
   return run(a, akf, bnf, tg_splits(g, B, 1), dx, s, defer);
 }
 
-// POINTWISE: out = dW [Co, C]; SMALL: out = dWbig^T [Co*OH*OW, C*H*W] (fold it into dW with
-// toeplitz_fold).  part: tg_splits(g, B, 2) * numel(out) floats.  defer (pointwise): leave
-// the split-K slabs in `part` and return how many (1 = `out` final).
+// out = dW [Co, C].  part: tg_splits(g, B, 2) * numel(out) floats.  defer: leave the split-K
+// slabs in `part` and return how many (1 = `out` final).
 int launch_tg_wgrad(const float* x, const float* dy, float* out, int B, const ConvGeom& g, float* part, hipStream_t s,
                     bool defer) {
   bool akf, bnf;
@@ -536,7 +461,7 @@ int launch_tg_wgrad(const float* x, const float* dy, float* out, int B, const Co
   a.b = x;
   a.c = out;
   a.part = part;
-  return run(a, akf, bnf, tg_splits(g, B, 2), out, s, defer && tg_class(g) == TG_POINTWISE);
+  return run(a, akf, bnf, tg_splits(g, B, 2), out, s, defer);
 }
 
 }  // namespace ndp

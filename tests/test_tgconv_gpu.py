@@ -1,13 +1,12 @@
 """csrc/tgemm.hip (ops/tgconv.py) vs an fp64 PyTorch reference: forward, grad-x, grad-W for
-the pointwise 1x1 family (ResNet-50/152 bottlenecks) and the small-map tabled family
-(ResNet layer3 / layer4 on 32x32 inputs), incl. split-K, in-place addends, branch links and
-deferred grad-W finishing; plus determinism."""
+the pointwise 1x1 family (ResNet-50/152 bottlenecks), incl. split-K, in-place addends, branch
+links and deferred grad-W finishing; plus determinism."""
 import pytest
 import torch
 import torch.nn.functional as F
 
 from network_distributed_pytorch_amd.ops.gradlink import BranchLink, GradLink
-from network_distributed_pytorch_amd.ops.tgconv import POINTWISE, SMALL, TgConvFn, tg_plan
+from network_distributed_pytorch_amd.ops.tgconv import POINTWISE, TgConvFn, tg_plan
 
 pytestmark = pytest.mark.gpu
 
@@ -17,36 +16,15 @@ POINTWISE_CASES = [
     (64, 256, 8, 8, 64, 1, 1, 0),     # R50 layer1 conv1, batch 64 (N = 8 shape)
     (16, 512, 4, 4, 128, 1, 1, 0),    # R50 layer2 conv1
     (32, 1024, 2, 2, 256, 1, 1, 0),   # R50 layer3 conv1
-    (64, 512, 1, 1, 2048, 1, 1, 0),   # R50 layer4 conv3 (1x1 map)
     (512, 64, 8, 8, 64, 1, 1, 0),     # batch 512: grad-W split-K over 32768 pixels
     (6, 36, 4, 4, 20, 1, 1, 0),       # ragged tiles (not multiples of 64)
 ]
-SMALL_CASES = [
-    (64, 256, 2, 2, 256, 3, 1, 1),    # R18 layer3 3x3
-    (64, 128, 4, 4, 256, 3, 2, 1),    # R18 layer3 entry 3x3/2
-    (64, 128, 4, 4, 256, 1, 2, 0),    # R18 layer3 downsample 1x1/2
-    (64, 256, 2, 2, 512, 3, 2, 1),    # R18 layer4 entry 3x3/2 (2x2 -> 1x1)
-    (64, 512, 1, 1, 512, 3, 1, 1),    # R18 layer4 3x3 on 1x1 (center tap only)
-    (512, 256, 2, 2, 256, 3, 1, 1),   # batch 512
-    (10, 24, 4, 4, 40, 3, 2, 1),      # ragged
-]
-
-
 def _run(device, case, addend=False):
     B, C, H, W, Co, k, s, p = case
     g = torch.Generator(device="cpu").manual_seed(hash(case) % 1000)
     x = torch.randn(B, C, H, W, generator=g).to(device)
     w = (torch.randn(Co, C, k, k, generator=g) / (C * k * k) ** 0.5).to(device)
-    from network_distributed_pytorch_amd.ops import tgconv
-
-    # the 1x1-map pointwise case and the small-map family are off by default (slower than the
-    # hipBLASLt GEMMs there): the kernels are still tested
-    saved = tgconv._PW1, tgconv._SMALL
-    tgconv._PW1 = tgconv._SMALL = True
-    try:
-        plan = tg_plan(x, w, s, p)
-    finally:
-        tgconv._PW1, tgconv._SMALL = saved
+    plan = tg_plan(x, w, s, p)
     assert plan is not None, case
     xr = x.double().requires_grad_()
     wr = w.double().requires_grad_()
@@ -74,59 +52,47 @@ def _close(a, ref, what, case):
     assert err < 2e-5, f"{what} {case}: rel err {err:.3g}"
 
 
-@pytest.mark.parametrize("case", POINTWISE_CASES + SMALL_CASES)
+@pytest.mark.parametrize("case", POINTWISE_CASES)
 def test_tgconv_matches_fp64(device, case):
     plan, (y, yr), (dx, rdx), (dw, rdw) = _run(device, case)
-    assert plan[1] == (POINTWISE if case in POINTWISE_CASES else SMALL)
+    assert plan[1] == POINTWISE
     _close(y, yr, "fwd", case)
     _close(dx, rdx, "dgrad", case)
     _close(dw, rdw, "wgrad", case)
 
 
-@pytest.mark.parametrize("case", [POINTWISE_CASES[1], SMALL_CASES[0], SMALL_CASES[5]])
+@pytest.mark.parametrize("case", [POINTWISE_CASES[1], POINTWISE_CASES[4]])
 def test_tgconv_addend_in_place(device, case):
     _, (y, yr), (dx, rdx), (dw, rdw) = _run(device, case, addend=True)
     _close(dx, rdx, "dgrad+addend", case)
 
 
-def test_tgconv_split_k_used(device):
-    # the N = 8 shapes must fill the GPU: split-K on the forward / grad-W of layer4
-    from network_distributed_pytorch_amd.ops import tgconv
-
+def test_tgconv_no_1x1_map_path(device):
+    # 1x1 convs on 1x1 maps stay on the plain hipBLASLt GEMM (Toeplitz path): measured faster
     x = torch.empty(64, 512, 1, 1, device=device)
-    w = torch.empty(512, 512, 3, 3, device=device)
-    saved, tgconv._SMALL = tgconv._SMALL, True
-    try:
-        plan = tg_plan(x, w, 1, 1)
-    finally:
-        tgconv._SMALL = saved
-    assert plan[2] > 1 or plan[4] > 1, plan
+    w = torch.empty(2048, 512, 1, 1, device=device)
+    assert tg_plan(x, w, 1, 0) is None
 
 
 def test_tgconv_branch_link_sums_two_convs(device):
-    """A downsample block's conv1 and 1x1 downsample share one grad-x buffer (BranchLink)."""
+    """Two 1x1 convs of one input (a Bottleneck block's conv1 and stride-1 downsample) share one
+    grad-x buffer (BranchLink)."""
     g = torch.Generator(device="cpu").manual_seed(3)
-    x = torch.randn(16, 128, 4, 4, generator=g).to(device)
-    w1 = torch.randn(256, 128, 3, 3, generator=g).to(device) * 0.05
-    w2 = torch.randn(256, 128, 1, 1, generator=g).to(device) * 0.05
+    x = torch.randn(16, 256, 4, 4, generator=g).to(device)
+    w1 = torch.randn(64, 256, 1, 1, generator=g).to(device) * 0.05
+    w2 = torch.randn(128, 256, 1, 1, generator=g).to(device) * 0.05
     xr = x.double().requires_grad_()
-    (F.conv2d(xr, w1.double(), stride=2, padding=1).sum() + 2 * F.conv2d(xr, w2.double(), stride=2).sum()).backward()
+    (F.conv2d(xr, w1.double()).sum() + 2 * F.conv2d(xr, w2.double()).sum()).backward()
     xg = x.clone().requires_grad_()
     br = BranchLink()
-    from network_distributed_pytorch_amd.ops import tgconv
-
-    saved, tgconv._SMALL = tgconv._SMALL, True
-    try:
-        p1, p2 = tg_plan(x, w1, 2, 1), tg_plan(x, w2, 2, 0)
-    finally:
-        tgconv._SMALL = saved
+    p1, p2 = tg_plan(x, w1, 1, 0), tg_plan(x, w2, 1, 0)
     a = TgConvFn.apply(xg, w1, p1, None, br)
     b = TgConvFn.apply(xg, w2, p2, None, br)
     (a.sum() + 2 * b.sum()).backward()
     _close(xg.grad, xr.grad, "branch dgrad", "branch")
 
 
-@pytest.mark.parametrize("case", [POINTWISE_CASES[5], SMALL_CASES[5]])
+@pytest.mark.parametrize("case", [POINTWISE_CASES[4], POINTWISE_CASES[1]])
 def test_tgconv_deterministic(device, case):
     r1 = _run(device, case)
     r2 = _run(device, case)

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""A/B of the tgemm conv path (csrc/tgemm.hip) against the previous paths (hipBLASLt Toeplitz
-GEMMs for small maps, MIOpen for 1x1 convs) on the ResNet shapes, per batch size.
+"""A/B of the tgemm pointwise conv path (csrc/tgemm.hip) against the previous path (MIOpen
+1x1 convs) on the ResNet-50/152 bottleneck shapes, per batch size.  (The small-map family this
+tool also measured in round 3, profiles/r3/tg_bench.md, was deleted in round 6.)
 
     python tools/tg_bench.py [--batches 64 512] [--iters 50]
 
@@ -20,17 +21,11 @@ from network_distributed_pytorch_amd.models.conv_gemm import GemmConv2d, Toeplit
 from network_distributed_pytorch_amd.ops import gemm_tuning, gradfinish, tgconv  # noqa: E402
 
 SHAPES = {  # name: (C, H, W, Co, k, stride, pad)
-    "r18.l3.conv": (256, 2, 2, 256, 3, 1, 1),
-    "r18.l3.entry": (128, 4, 4, 256, 3, 2, 1),
-    "r18.l3.ds": (128, 4, 4, 256, 1, 2, 0),
-    "r18.l4.conv": (512, 1, 1, 512, 3, 1, 1),
-    "r18.l4.entry": (256, 2, 2, 512, 3, 2, 1),
     "r50.l1.pw_in": (256, 8, 8, 64, 1, 1, 0),
     "r50.l1.pw_out": (64, 8, 8, 256, 1, 1, 0),
     "r50.l2.pw_in": (512, 4, 4, 128, 1, 1, 0),
     "r50.l3.pw_in": (1024, 2, 2, 256, 1, 1, 0),
     "r50.l3.pw_out": (256, 2, 2, 1024, 1, 1, 0),
-    "r50.l4.pw_out": (512, 1, 1, 2048, 1, 1, 0),
 }
 
 
