@@ -964,17 +964,30 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_kernel(
 // the bytes per address cycle.  A float4 holds whole channels' pixel runs: one channel (HW >= 4,
 // its HW/4 float4s on adjacent lanes) or 4 / HW channels (HW = 1, 2: separate sums per
 // channel).  Same fp64 sums, same fixed-order fold: deterministic run to run.
-template <int HW, int BWD, int CW, int MAXN = kFusedMaxN, int PAIR = 0>
+// SPLIT > 1 (the 8x8 maps at per-GPU batch <= 128, one channel per column block): the rows of a
+// column block are split over SPLIT workgroups that exchange their fp64 partial sums through the
+// sc1 form of cdna_hip_programming.md §6 Guideline 16 (write-through partial stores + vmcnt drain +
+// a relaxed monotonic arrival counter; every workgroup polls it relaxed, bounded, then reads the
+// SPLIT partials with sc1 loads in split order: the same totals, bitwise, in all of them).  One
+// workgroup per channel left 3/4 of the CUs idle and every thread held 4 rows.
+struct BnSplitCtx {
+  double* part;                 // [column block][SPLIT][4] partial sums
+  unsigned long long* ctr;      // [column block] arrival counters (monotonic, zeroed once)
+  unsigned max_spins;
+};
+
+template <int HW, int BWD, int CW, int MAXN = kFusedMaxN, int PAIR = 0, int SPLIT = 1>
 __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_v4_kernel(
     const float* __restrict__ x, const float* __restrict__ res, const float* __restrict__ dy,
     const float* __restrict__ yin, const float* __restrict__ gamma, const float* __restrict__ beta,
     float* __restrict__ rmean, float* __restrict__ rvar, int64_t* __restrict__ nbt, float* __restrict__ save_mean,
     float* __restrict__ save_invstd, float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ out,
     float* __restrict__ dres, int N, int C, float eps, float momentum, int relu, const float* __restrict__ src,
-    int nslab, BnPair p2) {
+    int nslab, BnPair p2, BnSplitCtx sx = BnSplitCtx{}) {
+  static_assert(SPLIT == 1 || (PAIR == 0 && HW >= 4 && CW == HW), "row splits: one channel per column block");
   constexpr int CT = CW / 4;                   // threads per row
   constexpr int RG = kFusedThreads / CT;       // row groups
-  constexpr int NP = (MAXN + RG - 1) / RG;     // rows per thread
+  constexpr int NP = (MAXN / SPLIT + RG - 1) / RG;  // rows per thread
   constexpr int NW = kFusedThreads / 64;
   constexpr int NCH = HW >= 4 ? 1 : 4 / HW;    // channels per float4
   constexpr int CPC = HW >= 4 ? 4 : HW;        // components per channel inside a float4
@@ -983,11 +996,17 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_v4_kernel(
   static_assert(CW % 4 == 0 && CW % HW == 0 && CT <= 64 && 64 % CT == 0, "bad column block");
   __shared__ double red[PAIR ? 4 : 2][NW][CPW];
   const int CHW = C * HW;
-  const int ct = threadIdx.x % CT, g = threadIdx.x / CT, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int cb = xcd_block((int)blockIdx.x, (int)gridDim.x);
+  const int ct = threadIdx.x % CT, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // the split's rows: row(k) = row0 + g + k RG for g + k RG < rps (SPLIT = 1: all N rows)
+  const int split = SPLIT > 1 ? (int)blockIdx.x % SPLIT : 0;
+  const int cb = SPLIT > 1 ? (int)blockIdx.x / SPLIT : xcd_block((int)blockIdx.x, (int)gridDim.x);
+  const int rps = SPLIT > 1 ? (N + SPLIT - 1) / SPLIT : N;
+  const int row0 = split * rps;
+  const int g = threadIdx.x / CT;
   const int j0 = cb * CW + 4 * ct;
   const bool ok_col = j0 < CHW;
   const int c0 = ok_col ? j0 / HW : 0;  // first channel of this float4
+  auto row_ok = [&](int k) { return g + k * RG < rps && row0 + g + k * RG < N; };
   float mean_s[NCH], invstd_s[NCH], gam[NCH], bet[NCH], rm[NCH], rv[NCH];
   float mean2[NCH], invstd2[NCH], gam2[NCH], bet2[NCH], rm2[NCH], rv2[NCH];
 #pragma unroll
@@ -1025,8 +1044,8 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_v4_kernel(
   const int64_t slab = (int64_t)N * CHW;
 #pragma unroll
   for (int k = 0; k < NP; ++k) {  // every load in flight before any use
-    const int n = g + k * RG;
-    const bool ok = ok_col && n < N;
+    const int n = row0 + g + k * RG;
+    const bool ok = ok_col && row_ok(k);
     const int64_t o = (int64_t)n * CHW + j0;
     f32x4 sum = zero;
     if (src != nullptr && ok) {  // deferred split-K sum, slab order (bitwise = conv_slab_sum)
@@ -1058,8 +1077,8 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_v4_kernel(
   if (!BWD && src != nullptr) {  // BN's saved input = the conv output
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
-      const int n = g + k * RG;
-      if (ok_col && n < N) *reinterpret_cast<f32x4*>(const_cast<float*>(x) + (int64_t)n * CHW + j0) = v[k];
+      const int n = row0 + g + k * RG;
+      if (ok_col && row_ok(k)) *reinterpret_cast<f32x4*>(const_cast<float*>(x) + (int64_t)n * CHW + j0) = v[k];
     }
   }
   if constexpr (PAIR) {
@@ -1079,7 +1098,7 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_v4_kernel(
     for (int i = 0; i < NCH; ++i) r[q][i] = 0.0;
 #pragma unroll
   for (int k = 0; k < NP; ++k) {
-    if (ok_col && g + k * RG < N) {
+    if (ok_col && row_ok(k)) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int i = e / CPC;
@@ -1131,11 +1150,51 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_v4_kernel(
 #pragma unroll
       for (int w = 0; w < NW; ++w) R[q][i] += red[q][w][slot + i];
     }
+  if constexpr (SPLIT > 1) {  // the column block's SPLIT partials (NCH = 1, slot = 0 here)
+    double* mine = sx.part + ((int64_t)cb * SPLIT + split) * 4;
+    if (threadIdx.x < NR) {
+#pragma unroll
+      for (int q = 0; q < NR; ++q)
+        if ((int)threadIdx.x == q) __hip_atomic_store(mine + q, R[q][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (threadIdx.x < 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the storing wave drains
+    __syncthreads();  // every wave has read red[] before it is reused as the flag below
+    if (threadIdx.x == 0) {
+      unsigned long long* ctr = sx.ctr + cb;
+      const unsigned long long old = __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long target = (old / SPLIT + 1) * SPLIT;
+      unsigned spins = 0;
+      int bad = 0;
+      while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > sx.max_spins) { bad = 1; break; }  // never hang the GPU: poison (below)
+      }
+      red[0][0][0] = bad ? __builtin_nan("") : 0.0;
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler order only: sc1 loads follow
+    const double poison = red[0][0][0];
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(sx.part + (int64_t)cb * SPLIT * 4, (short)0, SPLIT * 4 * 8,
+                                                      0x00020000);
+    double t[SPLIT][NR];
+#pragma unroll
+    for (int u = 0; u < SPLIT; ++u)
+#pragma unroll
+      for (int q = 0; q < NR; ++q)
+        t[u][q] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, (u * 4 + q) * 8, 0, 16));
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+      double acc = t[0][q];
+#pragma unroll
+      for (int u = 1; u < SPLIT; ++u) acc += t[u][q];
+      R[q][0] = acc + poison;
+    }
+  }
   const double* A = R[0];
   const double* B = R[1];
   if (!ok_col) return;
   const double M = (double)N * HW;
-  const bool writer = g == 0 && lead;
+  const bool writer = g == 0 && lead && split == 0;
   if (!BWD) {
     f32x4 sc, sh, sc2 = zero, sh2 = zero;
     if constexpr (PAIR) {
@@ -1192,8 +1251,8 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_v4_kernel(
     }
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
-      const int n = g + k * RG;
-      if (n < N) {
+      const int n = row0 + g + k * RG;
+      if (row_ok(k)) {
         f32x4 z;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -1231,8 +1290,8 @@ __global__ __launch_bounds__(kFusedThreads) void bn_small_fused_v4_kernel(
     }
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
-      const int n = g + k * RG;
-      if (n < N) {
+      const int n = row0 + g + k * RG;
+      if (row_ok(k)) {
         f32x4 o4, z4;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -1328,6 +1387,42 @@ static void launch_small_fused_cw(int HW, const float* x, const float* res, cons
 #undef NDP_BN_FUSED_P
 }
 
+// Row splits of the 8x8-map single-launch BN (bn_small_fused_v4_kernel SPLIT): workgroups per
+// channel.  NDP_BN_SPLIT = 1 / 2 / 4 (A/B); the exchange scratch is allocated once per device, on
+// the first (eager, never captured) call, and its counters are zeroed then.
+// Measured (ResNet-18 r=4, 1x MI355X, round 6): batch 64 split 1 / 2 / 4 = 0.7683 / 0.7607 /
+// 0.7671 ms, batch 128 split 1 / 4 = 0.8654 / 0.8547 ms — the launch stays latency-bound (~6 µs
+// for 1 MB), so the gain is small; default 2 below 128 rows, 4 from 128.
+static int bn_row_split(int N, int C) {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("NDP_BN_SPLIT");
+    v = e ? atoi(e) : 0;
+    if (v != 0 && v != 1 && v != 2 && v != 4) v = 0;
+  }
+  const int sp = v ? v : (N >= 128 ? 4 : 2);
+  if (C > 1024 || N < 8 * sp) return 1;
+  return sp;
+}
+
+static BnSplitCtx bn_split_ctx(int C, int split) {
+  constexpr int kCols = 1024;  // column blocks (channels) covered
+  struct Buf { double* part = nullptr; unsigned long long* ctr = nullptr; };
+  static Buf bufs[64];
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  Buf& b = bufs[dev & 63];
+  if (b.part == nullptr) {
+    (void)hipMalloc(&b.part, sizeof(double) * kCols * 4 * 4);
+    (void)hipMalloc(&b.ctr, sizeof(unsigned long long) * kCols * 3);
+    (void)hipMemset(b.ctr, 0, sizeof(unsigned long long) * kCols * 3);
+    (void)hipDeviceSynchronize();
+  }
+  (void)C;
+  // one counter range per split factor: a counter only ever moves in steps of its own SPLIT
+  return BnSplitCtx{b.part, b.ctr + (split == 2 ? 0 : kCols), 1u << 22};
+}
+
 template <int BWD>
 static void launch_small_fused(int HW, const float* x, const float* res, const float* dy, const float* yin,
                                const float* gamma, const float* beta, float* rmean, float* rvar, int64_t* nbt,
@@ -1337,7 +1432,17 @@ static void launch_small_fused(int HW, const float* x, const float* res, const f
   if (HW == 64) {  // one channel per workgroup (bn_fused_ok); float4 unless an operand is unaligned
     auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     if (pr != nullptr) return;  // (bn_pair_ok: no pair on the 8x8 maps)
-    if (a16(x) && a16(res) && a16(dy) && a16(yin) && a16(out) && a16(dres) && a16(src))
+    const int split = bn_row_split(N, C);
+    if (a16(x) && a16(res) && a16(dy) && a16(yin) && a16(out) && a16(dres) && a16(src) && split > 1) {
+      const BnSplitCtx sx = bn_split_ctx(C, split);
+#define NDP_BN_SPLIT_LAUNCH(SP)                                                                                  \
+  hipLaunchKernelGGL((bn_small_fused_v4_kernel<64, BWD, 64, kFusedMaxN64, 0, SP>), dim3((unsigned)(C * SP)),     \
+                     dim3(kFusedThreads), 0, s, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma,  \
+                     dbeta, out, dres, N, C, eps, momentum, relu, src, nslab, BnPair{}, sx)
+      if (split == 2) NDP_BN_SPLIT_LAUNCH(2);
+      else NDP_BN_SPLIT_LAUNCH(4);
+#undef NDP_BN_SPLIT_LAUNCH
+    } else if (a16(x) && a16(res) && a16(dy) && a16(yin) && a16(out) && a16(dres) && a16(src))
       hipLaunchKernelGGL((bn_small_fused_v4_kernel<64, BWD, 64, kFusedMaxN64>), dim3((unsigned)C),
                          dim3(kFusedThreads), 0, s, x, res, dy, yin, gamma, beta, rmean, rvar, nbt, sm, si, dgamma,
                          dbeta, out, dres, N, C, eps, momentum, relu, src, nslab, BnPair{});

@@ -56,13 +56,21 @@ def test_bn_act_train_fwd_bwd(device, shape, res, relu):
     assert torch.allclose(ye, yr, atol=2e-5, rtol=1e-4)
 
 
-def test_bn_deterministic(device):
+@pytest.mark.parametrize("n", [512, 64, 100])  # 64 / 100: the row-split single-launch kernel (8x8 maps)
+def test_bn_deterministic(device, n):
     torch.manual_seed(1)
     m = BatchNormAct2d(64).to(device)
-    x = torch.randn(512, 64, 8, 8, device=device)
-    a = m(x, relu=True)
-    b = m(x, relu=True)
-    assert torch.equal(a, b)
+    x = torch.randn(n, 64, 8, 8, device=device, requires_grad=True)
+    g = torch.randn(n, 64, 8, 8, device=device)
+    outs = []
+    for _ in range(2):
+        x.grad = None
+        m.weight.grad = None
+        y = m(x, relu=True)
+        y.backward(g)
+        outs.append((y.detach().clone(), x.grad.clone(), m.weight.grad.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
 
 
 def test_resnet18_fused_matches_unfused(device):
