@@ -705,10 +705,11 @@ void toeplitz_expand_many(const std::vector<std::tuple<torch::Tensor, torch::Ten
   check_launch("launch_toeplitz_expand_many");
 }
 
-// entries: [(dw_big, dw, geom)] -> every fold in one launch
-void toeplitz_fold_many(const std::vector<std::tuple<torch::Tensor, torch::Tensor, std::vector<int64_t>>>& entries) {
-  TORCH_CHECK(!entries.empty() && (int)entries.size() <= ndp::kMaxExpand, "toeplitz_fold_many: 1..",
-              ndp::kMaxExpand, " layers");
+using FoldEntries = std::vector<std::tuple<torch::Tensor, torch::Tensor, std::vector<int64_t>>>;
+using SlabEntries = std::vector<std::tuple<torch::Tensor, torch::Tensor, int64_t>>;
+
+ndp::FoldBatch fold_batch(const FoldEntries& entries) {
+  TORCH_CHECK((int)entries.size() <= ndp::kMaxExpand, "toeplitz_fold_many: at most ", ndp::kMaxExpand, " layers");
   ndp::FoldBatch b{};
   int64_t acc = 0;
   for (const auto& en : entries) {
@@ -727,14 +728,11 @@ void toeplitz_fold_many(const std::vector<std::tuple<torch::Tensor, torch::Tenso
     b.end[b.n] = acc;
     ++b.n;
   }
-  ndp::launch_toeplitz_fold_many(b, cur_stream());
-  check_launch("launch_toeplitz_fold_many");
+  return b;
 }
 
-// entries: [(part, dw, slices)] -> dw = sum_s part[s * numel(dw) :], every entry in one launch
-void slab_sum_many(const std::vector<std::tuple<torch::Tensor, torch::Tensor, int64_t>>& entries) {
-  TORCH_CHECK(!entries.empty() && (int)entries.size() <= ndp::kMaxExpand, "slab_sum_many: 1..", ndp::kMaxExpand,
-              " entries");
+ndp::SlabBatch slab_batch(const SlabEntries& entries) {
+  TORCH_CHECK((int)entries.size() <= ndp::kMaxExpand, "slab_sum_many: at most ", ndp::kMaxExpand, " entries");
   ndp::SlabBatch b{};
   int64_t blocks = 0;
   for (const auto& en : entries) {
@@ -754,8 +752,28 @@ void slab_sum_many(const std::vector<std::tuple<torch::Tensor, torch::Tensor, in
     b.end[b.n] = blocks;
     ++b.n;
   }
-  ndp::launch_slab_sum_many(b, cur_stream());
+  return b;
+}
+
+// entries: [(dw_big, dw, geom)] -> every fold in one launch
+void toeplitz_fold_many(const FoldEntries& entries) {
+  TORCH_CHECK(!entries.empty(), "toeplitz_fold_many: no entries");
+  ndp::launch_toeplitz_fold_many(fold_batch(entries), cur_stream());
+  check_launch("launch_toeplitz_fold_many");
+}
+
+// entries: [(part, dw, slices)] -> dw = sum_s part[s * numel(dw) :], every entry in one launch
+void slab_sum_many(const SlabEntries& entries) {
+  TORCH_CHECK(!entries.empty(), "slab_sum_many: no entries");
+  ndp::launch_slab_sum_many(slab_batch(entries), cur_stream());
   check_launch("launch_slab_sum_many");
+}
+
+// slab_sum_many(slabs) and toeplitz_fold_many(folds) in one launch (bitwise the same results)
+void gradw_finish(const SlabEntries& slabs, const FoldEntries& folds) {
+  if (slabs.empty() && folds.empty()) return;
+  ndp::launch_gradw_finish(slab_batch(slabs), fold_batch(folds), cur_stream());
+  check_launch("launch_gradw_finish");
 }
 
 void toeplitz_fold(torch::Tensor dwb, torch::Tensor dw, const std::vector<int64_t>& geom) {
@@ -1417,6 +1435,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("toeplitz_expand_many", &toeplitz_expand_many);
   m.def("toeplitz_fold_many", &toeplitz_fold_many);
   m.def("slab_sum_many", &slab_sum_many);
+  m.def("gradw_finish", &gradw_finish, py::arg("slabs"), py::arg("folds"));
   m.def("conv_plan", &conv_plan, py::arg("geom"), py::arg("batch"));
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("geom"), py::arg("part") = py::none(),
         py::arg("defer") = false, py::arg("stats") = py::none(), py::arg("wino_u") = py::none());

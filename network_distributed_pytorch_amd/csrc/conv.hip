@@ -249,9 +249,8 @@ __device__ __forceinline__ void fold_any(const float* __restrict__ dwt, const Co
 // in the kernel arguments.  A workgroup's 256 pairs own one contiguous run of 256 * KH*KW
 // weights, so the taps go through LDS and leave as coalesced float stores (a lane writing
 // its own 9 weights would stride the wave's stores by 36 B).
-__global__ __launch_bounds__(256) void toeplitz_fold_many_kernel(FoldBatch b) {
-  __shared__ float stage[256 * kFoldMaxTaps];
-  const int64_t base = (int64_t)blockIdx.x * 256;
+__device__ __forceinline__ void fold_many_block(const FoldBatch& b, int64_t blk, float* __restrict__ stage) {
+  const int64_t base = blk * 256;
   const int64_t i = base + threadIdx.x;
   const int64_t total = b.end[b.n - 1];
   int e = 0;
@@ -282,6 +281,11 @@ __global__ __launch_bounds__(256) void toeplitz_fold_many_kernel(FoldBatch b) {
 #pragma unroll
   for (int t = 0; t < kFoldMaxTaps; ++t)
     if (t < T) out[t] = acc[t];
+}
+
+__global__ __launch_bounds__(256) void toeplitz_fold_many_kernel(FoldBatch b) {
+  __shared__ float stage[256 * kFoldMaxTaps];
+  fold_many_block(b, blockIdx.x, stage);
 }
 
 void launch_toeplitz_fold_many(const FoldBatch& b, hipStream_t s) {
@@ -1112,9 +1116,7 @@ __global__ __launch_bounds__(256) void conv_slab_sum_kernel(const float* __restr
 // Every deferred grad-W slab sum of a backward pass in ONE launch (ops/gradfinish.py):
 // entry e owns blocks [end[e-1], end[e]); inside an entry the same 16-group fixed-order
 // tree as conv_slab_sum_kernel (bitwise identical results).
-__global__ __launch_bounds__(256) void conv_slab_sum_many_kernel(SlabBatch b) {
-  __shared__ f32x4c red[16][16];
-  const int64_t blk = blockIdx.x;
+__device__ __forceinline__ void slab_sum_many_block(const SlabBatch& b, int64_t blk, f32x4c (*red)[16]) {
   int e = 0;
   while (e + 1 < b.n && blk >= b.end[e]) ++e;
   const int64_t lb = blk - (e ? b.end[e - 1] : 0);
@@ -1139,6 +1141,31 @@ __global__ __launch_bounds__(256) void conv_slab_sum_many_kernel(SlabBatch b) {
     for (int k = 1; k < 16; ++k) t += red[k][col];
     *reinterpret_cast<f32x4c*>(b.dw[e] + i4) = t;
   }
+}
+
+__global__ __launch_bounds__(256) void conv_slab_sum_many_kernel(SlabBatch b) {
+  __shared__ f32x4c red[16][16];
+  slab_sum_many_block(b, blockIdx.x, red);
+}
+
+// The end-of-backward grad-W finish in ONE launch: blocks [0, slab blocks) run the slab sums,
+// the rest the Toeplitz folds (the two lists touch disjoint gradients).  Same per-block
+// bodies as the two kernels above, so the results are bitwise identical to them.
+__global__ __launch_bounds__(256) void gradw_finish_kernel(SlabBatch sb, FoldBatch fb) {
+  constexpr int kFloats = 256 * kFoldMaxTaps > 16 * 16 * 4 ? 256 * kFoldMaxTaps : 16 * 16 * 4;
+  __shared__ __attribute__((aligned(16))) float smem[kFloats];
+  const int64_t n_slab = sb.n > 0 ? sb.end[sb.n - 1] : 0;
+  const int64_t blk = blockIdx.x;
+  if (blk < n_slab) slab_sum_many_block(sb, blk, reinterpret_cast<f32x4c (*)[16]>(smem));
+  else fold_many_block(fb, blk - n_slab, smem);
+}
+
+void launch_gradw_finish(const SlabBatch& sb, const FoldBatch& fb, hipStream_t s) {
+  if (sb.n <= 0) return launch_toeplitz_fold_many(fb, s);
+  if (fb.n <= 0) return launch_slab_sum_many(sb, s);
+  const_cast<SlabBatch&>(sb).nt = 1;
+  const int64_t blocks = sb.end[sb.n - 1] + (fb.end[fb.n - 1] + 255) / 256;
+  hipLaunchKernelGGL(gradw_finish_kernel, dim3((unsigned)blocks), dim3(256), 0, s, sb, fb);
 }
 
 void launch_slab_sum_many(const SlabBatch& b, hipStream_t s) {

@@ -291,6 +291,8 @@ struct SlabBatch {
   int nt;  // non-temporal slab loads (set by launch_slab_sum_many)
 };
 void launch_slab_sum_many(const SlabBatch& b, hipStream_t s);
+// both of the above in one launch (the end-of-backward grad-W finish)
+void launch_gradw_finish(const SlabBatch& sb, const FoldBatch& fb, hipStream_t s);
 // dW [Co, C, KH, KW] <- fold of dWt_big [Co*OH*OW, C*H*W]  (fixed-order sum, deterministic)
 void launch_toeplitz_fold(const float* dwb, float* dw, const ConvGeom& g, hipStream_t s);
 // direct fp32-MFMA convolutions: shape class (-1 = none), images per workgroup / slice

@@ -3,8 +3,8 @@
 Each direct-conv grad-W ends with a split-slab sum and each Toeplitz conv grad-W with a
 fold of grad-W_big into the weight shape: ~20 small launches per ResNet-18 backward that
 are latency-bound (4-7 µs each).  Instead, the conv backward functions record them here
-and ONE ``slab_sum_many`` + ONE ``toeplitz_fold_many`` launch (csrc/conv.hip) finish them
-all when autograd's backward pass ends (``queue_callback`` on the execution engine: the
+and ONE ``gradw_finish`` launch (csrc/conv.hip: slab-sum blocks then fold blocks) finishes
+them all when autograd's backward pass ends (``queue_callback`` on the execution engine: the
 gradients are complete when ``backward()`` returns, exactly as without deferral), or
 earlier when a consumer needs them mid-backward (:func:`flush`: the overlapped gradient
 sync calls it before handing a group's gradients to the side stream).  Same summation
@@ -124,6 +124,9 @@ def flush() -> None:
     slabs, folds = list(_slabs), list(_folds)
     _slabs.clear()
     _folds.clear()
+    if len(slabs) <= _MAX and len(folds) <= _MAX:
+        X.gradw_finish(slabs, folds)  # both kinds in one launch (ResNet-18: 1 instead of 2)
+        return
     for i in range(0, len(slabs), _MAX):
         X.slab_sum_many(slabs[i: i + _MAX])
     for i in range(0, len(folds), _MAX):

@@ -163,3 +163,35 @@ def test_deferred_gradw_finishing_is_bitwise(device, batch):
         torch.backends.cudnn.deterministic = det
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_gradw_finish_one_launch_equals_two(device):
+    """gradw_finish(slabs, folds) (one launch: slab-sum blocks, then fold blocks) == the
+    separate slab_sum_many + toeplitz_fold_many launches, bitwise; either list may be empty."""
+    from network_distributed_pytorch_amd.ops._ext import ext
+
+    X = ext()
+    g = torch.Generator(device=device).manual_seed(0)
+    geoms = [(256, 2, 2, 256, 3, 3, 1, 1), (128, 4, 4, 256, 1, 1, 2, 0), (8, 3, 3, 16, 3, 3, 1, 1),
+             (512, 1, 1, 512, 3, 3, 1, 1)]
+    folds = []
+    for C, H, W, Co, kh, kw, s, p in geoms:
+        oh, ow = (H + 2 * p - kh) // s + 1, (W + 2 * p - kw) // s + 1
+        folds.append((torch.randn(Co * oh * ow, C * H * W, device=device, generator=g),
+                      torch.full((Co, C, kh, kw), float("nan"), device=device), [C, H, W, Co, kh, kw, s, p]))
+    slabs = []
+    for n, sl in ((64 * 64 * 9, 16), (36, 3), (128 * 64, 40)):
+        slabs.append((torch.randn(sl * n, device=device, generator=g), torch.full((n,), float("nan"), device=device), sl))
+
+    def fresh(lst):
+        return [(a, torch.full_like(b, float("nan")), c) for a, b, c in lst]
+
+    X.slab_sum_many(slabs)
+    X.toeplitz_fold_many(folds)
+    for s_in, f_in in ((fresh(slabs), fresh(folds)), (fresh(slabs), []), ([], fresh(folds))):
+        X.gradw_finish(s_in, f_in)
+        for (_, got, _), (_, ref, _) in zip(s_in, slabs):
+            assert torch.equal(got, ref)
+        for (_, got, geom), (_, ref, _) in zip(f_in, folds):
+            assert torch.equal(got, ref), geom
