@@ -954,7 +954,7 @@ int64_t conv_dgrad(torch::Tensor dy, torch::Tensor w, torch::Tensor dx, const st
 
 // dw None: write the per-slice partial slabs only (the caller sums them, batched)
 void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor part, c10::optional<torch::Tensor> dw_opt,
-                const std::vector<int64_t>& geom) {
+                const std::vector<int64_t>& geom, bool pair) {
   const ndp::ConvGeom g = conv_geom(geom);
   const int cls = ndp::conv_direct_class(g);
   TORCH_CHECK(cls >= 0, "conv_wgrad: no direct kernel for this geometry");
@@ -969,7 +969,8 @@ void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor part, c10::opti
   }
   check_f32(part, "part");
   TORCH_CHECK(part.numel() >= (int64_t)(B / imgs) * g.Co * g.C * g.KH * g.KW, "conv_wgrad: partial scratch too small");
-  ndp::launch_conv_wgrad(x.data_ptr<float>(), dy.data_ptr<float>(), part.data_ptr<float>(), dwp, B, g, cur_stream());
+  ndp::launch_conv_wgrad(x.data_ptr<float>(), dy.data_ptr<float>(), part.data_ptr<float>(), dwp, B, g, cur_stream(),
+                         pair && dy.is_contiguous() && x.is_contiguous());
   check_launch("launch_conv_wgrad");
 }
 
@@ -1457,7 +1458,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     if (cls < 0 || B <= 0 || B % ndp::conv_fwd_imgs(cls)) return 0;
     return ndp::conv_dgrad_stats_slices(cls, g, (int)B);
   }, py::arg("geom"), py::arg("batch"));
-  m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("part"), py::arg("dw"), py::arg("geom"));
+  m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("part"), py::arg("dw"), py::arg("geom"),
+        py::arg("pair") = false);
+  m.def("conv_flush_pending", []() {
+    ndp::conv_flush_pending();
+    check_launch("conv_flush_pending");
+  });
   m.def("tg_plan", &tg_plan);
   m.def("tg_describe", &tg_describe);
   m.def("tg_fwd", &tg_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("geom"), py::arg("part") = py::none(),

@@ -1463,6 +1463,27 @@ int launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvG
   }
 }
 
+// A layer1 Winograd grad-W held back by launch_conv_wgrad(pair = true) for the grad-x of the same
+// conv (host state only: set and consumed within one conv backward, capture-safe)
+namespace {
+struct PendingWgrad {
+  const float* x = nullptr;
+  const float* dy = nullptr;
+  float* part = nullptr;
+  int B = 0, imgs = 0;
+  ConvGeom g{};
+  hipStream_t s = nullptr;
+};
+PendingWgrad g_pending;
+}  // namespace
+
+void conv_flush_pending() {
+  if (g_pending.dy == nullptr) return;
+  const PendingWgrad p = g_pending;
+  g_pending = PendingWgrad{};
+  launch_wino_wgrad(p.x, p.dy, p.part, p.B, p.g.C, p.g.Co, p.g.H, p.imgs, p.s);
+}
+
 // dx[B, C, H, W] from dy[B, Co, OH, OW]
 int launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const ConvGeom& g, float* part,
                       hipStream_t s, const float* addend, bool defer, const ConvBnStats* bst, float* wino_u) {
@@ -1470,10 +1491,19 @@ int launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const C
   const int cls = conv_direct_class(g);
   const int ks = conv_ksplit(cls, g, B, true);
   if (wino_u != nullptr && conv_wino(cls, g, B, true)) {
-    launch_wino_conv(dy, wino_u, dx, B, g.Co, g.C, g.H, true, cls == 2 ? 2 : 1, addend,
-                     ks > 1 ? ConvBnStats{} : stats, ks, part, s);
+    const PendingWgrad& p = g_pending;
+    if (cls == 0 && p.dy == dy && p.s == s && p.B == B && p.g.C == g.C && p.g.Co == g.Co && p.g.H == 8) {
+      // this conv's grad-W is waiting: both in one launch
+      launch_wino_bwd_pair(dy, wino_u, dx, B, g.Co, g.C, addend, stats, ks, part, p.x, p.part, p.imgs, s);
+      g_pending = PendingWgrad{};
+    } else {
+      conv_flush_pending();
+      launch_wino_conv(dy, wino_u, dx, B, g.Co, g.C, g.H, true, cls == 2 ? 2 : 1, addend,
+                       ks > 1 ? ConvBnStats{} : stats, ks, part, s);
+    }
     return ks > 1 ? wino_slabs(part, dx, (int64_t)B * g.C * g.H * g.W, ks, defer, addend, s) : 1;
   }
+  conv_flush_pending();
   switch (cls) {
     case 0:
       return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true, true, 1, 2>(dy, w, dx, B, g.Co, g.C, ks, part, s,
@@ -1494,10 +1524,19 @@ int launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const C
 
 // part: (B / conv_wgrad_imgs) * Co * C * KH * KW floats of scratch
 void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, int B, const ConvGeom& g,
-                       hipStream_t s) {
+                       hipStream_t s, bool pair) {
+  conv_flush_pending();
   const int cls = conv_direct_class(g);
   const int imgs = conv_wgrad_imgs(cls, g, B);
   if (cls == 0 && wino_wgrad_ok(g.C, g.Co, g.H)) {
+    // held back for this conv's grad-x (launch_conv_dgrad) at the per-GPU batches that take the
+    // 4-wave grad-W (<= 128), where neither launch fills the CUs alone: ResNet-18 r=4 batch 64
+    // 0.7758 / 0.7656 -> 0.7498 / 0.7517 ms, 128 0.8676 -> 0.8434; at 512 the pair was slower,
+    // 1.4640 -> 1.4818 (the grad-W drops from 3 to 2 waves per SIMD; profiles/r6/bench_wino_pair.jsonl)
+    if (pair && dw == nullptr && wino_wgrad_red(B, imgs)) {
+      g_pending = PendingWgrad{x, dy, part, B, imgs, g, s};
+      return;
+    }
     // Winograd-domain grad-W (winograd.hip): same slab layout and slicing as the direct kernel.
     // Layer1 only: ResNet-18 at batch 512 90.7 vs 130.2 µs per step (4 launches), batch 64 31.1 vs
     // 38.5; the 4x4 maps (one tile per lane group and image: a load per 16 MFMAs) measured slower,

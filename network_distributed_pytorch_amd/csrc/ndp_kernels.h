@@ -365,9 +365,16 @@ void launch_wino_conv(const float* x, const float* u, float* y, int B, int inC, 
 // the split-K sums; out may alias addend
 void launch_slab_sum(const float* part, float* out, int64_t n, int nslab, hipStream_t s,
                      const float* addend = nullptr);
-// part: (B / conv_wgrad_imgs(cls, g, B)) * Co*C*KH*KW floats of scratch
+// part: (B / conv_wgrad_imgs(cls, g, B)) * Co*C*KH*KW floats of scratch.  pair: a layer1 Winograd
+// grad-W into `part` (dw == nullptr) may be held back and launched together with the next
+// launch_conv_dgrad of the same dY (one wino_bwd_pair_kernel launch); conv_flush_pending() launches
+// a held-back grad-W on its own (the caller's end of the conv backward)
 void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, int B, const ConvGeom& g,
-                       hipStream_t s);
+                       hipStream_t s, bool pair = false);
+void conv_flush_pending();
+void launch_wino_bwd_pair(const float* dy, const float* u, float* dx, int B, int inC, int outC, const float* addend,
+                          const ConvBnStats& st, int ks, float* part_x, const float* x, float* part_w, int imgs,
+                          hipStream_t s);
 
 // ---- strided / tabled implicit-GEMM convolutions (tgemm.hip) ------------------------------
 // operand index i -> element offset (i >> sh) * so + (i & (2^sh - 1)) * si

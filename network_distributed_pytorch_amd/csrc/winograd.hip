@@ -90,24 +90,42 @@ __device__ __forceinline__ float dppf(float v) {
 
 // H x H output maps (H = 8: layer1; H = 4: layer2, 4 images per wave so the 16 lanes of a channel
 // quad are still 16 tiles); IUPS = 2: grad-x of the stride-2 8x8 -> 4x4 conv on its zero-inserted dY
-template <int H, int IUPS>
-// Split-K (gridDim.z > 1, small batches): workgroup z reduces the input channels [z cps, (z + 1)
+// Split-K (grid z > 1, small batches): workgroup z reduces the input channels [z cps, (z + 1)
 // cps) x 16 into slab z of `part` (the output layout; no addend, no statistics) — the consumer sums
 // the slabs in z order like the direct kernels' (deterministic).
-__global__ __launch_bounds__(256, 2) void wino_dpp_kernel(const float* __restrict__ x, const float* __restrict__ u,
-                                                        float* __restrict__ y, int Cin, int Cout,
-                                                        const float* __restrict__ addend, ConvBnStats st,
-                                                        int cps, float* __restrict__ part, int64_t slab) {
+// (A device function of the workgroup's grid coordinates, so that wino_bwd_pair_kernel can run it
+// on one part of a combined grid.)
+struct WinoConvArgs {
+  const float* x;
+  const float* u;
+  float* y;
+  int Cin, Cout;
+  const float* addend;
+  ConvBnStats st;
+  int cps;
+  float* part;
+  int64_t slab;
+};
+template <int H, int IUPS>
+__device__ __forceinline__ void wino_dpp_body(const WinoConvArgs& A, const uint3 bid, const uint3 gdim,
+                                              float* __restrict__ smem) {
+  const float* __restrict__ x = A.x;
+  const float* __restrict__ u = A.u;
+  float* __restrict__ y = A.y;
+  const int Cin = A.Cin, Cout = A.Cout, cps = A.cps;
+  const float* __restrict__ addend = A.addend;
+  const ConvBnStats& st = A.st;
+  float* __restrict__ part = A.part;
+  const int64_t slab = A.slab;
   constexpr int TW = H / 2, TPI = TW * TW, IPW = 16 / TPI, HW = H * H;  // tiles per row / image, images per wave
   static_assert((H == 8 || H == 4) && (IUPS == 1 || H == 8), "shapes");
-  extern __shared__ __attribute__((aligned(16))) float smem[];
   float* Us = smem;  // [2][kWUS]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int j = lane & 15, kq = lane >> 4;
   const int ii = j / TPI, tj = j - ii * TPI, ty = tj / TW, tx = tj - ty * TW;
-  const int b0 = blockIdx.x * kWImgs * IPW, co0 = blockIdx.y * kWBM;
+  const int b0 = bid.x * kWImgs * IPW, co0 = bid.y * kWBM;
   const int img = b0 + wave * IPW + ii;
-  const int nchunks = cps, cz = blockIdx.z * cps;  // chunk range of this split
+  const int nchunks = cps, cz = bid.z * cps;  // chunk range of this split
   constexpr int IPL = HW / (IUPS * IUPS);  // input plane floats
 
   // core loads: IUPS 1: rows 2ty, 2ty + 1 x columns 2tx, 2tx + 1 of channel 4 kq + t; IUPS 2 (the
@@ -235,8 +253,8 @@ __global__ __launch_bounds__(256, 2) void wino_dpp_kernel(const float* __restric
     step(ch, core[0], core[1]);
     if (ch + 1 < nchunks) step(ch + 1, core[1], core[0]);
   }
-  if (gridDim.z > 1) {  // split-K: this slice's partial output
-    float* pz = part + (int64_t)blockIdx.z * slab;
+  if (gdim.z > 1) {  // split-K: this slice's partial output
+    float* pz = part + (int64_t)bid.z * slab;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int co = co0 + 4 * kq + r;
@@ -321,10 +339,17 @@ __global__ __launch_bounds__(256, 2) void wino_dpp_kernel(const float* __restric
       s0 += red[(w * kWBM + tid) * 2];
       s1 += red[(w * kWBM + tid) * 2 + 1];
     }
-    double* dd = st.out + ((int64_t)(co0 + tid) * gridDim.x + blockIdx.x) * 2;
+    double* dd = st.out + ((int64_t)(co0 + tid) * gdim.x + bid.x) * 2;
     dd[0] = s0;
     dd[1] = s1;
   }
+}
+
+template <int H, int IUPS>
+__global__ __launch_bounds__(256, 2) void wino_dpp_kernel(WinoConvArgs A) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  wino_dpp_body<H, IUPS>(A, make_uint3(blockIdx.x, blockIdx.y, blockIdx.z),
+                         make_uint3(gridDim.x, gridDim.y, gridDim.z), smem);
 }
 
 // ---- grad-W in the transform domain --------------------------------------------------------
@@ -341,16 +366,27 @@ __global__ __launch_bounds__(256, 2) void wino_dpp_kernel(const float* __restric
 // are summed through LDS in wave order before the single slab store — 4x fewer (larger) slices
 // for the same wave count, i.e. 4x less slab traffic for the grad-W sum.  RED = 1: a wave per
 // block (the slice's images all in one wave), for batches the 4-way split does not divide.
+struct WinoWgradArgs {
+  const float* x;
+  const float* dy;
+  float* part;
+  int Cin, Cout, imgs;
+};
+constexpr size_t kWgRedLds = (size_t)3 * 16 * 64 * sizeof(f32x4w);  // RED = 4: waves 1..3's blocks
 template <int H, int RED = 1>
-__global__ __launch_bounds__(256, 2) void wino_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy,
-                                                          float* __restrict__ part, int Cin, int Cout, int imgs) {
+__device__ __forceinline__ void wino_wgrad_body(const WinoWgradArgs& A, const uint3 bid, float* __restrict__ smem) {
+  const float* __restrict__ x = A.x;
+  const float* __restrict__ dy = A.dy;
+  float* __restrict__ part = A.part;
+  const int Cin = A.Cin, Cout = A.Cout;
+  int imgs = A.imgs;
   constexpr int TW = H / 2, TPL = TW * TW / 4, HW = H * H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i = lane & 15, kq = lane >> 4;
-  const int blk = RED == 4 ? blockIdx.y : blockIdx.y * 4 + wave, nbc = Cin / 16;
+  const int blk = RED == 4 ? (int)bid.y : (int)bid.y * 4 + wave, nbc = Cin / 16;
   const int cob = blk / nbc, cib = blk - cob * nbc;
   if (cob * 16 >= Cout) return;  // (RED = 4: uniform over the workgroup, before its barrier)
-  const int slice = blockIdx.x;
+  const int slice = bid.x;
   const int b0 = RED == 4 ? slice * imgs + wave * (imgs / 4) : slice * imgs;
   if (RED == 4) imgs /= 4;  // this wave's images
   // tile group kq: H = 8 -> tile row ty = kq (tiles tx = 0..3); H = 4 -> tile (kq / 2, kq % 2)
@@ -460,7 +496,7 @@ __global__ __launch_bounds__(256, 2) void wino_wgrad_kernel(const float* __restr
     }
   }
   if constexpr (RED == 4) {  // waves 1..3 -> LDS, wave 0 adds them in wave order
-    __shared__ __attribute__((aligned(16))) f32x4w red[3][16][64];
+    auto red = reinterpret_cast<f32x4w (*)[16][64]>(smem);  // [3][16][64]
     if (wave > 0) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) red[wave - 1][e][lane] = acc[e];
@@ -494,6 +530,31 @@ __global__ __launch_bounds__(256, 2) void wino_wgrad_kernel(const float* __restr
       o[3 * a + 1] = 0.5f * (t[a][1] - t[a][2]);
       o[3 * a + 2] = 0.5f * (t[a][1] + t[a][2]) + t[a][3];
     }
+  }
+}
+
+template <int H, int RED = 1>
+__global__ __launch_bounds__(256, 2) void wino_wgrad_kernel(WinoWgradArgs A) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  wino_wgrad_body<H, RED>(A, make_uint3(blockIdx.x, blockIdx.y, 0), smem);
+}
+
+// The layer1 backward pair in ONE launch: workgroups [0, n_dgrad) run the grad-x (wino_dpp_body on
+// the transposed-weight transform), the rest the Winograd grad-W of the same conv (both read only
+// dY / x / U and write disjoint outputs).  At the small per-GPU batches each of the two launches
+// fills about half of the CUs; together they run side by side instead of one after the other.
+// The grid is linearised x-fastest per part (the hardware's own dispatch order).
+template <int RED>
+__global__ __launch_bounds__(256, 2) void wino_bwd_pair_kernel(WinoConvArgs A, uint3 ga, WinoWgradArgs W, uint3 gw) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const unsigned na = ga.x * ga.y * ga.z;
+  unsigned b = blockIdx.x;
+  if (b < na) {
+    const uint3 id = make_uint3(b % ga.x, (b / ga.x) % ga.y, b / (ga.x * ga.y));
+    wino_dpp_body<8, 1>(A, id, ga, smem);
+  } else {
+    b -= na;
+    wino_wgrad_body<8, RED>(W, make_uint3(b % gw.x, b / gw.x, 0), smem);
   }
 }
 
@@ -599,9 +660,9 @@ static void run_wino(const float* x, const float* u, float* y, int B, int inC, i
     attr = true;
   }
   const int64_t slab = (int64_t)B * outC * H * H;
+  const WinoConvArgs a{x, u, y, inC, outC, ks > 1 ? nullptr : addend, st, (inC / kWCK) / ks, part, slab};
   hipLaunchKernelGGL((wino_dpp_kernel<H, IUPS>),
-                     dim3((unsigned)(B / wino_imgs(H)), (unsigned)(outC / kWBM), (unsigned)ks), dim3(256), kWLds, s,
-                     x, u, y, inC, outC, ks > 1 ? nullptr : addend, st, (inC / kWCK) / ks, part, slab);
+                     dim3((unsigned)(B / wino_imgs(H)), (unsigned)(outC / kWBM), (unsigned)ks), dim3(256), kWLds, s, a);
 }
 
 // y[B][outC][H][H] = conv3x3(x (zero-inserted 4x4 -> 8x8 when iups = 2), W) with u =
@@ -626,13 +687,42 @@ bool wino_wgrad_red(int B, int imgs) { return B <= 128 && imgs % 4 == 0; }
 void launch_wino_wgrad(const float* x, const float* dy, float* part, int B, int C, int Co, int H, int imgs,
                        hipStream_t s) {
   if (H != 8) return;
+  const WinoWgradArgs a{x, dy, part, C, Co, imgs};
   if (wino_wgrad_red(B, imgs)) {
     const dim3 grid((unsigned)(B / imgs), (unsigned)((Co / 16) * (C / 16)));
-    hipLaunchKernelGGL((wino_wgrad_kernel<8, 4>), grid, dim3(256), 0, s, x, dy, part, C, Co, imgs);
+    hipLaunchKernelGGL((wino_wgrad_kernel<8, 4>), grid, dim3(256), kWgRedLds, s, a);
   } else {
     const dim3 grid((unsigned)(B / imgs), (unsigned)(((Co / 16) * (C / 16) + 3) / 4));
-    hipLaunchKernelGGL((wino_wgrad_kernel<8, 1>), grid, dim3(256), 0, s, x, dy, part, C, Co, imgs);
+    hipLaunchKernelGGL((wino_wgrad_kernel<8, 1>), grid, dim3(256), 0, s, a);
   }
+}
+
+// grad-x (layer1 class, unsplit or split-K into `part_x`) and grad-W slabs of one conv in one launch
+void launch_wino_bwd_pair(const float* dy, const float* u, float* dx, int B, int inC, int outC, const float* addend,
+                          const ConvBnStats& st, int ks, float* part_x, const float* x, float* part_w, int imgs,
+                          hipStream_t s) {
+  // grad-x: inC = the forward's Co (dY channels), outC = the forward's C; grad-W of the forward
+  // conv C -> Co: x has outC channels, dY inC
+  const float* uk = u + 16 * (int64_t)inC * outC;
+  const WinoConvArgs a{dy, uk, dx, inC, outC, ks > 1 ? nullptr : addend, ks > 1 ? ConvBnStats{} : st, (inC / kWCK) / ks,
+                       part_x, (int64_t)B * outC * 64};
+  const uint3 ga = make_uint3((unsigned)(B / wino_imgs(8)), (unsigned)(outC / kWBM), (unsigned)ks);
+  const WinoWgradArgs w{x, dy, part_w, outC, inC, imgs};
+  const int C = outC, Co = inC;
+  const bool red = wino_wgrad_red(B, imgs);
+  const uint3 gw = make_uint3((unsigned)(B / imgs), (unsigned)(red ? (Co / 16) * (C / 16) : ((Co / 16) * (C / 16) + 3) / 4), 1);
+  const unsigned n = ga.x * ga.y * ga.z + gw.x * gw.y;
+  const size_t lds = kWLds > kWgRedLds ? kWLds : kWgRedLds;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(wino_bwd_pair_kernel<4>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)lds);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(wino_bwd_pair_kernel<1>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)lds);
+    attr = true;
+  }
+  if (red) hipLaunchKernelGGL(wino_bwd_pair_kernel<4>, dim3(n), dim3(256), lds, s, a, ga, w, gw);
+  else hipLaunchKernelGGL(wino_bwd_pair_kernel<1>, dim3(n), dim3(256), lds, s, a, ga, w, gw);
 }
 
 }  // namespace ndp

@@ -32,6 +32,8 @@ _STATS: dict = {}
 # BatchNorm statistics from the forward epilogue where the consuming BN takes the large-map
 # path (stem, layer1; ops/slablink.py).  NDP_FUSION_OFF=conv_bnstats restores the BN statistics pass.
 CONV_BN_STATS = fusion_on("conv_bnstats")
+# layer1 Winograd grad-x + grad-W of one conv in one launch (csrc/winograd.hip wino_bwd_pair_kernel)
+_PAIR = fusion_on("wino_pair")
 
 
 _WINO: dict = {}
@@ -201,10 +203,21 @@ class DirectConvFn(torch.autograd.Function):
             dw = grad_buffer(ctx.weight, weight)  # the dense arm's arena slice when registered
             part = torch.empty((B // wgrad_imgs) * weight.numel(), device=x.device, dtype=x.dtype)
             if gradfinish.can_defer(ctx.weight):  # slabs now, one batched sum later
-                ext().conv_wgrad(x, dy, part, None, list(geom))
+                # pair=True: a layer1 Winograd grad-W waits for this conv's grad-x below and both
+                # run in one launch (csrc/winograd.hip wino_bwd_pair_kernel); flushed at the end
+                ext().conv_wgrad(x, dy, part, None, list(geom), _PAIR)
                 gradfinish.defer_slab(part, dw, B // wgrad_imgs)
             else:
                 ext().conv_wgrad(x, dy, part, dw, list(geom))
+        try:
+            dx = DirectConvFn._grad_x(ctx, dy, x, weight, geom, s, p, dgrad_direct, ks_dgrad)
+        finally:
+            ext().conv_flush_pending()  # a grad-W the grad-x did not take (no-op otherwise)
+        return dx, dw, None, None, None, None, None, None
+
+    @staticmethod
+    def _grad_x(ctx, dy, x, weight, geom, s, p, dgrad_direct, ks_dgrad):
+        dx = None
         addend = ctx.link.take() if ctx.link is not None else None
         if ctx.needs_input_grad[0]:
             grad_slab = ctx.grad_slab
@@ -261,7 +274,7 @@ class DirectConvFn(torch.autograd.Function):
                 if br is not None and other is None:  # first of the two: the sibling adds onto it
                     br.put(dx)
                     dx = None
-        return dx, dw, None, None, None, None, None, None
+        return dx
 
 
 def _takes_addend(geom) -> bool:

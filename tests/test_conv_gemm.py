@@ -195,3 +195,34 @@ def test_gradw_finish_one_launch_equals_two(device):
             assert torch.equal(got, ref)
         for (_, got, geom), (_, ref, _) in zip(f_in, folds):
             assert torch.equal(got, ref), geom
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [512, 64, 24])
+def test_wino_bwd_pair_is_bitwise(device, batch):
+    """Layer1 Winograd grad-x + grad-W in one launch (csrc/winograd.hip wino_bwd_pair_kernel) ==
+    the two launches, bitwise, at an unsplit (512: 4-wave-free grad-W), a split-K (64: 4-wave
+    reduction) and a non-Winograd (24) per-GPU batch; nothing is left pending after backward()."""
+    from network_distributed_pytorch_amd.models import build_resnet
+    from network_distributed_pytorch_amd.ops import conv as conv_ops
+    from network_distributed_pytorch_amd.ops._ext import ext
+
+    det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
+    outs = []
+    try:
+        for pair in (False, True):
+            conv_ops._PAIR = pair
+            torch.manual_seed(3)
+            m = build_resnet(18, 10).to(device)
+            x = torch.randn(batch, 3, 32, 32, device=device, generator=torch.Generator(device=device).manual_seed(1))
+            for _ in range(2):
+                m.zero_grad()
+                m(x).square().mean().backward()
+            ext().conv_flush_pending()  # must be a no-op: every held-back grad-W was launched
+            outs.append([p.grad.clone() for p in m.parameters()])
+    finally:
+        conv_ops._PAIR = True
+        torch.backends.cudnn.deterministic = det
+    for (n, _), a, b in zip(m.named_parameters(), *outs):
+        assert torch.equal(a, b), n
