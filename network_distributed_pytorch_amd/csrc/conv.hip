@@ -12,6 +12,7 @@
 #include <stdlib.h>
 
 #include "ndp_kernels.h"
+#include "wino_dpp.h"
 
 namespace ndp {
 
@@ -910,17 +911,18 @@ struct ConvWgCfg {
   static_assert(P % 2 == 0 && PQ % 4 == 0 && HW % 4 == 0 && NSTEP % KB == 0, "pixel pairing / float4 loads");
 };
 
+// (a device function of the workgroup's grid coordinates: the layer2 backward pairs run it on
+// one part of a combined grid, launch_conv_dgrad)
 template <int R, int S, int ST, int PD, int H, int W, int CB, int BM, int NW, int NBPW, int KB>
-__global__ __launch_bounds__(64 * NW) void conv_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy,
-                                                             float* __restrict__ part, int Cin, int Kout,
-                                                             int imgs_per_slice) {
+__device__ __forceinline__ void conv_wgrad_body(const float* __restrict__ x, const float* __restrict__ dy,
+                                                float* __restrict__ part, int Cin, int Kout, int imgs_per_slice,
+                                                const uint3 bid, float* __restrict__ smem) {
   using G = ConvWgCfg<R, S, ST, PD, H, W, CB, BM, NW, NBPW, KB>;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
   float* As = smem;                 // [2][A_SZ]
   float* Bs = smem + 2 * G::A_SZ;   // [2][B_SZ]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, l32 = lane & 31;
-  const int slice = blockIdx.x, m0 = blockIdx.y * BM, c0 = blockIdx.z * CB;
+  const int slice = bid.x, m0 = bid.y * BM, c0 = bid.z * CB;
   const int bb = slice * imgs_per_slice;
 
   for (int i = tid; i < 2 * G::B_SZ; i += G::NT) Bs[i] = 0.f;
@@ -1084,6 +1086,37 @@ __global__ __launch_bounds__(64 * NW) void conv_wgrad_kernel(const float* __rest
         out[((int64_t)m * Cin + c0 + c) * G::RS + rs] = acc[t][r];
       }
     }
+  }
+}
+
+template <int R, int S, int ST, int PD, int H, int W, int CB, int BM, int NW, int NBPW, int KB>
+__global__ __launch_bounds__(64 * NW) void conv_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                                             float* __restrict__ part, int Cin, int Kout,
+                                                             int imgs_per_slice) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  conv_wgrad_body<R, S, ST, PD, H, W, CB, BM, NW, NBPW, KB>(x, dy, part, Cin, Kout, imgs_per_slice,
+                                                           make_uint3(blockIdx.x, blockIdx.y, blockIdx.z), smem);
+}
+
+// A layer2 backward pair in ONE launch: workgroups [0, n_dgrad) run the Winograd grad-x
+// (wino_dpp.h; 4x4 maps, or the 3x3/2 conv's zero-inserted 8x8 dY), the rest the direct grad-W of
+// the same conv (64 NW threads: the surplus wave leaves before any barrier, which then waits for
+// the live waves only).  Both read only dY / x / the weights and write disjoint outputs.
+template <int WH, int IUPS, int R, int S, int ST, int PD, int H, int W, int CB, int BM, int NW, int NBPW, int KB>
+__global__ __launch_bounds__(256, 2) void wino_direct_pair_kernel(WinoConvArgs A, uint3 ga, const float* __restrict__ x,
+                                                                  const float* __restrict__ dy, float* __restrict__ part,
+                                                                  int Cin, int Kout, int imgs, uint3 gw) {
+  static_assert(NW <= 4, "grad-W workgroup within the pair's 256 threads");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const unsigned na = ga.x * ga.y * ga.z;
+  unsigned b = blockIdx.x;
+  if (b < na) {
+    wino_dpp_body<WH, IUPS>(A, make_uint3(b % ga.x, (b / ga.x) % ga.y, b / (ga.x * ga.y)), ga, smem);
+  } else {
+    if (threadIdx.x >= 64 * NW) return;
+    b -= na;
+    conv_wgrad_body<R, S, ST, PD, H, W, CB, BM, NW, NBPW, KB>(
+        x, dy, part, Cin, Kout, imgs, make_uint3(b % gw.x, (b / gw.x) % gw.y, b / (gw.x * gw.y)), smem);
   }
 }
 
@@ -1470,18 +1503,38 @@ struct PendingWgrad {
   const float* x = nullptr;
   const float* dy = nullptr;
   float* part = nullptr;
-  int B = 0, imgs = 0;
+  int B = 0, imgs = 0, cls = -1;
   ConvGeom g{};
   hipStream_t s = nullptr;
 };
 PendingWgrad g_pending;
+
+// grad-x of a layer2 class on the Winograd kernel + the held-back direct grad-W, one launch
+template <int WH, int IUPS, int R, int S, int ST, int PD, int H, int W, int CB, int BM, int NW, int NBPW, int KB>
+void run_pair(const float* dy, const float* u, float* dx, int B, int inC, int outC, const float* addend,
+              const ConvBnStats& st, int ks, float* part_x, const PendingWgrad& p, hipStream_t s) {
+  using G = ConvWgCfg<R, S, ST, PD, H, W, CB, BM, NW, NBPW, KB>;
+  auto k = wino_direct_pair_kernel<WH, IUPS, R, S, ST, PD, H, W, CB, BM, NW, NBPW, KB>;
+  constexpr size_t lds = kWLds > G::LDS_BYTES ? kWLds : G::LDS_BYTES;
+  static bool attr = false;
+  if (!attr) { set_lds(k, lds); attr = true; }
+  const WinoConvArgs a{dy, u + 16 * (int64_t)inC * outC,  // the grad-x half of the transforms
+                       dx, inC, outC, ks > 1 ? nullptr : addend, ks > 1 ? ConvBnStats{} : st, (inC / kWCK) / ks,
+                       part_x, (int64_t)B * outC * WH * WH};
+  const uint3 ga = make_uint3((unsigned)(B / wino_imgs(WH)), (unsigned)(outC / kWBM), (unsigned)ks);
+  const uint3 gw = make_uint3((unsigned)(p.B / p.imgs), (unsigned)(p.g.Co / BM), (unsigned)((p.g.C + CB - 1) / CB));
+  const unsigned n = ga.x * ga.y * ga.z + gw.x * gw.y * gw.z;
+  hipLaunchKernelGGL(k, dim3(n), dim3(256), lds, s, a, ga, p.x, p.dy, p.part, p.g.C, p.g.Co, p.imgs, gw);
+}
 }  // namespace
 
 void conv_flush_pending() {
   if (g_pending.dy == nullptr) return;
   const PendingWgrad p = g_pending;
   g_pending = PendingWgrad{};
-  launch_wino_wgrad(p.x, p.dy, p.part, p.B, p.g.C, p.g.Co, p.g.H, p.imgs, p.s);
+  if (p.cls == 0) launch_wino_wgrad(p.x, p.dy, p.part, p.B, p.g.C, p.g.Co, p.g.H, p.imgs, p.s);
+  else if (p.cls == 1) run_wgrad<3, 3, 1, 1, 4, 4, 32, 32, 3, 3, 4>(p.x, p.dy, p.part, nullptr, p.B, p.g.C, p.g.Co, p.imgs, p.s);
+  else run_wgrad<3, 3, 2, 1, 8, 8, 32, 32, 3, 3, 4>(p.x, p.dy, p.part, nullptr, p.B, p.g.C, p.g.Co, p.imgs, p.s);
 }
 
 // dx[B, C, H, W] from dy[B, Co, OH, OW]
@@ -1492,9 +1545,14 @@ int launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const C
   const int ks = conv_ksplit(cls, g, B, true);
   if (wino_u != nullptr && conv_wino(cls, g, B, true)) {
     const PendingWgrad& p = g_pending;
-    if (cls == 0 && p.dy == dy && p.s == s && p.B == B && p.g.C == g.C && p.g.Co == g.Co && p.g.H == 8) {
+    if (p.cls == cls && p.dy == dy && p.s == s && p.B == B && p.g.C == g.C && p.g.Co == g.Co && p.g.H == g.H) {
       // this conv's grad-W is waiting: both in one launch
-      launch_wino_bwd_pair(dy, wino_u, dx, B, g.Co, g.C, addend, stats, ks, part, p.x, p.part, p.imgs, s);
+      if (cls == 0)
+        launch_wino_bwd_pair(dy, wino_u, dx, B, g.Co, g.C, addend, stats, ks, part, p.x, p.part, p.imgs, s);
+      else if (cls == 1)
+        run_pair<4, 1, 3, 3, 1, 1, 4, 4, 32, 32, 3, 3, 4>(dy, wino_u, dx, B, g.Co, g.C, addend, stats, ks, part, p, s);
+      else
+        run_pair<8, 2, 3, 3, 2, 1, 8, 8, 32, 32, 3, 3, 4>(dy, wino_u, dx, B, g.Co, g.C, addend, stats, ks, part, p, s);
       g_pending = PendingWgrad{};
     } else {
       conv_flush_pending();
@@ -1529,12 +1587,13 @@ void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, 
   const int cls = conv_direct_class(g);
   const int imgs = conv_wgrad_imgs(cls, g, B);
   if (cls == 0 && wino_wgrad_ok(g.C, g.Co, g.H)) {
-    // held back for this conv's grad-x (launch_conv_dgrad) at the per-GPU batches that take the
-    // 4-wave grad-W (<= 128), where neither launch fills the CUs alone: ResNet-18 r=4 batch 64
-    // 0.7758 / 0.7656 -> 0.7498 / 0.7517 ms, 128 0.8676 -> 0.8434; at 512 the pair was slower,
-    // 1.4640 -> 1.4818 (the grad-W drops from 3 to 2 waves per SIMD; profiles/r6/bench_wino_pair.jsonl)
-    if (pair && dw == nullptr && wino_wgrad_red(B, imgs)) {
-      g_pending = PendingWgrad{x, dy, part, B, imgs, g, s};
+    // held back for this conv's grad-x (launch_conv_dgrad) up to per-GPU batch 256, where neither
+    // launch fills the CUs alone.  ResNet-18 r=4, ms/step (profiles/r6/bench_wino_pair.jsonl):
+    // batch 64 0.7758 / 0.7656 -> 0.7498 / 0.7517, 128 0.8676 -> 0.8434, 256 (with the layer2 pairs)
+    // 1.0539 / 1.0572 -> 1.0303 / 1.0343; at 512 the pair was slower or even, 1.4640 -> 1.4818 and
+    // 1.4433 / 1.4427 -> 1.4546 / 1.4511 (the grad-W drops from 3 to 2 waves per SIMD)
+    if (pair && dw == nullptr && B <= 256) {
+      g_pending = PendingWgrad{x, dy, part, B, imgs, cls, g, s};
       return;
     }
     // Winograd-domain grad-W (winograd.hip): same slab layout and slicing as the direct kernel.
@@ -1547,6 +1606,13 @@ void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, 
       hipLaunchKernelGGL(conv_slab_sum_kernel, dim3((unsigned)((n / 4 + 15) / 16)), dim3(256), 0, s, part, dw, n,
                          B / imgs);
     }
+    return;
+  }
+  // the layer2 3x3 classes likewise, at every batch, when their grad-x takes the Winograd kernel
+  // (with / without the layer2 pairs, ms/step: batch 64 0.7381 / 0.7371 vs 0.7493 / 0.7495, 256
+  // 1.0539 / 1.0572 vs 1.0700 / 1.0783, 512 1.4433 / 1.4427 vs 1.4566 / 1.4542)
+  if (pair && dw == nullptr && (cls == 1 || cls == 2) && conv_wino(cls, g, B, true)) {
+    g_pending = PendingWgrad{x, dy, part, B, imgs, cls, g, s};
     return;
   }
   switch (cls) {
