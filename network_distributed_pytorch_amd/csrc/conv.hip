@@ -1555,13 +1555,13 @@ int launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const C
         run_pair<8, 2, 3, 3, 2, 1, 8, 8, 32, 32, 3, 3, 4>(dy, wino_u, dx, B, g.Co, g.C, addend, stats, ks, part, p, s);
       g_pending = PendingWgrad{};
     } else {
-      conv_flush_pending();
+      if (p.dy == dy) conv_flush_pending();  // this conv's own grad-W, not pairable after all
       launch_wino_conv(dy, wino_u, dx, B, g.Co, g.C, g.H, true, cls == 2 ? 2 : 1, addend,
                        ks > 1 ? ConvBnStats{} : stats, ks, part, s);
     }
     return ks > 1 ? wino_slabs(part, dx, (int64_t)B * g.C * g.H * g.W, ks, defer, addend, s) : 1;
   }
-  conv_flush_pending();
+  if (g_pending.dy == dy) conv_flush_pending();
   switch (cls) {
     case 0:
       return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true, true, 1, 2>(dy, w, dx, B, g.Co, g.C, ks, part, s,
@@ -1583,7 +1583,8 @@ int launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const C
 // part: (B / conv_wgrad_imgs) * Co * C * KH * KW floats of scratch
 void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, int B, const ConvGeom& g,
                        hipStream_t s, bool pair) {
-  conv_flush_pending();
+  // a grad-W held back earlier stays held (its grad-x may come later, e.g. from the BranchLink
+  // sibling's backward) unless this one takes the single slot
   const int cls = conv_direct_class(g);
   const int imgs = conv_wgrad_imgs(cls, g, B);
   if (cls == 0 && wino_wgrad_ok(g.C, g.Co, g.H)) {
@@ -1593,6 +1594,7 @@ void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, 
     // 1.0539 / 1.0572 -> 1.0303 / 1.0343; at 512 the pair was slower or even, 1.4640 -> 1.4818 and
     // 1.4433 / 1.4427 -> 1.4546 / 1.4511 (the grad-W drops from 3 to 2 waves per SIMD)
     if (pair && dw == nullptr && B <= 256) {
+      conv_flush_pending();
       g_pending = PendingWgrad{x, dy, part, B, imgs, cls, g, s};
       return;
     }
@@ -1608,10 +1610,13 @@ void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, 
     }
     return;
   }
-  // the layer2 3x3 classes likewise, at every batch, when their grad-x takes the Winograd kernel
-  // (with / without the layer2 pairs, ms/step: batch 64 0.7381 / 0.7371 vs 0.7493 / 0.7495, 256
-  // 1.0539 / 1.0572 vs 1.0700 / 1.0783, 512 1.4433 / 1.4427 vs 1.4566 / 1.4542)
-  if (pair && dw == nullptr && (cls == 1 || cls == 2) && conv_wino(cls, g, B, true)) {
+  // the layer2 3x3 classes likewise when their grad-x takes the Winograd kernel: the 3x3 class at
+  // every batch (with / without, ms/step: batch 64 0.7381 / 0.7371 vs 0.7493 / 0.7495, 256
+  // 1.0539 / 1.0572 vs 1.0700 / 1.0783, 512 1.4433 / 1.4427 vs 1.4566 / 1.4542); the 3x3/2 class
+  // (its grad-x comes from the downsample sibling's backward) up to 256 (128 0.8243 vs 0.8303, 256
+  // 1.0196 vs 1.0339, 64 0.7295-0.7439 vs 0.7329-0.7385; 512 1.4504 / 1.4453 vs 1.4470 / 1.4431)
+  if (pair && dw == nullptr && (cls == 1 || (cls == 2 && B <= 256)) && conv_wino(cls, g, B, true)) {
+    conv_flush_pending();
     g_pending = PendingWgrad{x, dy, part, B, imgs, cls, g, s};
     return;
   }

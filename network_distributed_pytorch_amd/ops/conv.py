@@ -203,16 +203,14 @@ class DirectConvFn(torch.autograd.Function):
             dw = grad_buffer(ctx.weight, weight)  # the dense arm's arena slice when registered
             part = torch.empty((B // wgrad_imgs) * weight.numel(), device=x.device, dtype=x.dtype)
             if gradfinish.can_defer(ctx.weight):  # slabs now, one batched sum later
-                # pair=True: a layer1 Winograd grad-W waits for this conv's grad-x below and both
-                # run in one launch (csrc/winograd.hip wino_bwd_pair_kernel); flushed at the end
+                # pair=True: a Winograd-class grad-W waits for this conv's grad-x (below, or in the
+                # BranchLink sibling's backward) and both run in one launch (csrc/conv.hip
+                # launch_conv_dgrad); one that no grad-x took is launched by gradfinish.flush()
                 ext().conv_wgrad(x, dy, part, None, list(geom), _PAIR)
-                gradfinish.defer_slab(part, dw, B // wgrad_imgs)
+                gradfinish.defer_slab(part, dw, B // wgrad_imgs, keep=(x, dy) if _PAIR else ())
             else:
                 ext().conv_wgrad(x, dy, part, dw, list(geom))
-        try:
-            dx = DirectConvFn._grad_x(ctx, dy, x, weight, geom, s, p, dgrad_direct, ks_dgrad)
-        finally:
-            ext().conv_flush_pending()  # a grad-W the grad-x did not take (no-op otherwise)
+        dx = DirectConvFn._grad_x(ctx, dy, x, weight, geom, s, p, dgrad_direct, ks_dgrad)
         return dx, dw, None, None, None, None, None, None
 
     @staticmethod

@@ -29,6 +29,7 @@ _ENABLED = fusion_on("defer_gradw")
 _slabs: list = []
 _folds: list = []
 _queued = [False]
+_keep: list = []
 
 
 def enabled() -> bool:
@@ -104,9 +105,12 @@ def _alias(t: torch.Tensor) -> torch.Tensor:
                                                                t.stride())
 
 
-def defer_slab(part: torch.Tensor, dw: torch.Tensor, slices: int) -> None:
-    """``dw`` (the buffer the backward returns) = sum over ``slices`` slabs of ``part``, later."""
+def defer_slab(part: torch.Tensor, dw: torch.Tensor, slices: int, keep=()) -> None:
+    """``dw`` (the buffer the backward returns) = sum over ``slices`` slabs of ``part``, later.
+    ``keep``: tensors a held-back grad-W launch still reads (csrc/conv.hip conv_flush_pending:
+    the grad-W waits for its conv's grad-x to share one launch), kept alive until the flush."""
     _slabs.append((part, _alias(dw), int(slices)))
+    _keep.extend(keep)
     _queue()
 
 
@@ -121,6 +125,8 @@ def flush() -> None:
     if not _slabs and not _folds:
         return
     X = ext()
+    X.conv_flush_pending()  # a grad-W still held back for a grad-x that never came: its slabs first
+    _keep.clear()
     slabs, folds = list(_slabs), list(_folds)
     _slabs.clear()
     _folds.clear()
