@@ -474,26 +474,28 @@ struct ConvFwdCfg {
 // correlation of the zero-inserted dY with the flipped weights:
 //   dX[c, h, w] = sum_{k,r,s} W[k, c, 2-r, 2-s] * Z[k, h-1+r, w-1+s],  Z[k, 2p, 2q] = dY[k, p, q]
 
+// (a device function of the workgroup's grid coordinates: the downsample-conv backward pairs run it
+// on one part of a combined grid, launch_conv_dgrad)
 template <int R, int S, int ST, int PD, int H, int W, int CK, int BM, int IMGS, int WM, int NBUF, int KB, bool TRANSW,
           bool VEC, int UPS = 1, int SCH = 0, int IUPS = 1, int PSPLIT = 1>
-__global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                                       float* __restrict__ y, float* __restrict__ part, int Cin,
-                                                       int Kout, int cps, int64_t slab,
-                                                       const float* __restrict__ addend, ConvBnStats st) {
+__device__ __forceinline__ void conv_fwd_body(const float* __restrict__ x, const float* __restrict__ w,
+                                              float* __restrict__ y, float* __restrict__ part, int Cin, int Kout,
+                                              int cps, int64_t slab, const float* __restrict__ addend,
+                                              const ConvBnStats& st, const uint3 bid, const uint3 gdim,
+                                              float* __restrict__ smem) {
   using G = ConvFwdCfg<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW, PSPLIT>;
   constexpr int AE = (BM * G::KK + 3) / 4;  // float4 slots (scalar path: 4 scalars per slot)
   constexpr int A_PER_T = (AE + 255) / 256;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
   float* As = smem;
   float* Bs = smem + NBUF * G::A_SZ;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
   const int h = lane >> 5, l32 = lane & 31;
-  const int m0 = blockIdx.y * BM;
-  const int b0 = (PSPLIT == 1 ? blockIdx.x : blockIdx.x / PSPLIT) * IMGS;
-  const int prow0 = PSPLIT == 1 ? 0 : (blockIdx.x % PSPLIT) * (G::P / PSPLIT);  // first output row
+  const int m0 = bid.y * BM;
+  const int b0 = (PSPLIT == 1 ? bid.x : bid.x / PSPLIT) * IMGS;
+  const int prow0 = PSPLIT == 1 ? 0 : (bid.x % PSPLIT) * (G::P / PSPLIT);  // first output row
   // split-K: workgroup z reduces channel chunks [ch0, ch0 + nchunks) into output slab z
-  const int ch0 = blockIdx.z * cps;
+  const int ch0 = bid.z * cps;
   const int nchunks = min((Cin + CK - 1) / CK - ch0, cps);
 
   for (int i = tid; i < NBUF * G::B_SZ; i += 256) Bs[i] = 0.f;  // zero borders (never rewritten)
@@ -731,8 +733,8 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
   // (deterministic).  A last-arrival fixup inside this kernel was measured 4x slower: the
   // agent-scope release fence writes the XCD's L2 back and the fixing workgroup re-reads
   // the other XCDs' slabs from HBM on a serial dependency chain.
-  if (gridDim.z > 1) {
-    float* pz = part + (int64_t)blockIdx.z * slab;
+  if (gdim.z > 1) {
+    float* pz = part + (int64_t)bid.z * slab;
 #pragma unroll
     for (int tm = 0; tm < G::TM; ++tm)
 #pragma unroll
@@ -862,12 +864,24 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
         sq += __shfl_xor(sq, o, 64);
       }
       if (j == 0) {
-        double* d = st.out + ((int64_t)(m0 + c) * gridDim.x + blockIdx.x) * 2;
+        double* d = st.out + ((int64_t)(m0 + c) * gdim.x + bid.x) * 2;
         d[0] = sum;
         d[1] = sq;
       }
     }
   }
+}
+
+template <int R, int S, int ST, int PD, int H, int W, int CK, int BM, int IMGS, int WM, int NBUF, int KB, bool TRANSW,
+          bool VEC, int UPS = 1, int SCH = 0, int IUPS = 1, int PSPLIT = 1>
+__global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                       float* __restrict__ y, float* __restrict__ part, int Cin,
+                                                       int Kout, int cps, int64_t slab,
+                                                       const float* __restrict__ addend, ConvBnStats st) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  conv_fwd_body<R, S, ST, PD, H, W, CK, BM, IMGS, WM, NBUF, KB, TRANSW, VEC, UPS, SCH, IUPS, PSPLIT>(
+      x, w, y, part, Cin, Kout, cps, slab, addend, st, make_uint3(blockIdx.x, blockIdx.y, blockIdx.z),
+      make_uint3(gridDim.x, gridDim.y, gridDim.z), smem);
 }
 
 // ---- grad-W -----------------------------------------------------------------------------
@@ -1243,6 +1257,39 @@ static void set_lds(KernelT k, size_t bytes) {
   hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
+// A downsample conv's backward pair (the 1x1 stride-2 classes) in ONE launch: workgroups
+// [0, n_dgrad) run the direct grad-x (conv_fwd_body on the transposed weights, UPS = 2 epilogue),
+// the rest the direct grad-W (64 NW threads; the surplus waves leave before any barrier).
+struct DirectDgradArgs {
+  const float* dy;
+  const float* w;
+  float* dx;
+  float* part;
+  int Cin, Kout, cps;
+  int64_t slab;
+  const float* addend;
+};
+template <int DH, int DW, int DBM, int DIMGS, int R, int S, int ST, int PD, int H, int W, int CB, int BM, int NW,
+          int NBPW, int KB>
+__global__ __launch_bounds__(256) void direct_pair_kernel(DirectDgradArgs A, uint3 ga, const float* __restrict__ x,
+                                                          const float* __restrict__ dy, float* __restrict__ part,
+                                                          int Cin, int Kout, int imgs, uint3 gw) {
+  static_assert(NW <= 4, "grad-W workgroup within the pair's 256 threads");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const unsigned na = ga.x * ga.y * ga.z;
+  unsigned b = blockIdx.x;
+  if (b < na) {
+    conv_fwd_body<1, 1, 1, 0, DH, DW, 8, DBM, DIMGS, 2, 2, 4, true, true, 2>(
+        A.dy, A.w, A.dx, A.part, A.Cin, A.Kout, A.cps, A.slab, A.addend, ConvBnStats{},
+        make_uint3(b % ga.x, (b / ga.x) % ga.y, b / (ga.x * ga.y)), ga, smem);
+  } else {
+    if (threadIdx.x >= 64 * NW) return;
+    b -= na;
+    conv_wgrad_body<R, S, ST, PD, H, W, CB, BM, NW, NBPW, KB>(
+        x, dy, part, Cin, Kout, imgs, make_uint3(b % gw.x, (b / gw.x) % gw.y, b / (gw.x * gw.y)), smem);
+  }
+}
+
 // ksplit > 1: the ksplit workgroups of an output tile each reduce 1/ksplit of the input
 // channels into their own slab of `part`; conv_slab_sum(_ups) adds the slabs in split order
 // (deterministic).  Used where B / IMGS * Kout / BM alone cannot fill the 256 CUs
@@ -1507,7 +1554,43 @@ struct PendingWgrad {
   ConvGeom g{};
   hipStream_t s = nullptr;
 };
-PendingWgrad g_pending;
+// two slots: a downsample block's two sibling convs (3x3/2 and 1x1/2) each hold one while the
+// BranchLink defers one of their grad-x launches into the other's backward
+constexpr int kPendingSlots = 2;
+PendingWgrad g_pending[kPendingSlots];
+unsigned g_pending_seq[kPendingSlots];
+unsigned g_seq = 0;
+
+void launch_pending(const PendingWgrad& p);
+// the held-back grad-W of THIS grad-x's conv (same dY, same geometry and stream), or nullptr
+PendingWgrad* find_pending(const float* dy, int cls, int B, const ConvGeom& g, hipStream_t s) {
+  for (auto& p : g_pending)
+    if (p.dy == dy && p.cls == cls && p.s == s && p.B == B && p.g.C == g.C && p.g.Co == g.Co && p.g.H == g.H) return &p;
+  return nullptr;
+}
+// launch (alone) whatever is held for this dY
+void flush_pending_dy(const float* dy) {
+  for (auto& p : g_pending)
+    if (p.dy == dy) {
+      const PendingWgrad q = p;
+      p = PendingWgrad{};
+      launch_pending(q);
+    }
+}
+// hold a grad-W: a free slot, else the oldest one is launched alone first
+void hold_pending(const PendingWgrad& q) {
+  int k = -1;
+  for (int i = 0; i < kPendingSlots; ++i)
+    if (g_pending[i].dy == nullptr) { k = i; break; }
+  if (k < 0) {
+    k = g_pending_seq[0] <= g_pending_seq[1] ? 0 : 1;
+    const PendingWgrad old = g_pending[k];
+    g_pending[k] = PendingWgrad{};
+    launch_pending(old);
+  }
+  g_pending[k] = q;
+  g_pending_seq[k] = ++g_seq;
+}
 
 // grad-x of a layer2 class on the Winograd kernel + the held-back direct grad-W, one launch
 template <int WH, int IUPS, int R, int S, int ST, int PD, int H, int W, int CB, int BM, int NW, int NBPW, int KB>
@@ -1526,15 +1609,54 @@ void run_pair(const float* dy, const float* u, float* dx, int B, int inC, int ou
   const unsigned n = ga.x * ga.y * ga.z + gw.x * gw.y * gw.z;
   hipLaunchKernelGGL(k, dim3(n), dim3(256), lds, s, a, ga, p.x, p.dy, p.part, p.g.C, p.g.Co, p.imgs, gw);
 }
-}  // namespace
+// the 1x1 stride-2 grad-x (run_fwd's UPS = 2 path, incl. its split-K slab sum) + the held-back direct
+// grad-W of the same conv, one launch
+template <int DH, int DW, int DIMGS, int R, int S, int ST, int PD, int H, int W, int CB, int BM, int NW, int NBPW,
+          int KB>
+int run_direct_pair(const float* dy, const float* w, float* dx, int B, int Cin, int Kout, int ksplit, float* part,
+                    const float* addend, const PendingWgrad& p, hipStream_t s) {
+  using GF = ConvFwdCfg<1, 1, 1, 0, DH, DW, 8, 64, DIMGS, 2, 2, 4, true, 1>;
+  using GW = ConvWgCfg<R, S, ST, PD, H, W, CB, BM, NW, NBPW, KB>;
+  auto k = direct_pair_kernel<DH, DW, 64, DIMGS, R, S, ST, PD, H, W, CB, BM, NW, NBPW, KB>;
+  constexpr size_t lds = GF::LDS_BYTES > GW::LDS_BYTES ? GF::LDS_BYTES : GW::LDS_BYTES;
+  static bool attr = false;
+  if (!attr) { set_lds(k, lds); attr = true; }
+  const int nchunks = (Cin + 7) / 8;
+  if (ksplit < 1 || part == nullptr) ksplit = 1;
+  const int cps = (nchunks + ksplit - 1) / ksplit;
+  ksplit = (nchunks + cps - 1) / cps;
+  const int64_t slab = (int64_t)B * Kout * GF::PQ;
+  const DirectDgradArgs a{dy, w, dx, part, Cin, Kout, cps, slab, ksplit > 1 ? nullptr : addend};
+  const uint3 ga = make_uint3((unsigned)(B / DIMGS), (unsigned)(Kout / 64), (unsigned)ksplit);
+  const uint3 gw = make_uint3((unsigned)(p.B / p.imgs), (unsigned)(p.g.Co / BM), (unsigned)((p.g.C + CB - 1) / CB));
+  const unsigned n = ga.x * ga.y * ga.z + gw.x * gw.y * gw.z;
+  hipLaunchKernelGGL(k, dim3(n), dim3(256), lds, s, a, ga, p.x, p.dy, p.part, p.g.C, p.g.Co, p.imgs, gw);
+  if (ksplit > 1)
+    hipLaunchKernelGGL((conv_slab_sum_ups_kernel<GF::P, GF::Q>), dim3((unsigned)((slab + 255) / 256)), dim3(256), 0, s,
+                       part, dx, slab, ksplit, addend);
+  return 1;
+}
 
-void conv_flush_pending() {
-  if (g_pending.dy == nullptr) return;
-  const PendingWgrad p = g_pending;
-  g_pending = PendingWgrad{};
+void launch_pending(const PendingWgrad& p) {
   if (p.cls == 0) launch_wino_wgrad(p.x, p.dy, p.part, p.B, p.g.C, p.g.Co, p.g.H, p.imgs, p.s);
   else if (p.cls == 1) run_wgrad<3, 3, 1, 1, 4, 4, 32, 32, 3, 3, 4>(p.x, p.dy, p.part, nullptr, p.B, p.g.C, p.g.Co, p.imgs, p.s);
-  else run_wgrad<3, 3, 2, 1, 8, 8, 32, 32, 3, 3, 4>(p.x, p.dy, p.part, nullptr, p.B, p.g.C, p.g.Co, p.imgs, p.s);
+  else if (p.cls == 2) run_wgrad<3, 3, 2, 1, 8, 8, 32, 32, 3, 3, 4>(p.x, p.dy, p.part, nullptr, p.B, p.g.C, p.g.Co, p.imgs, p.s);
+  else if (p.cls == 4) run_wgrad<1, 1, 2, 0, 8, 8, 32, 32, 1, 1, 4>(p.x, p.dy, p.part, nullptr, p.B, p.g.C, p.g.Co, p.imgs, p.s);
+  else run_wgrad<1, 1, 2, 0, 4, 4, 32, 32, 1, 1, 2>(p.x, p.dy, p.part, nullptr, p.B, p.g.C, p.g.Co, p.imgs, p.s);
+}
+}  // namespace
+
+// every held-back grad-W, oldest first
+void conv_flush_pending() {
+  while (true) {
+    int k = -1;
+    for (int i = 0; i < kPendingSlots; ++i)
+      if (g_pending[i].dy != nullptr && (k < 0 || g_pending_seq[i] < g_pending_seq[k])) k = i;
+    if (k < 0) return;
+    const PendingWgrad p = g_pending[k];
+    g_pending[k] = PendingWgrad{};
+    launch_pending(p);
+  }
 }
 
 // dx[B, C, H, W] from dy[B, Co, OH, OW]
@@ -1544,24 +1666,32 @@ int launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const C
   const int cls = conv_direct_class(g);
   const int ks = conv_ksplit(cls, g, B, true);
   if (wino_u != nullptr && conv_wino(cls, g, B, true)) {
-    const PendingWgrad& p = g_pending;
-    if (p.cls == cls && p.dy == dy && p.s == s && p.B == B && p.g.C == g.C && p.g.Co == g.Co && p.g.H == g.H) {
+    if (PendingWgrad* pp = find_pending(dy, cls, B, g, s)) {
       // this conv's grad-W is waiting: both in one launch
+      const PendingWgrad p = *pp;
+      *pp = PendingWgrad{};
       if (cls == 0)
         launch_wino_bwd_pair(dy, wino_u, dx, B, g.Co, g.C, addend, stats, ks, part, p.x, p.part, p.imgs, s);
       else if (cls == 1)
         run_pair<4, 1, 3, 3, 1, 1, 4, 4, 32, 32, 3, 3, 4>(dy, wino_u, dx, B, g.Co, g.C, addend, stats, ks, part, p, s);
       else
         run_pair<8, 2, 3, 3, 2, 1, 8, 8, 32, 32, 3, 3, 4>(dy, wino_u, dx, B, g.Co, g.C, addend, stats, ks, part, p, s);
-      g_pending = PendingWgrad{};
     } else {
-      if (p.dy == dy) conv_flush_pending();  // this conv's own grad-W, not pairable after all
+      flush_pending_dy(dy);  // this conv's own grad-W, not pairable after all
       launch_wino_conv(dy, wino_u, dx, B, g.Co, g.C, g.H, true, cls == 2 ? 2 : 1, addend,
                        ks > 1 ? ConvBnStats{} : stats, ks, part, s);
     }
     return ks > 1 ? wino_slabs(part, dx, (int64_t)B * g.C * g.H * g.W, ks, defer, addend, s) : 1;
   }
-  if (g_pending.dy == dy) conv_flush_pending();
+  if (PendingWgrad* pp = (cls == 4 || cls == 5) ? find_pending(dy, cls, B, g, s) : nullptr) {
+    // the downsample conv's grad-W is waiting: both in one launch
+    const PendingWgrad p = *pp;
+    *pp = PendingWgrad{};
+    return cls == 4
+        ? run_direct_pair<4, 4, 4, 1, 1, 2, 0, 8, 8, 32, 32, 1, 1, 4>(dy, w, dx, B, g.Co, g.C, ks, part, addend, p, s)
+        : run_direct_pair<2, 2, 16, 1, 1, 2, 0, 4, 4, 32, 32, 1, 1, 2>(dy, w, dx, B, g.Co, g.C, ks, part, addend, p, s);
+  }
+  flush_pending_dy(dy);
   switch (cls) {
     case 0:
       return run_fwd<3, 3, 1, 1, 8, 8, 8, 64, 1, 2, 2, 4, true, true, 1, 2>(dy, w, dx, B, g.Co, g.C, ks, part, s,
@@ -1584,7 +1714,7 @@ int launch_conv_dgrad(const float* dy, const float* w, float* dx, int B, const C
 void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, int B, const ConvGeom& g,
                        hipStream_t s, bool pair) {
   // a grad-W held back earlier stays held (its grad-x may come later, e.g. from the BranchLink
-  // sibling's backward) unless this one takes the single slot
+  // sibling's backward) unless this one needs its slot
   const int cls = conv_direct_class(g);
   const int imgs = conv_wgrad_imgs(cls, g, B);
   if (cls == 0 && wino_wgrad_ok(g.C, g.Co, g.H)) {
@@ -1594,8 +1724,7 @@ void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, 
     // 1.0539 / 1.0572 -> 1.0303 / 1.0343; at 512 the pair was slower or even, 1.4640 -> 1.4818 and
     // 1.4433 / 1.4427 -> 1.4546 / 1.4511 (the grad-W drops from 3 to 2 waves per SIMD)
     if (pair && dw == nullptr && B <= 256) {
-      conv_flush_pending();
-      g_pending = PendingWgrad{x, dy, part, B, imgs, cls, g, s};
+      hold_pending(PendingWgrad{x, dy, part, B, imgs, cls, g, s});
       return;
     }
     // Winograd-domain grad-W (winograd.hip): same slab layout and slicing as the direct kernel.
@@ -1615,9 +1744,12 @@ void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, 
   // 1.0539 / 1.0572 vs 1.0700 / 1.0783, 512 1.4433 / 1.4427 vs 1.4566 / 1.4542); the 3x3/2 class
   // (its grad-x comes from the downsample sibling's backward) up to 256 (128 0.8243 vs 0.8303, 256
   // 1.0196 vs 1.0339, 64 0.7295-0.7439 vs 0.7329-0.7385; 512 1.4504 / 1.4453 vs 1.4470 / 1.4431)
-  if (pair && dw == nullptr && (cls == 1 || (cls == 2 && B <= 256)) && conv_wino(cls, g, B, true)) {
-    conv_flush_pending();
-    g_pending = PendingWgrad{x, dy, part, B, imgs, cls, g, s};
+  // The 1x1 stride-2 downsample classes (direct grad-x + direct grad-W, direct_pair_kernel) at every
+  // batch: 64 0.7218 / 0.7264 vs 0.7301 / 0.7311, 256 1.0125 vs 1.0256, 512 1.4396 / 1.4355 vs
+  // 1.4469 / 1.4360.
+  if (pair && dw == nullptr &&
+      (((cls == 1 || (cls == 2 && B <= 256)) && conv_wino(cls, g, B, true)) || cls == 4 || cls == 5)) {
+    hold_pending(PendingWgrad{x, dy, part, B, imgs, cls, g, s});
     return;
   }
   switch (cls) {
