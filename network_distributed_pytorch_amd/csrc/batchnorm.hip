@@ -22,6 +22,7 @@
 #include <string>
 
 #include "ndp_kernels.h"
+#include "pool_route.h"
 
 namespace ndp {
 
@@ -345,6 +346,68 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
       if (dres) dres[o] = dz;
     });
   }
+}
+
+// ---- stem tail backward: max-pool routing + ReLU mask + BN backward apply in one pass ---------
+// The pool backward (pool.hip, statistics only) has folded sum dz / sum dz * xhat per (channel,
+// image) with dz = routed gradient * ReLU mask; this pass re-routes the pooled gradient (the 8x8
+// dY and its uint8 argmax: 1/4 of the 16x16 plane's bytes, plus x) and writes the BN input
+// gradient directly — the routed 16x16 gradient is never stored and never re-read (2 x 33 MB at
+// batch 512).  Per element the same operations in the same order as maxpool_bwd_s2_kernel +
+// bn_bwd_apply_kernel (mbet mask, Sp = N statistics): bitwise equal.  Grid (S, C); 64 threads
+// per 8x8 pooled plane, 4 planes per pass.
+__global__ __launch_bounds__(256) void stem_pool_bwd_apply_kernel(
+    const float* __restrict__ dy, const uint8_t* __restrict__ idx, const float* __restrict__ x,
+    const float* __restrict__ gamma, const float* __restrict__ beta, const float* __restrict__ save_mean,
+    const float* __restrict__ save_invstd, const double* __restrict__ stats, float* __restrict__ dx,
+    float* __restrict__ dgamma, float* __restrict__ dbeta, int N, int C, int H, int W) {
+  __shared__ double red[16];
+  const int s = blockIdx.x, c = blockIdx.y, S = gridDim.x;
+  const float mean = save_mean[c], invstd = save_invstd[c];
+  const float g = gamma ? gamma[c] : 1.f;
+  const float msc = __fmul_rn(g, invstd);
+  const float msh = __fsub_rn(beta ? beta[c] : 0.f, __fmul_rn(mean, msc));
+  double sdz, sdzx;
+  slice_sums_block(stats, c, N, sdz, sdzx, red);
+  if (s == 0 && threadIdx.x == 0) {
+    if (dgamma) dgamma[c] = (float)sdzx;
+    if (dbeta) dbeta[c] = (float)sdz;
+  }
+  const double M = (double)N * H * W;
+  const float k1 = g * invstd;
+  const float mdz = (float)(sdz / M);
+  const float mdzx = (float)(sdzx / M);
+  const int OH = H / 2, OW = W / 2;  // 64 outputs per plane (launcher-checked)
+  const BnSlice sl = slice_of(N, S, s);
+  const int o = threadIdx.x & 63, i = o / OW, j = o - i * OW;
+  for (int64_t n = sl.n0 + (threadIdx.x >> 6); n < sl.n1; n += 4) {
+    const int64_t plane = n * C + c;
+    float d[4];
+    pool_s2_route(dy + plane * 64, idx + plane * 64, i, j, OH, OW, d[0], d[1], d[2], d[3]);
+    const int64_t off = plane * H * W + (int64_t)(2 * i) * W + 2 * j;
+    const float2 x0 = *reinterpret_cast<const float2*>(x + off), x1 = *reinterpret_cast<const float2*>(x + off + W);
+    const float xs[4] = {x0.x, x0.y, x1.x, x1.y};
+    float out[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float dz = (fmaf(xs[k], msc, msh) > 0.f) ? d[k] : 0.f;
+      const float xh = (xs[k] - mean) * invstd;
+      out[k] = k1 * (dz - mdz - xh * mdzx);
+    }
+    *reinterpret_cast<float2*>(dx + off) = make_float2(out[0], out[1]);
+    *reinterpret_cast<float2*>(dx + off + W) = make_float2(out[2], out[3]);
+  }
+}
+
+void launch_stem_pool_bwd_apply(const float* dy, const uint8_t* idx, const float* x, const float* gamma,
+                                const float* beta, const float* save_mean, const float* save_invstd,
+                                const double* stats, float* dx, float* dgamma, float* dbeta, int N, int C, int H,
+                                int W, hipStream_t s) {
+  // slices: 4 images per workgroup at small batches, at most 16 slices (each workgroup folds the
+  // channel's N statistics partials)
+  const int S = N / 4 < 1 ? 1 : (N / 4 > 16 ? 16 : N / 4);
+  hipLaunchKernelGGL(stem_pool_bwd_apply_kernel, dim3((unsigned)S, (unsigned)C), dim3(256), 0, s, dy, idx, x, gamma,
+                     beta, save_mean, save_invstd, stats, dx, dgamma, dbeta, N, C, H, W);
 }
 
 // ---- stem tail: BN (training) -> ReLU -> MaxPool(3, 2, 1) in one pass ----------------------

@@ -587,14 +587,20 @@ void maxpool_bwd(torch::Tensor dy, torch::Tensor idx, torch::Tensor dx, int64_t 
 }
 
 // MaxPool(3, 2, 1) backward of the fused stem tail + its BN's backward statistics ([C][N][2])
-void maxpool_bwd_bnstats(torch::Tensor dy, torch::Tensor idx, torch::Tensor dx, torch::Tensor x,
+// dx = None: statistics only (the routed gradient is re-formed by stem_pool_bwd_apply)
+void maxpool_bwd_bnstats(torch::Tensor dy, torch::Tensor idx, c10::optional<torch::Tensor> dx_opt, torch::Tensor x,
                          c10::optional<torch::Tensor> gamma, c10::optional<torch::Tensor> beta, torch::Tensor mean,
                          torch::Tensor invstd, torch::Tensor stats) {
-  check_f32(dy, "dy"); check_f32(dx, "dx"); check_f32(x, "x"); check_dev(idx, "idx");
+  check_f32(dy, "dy"); check_f32(x, "x"); check_dev(idx, "idx");
   check_f32(mean, "mean"); check_f32(invstd, "invstd"); check_dev(stats, "stats");
   TORCH_CHECK(idx.scalar_type() == torch::kUInt8 && idx.sizes() == dy.sizes() && idx.is_contiguous(),
               "maxpool: idx must be contiguous uint8 shaped like dy");
-  TORCH_CHECK(x.sizes() == dx.sizes() && x.is_contiguous() && dx.dim() == 4, "maxpool_bwd_bnstats: x shaped like dx");
+  if (dx_opt.has_value()) {
+    check_f32(*dx_opt, "dx");
+    TORCH_CHECK(x.sizes() == dx_opt->sizes(), "maxpool_bwd_bnstats: x shaped like dx");
+  }
+  TORCH_CHECK(x.is_contiguous() && x.dim() == 4, "maxpool_bwd_bnstats: contiguous 4-d x");
+  const torch::Tensor& dx = x;  // geometry only
   const ndp::PoolGeom g = pool_geom(dx, dy, 3, 2, 1);
   TORCH_CHECK(ndp::maxpool_bwd_bnstats_ok(g), "maxpool_bwd_bnstats: needs the 16x16 -> 8x8 stem window");
   const int N = (int)dx.size(0), C = (int)dx.size(1);
@@ -603,9 +609,35 @@ void maxpool_bwd_bnstats(torch::Tensor dy, torch::Tensor idx, torch::Tensor dx, 
   TORCH_CHECK(mean.numel() >= C && invstd.numel() >= C, "maxpool_bwd_bnstats: statistics size");
   const ndp::PoolBnStats bs{x.data_ptr<float>(), opt_f32(gamma, "gamma"), opt_f32(beta, "beta"),
                             mean.data_ptr<float>(), invstd.data_ptr<float>(), stats.data_ptr<double>(), C, N};
-  ndp::launch_maxpool_bwd(dy.data_ptr<float>(), idx.data_ptr<uint8_t>(), dx.data_ptr<float>(), N * C, g, cur_stream(),
-                          bs);
+  ndp::launch_maxpool_bwd(dy.data_ptr<float>(), idx.data_ptr<uint8_t>(),
+                          dx_opt.has_value() ? dx_opt->data_ptr<float>() : nullptr, N * C, g, cur_stream(), bs);
   check_launch("launch_maxpool_bwd");
+}
+
+// the stem BN's input gradient from the pooled gradient and the statistics-only pool backward
+void stem_pool_bwd_apply(torch::Tensor dy, torch::Tensor idx, torch::Tensor x, c10::optional<torch::Tensor> gamma,
+                         c10::optional<torch::Tensor> beta, torch::Tensor mean, torch::Tensor invstd,
+                         torch::Tensor stats, torch::Tensor dx, c10::optional<torch::Tensor> dgamma,
+                         c10::optional<torch::Tensor> dbeta) {
+  check_f32(dy, "dy"); check_f32(x, "x"); check_f32(dx, "dx"); check_dev(idx, "idx");
+  check_f32(mean, "mean"); check_f32(invstd, "invstd"); check_dev(stats, "stats");
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous() && dx.sizes() == x.sizes() && dx.is_contiguous(),
+              "stem_pool_bwd_apply: contiguous x / dx of one shape");
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  TORCH_CHECK(H == 16 && W == 16 && dy.dim() == 4 && dy.size(0) == N && dy.size(1) == C && dy.size(2) == 8 &&
+                  dy.size(3) == 8 && dy.is_contiguous(),
+              "stem_pool_bwd_apply: 16x16 -> 8x8 stem maps");
+  TORCH_CHECK(idx.scalar_type() == torch::kUInt8 && idx.sizes() == dy.sizes() && idx.is_contiguous(),
+              "stem_pool_bwd_apply: idx must be contiguous uint8 shaped like dy");
+  TORCH_CHECK(stats.scalar_type() == torch::kFloat64 && stats.numel() >= (int64_t)C * N * 2 && mean.numel() >= C &&
+                  invstd.numel() >= C,
+              "stem_pool_bwd_apply: statistics sizes");
+  ndp::launch_stem_pool_bwd_apply(dy.data_ptr<float>(), idx.data_ptr<uint8_t>(), x.data_ptr<float>(),
+                                  opt_f32(gamma, "gamma"), opt_f32(beta, "beta"), mean.data_ptr<float>(),
+                                  invstd.data_ptr<float>(), stats.data_ptr<double>(), dx.data_ptr<float>(),
+                                  dgamma.has_value() ? dgamma->data_ptr<float>() : nullptr,
+                                  dbeta.has_value() ? dbeta->data_ptr<float>() : nullptr, N, C, H, W, cur_stream());
+  check_launch("launch_stem_pool_bwd_apply");
 }
 
 int bn_slices(int N, int C, int HW) { return ndp::bn_slices(N, C, HW); }
@@ -1427,6 +1459,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("maxpool_bwd_bnstats", &maxpool_bwd_bnstats, py::arg("dy"), py::arg("idx"), py::arg("dx"), py::arg("x"),
         py::arg("gamma"), py::arg("beta"), py::arg("mean"), py::arg("invstd"), py::arg("stats"));
+  m.def("stem_pool_bwd_apply", &stem_pool_bwd_apply);
   m.def("checksum", &checksum);
   m.def("flag_signal", &flag_signal);
   m.def("flag_wait", &flag_wait, py::arg("flags"), py::arg("i"), py::arg("seen"), py::arg("err"),

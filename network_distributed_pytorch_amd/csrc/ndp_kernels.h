@@ -448,6 +448,12 @@ struct PoolBnStats {
   int C, N;
 };
 bool maxpool_bwd_bnstats_ok(const PoolGeom& g);
+// the stem BN input gradient straight from the pooled gradient (batchnorm.hip): 16x16 -> 8x8 maps,
+// statistics [C][N][2] from the statistics-only pool backward
+void launch_stem_pool_bwd_apply(const float* dy, const uint8_t* idx, const float* x, const float* gamma,
+                                const float* beta, const float* save_mean, const float* save_invstd,
+                                const double* stats, float* dx, float* dgamma, float* dbeta, int N, int C, int H,
+                                int W, hipStream_t s);
 void launch_maxpool_bwd(const float* dy, const uint8_t* idx, float* dx, int planes, const PoolGeom& g,
                         hipStream_t s,
                         const PoolBnStats& bs = PoolBnStats{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0});

@@ -20,6 +20,7 @@
 #include <math.h>
 
 #include "ndp_kernels.h"
+#include "pool_route.h"
 
 namespace ndp {
 
@@ -193,26 +194,13 @@ __global__ __launch_bounds__(kPoolThreads) void maxpool_bwd_s2_kernel(const floa
   const int i = (int)fdiv(o, a.ow), j = (int)(o - (uint32_t)i * a.ow.d);
   const float* dyp = dy + (size_t)plane * a.out_plane.d;
   const uint8_t* ip = idx + (size_t)plane * a.out_plane.d;
-  const bool right = j + 1 < OW, down = i + 1 < OH;
-  const int c = i * OW + j;
-  const float g00 = dyp[c], g01 = right ? dyp[c + 1] : 0.f, g10 = down ? dyp[c + OW] : 0.f,
-              g11 = (right && down) ? dyp[c + OW + 1] : 0.f;
-  const int a00 = ip[c], a01 = right ? ip[c + 1] : -1, a10 = down ? ip[c + OW] : -1,
-            a11 = (right && down) ? ip[c + OW + 1] : -1;
-  // window (oh, ow) covers input rows 2oh-1 .. 2oh+1: tap kh = h - 2oh + 1
-  float d00 = 0.f, d01 = 0.f, d10 = 0.f, d11 = 0.f;
-  if (a00 == 4) d00 += g00;                     // (2i, 2j)     <- (i, j) tap (1,1)
-  if (a00 == 5) d01 += g00;                     // (2i, 2j+1)   <- (i, j) tap (1,2)
-  if (a01 == 3) d01 += g01;                     //              <- (i, j+1) tap (1,0)
-  if (a00 == 7) d10 += g00;                     // (2i+1, 2j)   <- (i, j) tap (2,1)
-  if (a10 == 1) d10 += g10;                     //              <- (i+1, j) tap (0,1)
-  if (a00 == 8) d11 += g00;                     // (2i+1, 2j+1) <- (i, j) tap (2,2)
-  if (a01 == 6) d11 += g01;                     //              <- (i, j+1) tap (2,0)
-  if (a10 == 2) d11 += g10;                     //              <- (i+1, j) tap (0,2)
-  if (a11 == 0) d11 += g11;                     //              <- (i+1, j+1) tap (0,0)
-  float* dxp = dx + (size_t)plane * a.in_plane.d + (size_t)(2 * i) * W + 2 * j;
-  *reinterpret_cast<float2*>(dxp) = make_float2(d00, d01);
-  *reinterpret_cast<float2*>(dxp + W) = make_float2(d10, d11);
+  float d00, d01, d10, d11;
+  pool_s2_route(dyp, ip, i, j, OH, OW, d00, d01, d10, d11);
+  if (dx != nullptr) {  // (null: statistics only — the fused stem BN backward re-routes the gradient)
+    float* dxp = dx + (size_t)plane * a.in_plane.d + (size_t)(2 * i) * W + 2 * j;
+    *reinterpret_cast<float2*>(dxp) = make_float2(d00, d01);
+    *reinterpret_cast<float2*>(dxp + W) = make_float2(d10, d11);
+  }
   if (bs.stats != nullptr) {
     // the BN backward's statistics of this plane (64 outputs = this wave, launcher-checked):
     // dz = d * mask with the ReLU mask recomputed from the BN input x exactly as the fused

@@ -27,6 +27,7 @@ FUSIONS = {
     "winograd": "F(2x2,3x3) Winograd for the layer1 3x3 forward / grad-x (csrc/winograd.hip)",
     "wino_pair": "layer1 Winograd grad-x and grad-W of a conv in one launch (csrc/winograd.hip)",
     "stem_pool": "stem BN -> ReLU -> max-pool in one pass (ops/batchnorm.py)",
+    "stem_bwd": "stem max-pool backward + BN backward apply from the pooled gradient in one pass (ops/batchnorm.py)",
     "bn_pair": "downsample block's bn2 + downsample BN + ReLU in one launch per direction (ops/batchnorm.py)",
     "defer_gradw": "grad-W slab sums / folds batched at the end of backward (ops/gradfinish.py)",
     "grad_arena": "dense-arm gradients written straight into the bucket arena (ops/gradarena.py)",

@@ -105,11 +105,20 @@ class _BNReluPoolFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, weight, bias, save_mean, save_invstd, part, idx = ctx.saved_tensors
-        dz = torch.empty_like(x)  # gradient of the (unstored) BN output = the pool's input
         dx = torch.empty_like(x)
         dgamma = grad_buffer(ctx.params[0], weight)
         dbeta = grad_buffer(ctx.params[1], weight)
         N, C, H, W = x.shape
+        if _BWD_STATS and _STEM_BWD and H == 16 and W == 16:
+            # statistics-only pool backward, then ONE pass from the pooled gradient to the BN input
+            # gradient (csrc/batchnorm.hip stem_pool_bwd_apply_kernel): the routed 16x16 gradient
+            # is never stored (bitwise equal to the two-pass path below)
+            dy = dy.contiguous()
+            stats = torch.empty(C * N * 2, device=x.device, dtype=torch.float64)
+            ext().maxpool_bwd_bnstats(dy, idx, None, x, weight, bias, save_mean, save_invstd, stats)
+            ext().stem_pool_bwd_apply(dy, idx, x, weight, bias, save_mean, save_invstd, stats, dx, dgamma, dbeta)
+            return dx, dgamma, dbeta, None, None, None, None, None, None, None, None
+        dz = torch.empty_like(x)  # gradient of the (unstored) BN output = the pool's input
         if _BWD_STATS and H == 16 and W == 16:  # the pool backward also emits the BN's statistics
             stats = torch.empty(C * N * 2, device=x.device, dtype=torch.float64)
             ext().maxpool_bwd_bnstats(dy.contiguous(), idx, dz, x, weight, bias, save_mean, save_invstd, stats)
@@ -191,6 +200,9 @@ _BWD_STATS = fusion_on("bn_bwd_stats")
 
 # the stem tail BN -> ReLU -> MaxPool in one pass (NDP_FUSION_OFF=stem_pool: BN kernel + pool kernel)
 STEM_POOL = fusion_on("stem_pool")
+# its backward without the stored 16x16 pool gradient (NDP_FUSION_OFF=stem_bwd: pool backward +
+# BN backward apply)
+_STEM_BWD = fusion_on("stem_bwd")
 
 
 def bn_act(x, weight, bias, running_mean, running_var, nbt, part, training, momentum, eps,

@@ -89,3 +89,25 @@ def test_resnet18_stem_pool_matches_unfused(device, monkeypatch):
     for k in s0:
         if s0[k].dtype.is_floating_point:
             assert torch.allclose(s0[k], s1[k], rtol=1e-5, atol=1e-6), k
+
+
+@pytest.mark.parametrize("N", [64, 512, 6])
+def test_stem_pool_bwd_one_pass_is_bitwise(device, monkeypatch, N):
+    """The stem backward from the pooled gradient in one pass (statistics-only pool backward +
+    csrc/batchnorm.hip stem_pool_bwd_apply_kernel) == pool backward + BN backward apply, bitwise."""
+    torch.manual_seed(0)
+    C, H = 64, 16
+    x = torch.randn(N, C, H, H, device=device)
+    pool = MaxPool2d(3, 2, 1)
+    outs = []
+    for on in (False, True):
+        monkeypatch.setattr(bn_mod, "_STEM_BWD", on)
+        torch.manual_seed(1)
+        bn = BatchNormAct2d(C).to(device)
+        with torch.no_grad():
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.5, 0.5)
+        g = torch.randn(N, C, H // 2, H // 2, device=device, generator=torch.Generator(device=device).manual_seed(2))
+        outs.append(_run(bn, pool, x, g, True))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
