@@ -911,7 +911,7 @@ void wino_weights_many(const std::vector<std::pair<torch::Tensor, torch::Tensor>
 // defer: split-K slabs are left in `part` for the consumer; returns how many (1 = y final)
 int64_t conv_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, const std::vector<int64_t>& geom,
                  c10::optional<torch::Tensor> part, bool defer, c10::optional<torch::Tensor> stats,
-                 c10::optional<torch::Tensor> wino_u) {
+                 c10::optional<torch::Tensor> wino_u, bool pair) {
   const ndp::ConvGeom g = conv_geom(geom);
   const int cls = ndp::conv_direct_class(g);
   const int B = conv_batch(x, g, ndp::conv_fwd_imgs(cls));
@@ -932,7 +932,8 @@ int64_t conv_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor y, const std::v
   }
   torch::Tensor wu = wino_u_for(wino_u, w, g, ndp::conv_wino(cls, g, B, false));
   const int left = ndp::launch_conv_fwd(x.data_ptr<float>(), w.data_ptr<float>(), y.data_ptr<float>(), B, g, pp,
-                                        cur_stream(), defer, st, wu.defined() ? wu.data_ptr<float>() : nullptr);
+                                        cur_stream(), defer, st, wu.defined() ? wu.data_ptr<float>() : nullptr,
+                                        pair && x.is_contiguous());
   check_launch("launch_conv_fwd");
   return left;
 }
@@ -1472,7 +1473,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gradw_finish", &gradw_finish, py::arg("slabs"), py::arg("folds"));
   m.def("conv_plan", &conv_plan, py::arg("geom"), py::arg("batch"));
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("geom"), py::arg("part") = py::none(),
-        py::arg("defer") = false, py::arg("stats") = py::none(), py::arg("wino_u") = py::none());
+        py::arg("defer") = false, py::arg("stats") = py::none(), py::arg("wino_u") = py::none(),
+        py::arg("pair") = false);
+  m.def("conv_flush_pending_fwd", []() {
+    ndp::conv_flush_pending_fwd();
+    check_launch("conv_flush_pending_fwd");
+  });
   m.def("wino_weights", &wino_weights);
   m.def("wino_weights_many", &wino_weights_many);
   m.def("conv_wino", [](const std::vector<int64_t>& geom, int64_t B, bool dgrad) {

@@ -1327,6 +1327,44 @@ static int run_fwd(const float* x, const float* w, float* y, int B, int Cin, int
   return 1;
 }
 
+// ---- the downsample block's two forward convs in ONE launch --------------------------------
+// conv1 (3x3 stride 2, class 2) and the 1x1 stride-2 downsample (class 4) read the same block
+// input; the downsample's launch is held back (launch_conv_fwd pair = true) and conv1's launch
+// runs both bodies on one grid: conv1's workgroups first (its output feeds bn1 right after).
+struct FwdPart {
+  const float* x;
+  const float* w;
+  float* y;
+  float* part;
+  int Cin, Kout, cps;
+  int64_t slab;
+};
+__global__ __launch_bounds__(256) void ds_fwd_pair_kernel(FwdPart a, uint3 ga, FwdPart b, uint3 gb) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const unsigned na = ga.x * ga.y * ga.z;
+  unsigned k = blockIdx.x;
+  if (k < na) {
+    conv_fwd_body<3, 3, 2, 1, 8, 8, 8, 64, 4, 2, 2, 4, false, true>(
+        a.x, a.w, a.y, a.part, a.Cin, a.Kout, a.cps, a.slab, nullptr, ConvBnStats{},
+        make_uint3(k % ga.x, (k / ga.x) % ga.y, k / (ga.x * ga.y)), ga, smem);
+  } else {
+    k -= na;
+    conv_fwd_body<1, 1, 2, 0, 8, 8, 8, 64, 4, 2, 2, 4, false, true>(
+        b.x, b.w, b.y, b.part, b.Cin, b.Kout, b.cps, b.slab, nullptr, ConvBnStats{},
+        make_uint3(k % gb.x, (k / gb.x) % gb.y, k / (gb.x * gb.y)), gb, smem);
+  }
+}
+
+// the split of a class-2 / class-4 forward as run_fwd normalises it
+template <typename G>
+static FwdPart fwd_part(const float* x, const float* w, float* y, float* part, int B, int Cin, int Kout, int& ksplit) {
+  const int nchunks = (Cin + 8 - 1) / 8;
+  if (ksplit < 1 || part == nullptr) ksplit = 1;
+  const int cps = (nchunks + ksplit - 1) / ksplit;
+  ksplit = (nchunks + cps - 1) / cps;
+  return FwdPart{x, w, y, part, Cin, Kout, cps, (int64_t)B * Kout * G::PQ};
+}
+
 void launch_slab_sum(const float* part, float* out, int64_t n, int nslab, hipStream_t s, const float* addend) {
   hipLaunchKernelGGL(conv_slab_sum_kernel, dim3((unsigned)((n / 4 + 15) / 16)), dim3(256), 0, s, part, out, n, nslab,
                      addend);
@@ -1425,6 +1463,10 @@ static constexpr int kConvMaxSplit = 4;
 // two <= the channel chunks, so that (B / IMGS) * (outC / 64) * ksplit >= kFillWgs
 int conv_ksplit(int cls, const ConvGeom& g, int B, bool dgrad) {
   if (cls < 0 || cls == 3) return 1;
+  // the 1x1/2 grad-x runs in one launch with its grad-W (direct_pair_kernel), whose workgroups fill
+  // the CUs: unsplit from batch 512 (no slab-sum launch; 1.4306 / 1.4308 -> 1.4192 / 1.4229 ms, at
+  // 256 even: 1.0053 vs 1.0076)
+  if (dgrad && (cls == 4 || cls == 5) && B >= 512) return 1;
   const int inC = dgrad ? g.Co : g.C, outC = dgrad ? g.C : g.Co;
   const int imgs = (dgrad && cls == 2) ? 1 : conv_fwd_imgs(cls);  // class-2 grad-x: 8x8 tiles, 1 image
   const int base = (B / imgs) * (outC / 64);
@@ -1502,11 +1544,64 @@ bool conv_dgrad_direct(int cls) { return cls >= 0 && cls <= 5 && cls != 3; }
 // batch 512, 1.0582 / 1.0627 -> 1.0546 / 1.0569 at batch 64 against the compiler's schedule
 // (iglp_opt(0): 2.0043 / 1.0602; the pinned interleave on the stem / 3x3-2 / 1x1-2 forwards
 // and 16-channel chunks or two-image layer1 tiles were slower — round 3 A/Bs)
+namespace {
+struct PendingFwd {  // the downsample conv's forward, held for its block's conv1 (class 2)
+  const float* x = nullptr;
+  const float* w = nullptr;
+  float* y = nullptr;
+  float* part = nullptr;
+  int B = 0, ks = 1;
+  bool defer = false;
+  ConvGeom g{};
+  hipStream_t s = nullptr;
+};
+PendingFwd g_pending_fwd;
+using CfgC2 = ConvFwdCfg<3, 3, 2, 1, 8, 8, 8, 64, 4, 2, 2, 4, false, 1>;
+using CfgC4 = ConvFwdCfg<1, 1, 2, 0, 8, 8, 8, 64, 4, 2, 2, 4, false, 1>;
+}  // namespace
+
+void conv_flush_pending_fwd() {
+  if (g_pending_fwd.x == nullptr) return;
+  const PendingFwd p = g_pending_fwd;
+  g_pending_fwd = PendingFwd{};
+  run_fwd<1, 1, 2, 0, 8, 8, 8, 64, 4, 2, 2, 4, false, true>(p.x, p.w, p.y, p.B, p.g.C, p.g.Co, p.ks, p.part, p.s,
+                                                           nullptr, p.defer);
+}
+
 int launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s,
-                    bool defer, double* stats_out, float* wino_u) {
+                    bool defer, double* stats_out, float* wino_u, bool pair) {
   const ConvBnStats stats{stats_out, nullptr, nullptr, nullptr, nullptr};
   const int cls = conv_direct_class(g);
   const int ks = conv_ksplit(cls, g, B, false);
+  if (cls == 4 && pair && stats_out == nullptr) {  // held for conv1 (ds_fwd_pair_kernel); same return as run_fwd
+    conv_flush_pending_fwd();
+    int k = ks;
+    fwd_part<CfgC4>(x, w, y, part, B, g.C, g.Co, k);
+    g_pending_fwd = PendingFwd{x, w, y, part, B, ks, defer, g, s};
+    return (k > 1 && defer) ? k : 1;
+  }
+  if (cls == 2 && g_pending_fwd.x == x && g_pending_fwd.s == s && g_pending_fwd.B == B && stats_out == nullptr) {
+    const PendingFwd p = g_pending_fwd;
+    g_pending_fwd = PendingFwd{};
+    int ka = ks, kb = p.ks;
+    const FwdPart a = fwd_part<CfgC2>(x, w, y, part, B, g.C, g.Co, ka);
+    const FwdPart b = fwd_part<CfgC4>(p.x, p.w, p.y, p.part, B, p.g.C, p.g.Co, kb);
+    const uint3 ga = make_uint3((unsigned)(B / 4), (unsigned)(g.Co / 64), (unsigned)ka);
+    const uint3 gb = make_uint3((unsigned)(B / 4), (unsigned)(p.g.Co / 64), (unsigned)kb);
+    constexpr size_t lds = CfgC2::LDS_BYTES > CfgC4::LDS_BYTES ? CfgC2::LDS_BYTES : CfgC4::LDS_BYTES;
+    static bool attr = false;
+    if (!attr) { set_lds(ds_fwd_pair_kernel, lds); attr = true; }
+    hipLaunchKernelGGL(ds_fwd_pair_kernel, dim3(ga.x * ga.y * ga.z + gb.x * gb.y * gb.z), dim3(256), lds, s, a, ga, b, gb);
+    if (kb > 1 && !p.defer)
+      hipLaunchKernelGGL(conv_slab_sum_kernel, dim3((unsigned)((b.slab / 4 + 15) / 16)), dim3(256), 0, s, p.part, p.y,
+                         b.slab, kb, nullptr);
+    if (ka > 1 && defer) return ka;
+    if (ka > 1)
+      hipLaunchKernelGGL(conv_slab_sum_kernel, dim3((unsigned)((a.slab / 4 + 15) / 16)), dim3(256), 0, s, part, y,
+                         a.slab, ka, nullptr);
+    return 1;
+  }
+  conv_flush_pending_fwd();
   if (wino_u != nullptr && conv_wino(cls, g, B, false)) {
     launch_wino_conv(x, wino_u, y, B, g.C, g.Co, g.H, false, 1, nullptr, ks > 1 ? ConvBnStats{} : stats, ks, part, s);
     return ks > 1 ? wino_slabs(part, y, (int64_t)B * g.Co * g.H * g.W, ks, defer, nullptr, s) : 1;

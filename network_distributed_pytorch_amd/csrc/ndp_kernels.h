@@ -321,8 +321,11 @@ struct ConvBnStats {
 };
 // wino_u (nullable): the conv's Winograd weight transforms (launch_wino_weights: forward + grad-x
 // layouts, 32 * Co * C floats) when conv_wino(cls, g, B, dgrad) — the launch then runs the Winograd kernel
+// pair: a downsample conv (class 4) forward may be held back and launched together with the next
+// class-2 forward of the same input (ds_fwd_pair_kernel); conv_flush_pending_fwd() launches it alone
 int launch_conv_fwd(const float* x, const float* w, float* y, int B, const ConvGeom& g, float* part, hipStream_t s,
-                    bool defer = false, double* stats = nullptr, float* wino_u = nullptr);
+                    bool defer = false, double* stats = nullptr, float* wino_u = nullptr, bool pair = false);
+void conv_flush_pending_fwd();
 // stem forward output-row blocks per image (by batch; A/B override 1 / 2 / 4, 0 = auto)
 int stem_psplit(int B);
 void conv_set_stem_psplit(int p);

@@ -25,7 +25,8 @@ FUSIONS = {
     "bn_bwd_stats": "BN backward statistics from the grad-x epilogue / pool backward (ops/batchnorm.py)",
     "bn_vec4": "float4 single-launch small-map BN kernel (csrc/batchnorm.hip; off: the scalar one)",
     "winograd": "F(2x2,3x3) Winograd for the layer1 3x3 forward / grad-x (csrc/winograd.hip)",
-    "wino_pair": "layer1 Winograd grad-x and grad-W of a conv in one launch (csrc/winograd.hip)",
+    "wino_pair": "a conv's grad-x and grad-W in one launch (csrc/winograd.hip, csrc/conv.hip pairs)",
+    "ds_fwd_pair": "a downsample block's conv1 and 1x1 downsample forward in one launch (csrc/conv.hip)",
     "stem_pool": "stem BN -> ReLU -> max-pool in one pass (ops/batchnorm.py)",
     "stem_bwd": "stem max-pool backward + BN backward apply from the pooled gradient in one pass (ops/batchnorm.py)",
     "bn_pair": "downsample block's bn2 + downsample BN + ReLU in one launch per direction (ops/batchnorm.py)",

@@ -27,7 +27,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.batchnorm import BatchNormAct2d, bn_pair_act
-from ..ops.conv import WinoBank
+from ..ops.conv import WinoBank, flush_forward, hold_forward
 from ..ops.gradlink import BranchLink, GradLink
 from ..ops.linear import Linear
 from ..ops.pool import MaxPool2d
@@ -96,14 +96,20 @@ class BasicBlock(nn.Module):
                 # as unsummed slabs for the previous BN2
                 grad_in = None
             cds = None  # the downsample conv's output, its BN paired with bn2 (bn_pair_act)
+            held = False
             if self.downsample is not None:
                 ds = self.downsample
                 if train and len(ds) == 2 and isinstance(ds[0], GemmConv2d) and isinstance(ds[1], BatchNormAct2d):
-                    cds = ds[0](x, slab_out=sd, branch=br)
+                    # its forward may wait for conv1's and share the launch (ops/conv.hold_forward)
+                    held = x.is_cuda
+                    with hold_forward(held):
+                        cds = ds[0](x, slab_out=sd, branch=br)
                 else:
                     identity = ds(x)
-            out = self.bn1(self.conv1(x, link=link, slab_out=s1, grad_slab=grad_in, branch=br), relu=True,
-                           slab_in=s1, grad_slab=g1)
+            c1 = self.conv1(x, link=link, slab_out=s1, grad_slab=grad_in, branch=br)
+            if held:
+                flush_forward()  # the downsample forward, if conv1 did not take it
+            out = self.bn1(c1, relu=True, slab_in=s1, grad_slab=g1)
             c2 = self.conv2(out, slab_out=s2, grad_slab=g1)
             if cds is not None:
                 y = bn_pair_act(self.bn2, self.downsample[1], c2, cds, slab_in=s2, slab_in2=sd, grad_slab=grad_out)

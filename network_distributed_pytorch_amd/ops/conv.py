@@ -24,7 +24,7 @@ from ._ext import ext
 from .gradarena import grad_buffer
 from ..knobs import fusion_on
 
-__all__ = ["direct_plan", "conv2d_direct", "DirectConvFn", "WinoBank", "set_winograd"]
+__all__ = ["direct_plan", "conv2d_direct", "DirectConvFn", "WinoBank", "set_winograd", "hold_forward", "flush_forward"]
 
 _PLANS: dict = {}
 _STATS: dict = {}
@@ -34,6 +34,32 @@ _STATS: dict = {}
 CONV_BN_STATS = fusion_on("conv_bnstats")
 # layer1 Winograd grad-x + grad-W of one conv in one launch (csrc/winograd.hip wino_bwd_pair_kernel)
 _PAIR = fusion_on("wino_pair")
+# a downsample block's 1x1/2 forward held for conv1's launch (csrc/conv.hip ds_fwd_pair_kernel)
+_DS_FWD_PAIR = fusion_on("ds_fwd_pair")
+_HOLD_FWD = [False]
+_HELD: list = []
+
+
+class hold_forward:
+    """Within the block, a direct 1x1 stride-2 forward may be held back by the extension and run
+    in the same launch as the next 3x3 stride-2 forward of the same input (the downsample block's
+    conv1); :func:`flush_forward` launches one that was not taken.  Used by models/resnet.py."""
+
+    def __init__(self, on: bool):
+        self.on = bool(on) and _DS_FWD_PAIR
+
+    def __enter__(self):
+        _HOLD_FWD[0] = self.on
+        return self
+
+    def __exit__(self, *exc):
+        _HOLD_FWD[0] = False
+        return False
+
+
+def flush_forward() -> None:
+    ext().conv_flush_pending_fwd()
+    _HELD.clear()  # every held launch is enqueued: its scratch may be reused by later launches
 
 
 _WINO: dict = {}
@@ -180,7 +206,9 @@ class DirectConvFn(torch.autograd.Function):
             wu = torch.empty(32 * weight.numel() // 9, device=x.device, dtype=x.dtype)  # fwd + grad-x layouts
             ext().wino_weights(weight, wu)
         left = ext().conv_fwd(x, weight, y, list(geom), part, slab_out is not None and part is not None, stats,
-                              wu if wf else None)
+                              wu if wf else None, _HOLD_FWD[0])
+        if _HOLD_FWD[0]:  # a held launch still writes its split-K scratch: alive until flush_forward()
+            _HELD.append(part)
         ctx.wu = wu if wd else None
         if left > 1:
             slab_out.put_fwd(part, left)  # y is filled by the consuming BN kernel
