@@ -383,7 +383,7 @@ __global__ __launch_bounds__(256) void stem_pool_bwd_apply_kernel(
   for (int64_t n = sl.n0 + (threadIdx.x >> 6); n < sl.n1; n += 4) {
     const int64_t plane = n * C + c;
     float d[4];
-    pool_s2_route(dy + plane * 64, idx + plane * 64, i, j, OH, OW, d[0], d[1], d[2], d[3]);
+    pool_s2_route_wave(dy[plane * 64 + o], idx[plane * 64 + o], i, j, d[0], d[1], d[2], d[3]);
     const int64_t off = plane * H * W + (int64_t)(2 * i) * W + 2 * j;
     const float2 x0 = *reinterpret_cast<const float2*>(x + off), x1 = *reinterpret_cast<const float2*>(x + off + W);
     const float xs[4] = {x0.x, x0.y, x1.x, x1.y};

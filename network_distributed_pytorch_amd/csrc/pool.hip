@@ -195,7 +195,10 @@ __global__ __launch_bounds__(kPoolThreads) void maxpool_bwd_s2_kernel(const floa
   const float* dyp = dy + (size_t)plane * a.out_plane.d;
   const uint8_t* ip = idx + (size_t)plane * a.out_plane.d;
   float d00, d01, d10, d11;
-  pool_s2_route(dyp, ip, i, j, OH, OW, d00, d01, d10, d11);
+  if (OH == 8 && OW == 8)  // the stem's 8x8 planes: one wave per plane, neighbours by shuffle
+    pool_s2_route_wave(dyp[o], ip[o], i, j, d00, d01, d10, d11);
+  else
+    pool_s2_route(dyp, ip, i, j, OH, OW, d00, d01, d10, d11);
   if (dx != nullptr) {  // (null: statistics only — the fused stem BN backward re-routes the gradient)
     float* dxp = dx + (size_t)plane * a.in_plane.d + (size_t)(2 * i) * W + 2 * j;
     *reinterpret_cast<float2*>(dxp) = make_float2(d00, d01);

@@ -32,4 +32,29 @@ __device__ __forceinline__ void pool_s2_route(const float* __restrict__ dyp, con
   if (a11 == 0) d11 += g11;                     //              <- (i+1, j+1) tap (0,0)
 }
 
+// The same routing when the 64 lanes of a wave are one 8x8 pooled plane (lane = 8 i + j): each lane
+// loads only its own dY / argmax and takes its right / lower / diagonal neighbours' by lane shuffle
+// (4x fewer loads; the sums are the same, in the same order).
+__device__ __forceinline__ void pool_s2_route_wave(float g00, int a00, int i, int j, float& d00, float& d01,
+                                                   float& d10, float& d11) {
+  const int lane = (int)(threadIdx.x & 63);
+  const bool right = j + 1 < 8, down = i + 1 < 8;
+  const float s01 = __shfl(g00, (lane + 1) & 63, 64), s10 = __shfl(g00, (lane + 8) & 63, 64),
+              s11 = __shfl(g00, (lane + 9) & 63, 64);
+  const int t01 = __shfl(a00, (lane + 1) & 63, 64), t10 = __shfl(a00, (lane + 8) & 63, 64),
+            t11 = __shfl(a00, (lane + 9) & 63, 64);
+  const float g01 = right ? s01 : 0.f, g10 = down ? s10 : 0.f, g11 = (right && down) ? s11 : 0.f;
+  const int a01 = right ? t01 : -1, a10 = down ? t10 : -1, a11 = (right && down) ? t11 : -1;
+  d00 = d01 = d10 = d11 = 0.f;
+  if (a00 == 4) d00 += g00;
+  if (a00 == 5) d01 += g00;
+  if (a01 == 3) d01 += g01;
+  if (a00 == 7) d10 += g00;
+  if (a10 == 1) d10 += g10;
+  if (a00 == 8) d11 += g00;
+  if (a01 == 6) d11 += g01;
+  if (a10 == 2) d11 += g10;
+  if (a11 == 0) d11 += g11;
+}
+
 }  // namespace ndp
