@@ -1813,12 +1813,12 @@ void launch_conv_wgrad(const float* x, const float* dy, float* part, float* dw, 
   const int cls = conv_direct_class(g);
   const int imgs = conv_wgrad_imgs(cls, g, B);
   if (cls == 0 && wino_wgrad_ok(g.C, g.Co, g.H)) {
-    // held back for this conv's grad-x (launch_conv_dgrad) up to per-GPU batch 256, where neither
-    // launch fills the CUs alone.  ResNet-18 r=4, ms/step (profiles/r6/bench_wino_pair.jsonl):
-    // batch 64 0.7758 / 0.7656 -> 0.7498 / 0.7517, 128 0.8676 -> 0.8434, 256 (with the layer2 pairs)
-    // 1.0539 / 1.0572 -> 1.0303 / 1.0343; at 512 the pair was slower or even, 1.4640 -> 1.4818 and
-    // 1.4433 / 1.4427 -> 1.4546 / 1.4511 (the grad-W drops from 3 to 2 waves per SIMD)
-    if (pair && dw == nullptr && B <= 256) {
+    // held back for this conv's grad-x (launch_conv_dgrad).  ResNet-18 r=4, ms/step
+    // (profiles/r6/bench_wino_pair.jsonl): batch 64 0.7758 / 0.7656 -> 0.7498 / 0.7517, 128
+    // 0.8676 -> 0.8434, 256 (with the layer2 pairs) 1.0539 / 1.0572 -> 1.0303 / 1.0343; at 512 the
+    // pair was slower with the one-wave-per-block grad-W (1.4640 -> 1.4818), faster with the
+    // two-wave one (winograd.hip wgrad_red: 1.4143 / 1.4147 -> 1.3934 / 1.3966)
+    if (pair && dw == nullptr) {
       hold_pending(PendingWgrad{x, dy, part, B, imgs, cls, g, s});
       return;
     }

@@ -84,12 +84,14 @@ __device__ __forceinline__ void wino_wgrad_body(const WinoWgradArgs& A, const ui
   constexpr int TW = H / 2, TPL = TW * TW / 4, HW = H * H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i = lane & 15, kq = lane >> 4;
-  const int blk = RED == 4 ? (int)bid.y : (int)bid.y * 4 + wave, nbc = Cin / 16;
+  // RED waves per block: the block is wave / RED-th of the workgroup's 4 / RED, the images the
+  // (wave % RED)-th 1 / RED of the slice's
+  const int blk = (int)bid.y * (4 / RED) + wave / RED, nbc = Cin / 16;
   const int cob = blk / nbc, cib = blk - cob * nbc;
-  if (cob * 16 >= Cout) return;  // (RED = 4: uniform over the workgroup, before its barrier)
+  if (cob * 16 >= Cout) return;  // (RED > 1: uniform over the workgroup, before its barrier)
   const int slice = bid.x;
-  const int b0 = RED == 4 ? slice * imgs + wave * (imgs / 4) : slice * imgs;
-  if (RED == 4) imgs /= 4;  // this wave's images
+  const int b0 = slice * imgs + (wave % RED) * (imgs / RED);
+  imgs /= RED;  // this wave's images
   // tile group kq: H = 8 -> tile row ty = kq (tiles tx = 0..3); H = 4 -> tile (kq / 2, kq % 2)
   const int ty = H == 8 ? kq : kq >> 1, tx0 = H == 8 ? 0 : (kq & 1);
   const float* xp = x + ((int64_t)b0 * Cin + cib * 16 + i) * HW;
@@ -208,6 +210,16 @@ __device__ __forceinline__ void wino_wgrad_body(const WinoWgradArgs& A, const ui
     for (int w = 0; w < 3; ++w)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[e] += red[w][e][lane];
+  } else if constexpr (RED == 2) {  // the odd wave of each pair -> LDS, the even one adds it
+    auto red = reinterpret_cast<f32x4w (*)[16][64]>(smem);  // [2][16][64]
+    if (wave & 1) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) red[wave >> 1][e][lane] = acc[e];
+    }
+    __syncthreads();
+    if (wave & 1) return;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] += red[wave >> 1][e][lane];
   }
   // dW = G^T dU G per (co, ci) = (row 4 kq + r, column i) of the block, lane-local
   float* out = part + (int64_t)slice * Cout * Cin * 9;
@@ -385,13 +397,26 @@ bool wino_wgrad_ok(int C, int Co, int H) { return H == 8 && C % 16 == 0 && Co % 
 // the 4-wave reduction at per-GPU batch <= 128 for slices of imgs % 4 == 0 images (conv.hip
 // conv_wgrad_imgs sizes the slices for it: one workgroup per block and slice)
 bool wino_wgrad_red(int B, int imgs) { return B <= 128 && imgs % 4 == 0; }
+// waves per (co, ci) block: 4 (above); 2 from batch 512 — the slice's images split over two waves
+// summed through LDS: twice the workgroups of RED = 1 at the same slab count, two waves per SIMD
+// instead of one (the 8x8 kernel keeps one image's operands in flight and relies on a second wave
+// to hide the loads).  ResNet-18 r=4 batch 512: alone even (1.4143 / 1.4147 vs 1.4184 / 1.4140 ms),
+// with the layer1 grad-x pair it enables 1.3934 / 1.3966; batch 256: 1.0141 vs 0.9998 (kept at 1)
+static int wgrad_red(int B, int C, int Co, int imgs) {
+  if (wino_wgrad_red(B, imgs)) return 4;
+  return (B >= 512 && imgs % 2 == 0 && ((Co / 16) * (C / 16)) % 2 == 0) ? 2 : 1;
+}
 void launch_wino_wgrad(const float* x, const float* dy, float* part, int B, int C, int Co, int H, int imgs,
                        hipStream_t s) {
   if (H != 8) return;
   const WinoWgradArgs a{x, dy, part, C, Co, imgs};
-  if (wino_wgrad_red(B, imgs)) {
+  const int red = wgrad_red(B, C, Co, imgs);
+  if (red == 4) {
     const dim3 grid((unsigned)(B / imgs), (unsigned)((Co / 16) * (C / 16)));
     hipLaunchKernelGGL((wino_wgrad_kernel<8, 4>), grid, dim3(256), kWgRedLds, s, a);
+  } else if (red == 2) {
+    const dim3 grid((unsigned)(B / imgs), (unsigned)((Co / 16) * (C / 16) / 2));
+    hipLaunchKernelGGL((wino_wgrad_kernel<8, 2>), grid, dim3(256), kWgRedLds, s, a);
   } else {
     const dim3 grid((unsigned)(B / imgs), (unsigned)(((Co / 16) * (C / 16) + 3) / 4));
     hipLaunchKernelGGL((wino_wgrad_kernel<8, 1>), grid, dim3(256), 0, s, a);
@@ -410,8 +435,9 @@ void launch_wino_bwd_pair(const float* dy, const float* u, float* dx, int B, int
   const uint3 ga = make_uint3((unsigned)(B / wino_imgs(8)), (unsigned)(outC / kWBM), (unsigned)ks);
   const WinoWgradArgs w{x, dy, part_w, outC, inC, imgs};
   const int C = outC, Co = inC;
-  const bool red = wino_wgrad_red(B, imgs);
-  const uint3 gw = make_uint3((unsigned)(B / imgs), (unsigned)(red ? (Co / 16) * (C / 16) : ((Co / 16) * (C / 16) + 3) / 4), 1);
+  const int red = wgrad_red(B, C, Co, imgs);
+  const int nb = (Co / 16) * (C / 16);
+  const uint3 gw = make_uint3((unsigned)(B / imgs), (unsigned)(red == 4 ? nb : red == 2 ? nb / 2 : (nb + 3) / 4), 1);
   const unsigned n = ga.x * ga.y * ga.z + gw.x * gw.y;
   const size_t lds = kWLds > kWgRedLds ? kWLds : kWgRedLds;
   static bool attr = false;
@@ -420,9 +446,12 @@ void launch_wino_bwd_pair(const float* dy, const float* u, float* dx, int B, int
                         (int)lds);
     hipFuncSetAttribute(reinterpret_cast<const void*>(wino_bwd_pair_kernel<1>), hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)lds);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(wino_bwd_pair_kernel<2>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)lds);
     attr = true;
   }
-  if (red) hipLaunchKernelGGL(wino_bwd_pair_kernel<4>, dim3(n), dim3(256), lds, s, a, ga, w, gw);
+  if (red == 4) hipLaunchKernelGGL(wino_bwd_pair_kernel<4>, dim3(n), dim3(256), lds, s, a, ga, w, gw);
+  else if (red == 2) hipLaunchKernelGGL(wino_bwd_pair_kernel<2>, dim3(n), dim3(256), lds, s, a, ga, w, gw);
   else hipLaunchKernelGGL(wino_bwd_pair_kernel<1>, dim3(n), dim3(256), lds, s, a, ga, w, gw);
 }
 

@@ -202,8 +202,9 @@ def test_gradw_finish_one_launch_equals_two(device):
 def test_wino_bwd_pair_is_bitwise(device, batch):
     """A conv's Winograd grad-x + grad-W in one launch (layer1: csrc/winograd.hip
     wino_bwd_pair_kernel; layer2 3x3 and 3x3/2: csrc/conv.hip wino_direct_pair_kernel with the direct
-    grad-W) == the two launches, bitwise: layer2 pairs only (512), both (256; 64 with split-K grad-x
-    and the 4-wave grad-W) and no layer2 Winograd (24); nothing is left pending after backward()."""
+    grad-W) == the two launches, bitwise: both with the 2-wave Winograd grad-W (512), the 1-wave one
+    (256), split-K grad-x and the 4-wave grad-W (64), and no layer2 Winograd (24); nothing is left
+    pending after backward()."""
     from network_distributed_pytorch_amd.models import build_resnet
     from network_distributed_pytorch_amd.ops import conv as conv_ops
     from network_distributed_pytorch_amd.ops._ext import ext
