@@ -1445,6 +1445,13 @@ int conv_wgrad_imgs(int cls, const ConvGeom& g, int B) {
     while (d > 4 && (B % d != 0 || (B / d) * per_slice < kFillWgs)) d /= 2;
     if (B % d == 0 && wino_wgrad_red(B, d)) return d;
   }
+  if (cls == 0 && g.H == 8 && g.C % 16 == 0 && g.Co % 16 == 0 && B >= 256 && B % 16 == 0 && wino_wgrad_red(B, 16)) {
+    // from batch 256: 16-image slices over the 4-wave reduction (4 images per wave) — half the
+    // slabs of 8-image slices, two workgroups per CU at 512.  ResNet-18 r=4, ms/step: batch 512
+    // 1.3866 / 1.3908 vs 1.4043 / 1.4021 (8-image, 2-wave), batch 256 0.9942 / 0.9993 vs 1.0035 /
+    // 1.0046 (8-image, 1-wave); 32-image slices 1.4103 (profiles/r6/bench_l1_wgrad_slices.jsonl)
+    return 16;
+  }
   int def = cls == 0 ? 8 : cls == 1 ? 16 : cls == 2 ? 16 : cls == 4 ? 8 : cls == 5 ? 16 : 4;
   const int cb = cls == 3 ? 3 : 32;
   const int per_slice = (g.Co / 32) * ((g.C + cb - 1) / cb);

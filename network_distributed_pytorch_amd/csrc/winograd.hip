@@ -394,9 +394,9 @@ void launch_wino_conv(const float* x, const float* u, float* y, int B, int inC, 
 // instantiation (one tile per lane group and image: a load per 16 MFMAs) measured slower than the
 // direct grad-W kernel (conv.hip launch_conv_wgrad) and is not built
 bool wino_wgrad_ok(int C, int Co, int H) { return H == 8 && C % 16 == 0 && Co % 16 == 0 && !wino_disabled(); }
-// the 4-wave reduction at per-GPU batch <= 128 for slices of imgs % 4 == 0 images (conv.hip
-// conv_wgrad_imgs sizes the slices for it: one workgroup per block and slice)
-bool wino_wgrad_red(int B, int imgs) { return B <= 128 && imgs % 4 == 0; }
+// the 4-wave reduction at per-GPU batch <= 128 for slices of imgs % 4 == 0 images, and from 256 for
+// 16-image slices (conv.hip conv_wgrad_imgs sizes the slices for it: one workgroup per block and slice)
+bool wino_wgrad_red(int B, int imgs) { return imgs % 4 == 0 && (B <= 128 || (B >= 256 && imgs == 16)); }
 // waves per (co, ci) block: 4 (above); 2 from batch 512 — the slice's images split over two waves
 // summed through LDS: twice the workgroups of RED = 1 at the same slab count, two waves per SIMD
 // instead of one (the 8x8 kernel keeps one image's operands in flight and relies on a second wave
