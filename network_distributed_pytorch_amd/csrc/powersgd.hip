@@ -310,6 +310,35 @@ __global__ __launch_bounds__(256) void psgd_p_wide_kernel(const MatGeom* __restr
   float acc[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) acc[v] = 0.f;
+  // One load group (SB == NS): the M = g + e rows stay in registers and are stored only after
+  // the split-K arrival — the arrival's vmcnt(0) drain then waits for the partial store alone,
+  // not for the whole e stream's write acknowledgements.
+  constexpr bool kLateE = SB == NS;
+  f32x4 late[kLateE ? 4 : 1][kLateE ? SB : 1];
+  auto store_e = [&](int i, int b, f32x4 v) {
+    if (arow0 + i >= n) return;
+    const int64_t o = (int64_t)(arow0 + i) * m + b;
+    if (g.vec) {
+      if (b < it.k1) {
+        if constexpr (NT >= 2) __builtin_nontemporal_store(v, reinterpret_cast<f32x4 NDP_GLOBAL*>(pt.e + o));
+        else st4(pt.e + o, v);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (b + j < it.k1) pt.e[o + j] = v[j];
+    }
+  };
+  auto store_late = [&]() {
+    if constexpr (kLateE) {
+      if (active && fuse_ef) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int sb = 0; sb < SB; ++sb) store_e(i, it.k0 + 256 * sb + 4 * lane, late[i][sb]);
+      }
+    }
+  };
 
   if (active) {
 #pragma unroll
@@ -393,19 +422,8 @@ __global__ __launch_bounds__(256) void psgd_p_wide_kernel(const MatGeom* __restr
             e4 = e4 - o;
           }
           mv[i][sb] = mv[i][sb] + e4;  // send = g + e   (ddp_init.py:156-157)
-          if (arow0 + i < n) {
-            const int64_t o = (int64_t)(arow0 + i) * m + b;
-            if (g.vec) {
-              if (b < it.k1) {
-                if constexpr (NT >= 2) __builtin_nontemporal_store(mv[i][sb], reinterpret_cast<f32x4 NDP_GLOBAL*>(pt.e + o));
-                else st4(pt.e + o, mv[i][sb]);
-              }
-            } else {
-#pragma unroll
-              for (int j = 0; j < 4; ++j)
-                if (b + j < it.k1) pt.e[o + j] = mv[i][sb][j];
-            }
-          }
+          if constexpr (kLateE) late[i][sb] = mv[i][sb];
+          else store_e(i, b, mv[i][sb]);
         }
       }
 #pragma unroll
@@ -426,14 +444,18 @@ __global__ __launch_bounds__(256) void psgd_p_wide_kernel(const MatGeom* __restr
   const int chunks = g.p_chunks;
   if (fin.out == nullptr) {  // partials for a separate seg_reduce
     if (wr) p_part[g.pp_off + (int64_t)it.chunk * n * r + (int64_t)a * r + c] = acc[0];
+    store_late();
     return;
   }
   if (chunks == 1) {  // unsplit: the item IS the row block's P
     if (wr) fin.out[g.p_off + (int64_t)a * r + c] = acc[0];
+    store_late();
     return;
   }
   if (wr) st_sc1(p_part + g.pp_off + (int64_t)it.chunk * n * r + (int64_t)a * r + c, acc[0]);
-  if (!last_arrival(fin.ctr + it.rb, chunks, &last_flag)) return;
+  const bool last = last_arrival(fin.ctr + it.rb, chunks, &last_flag);
+  store_late();
+  if (!last) return;
   const int rows = min(kPWRows, n - it.row0);
   for (int t = threadIdx.x; t < rows * r; t += 256) {
     const int64_t o = (int64_t)it.row0 * r + t;  // row-major n x r: the block's rows are contiguous

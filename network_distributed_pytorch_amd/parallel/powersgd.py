@@ -280,6 +280,8 @@ class _PlanBuffers:
     def _patch_geom(host: torch.Tensor, vec: List[int], tz: List[Tuple[int, int]]) -> torch.Tensor:
         """A copy of MatGeom host bytes with ``vec`` and the Toeplitz-image words set."""
         geom = host.clone()
+        if not vec:  # no high-rank matrices (rank-1 group only)
+            return geom
         gi = geom.view(torch.int32).view(len(vec), -1)
         gi[:, 3] = torch.tensor(vec, dtype=torch.int32)            # MatGeom.vec
         gi[:, 10:12] = torch.tensor(tz, dtype=torch.int32).view(-1, 2)  # MatGeom.tz0, tz1
