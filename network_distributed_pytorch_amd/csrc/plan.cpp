@@ -21,10 +21,13 @@ namespace ndp {
 // columns per wide P item: 1024 (default), 512 or 256 (NDP_PSGD_PKW, A/B).  Round 5 measured
 // narrower items slower (profiles/r5/bench_psgd_pkw_ab.jsonl) with a kernel that still looped over
 // 1024 columns (3/4 of its loads masked off); the kernel now has one instance per width.
-// Default by the plan's max rank (tools/psgd_bench.py, round 6): rank <= 4 -> 512 (ResNet-18 r=4
-// reducer 112.0 -> 106.4 µs; 256: 109.1), else 1024 (DistilBERT r=8: 676 µs; 512: 700, 256: 799).
+// Default by the plan's max rank (tools/psgd_bench.py, round 6): rank <= 8 -> 512 (ResNet-18 r=4
+// reducer 112.0 -> 106.4 µs; 256: 109.1.  DistilBERT r=8: 676 µs at 1024 against 700 at 512 until
+// the P pass kept its single load group's e stores past the split-K arrival; since, 1024: 685.7 /
+// 686.1 / 684.7 / 686.7, 512: 678.7 / 679.1, 256: 808.7 / 806.8 — profiles/r6/psgd_pkw_bert8.jsonl),
+// else 1024.
 int64_t p_item_cols(int plan_rank) {
-  const int64_t dflt = plan_rank <= 4 ? 512 : kPKW;
+  const int64_t dflt = plan_rank <= 8 ? 512 : kPKW;
   const char* e = getenv("NDP_PSGD_PKW");
   const int64_t v = e ? atoll(e) : dflt;
   return (v == 256 || v == 512 || v == 1024) ? v : dflt;
