@@ -20,17 +20,12 @@ struct MatGeom {
   int32_t p_off, q_off; // element offsets into the flat P / Q buffers (reference order)
   int32_t pp_off, qp_off;     // element offsets into the P / Q split-K partial scratch
   int32_t p_chunks, q_chunks; // number of split-K slabs for P (over m) and Q (over n)
-  // Toeplitz image of the parameter kept by the update pass (engine modes 1 / 2, MatPtrs.out):
-  // tz0 = H | W << 5 | OH << 10 | OW << 15 | KH << 20 | KW << 25, tz1 = stride | pad << 8
-  // (models/conv_gemm.py ToeplitzBank; 0 = no image)
-  int32_t tz0, tz1;
-  int32_t pad[4];
+  int32_t pad[6];
 };
 
 // ---- per-matrix bound pointers (64 B) -------------------------------------------
 // engine mode : min = grad, e = error memory (M = g + e is written back into e),
-//               mread = e, mom = momentum, x = parameter, g = grad (optional write),
-//               out = the parameter's Toeplitz image W_big^T (optional, MatGeom.tz0/tz1)
+//               mread = e, mom = momentum, x = parameter, g = grad (optional write)
 // api mode    : min = M (caller's send buffer), e = nullptr, mread = M,
 //               out = grad_out, mem = memory_out
 struct MatPtrs {

@@ -608,27 +608,6 @@ __global__ __launch_bounds__(256) void psgd_q_kernel(const MatGeom* __restrict__
 // (16-B accesses of e / m / x).  Qs = Q_sum / q_div (reducer.py:147).  One designated
 // wave per column block also writes Qs into the warm-start buffer (reducer.py:101-111).
 // ----------------------------------------------------------------------------------
-// Toeplitz image (models/conv_gemm.py): W_big^T[(co, oh, ow)][(ci, ih, iw)] = W[co, ci, kh, kw]
-// with ih = oh*s - p + kh.  The update pass stores each new parameter value to the <= OH*OW
-// image cells it feeds, so the next forward needs no expand launch (the image's zero cells
-// were written once, by the expand that built it, and nothing writes them again).
-__device__ __forceinline__ void tz_store(float NDP_GLOBAL* img, const MatGeom& g, int co, int col, float v) {
-  const int H = g.tz0 & 31, W = (g.tz0 >> 5) & 31, OH = (g.tz0 >> 10) & 31, OW = (g.tz0 >> 15) & 31;
-  const int KH = (g.tz0 >> 20) & 31, KW = (g.tz0 >> 25) & 31, s = g.tz1 & 255, p = (g.tz1 >> 8) & 255;
-  const int kk = KH * KW;
-  const int ci = col / kk, t = col - ci * kk, kh = t / KW, kw = t - kh * KW;
-  const int64_t K = (int64_t)(g.m / kk) * H * W;
-  for (int oh = 0; oh < OH; ++oh) {
-    const int ih = oh * s - p + kh;
-    if (ih < 0 || ih >= H) continue;
-    for (int ow = 0; ow < OW; ++ow) {
-      const int iw = ow * s - p + kw;
-      if (iw < 0 || iw >= W) continue;
-      img[((int64_t)(co * OH + oh) * OW + ow) * K + (ci * H + ih) * W + iw] = v;
-    }
-  }
-}
-
 __global__ __launch_bounds__(256) void psgd_update_kernel(
     const MatGeom* __restrict__ geom, const MatPtrs* __restrict__ ptrs,
     const UItem* __restrict__ items, const float* __restrict__ p_hat,
@@ -706,10 +685,6 @@ __global__ __launch_bounds__(256) void psgd_update_kernel(
         st4(pt.mom + ro + b, mm);
         st4(pt.x + ro + b, xx);
         if (mode == 2) st4(pt.g + ro + b, up);
-        if (pt.out != nullptr) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) tz_store(pt.out, g, aL, b + j, xx[j]);
-        }
       }
     } else {
 #pragma unroll
@@ -725,10 +700,8 @@ __global__ __launch_bounds__(256) void psgd_update_kernel(
           const float mm = __fadd_rn(__fmul_rn(pt.mom[k], momentum), o[j]);
           pt.mom[k] = mm;
           const float up = o[j] + mm;
-          const float xn = fmaf(-lr, up, pt.x[k]);
-          pt.x[k] = xn;
+          pt.x[k] = fmaf(-lr, up, pt.x[k]);
           if (mode == 2) pt.g[k] = up;
-          if (pt.out != nullptr) tz_store(pt.out, g, aL, b + j, xn);
         }
       }
     }
@@ -792,9 +765,6 @@ __global__ __launch_bounds__(256) void psgd_update_wide_kernel(
   }
   const int b = it.col0 + 4 * lane;
   const int nb = max(0, min(4, m - b));  // valid columns of this lane (vec: 0 or 4)
-  // the new parameter rows, kept for the Toeplitz image pass below (wave-private)
-  __shared__ float xs[4][kURowsPerWave][kUWideCols];
-  const bool img = (mode == 1 || mode == 2) && pt.out != nullptr;
   // the HBM stream first: M (= g + e), momentum, parameters of every row of the wave
   f32x4 Mv[kURowsPerWave], Mm[kURowsPerWave], Xv[kURowsPerWave];
   if (g.vec) {
@@ -866,7 +836,6 @@ __global__ __launch_bounds__(256) void psgd_update_wide_kernel(
         else st4(pt.mom + ro + b, mm);
         st4(pt.x + ro + b, xx);
         if (mode == 2) st4(pt.g + ro + b, up);
-        if (img) *reinterpret_cast<f32x4*>(&xs[wave][i][4 * lane]) = xx;
       }
     } else {
 #pragma unroll
@@ -884,56 +853,8 @@ __global__ __launch_bounds__(256) void psgd_update_wide_kernel(
           const float mm = __fadd_rn(__fmul_rn(pt.mom[k], momentum), o[j]);
           pt.mom[k] = mm;
           const float up = o[j] + mm;
-          const float xn = fmaf(-lr, up, pt.x[k]);
-          pt.x[k] = xn;
+          pt.x[k] = fmaf(-lr, up, pt.x[k]);
           if (mode == 2) pt.g[k] = up;
-          if (img) xs[wave][i][4 * lane + j] = xn;
-        }
-      }
-    }
-  }
-  if (!img) return;
-  // Toeplitz image (models/conv_gemm.py): W_big^T[(co, oh, ow)][(ci, ih, iw)] = W[co, ci, kh, kw],
-  // kh = ih - oh*s + p.  A lane takes 4 consecutive image cells of the tile's channels (one
-  // float4 store when all 4 come from this tile) and copies each cell whose tap lies in the
-  // tile from LDS; cells of taps outside the kernel stay the zeros the building expand wrote.
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const int H = g.tz0 & 31, W = (g.tz0 >> 5) & 31, OH = (g.tz0 >> 10) & 31, OW = (g.tz0 >> 15) & 31;
-  const int KH = (g.tz0 >> 20) & 31, KW = (g.tz0 >> 25) & 31, sd = g.tz1 & 255, pd = (g.tz1 >> 8) & 255;
-  const int kk = KH * KW, HW = H * W;
-  const int c_end = min(it.col0 + kUWideCols, m);
-  const int cell0 = it.col0 / kk * HW, cell1 = ((c_end - 1) / kk + 1) * HW;  // the tile's channels
-  const int64_t K = (int64_t)(m / kk) * HW;
-  const bool k4 = (K & 3) == 0;  // 16-B aligned rows: float4 stores of 4 consecutive cells
-  for (int i = 0; i < kURowsPerWave; ++i) {
-    const int a = arow0 + i;
-    if (a >= n) break;  // wave-uniform
-    const float* xr = xs[wave][i];
-    for (int q = 0; q < OH * OW; ++q) {
-      const int oh = q / OW, ow = q - oh * OW;
-      const int dh = pd - oh * sd, dw = pd - ow * sd;  // kh = ih + dh, kw = iw + dw
-      float NDP_GLOBAL* row = pt.out + ((int64_t)a * OH * OW + q) * K;
-      for (int u = (cell0 >> 2) + lane; 4 * u < cell1; u += 64) {
-        int c = 4 * u, cl = c / HW, rr = c - cl * HW, ih = rr / W, iw = rr - ih * W;
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        int ok = 0;
-#pragma unroll
-        for (int e = 0; e < 4; ++e, ++c) {
-          const int kh = ih + dh, kw = iw + dw, col = cl * kk + kh * KW + kw;
-          if (c >= cell0 && c < cell1 && kh >= 0 && kh < KH && kw >= 0 && kw < KW && col >= it.col0 && col < c_end) {
-            v[e] = xr[col - it.col0];
-            ok |= 1 << e;
-          }
-          if (++iw == W) { iw = 0; if (++ih == H) { ih = 0; ++cl; } }
-        }
-        if (ok == 15 && k4) {
-          st4(row + 4 * u, v);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if ((ok >> e) & 1) row[4 * u + e] = v[e];
         }
       }
     }

@@ -33,7 +33,6 @@ FUSIONS = {
     "defer_gradw": "grad-W slab sums / folds batched at the end of backward (ops/gradfinish.py)",
     "grad_arena": "dense-arm gradients written straight into the bucket arena (ops/gradarena.py)",
     "tgemm": "strided / tabled MFMA GEMM convs for 1x1 layers (ops/tgconv.py)",
-    "tz_upd": "PowerSGD update pass writes the layer3 / layer4 Toeplitz weight images (no expand launch, models/conv_gemm.py)",
     "tuned_gemms": "hipBLASLt algorithm table for the Toeplitz GEMMs (ops/gemm_tuning.py)",
     "lazy_ef": "PowerSGD error feedback formed in the next P pass (parallel/powersgd.py)",
     "psgd_fin": "PowerSGD P / Q split-K sums, rank-1 pack and rank-1 step inside the P / Q / update launches",

@@ -28,7 +28,6 @@ Toeplitz GEMMs in the step — profiles/r4/smallconv.md — and were removed in 
 """
 from __future__ import annotations
 
-import weakref
 from typing import Dict, Tuple
 
 import torch
@@ -42,7 +41,7 @@ from ..ops.gradarena import grad_buffer
 from ..ops.gradlink import InjectGrad
 from ..ops.tgconv import TgConvFn, tg_plan
 
-__all__ = ["GemmConv2d", "ToeplitzBank", "toeplitz_maps", "eligible", "refresh_images", "stale_images"]
+__all__ = ["GemmConv2d", "ToeplitzBank", "toeplitz_maps", "eligible"]
 
 
 def eligible(h: int, w: int, oh: int, ow: int) -> bool:
@@ -83,13 +82,6 @@ class ToeplitzBank:
     in a pass — forward order is fixed — expands every member; the others reuse their
     buffer.  Valid because weights only change between passes (optimizer step); a
     ``w_big`` saved for backward is rebuilt by the NEXT forward, i.e. after that backward.
-
-    Owned members (:meth:`own`): the PowerSGD update pass writes the new weights into the
-    image as well (csrc/powersgd.hip ``tz_store``), so no forward expands them — the image's
-    zero cells were written by the expand that built it and nothing writes them again.  A
-    torch-side write to the weight or to the optimizer's arena (``load_state_dict``, a
-    snapshot restore) bumps a version counter: the member is then stale and is expanded
-    again by the next forward, or by :func:`refresh_images` before a graph replay.
     """
 
     MAX_EXPAND = 24  # csrc/ndp_kernels.h kMaxExpand
@@ -97,41 +89,6 @@ class ToeplitzBank:
     def __init__(self):
         self.members: list = []  # [(layer, geom, w_big)]
         self._index: dict = {}
-        self._owned: dict = {}   # id(layer) -> [w_big, arena, versions when last current]
-        _BANKS.add(self)
-
-    @staticmethod
-    def _versions(weight, arena):
-        return weight._version, arena._version
-
-    def own(self, weight: torch.Tensor, arena: torch.Tensor):
-        """Called by the optimizer that updates ``weight`` in place inside ``arena`` when it
-        binds it: from now on its update pass keeps this member's image current.  Returns
-        (w_big, geom), or None if ``weight`` is not a member."""
-        for layer, geom, w_big in self.members:
-            if layer.weight is weight and w_big.device == weight.device:
-                self._owned[id(layer)] = [w_big, arena, self._versions(weight, arena)]
-                return w_big, geom
-        return None
-
-    def _current(self, layer, w_big) -> bool:
-        o = self._owned.get(id(layer))
-        return o is not None and o[0] is w_big and o[2] == self._versions(layer.weight, o[1])
-
-    def stale(self) -> list:
-        return [m for m in self.members if not self._current(m[0], m[2])]
-
-    def expand(self, members: list):
-        """Rebuild ``members``' images (<= MAX_EXPAND layers per launch: kernel-argument table)."""
-        batch = [(m.weight, wb, list(g)) for m, g, wb in members]
-        for j in range(0, len(batch), self.MAX_EXPAND):
-            ext().toeplitz_expand_many(batch[j: j + self.MAX_EXPAND])
-        if torch.cuda.is_current_stream_capturing():
-            return  # recorded, not run: owned members stay stale for the eager side
-        for m, _, wb in members:
-            o = self._owned.get(id(m))
-            if o is not None and o[0] is wb:
-                o[2] = self._versions(m.weight, o[1])
 
     def get(self, layer, weight: torch.Tensor, geom: tuple, n: int, k: int) -> torch.Tensor:
         key = id(layer)
@@ -140,39 +97,17 @@ class ToeplitzBank:
             assert not torch.cuda.is_current_stream_capturing(), "Toeplitz bank grows during capture"
             w_big = torch.empty(n, k, device=weight.device, dtype=torch.float32)
             ext().toeplitz_expand(weight.contiguous(), w_big, list(geom))
-            layer.weight._ndp_tbank = self  # parallel/powersgd.py: the update pass may own it
             if i is None:
                 self._index[key] = len(self.members)
                 self.members.append((layer, geom, w_big))
             else:
                 self.members[i] = (layer, geom, w_big)
             return w_big
-        if i == 0:
-            stale = self.stale()
-            if stale:
-                self.expand(stale)
+        if i == 0:  # <= MAX_EXPAND layers per launch (kernel-argument table)
+            batch = [(m.weight, wb, list(g)) for m, g, wb in self.members]
+            for j in range(0, len(batch), self.MAX_EXPAND):
+                ext().toeplitz_expand_many(batch[j: j + self.MAX_EXPAND])
         return self.members[i][2]
-
-
-_BANKS: "weakref.WeakSet[ToeplitzBank]" = weakref.WeakSet()
-
-
-def stale_images() -> list:
-    """[(bank, members)] of owned Toeplitz images a torch-side weight write left stale."""
-    out = []
-    for bank in list(_BANKS):
-        if bank._owned:
-            st = [m for m in bank.stale() if id(m[0]) in bank._owned]
-            if st:
-                out.append((bank, st))
-    return out
-
-
-def refresh_images(stale: "list | None" = None):
-    """Rebuild every stale owned Toeplitz image now (before a graph replay, after a snapshot
-    restore): a captured forward expands none of the owned members."""
-    for bank, members in (stale_images() if stale is None else stale):
-        bank.expand(members)
 
 
 class _ToeplitzConv(torch.autograd.Function):

@@ -253,39 +253,27 @@ class _PlanBuffers:
             raise RuntimeError("PowerSGD orthogonalisation: a cross-workgroup barrier timed out; P-hat "
                                "was poisoned with NaN (co-residency violated)")
 
-    def bind(self, rows: List[List[int]], vec: List[int], tz: Optional[List[Tuple[int, int]]] = None) -> bool:
-        """Point the grouped kernels at new tensors; returns True if the tables changed.
-        ``tz``: per matrix (MatGeom.tz0, tz1) of the Toeplitz image bound as MatPtrs.out."""
-        tz = tz or [(0, 0)] * len(rows)
-        key = (upload_epoch(), tuple(map(tuple, rows)), tuple(vec), tuple(tz))
+    def bind(self, rows: List[List[int]], vec: List[int]) -> bool:
+        """Point the grouped kernels at new tensors; returns True if the tables changed."""
+        key = (upload_epoch(), tuple(map(tuple, rows)), tuple(vec))
         if key == self._bind_key:
             return False
         X = ext()
-        upload(self.geom, self._patch_geom(self._geom_host, vec, tz))
+        upload(self.geom, X.patch_geom_vec(self._geom_host, vec))
         upload(self.ptrs, X.make_mat_ptrs(rows))
         self._bind_key = key
         return True
 
-    def bind_range(self, lo: int, rows: List[List[int]], vec: List[int],
-                   tz: Optional[List[Tuple[int, int]]] = None):
+    def bind_range(self, lo: int, rows: List[List[int]], vec: List[int]):
         """Upload geometry + pointer rows of matrices [lo, lo + len(rows)) only."""
         X = ext()
         sz = X.SIZEOF_MATGEOM
         hi = lo + len(rows)
-        geom = self._patch_geom(self._geom_host[lo * sz: hi * sz], vec, tz or [(0, 0)] * len(rows))
+        geom = self._geom_host[lo * sz: hi * sz].clone()
+        gi = geom.view(torch.int32).view(hi - lo, sz // 4)
+        gi[:, 3] = torch.tensor(vec, dtype=torch.int32)  # MatGeom.vec
         upload(self.geom[lo * sz: hi * sz], geom)
         upload(self.ptrs[lo * X.SIZEOF_MATPTRS: hi * X.SIZEOF_MATPTRS], X.make_mat_ptrs(rows))
-
-    @staticmethod
-    def _patch_geom(host: torch.Tensor, vec: List[int], tz: List[Tuple[int, int]]) -> torch.Tensor:
-        """A copy of MatGeom host bytes with ``vec`` and the Toeplitz-image words set."""
-        geom = host.clone()
-        if not vec:  # no high-rank matrices (rank-1 group only)
-            return geom
-        gi = geom.view(torch.int32).view(len(vec), -1)
-        gi[:, 3] = torch.tensor(vec, dtype=torch.int32)            # MatGeom.vec
-        gi[:, 10:12] = torch.tensor(tz, dtype=torch.int32).view(-1, 2)  # MatGeom.tz0, tz1
-        return geom
 
     def p_view(self, i):
         n, _ = self.shapes[i]
@@ -430,9 +418,6 @@ class PowerSGDReducer(Reducer):
 
 
 _LAZY_MAX_RANK = 16  # csrc/ndp_kernels.h kUWideMaxRank: the wide P / update kernels
-# the update pass also writes the Toeplitz images of the layer3 / layer4 weights (no expand
-# launch in the next forward, models/conv_gemm.py ToeplitzBank)
-_TZ_UPD = fusion_on("tz_upd")
 # Q split-K chunks the Q kernel's last arriver sums itself; taller matrices (DistilBERT's 30522-row
 # embedding: 120 chunks) keep a seg_reduce launch, which spreads that sum over the whole device
 Q_FIN_MAX = int(os.environ.get("NDP_QFIN_MAX", "32"))
@@ -627,17 +612,15 @@ class PowerSGDOptimizer:
         key = (upload_epoch(),) + tuple(t.data_ptr() for t in grads)
         if key == g.key:
             return
-        rows, vec, tz = [], [], []
+        rows, vec = [], []
         for p, gr, (n, m) in zip(g.params, grads, B.shapes[g.lo:g.hi]):
             assert gr.is_contiguous() and gr.dtype == torch.float32, "PowerSGD needs dense fp32 grads"
             s = self.offsets[id(p)]
             e, mo, x = (t[s:].data_ptr() for t in (self._e, self.m, self.x))
-            img, words = self._image(p)
-            row = [gr.data_ptr(), e, e, img, 0, mo, x, gr.data_ptr()]
+            row = [gr.data_ptr(), e, e, 0, 0, mo, x, gr.data_ptr()]
             rows.append(row)
             vec.append(_vec_ok(m, row))
-            tz.append(words)
-        B.bind_range(g.lo, rows, vec, tz)
+        B.bind_range(g.lo, rows, vec)
         g.p_seg.set(B.p_seg_specs(g.lo, g.hi))
         g.key = key
 
@@ -709,21 +692,6 @@ class PowerSGDOptimizer:
         self.comm.side_join()
 
     # -- helpers -------------------------------------------------------------------------
-    def _image(self, p) -> Tuple[int, Tuple[int, int]]:
-        """(address, (tz0, tz1)) of ``p``'s Toeplitz image when the update pass can keep it
-        current (models/conv_gemm.ToeplitzBank.own), else (0, (0, 0))."""
-        bank = getattr(p, "_ndp_tbank", None)
-        if bank is None or not self.native or not _TZ_UPD:
-            return 0, (0, 0)
-        got = bank.own(p, self.x)
-        if got is None:
-            return 0, (0, 0)
-        w_big, (C, H, W, Co, KH, KW, s, pad) = got
-        OH = (H + 2 * pad - KH) // s + 1
-        OW = (W + 2 * pad - KW) // s + 1
-        tz0 = H | W << 5 | OH << 10 | OW << 15 | KH << 20 | KW << 25
-        return w_big.data_ptr(), (tz0, s | pad << 8)
-
     def zero_grad(self, set_to_none: bool = True):
         for p in self.params:
             if set_to_none:
@@ -758,17 +726,15 @@ class PowerSGDOptimizer:
         if key == self._grad_key:
             return
         B = self.buf
-        rows, vec, tz = [], [], []
+        rows, vec = [], []
         for p, (n, m) in zip(self.high, B.shapes):
             s = self.offsets[id(p)]
             g = gmap[id(p)].data_ptr()
             e, mo, x = (t[s:].data_ptr() for t in (self._e, self.m, self.x))
-            img, words = self._image(p)
-            row = [g, e, e, img, 0, mo, x, g]
+            row = [g, e, e, 0, 0, mo, x, g]
             rows.append(row)
             vec.append(_vec_ok(m, row))
-            tz.append(words)
-        B.bind(rows, vec, tz)
+        B.bind(rows, vec)
         pack, outs = [], []
         for p in self.rank1:
             s = self.offsets[id(p)] - self.r1_start
@@ -1013,8 +979,6 @@ class PowerSGDOptimizer:
         self.bits_communicated = snap["bits"]
         self._q_ready = snap["q_ready"]
         self.rng.set_state(snap["rng"])
-        from ..models.conv_gemm import refresh_images
-        refresh_images()  # the owned Toeplitz images follow the restored weights
 
     # -- checkpoint / resume ---------------------------------------------------------------
     def state_dict(self):

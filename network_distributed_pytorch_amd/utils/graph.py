@@ -233,11 +233,6 @@ class StepRunner:
             self.capture()
         # an eager step since capture may have re-bound a table the graph reads
         self._upload_gen = _UPLOADS.ensure(self._uploads, self._upload_gen)
-        from ..models.conv_gemm import refresh_images, stale_images
-        stale = stale_images()  # owned Toeplitz images a torch-side weight write left stale
-        if stale:
-            self.join()
-            refresh_images(stale)
         if self.side_graphs:
             if self._comm.host_flag_error():  # a wait of an earlier replay timed out: stop now
                 self._comm.raise_flag_error()

@@ -265,68 +265,6 @@ def test_tables_reuploaded_after_graph_restore(device):
     assert torch.equal(ref, got), (ref - got).abs().max()
 
 
-def _train_tz(device, mode, on, steps=4, poke=None):
-    """ResNet-18 PowerSGD steps with the update pass owning the Toeplitz images (``on``) or
-    the forward expanding them; ``poke``: a step index before which every conv weight is
-    scaled by a torch op (a version bump the bank must notice)."""
-    import network_distributed_pytorch_amd.parallel.powersgd as ps
-
-    old = ps._TZ_UPD
-    ps._TZ_UPD = on
-    try:
-        torch.manual_seed(5)
-        model = _resnet(device)
-        comm = Communicator(device=device)
-        sync = build_grad_sync("powersgd", model, comm, lr=1e-2, momentum=0.9, rank=4, overlap=False)
-        batches = _batches(device, "resnet", steps)
-        static = [batches[0][0].clone(), batches[0][1].clone()]
-
-        def pre():
-            sync.zero_grad()
-            torch.nn.functional.cross_entropy(model(static[0]), static[1]).backward()
-
-        runner = StepRunner(pre, sync, mode=mode, warmup=2, state_tensors=list(model.buffers()))
-        for i, (x, y) in enumerate(batches):
-            if poke is not None and i == poke:
-                with torch.no_grad():
-                    for p in model.parameters():
-                        if p.dim() == 4:
-                            p.mul_(0.75)
-            static[0].copy_(x)
-            static[1].copy_(y)
-            runner()
-        torch.cuda.synchronize()
-        out = torch.cat([p.detach().reshape(-1) for p in model.parameters()]).clone()
-        bank = next(m.bank for m in model.modules() if getattr(m, "bank", None) is not None)
-        comm.close()
-        return out, bank
-    finally:
-        ps._TZ_UPD = old
-
-
-@pytest.mark.parametrize("mode", ["none", "full"])
-@pytest.mark.parametrize("poke", [None, 2])
-def test_toeplitz_images_kept_by_update_pass(device, mode, poke):
-    """csrc/powersgd.hip tz_store: the update pass writes the layer3/4 Toeplitz images and
-    the forward skips their expand.  Training is bitwise the expand-every-forward arm, eager
-    and whole-step graph (the snapshot restore after capture and a torch-side weight write
-    both leave the images stale; they are rebuilt), and every owned image equals a fresh
-    expand of its weight."""
-    from network_distributed_pytorch_amd.ops._ext import ext
-
-    with deterministic():
-        ref, _ = _train_tz(device, mode, on=False, poke=poke)
-        got, bank = _train_tz(device, mode, on=True, poke=poke)
-    assert torch.isfinite(ref).all()
-    assert torch.equal(ref, got), (ref - got).abs().max()
-    assert len(bank._owned) >= 7, len(bank._owned)  # layer3/4 3x3 convs + the layer4 downsample
-    assert not bank.stale()
-    for layer, geom, w_big in bank.members:
-        fresh = torch.empty_like(w_big)
-        ext().toeplitz_expand(layer.weight.detach().contiguous(), fresh, list(geom))
-        assert torch.equal(fresh, w_big), geom
-
-
 @pytest.mark.parametrize("link", ["100g", "10g"])
 def test_link_pacing_matches_model(device, link):
     """1-GPU link emulation: the stall charged on the stream for an
