@@ -78,6 +78,32 @@ __device__ __forceinline__ BnSlice slice_of(int N, int S, int s) {
   return {n0, n0 + base + (s < rem ? 1 : 0)};
 }
 
+// for_slice<4> with the thread's FIRST access loaded (ld) before pre() runs — the per-channel
+// statistics reduction of an apply kernel — so its HBM latency overlaps that reduction instead
+// of following it; then f(o, loaded) for every access in for_slice order.  At the ResNet apply
+// shapes a thread's first access is usually its only one.
+template <typename T, typename L, typename P, typename F>
+__device__ __forceinline__ void for_slice4_pf(int64_t n0, int64_t n1, int C, int c, int HW, L ld, P pre, F f) {
+  const int per = HW / 4;
+  if (per <= 256 && (256 % per) == 0) {
+    const int q = (int)threadIdx.x % per, r = (int)threadIdx.x / per, step = 256 / per;
+    int64_t n = n0 + r;
+    const bool has = n < n1;
+    const int64_t o0 = (n * C + c) * HW + 4 * q;
+    T first{};
+    if (has) first = ld(o0);
+    pre();
+    if (has) f(o0, first);
+    for (n += step; n < n1; n += step) {
+      const int64_t o = (n * C + c) * HW + 4 * q;
+      f(o, ld(o));
+    }
+  } else {
+    pre();
+    for_slice<4>(n0, n1, C, c, HW, [&](int64_t o) { f(o, ld(o)); });
+  }
+}
+
 // sums of the S slice partials [c][s][2] of channel c: 8 loads in flight, adds in slice order
 __device__ __forceinline__ void slice_sums(const double* __restrict__ part, int c, int S, double& a, double& b) {
   a = 0.0;
@@ -173,47 +199,58 @@ __global__ __launch_bounds__(256) void bn_fwd_apply_kernel(
   const float gam = gamma ? gamma[c] : 1.f, bet = beta ? beta[c] : 0.f;
   const bool writer = training && s == 0 && threadIdx.x == 0 && rmean != nullptr;
   const float rm = writer ? rmean[c] : 0.f, rv = writer ? rvar[c] : 0.f;
-  float mean, invstd;
-  if (training) {
-    double sum, sq;
-    if (Sp > 0) slice_sums_block(part, c, Sp, sum, sq, red);
-    else slice_sums(part, c, S, sum, sq);
-    const double M = (double)N * HW;
-    const double mu = sum / M;
-    double var = sq / M - mu * mu;
-    if (var < 0.0) var = 0.0;
-    mean = (float)mu;
-    invstd = (float)(1.0 / sqrt(var + (double)eps));
-    if (s == 0 && threadIdx.x == 0) {
-      save_mean[c] = mean;
-      save_invstd[c] = invstd;
-      if (rmean != nullptr) {
-        const double unb = M > 1.0 ? var * M / (M - 1.0) : var;
-        rmean[c] = (float)((1.0 - momentum) * (double)rm + momentum * mu);
-        rvar[c] = (float)((1.0 - momentum) * (double)rv + momentum * unb);
+  float scale = 0.f, shift = 0.f;
+  auto coefficients = [&]() {
+    float mean, invstd;
+    if (training) {
+      double sum, sq;
+      if (Sp > 0) slice_sums_block(part, c, Sp, sum, sq, red);
+      else slice_sums(part, c, S, sum, sq);
+      const double M = (double)N * HW;
+      const double mu = sum / M;
+      double var = sq / M - mu * mu;
+      if (var < 0.0) var = 0.0;
+      mean = (float)mu;
+      invstd = (float)(1.0 / sqrt(var + (double)eps));
+      if (s == 0 && threadIdx.x == 0) {
+        save_mean[c] = mean;
+        save_invstd[c] = invstd;
+        if (rmean != nullptr) {
+          const double unb = M > 1.0 ? var * M / (M - 1.0) : var;
+          rmean[c] = (float)((1.0 - momentum) * (double)rm + momentum * mu);
+          rvar[c] = (float)((1.0 - momentum) * (double)rv + momentum * unb);
+        }
+        if (nbt != nullptr && c == 0) nbt[0] += 1;
       }
-      if (nbt != nullptr && c == 0) nbt[0] += 1;
+    } else {
+      mean = rmean[c];
+      invstd = 1.0f / sqrtf(rvar[c] + eps);
     }
-  } else {
-    mean = rmean[c];
-    invstd = 1.0f / sqrtf(rvar[c] + eps);
-  }
-  const float scale = gam * invstd;
-  const float shift = bet - mean * scale;
+    scale = gam * invstd;
+    shift = bet - mean * scale;
+  };
   const BnSlice sl = slice_of(N, S, s);
   if (VEC) {
-    for_slice<4>(sl.n0, sl.n1, C, c, HW, [&](int64_t o) {
-      f32x4 v = *reinterpret_cast<const f32x4*>(x + o);
-      f32x4 r = {0.f, 0.f, 0.f, 0.f};
-      if (res) r = *reinterpret_cast<const f32x4*>(res + o);
+    struct XR { f32x4 v, r; };
+    for_slice4_pf<XR>(
+        sl.n0, sl.n1, C, c, HW,
+        [&](int64_t o) {
+          XR t;
+          t.v = *reinterpret_cast<const f32x4*>(x + o);
+          t.r = res ? *reinterpret_cast<const f32x4*>(res + o) : f32x4{0.f, 0.f, 0.f, 0.f};
+          return t;
+        },
+        coefficients,
+        [&](int64_t o, XR t) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float z = fmaf(v[j], scale, shift) + r[j];
-        v[j] = relu ? fmaxf(z, 0.f) : z;
-      }
-      *reinterpret_cast<f32x4*>(y + o) = v;
-    });
+          for (int j = 0; j < 4; ++j) {
+            const float z = fmaf(t.v[j], scale, shift) + t.r[j];
+            t.v[j] = relu ? fmaxf(z, 0.f) : z;
+          }
+          *reinterpret_cast<f32x4*>(y + o) = t.v;
+        });
   } else {
+    coefficients();
     for_slice<1>(sl.n0, sl.n1, C, c, HW, [&](int64_t o) {
       const float z = fmaf(x[o], scale, shift) + (res ? res[o] : 0.f);
       y[o] = relu ? fmaxf(z, 0.f) : z;
@@ -305,40 +342,50 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   // mbet: ReLU mask recomputed from x (bn_bwd_stats_kernel)
   const float msc = mbet ? __fmul_rn(g, invstd) : 0.f;
   const float msh = mbet ? __fsub_rn(mbet[c], __fmul_rn(mean, msc)) : 0.f;
-  double sdz, sdzx;
-  if (Sp > 0) slice_sums_block(part, c, Sp, sdz, sdzx, red);
-  else slice_sums(part, c, S, sdz, sdzx);
-  if (s == 0 && threadIdx.x == 0) {
-    if (dgamma) dgamma[c] = (float)sdzx;
-    if (dbeta) dbeta[c] = (float)sdz;
-  }
-  const double M = (double)N * HW;
-  const float k1 = g * invstd;                    // dx = k1 * (dz - mdz - xhat * mdzx)
-  const float mdz = (float)(sdz / M);
-  const float mdzx = (float)(sdzx / M);
+  float k1 = 0.f, mdz = 0.f, mdzx = 0.f;  // dx = k1 * (dz - mdz - xhat * mdzx)
+  auto coefficients = [&]() {
+    double sdz, sdzx;
+    if (Sp > 0) slice_sums_block(part, c, Sp, sdz, sdzx, red);
+    else slice_sums(part, c, S, sdz, sdzx);
+    if (s == 0 && threadIdx.x == 0) {
+      if (dgamma) dgamma[c] = (float)sdzx;
+      if (dbeta) dbeta[c] = (float)sdz;
+    }
+    const double M = (double)N * HW;
+    k1 = g * invstd;
+    mdz = (float)(sdz / M);
+    mdzx = (float)(sdzx / M);
+  };
   const BnSlice sl = slice_of(N, S, s);
   if (VEC) {
-    for_slice<4>(sl.n0, sl.n1, C, c, HW, [&](int64_t o) {
-      const f32x4 gy = *reinterpret_cast<const f32x4*>(dy + o);
-      const f32x4 xv = *reinterpret_cast<const f32x4*>(x + o);
-      f32x4 yv = {1.f, 1.f, 1.f, 1.f};
-      if (mbet) {
+    struct GXY { f32x4 gy, xv, yv; };
+    for_slice4_pf<GXY>(
+        sl.n0, sl.n1, C, c, HW,
+        [&](int64_t o) {
+          GXY t;
+          t.gy = *reinterpret_cast<const f32x4*>(dy + o);
+          t.xv = *reinterpret_cast<const f32x4*>(x + o);
+          t.yv = (!mbet && relu) ? *reinterpret_cast<const f32x4*>(y + o) : f32x4{1.f, 1.f, 1.f, 1.f};
+          return t;
+        },
+        coefficients,
+        [&](int64_t o, GXY t) {
+          if (mbet) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) yv[j] = fmaf(xv[j], msc, msh);
-      } else if (relu) {
-        yv = *reinterpret_cast<const f32x4*>(y + o);
-      }
-      f32x4 dz, out;
+            for (int j = 0; j < 4; ++j) t.yv[j] = fmaf(t.xv[j], msc, msh);
+          }
+          f32x4 dz, out;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        dz[j] = (yv[j] > 0.f) ? gy[j] : 0.f;
-        const float xh = (xv[j] - mean) * invstd;
-        out[j] = k1 * (dz[j] - mdz - xh * mdzx);
-      }
-      *reinterpret_cast<f32x4*>(dx + o) = out;
-      if (dres) *reinterpret_cast<f32x4*>(dres + o) = dz;
-    });
+          for (int j = 0; j < 4; ++j) {
+            dz[j] = (t.yv[j] > 0.f) ? t.gy[j] : 0.f;
+            const float xh = (t.xv[j] - mean) * invstd;
+            out[j] = k1 * (dz[j] - mdz - xh * mdzx);
+          }
+          *reinterpret_cast<f32x4*>(dx + o) = out;
+          if (dres) *reinterpret_cast<f32x4*>(dres + o) = dz;
+        });
   } else {
+    coefficients();
     for_slice<1>(sl.n0, sl.n1, C, c, HW, [&](int64_t o) {
       const float dz = (!relu || y[o] > 0.f) ? dy[o] : 0.f;
       const float xh = (x[o] - mean) * invstd;
