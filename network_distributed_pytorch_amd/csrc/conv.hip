@@ -1452,7 +1452,11 @@ int conv_wgrad_imgs(int cls, const ConvGeom& g, int B) {
     // 1.0046 (8-image, 1-wave); 32-image slices 1.4103 (profiles/r6/bench_l1_wgrad_slices.jsonl)
     return 16;
   }
-  int def = cls == 0 ? 8 : cls == 1 ? 16 : cls == 2 ? 16 : cls == 4 ? 8 : cls == 5 ? 16 : 4;
+  // layer2 (class 1) from batch 512: 32-image slices, half the slabs.  Its grad-W now runs in one
+  // launch with its grad-x (wino_direct_pair_kernel), which fills the CUs: ResNet-18 r=4 batch 512
+  // 1.3711 / 1.3692 vs 1.3775 / 1.3804 ms (16-image), and 1.3806 / 1.3819 vs 1.3877 / 1.3886 on a
+  // second box; batch 256 unchanged (0.9927 vs 0.9920 / 0.9914) (profiles/r6/bench_l2_wgrad_slices.jsonl)
+  int def = cls == 0 ? 8 : cls == 1 ? (B >= 512 ? 32 : 16) : cls == 2 ? 16 : cls == 4 ? 8 : cls == 5 ? 16 : 4;
   const int cb = cls == 3 ? 3 : 32;
   const int per_slice = (g.Co / 32) * ((g.C + cb - 1) / cb);
   while (def > 1 && B % def != 0) def /= 2;  // a batch that is not a multiple of the default
